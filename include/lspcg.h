@@ -1,0 +1,141 @@
+/*
+ * lspcg.h -- C ABI of the MI355X-native PCG hot path (liblspcg_hip.so, gfx950).
+ *
+ * This is the drop-in boundary for the reference's native solver and GNN kernels.
+ * Every entry point names the reference interface it replaces:
+ *
+ *   pymathprim.linalg.PreconditionedConjugateGradient(A, device, preconditioner, dtype)
+ *       (unvendored; call sites neural_cg/utils/validate.py:73,79-80,110,116-117,145,151-156)
+ *       -> lspcg_solver_create / lspcg_solver_set_spai / lspcg_solver_solve
+ *   scipy csr_matvec inside the PCG (validate.py:102, 182)      -> lspcg_spmv
+ *   neural_cg/utils/validate.py:22-51 to_csr_cpu
+ *       + neural_cg/data.py:134-170 (make_bsr_from_coo_inds, apply_dbc_masking)
+ *                                                                -> lspcg_assemble
+ *   csr_matrix(spai.T) (validate.py:176)                         -> lspcg_mat_transpose
+ *   A.diagonal() (validate.py:243, 280)                          -> lspcg_mat_diagonal
+ *   csr @ diags(rsqrt_diag) (scaled_workspace.py:210-211)        -> lspcg_mat_scale_columns
+ *   neural_cg/nn/gnns.py:77-97 NodeEdgeProcessing.forward
+ *       (+ basic_layers.py:73-109 FeedForward, :145-225 MPLayer) -> lspcg_gnn_forward
+ *
+ * Conventions: plain pointers and sizes only.  Vector arguments of compute calls are
+ * DEVICE pointers; matrix/weight uploads accept host or device pointers.  All work is
+ * issued on the context's stream.  Every call returns LSPCG_OK (0), LSPCG_NOT_CONVERGED
+ * (1, solve only) or a negative error code; lspcg_last_error() describes the last error
+ * of the calling thread.
+ */
+#ifndef LSPCG_H_
+#define LSPCG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSPCG_OK 0
+#define LSPCG_NOT_CONVERGED 1
+#define LSPCG_ERR_ARG (-1)
+#define LSPCG_ERR_HIP (-2)
+#define LSPCG_ERR_UNSUPPORTED (-3)
+#define LSPCG_ERR_FORMAT (-4)
+
+#define LSPCG_F32 0
+#define LSPCG_F64 1
+
+/* preconditioner kinds (pymathprim names: none / diagonal / ext_spai / ext_spai_scaled) */
+#define LSPCG_PRECOND_NONE 0
+#define LSPCG_PRECOND_DIAGONAL 1
+#define LSPCG_PRECOND_EXT_SPAI 2
+#define LSPCG_PRECOND_EXT_SPAI_SCALED 3
+
+typedef struct lspcg_ctx lspcg_ctx;
+typedef struct lspcg_mat lspcg_mat;
+typedef struct lspcg_solver lspcg_solver;
+typedef struct lspcg_gnn lspcg_gnn;
+
+const char* lspcg_last_error(void);
+int lspcg_version(void);
+
+/* ---- context: one per GPU per host thread; stream NULL = the default (null) stream ---- */
+int lspcg_ctx_create(int device, void* stream, lspcg_ctx** out);
+int lspcg_ctx_destroy(lspcg_ctx* ctx);
+int lspcg_ctx_synchronize(lspcg_ctx* ctx);
+
+/* ---- sparse matrices (device copies owned by the handle) ---- */
+/* scalar CSR, n x n, int32 indptr[n+1] / indices[nnz], vals[nnz] of dtype */
+int lspcg_mat_create_csr(lspcg_ctx* ctx, int64_t n, int64_t nnz, const int32_t* indptr,
+                         const int32_t* indices, const void* vals, int dtype, lspcg_mat** out);
+/* block CSR, nb x nb blocks of bs x bs (bs in {1,3}), vals[nnzb][bs][bs] row-major */
+int lspcg_mat_create_bsr(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, const int32_t* indptr,
+                         const int32_t* indices, const void* vals, int dtype, lspcg_mat** out);
+int lspcg_mat_destroy(lspcg_mat* A);
+/* n = scalar rows, nnzb = stored blocks (= scalar nnz when bs == 1) */
+int lspcg_mat_info(const lspcg_mat* A, int64_t* n, int64_t* nnzb, int* bs, int* dtype);
+/* copy the handle's arrays out (host or device destinations; NULL skips an array) */
+int lspcg_mat_copy_out(const lspcg_mat* A, int32_t* indptr, int32_t* indices, void* vals);
+/* explicit transpose (sorted), replaces csr_matrix(spai.T) of validate.py:176 */
+int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out);
+/* d[i] = A[i,i] (0 where absent), device pointer of the matrix dtype, length n */
+int lspcg_mat_diagonal(const lspcg_mat* A, void* d);
+/* A <- A diag(d): column scaling, d device pointer of the matrix dtype, length n */
+int lspcg_mat_scale_columns(lspcg_mat* A, const void* d);
+
+/* ---- kernels ---- */
+/* y = A x (scipy csr_matvec bit pattern: per-row sequential sum in index order) */
+int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y);
+/* reps back-to-back SpMVs bracketed by HIP events on the ctx stream; average ms per launch */
+int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y, int reps,
+                     double* avg_ms);
+/* compensated, deterministic dot product of two device vectors; result to host */
+int lspcg_dot(lspcg_ctx* ctx, int64_t n, int dtype, const void* x, const void* y, double* out);
+
+/* ---- PCG solver (pymathprim.linalg.PreconditionedConjugateGradient) ---- */
+int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_solver** out);
+/* ext_spai=(L, eps): builds Lᵀ (and diag(A) for the scaled variant) on device.
+ * t_prec_ms (nullable) receives the device time of that setup. L must outlive solves. */
+int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, double* t_prec_ms);
+/* Solve A x = b from x (x0, in/out).  Semantics of scipy.sparse.linalg.cg (iterative.py
+ * 359-418): atol = rtol*||b||, ||r|| checked at the top of each iteration, iters = number
+ * of completed iterations, max_iter <= 0 means n.  res_hist (host, nullable, length
+ * max_iter+2) receives ||r_k|| for k = 0..iters.  t_solve_ms = device time of the solve.
+ * Returns LSPCG_OK when converged, LSPCG_NOT_CONVERGED when max_iter was reached. */
+int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int64_t max_iter,
+                       int64_t* iters, double* res_hist, double* t_solve_ms);
+int lspcg_solver_destroy(lspcg_solver* s);
+
+/* ---- CSR assembly with Dirichlet masking (to_csr_cpu on device) ----
+ * edge_index: device int64 [2,E] (row-major sorted, duplicate free -- checked);
+ * blocks: device [E,bs,bs] of in_dtype; mask: device [nb*bs] of mask_dtype or NULL.
+ * out_block = 0: scalar CSR exactly as to_csr_cpu (zeros dropped, sorted);
+ * out_block = 1: BSR (bs x bs blocks, masking applied, zeros kept) for the block kernels. */
+int lspcg_assemble(lspcg_ctx* ctx, int64_t nb, int64_t E, int bs, const int64_t* edge_index,
+                   const void* blocks, int in_dtype, const void* mask, int mask_dtype,
+                   int out_dtype, int out_block, lspcg_mat** out);
+
+/* ---- GNN (NodeEdgeProcessing, F = hidden = 16, FeedForward num_layers = 2) ---- */
+typedef struct lspcg_gnn_desc {
+  int node_in;        /* node input features (x.shape[1]) */
+  int edge_in;        /* edge input features (edge_attr.shape[1]) */
+  int hidden;         /* node_features = edge_features = MLP hidden channels (16) */
+  int mlp_layers;     /* FeedForward num_layers (2 -> three Linear layers) */
+  int num_mp_layers;  /* MPLayer count (4) */
+  int edge_out;       /* block_size * block_size */
+  int node_residual;  /* gnn.yaml node_residual */
+  int edge_residual;  /* gnn.yaml edge_residual */
+} lspcg_gnn_desc;
+
+/* weights: packed fp32 blob in the order documented in learningsparsepreconditioner4gpu_amd/nn.py
+ * (pack_weights); host or device pointer */
+int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* weights,
+                     int64_t nweights, lspcg_gnn** out);
+/* x [N,node_in], edge_index device int64 [2,E], edge_attr [E,edge_in] -> out [E,edge_out]
+ * (all fp32 device).  Message aggregation order is deterministic. */
+int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const int64_t* edge_index,
+                      const float* edge_attr, float* out);
+int lspcg_gnn_destroy(lspcg_gnn* g);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LSPCG_H_ */

@@ -1,0 +1,396 @@
+// Context, sparse-matrix handles, transpose / diagonal / column scaling, SpMV and dot
+// entry points of liblspcg_hip.so (C ABI: include/lspcg.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "lspcg_internal.hpp"
+#include "lspcg_spmv.hpp"
+
+namespace lspcg {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+static size_t dtype_size(int dtype) { return dtype == LSPCG_F32 ? 4 : 8; }
+
+// ---------------------------------------------------------------------------
+// Transpose: counting sort by column with atomics, then a per-row insertion sort of
+// the (original row, source position) pairs -> deterministic, sorted output.
+// ---------------------------------------------------------------------------
+__global__ void k_count_cols(int64_t nnzb, const int32_t* __restrict__ colind, int32_t* __restrict__ cnt) {
+  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < nnzb; k += int64_t(gridDim.x) * blockDim.x)
+    atomicAdd(&cnt[colind[k]], 1);
+}
+
+__global__ void k_scatter_transpose(int64_t nb, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                                    const int32_t* __restrict__ tptr, int32_t* __restrict__ fill,
+                                    int32_t* __restrict__ trow, int64_t* __restrict__ tsrc) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nb; i += int64_t(gridDim.x) * blockDim.x) {
+    for (int32_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+      const int32_t c = colind[k];
+      const int32_t pos = tptr[c] + atomicAdd(&fill[c], 1);
+      trow[pos] = int32_t(i);
+      tsrc[pos] = k;
+    }
+  }
+}
+
+template <typename T, int BS>
+__global__ void k_sort_gather_transpose(int64_t nb, const int32_t* __restrict__ tptr, int32_t* __restrict__ trow,
+                                        int64_t* __restrict__ tsrc, const T* __restrict__ vals, T* __restrict__ tvals) {
+  for (int64_t j = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j < nb; j += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t b = tptr[j], e = tptr[j + 1];
+    for (int32_t k = b + 1; k < e; ++k) {  // insertion sort by original row (unique keys)
+      const int32_t r = trow[k];
+      const int64_t s = tsrc[k];
+      int32_t m = k - 1;
+      while (m >= b && trow[m] > r) {
+        trow[m + 1] = trow[m];
+        tsrc[m + 1] = tsrc[m];
+        --m;
+      }
+      trow[m + 1] = r;
+      tsrc[m + 1] = s;
+    }
+    for (int32_t k = b; k < e; ++k) {
+      const T* src = vals + tsrc[k] * BS * BS;
+      T* dst = tvals + int64_t(k) * BS * BS;
+#pragma unroll
+      for (int p = 0; p < BS; ++p)
+#pragma unroll
+        for (int q = 0; q < BS; ++q) dst[p * BS + q] = src[q * BS + p];
+    }
+  }
+}
+
+template <typename T, int BS>
+__global__ void k_diagonal(int64_t nb, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                           const T* __restrict__ vals, T* __restrict__ d) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nb; i += int64_t(gridDim.x) * blockDim.x) {
+    int32_t lo = rowptr[i], hi = rowptr[i + 1];
+    while (lo < hi) {  // binary search for column i (indices sorted)
+      const int32_t mid = (lo + hi) >> 1;
+      if (colind[mid] < i) lo = mid + 1; else hi = mid;
+    }
+    const bool found = lo < rowptr[i + 1] && colind[lo] == i;
+#pragma unroll
+    for (int a = 0; a < BS; ++a) d[i * BS + a] = found ? vals[int64_t(lo) * BS * BS + a * BS + a] : T(0);
+  }
+}
+
+template <typename T, int BS>
+__global__ void k_scale_columns(int64_t nnzb, const int32_t* __restrict__ colind, T* __restrict__ vals,
+                                const T* __restrict__ d) {
+  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < nnzb * BS * BS;
+       k += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t kb = k / (BS * BS);
+    const int q = int(k % BS);
+    vals[k] = vals[k] * d[int64_t(colind[kb]) * BS + q];
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_dot(int64_t n, const T* __restrict__ x, const T* __restrict__ y,
+                                                  double* partials, unsigned* ticket, double* out) {
+  DD d[1] = {dd_zero()};
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    dd_fma(d[0], double(x[i]), double(y[i]));
+  grid_reduce_dd<1>(d, partials, ticket, [&](const double* v) { out[0] = v[0]; });
+}
+
+static int grid_for(int64_t n) {
+  int64_t g = (n + kThreads - 1) / kThreads;
+  return int(std::max<int64_t>(1, std::min<int64_t>(g, kElemBlocksMax)));
+}
+
+template <typename T, int BS>
+inline void launch_transpose_fill(const lspcg_mat* A, lspcg_mat* Tm, int32_t* fill, int32_t* trow, int64_t* tsrc,
+                                  hipStream_t st) {
+  const int g = grid_for(A->nb);
+  hipLaunchKernelGGL(k_scatter_transpose, dim3(g), dim3(kThreads), 0, st, A->nb, A->rowptr, A->colind, Tm->rowptr,
+                     fill, trow, tsrc);
+  hipLaunchKernelGGL((k_sort_gather_transpose<T, BS>), dim3(g), dim3(kThreads), 0, st, A->nb, Tm->rowptr, trow, tsrc,
+                     static_cast<const T*>(A->vals), static_cast<T*>(Tm->vals));
+}
+
+}  // namespace lspcg
+
+using namespace lspcg;
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+const char* lspcg_last_error(void) { return g_last_error.c_str(); }
+int lspcg_version(void) { return 10000; }
+
+int lspcg_ctx_create(int device, void* stream, lspcg_ctx** out) {
+  LSPCG_CHECK(out != nullptr, LSPCG_ERR_ARG, "ctx_create: out is NULL");
+  int ndev = 0;
+  LSPCG_HIP(hipGetDeviceCount(&ndev));
+  LSPCG_CHECK(device >= 0 && device < ndev, LSPCG_ERR_ARG, "ctx_create: invalid device " + std::to_string(device));
+  LSPCG_HIP(hipSetDevice(device));
+  std::unique_ptr<lspcg_ctx> c(new lspcg_ctx());
+  c->device = device;
+  // NULL selects the device's default (null) stream, which PyTorch also uses by default,
+  // so library work is ordered with the caller's tensor producers/consumers.
+  c->stream = static_cast<hipStream_t>(stream);
+  *out = c.release();
+  return LSPCG_OK;
+}
+
+int lspcg_ctx_destroy(lspcg_ctx* ctx) {
+  if (!ctx) return LSPCG_OK;
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return LSPCG_OK;
+}
+
+int lspcg_ctx_synchronize(lspcg_ctx* ctx) {
+  LSPCG_CHECK(ctx, LSPCG_ERR_ARG, "ctx is NULL");
+  LSPCG_HIP(hipStreamSynchronize(ctx->stream));
+  return LSPCG_OK;
+}
+
+static int mat_alloc(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, int dtype, lspcg_mat** out) {
+  LSPCG_CHECK(ctx && out, LSPCG_ERR_ARG, "mat: NULL ctx/out");
+  LSPCG_CHECK(bs == 1 || bs == 3, LSPCG_ERR_UNSUPPORTED, "mat: block size must be 1 or 3");
+  LSPCG_CHECK(dtype == LSPCG_F32 || dtype == LSPCG_F64, LSPCG_ERR_ARG, "mat: bad dtype");
+  LSPCG_CHECK(nb >= 0 && nnzb >= 0 && nnzb < (int64_t(1) << 31) && nb < (int64_t(1) << 31) / bs, LSPCG_ERR_ARG,
+              "mat: sizes out of int32 range");
+  LSPCG_HIP(hipSetDevice(ctx->device));
+  std::unique_ptr<lspcg_mat> m(new lspcg_mat());
+  m->ctx = ctx;
+  m->block_size = bs;
+  m->dtype = dtype;
+  m->nb = nb;
+  m->n = nb * bs;
+  m->nnzb = nnzb;
+  LSPCG_HIP(hipMalloc(&m->rowptr, sizeof(int32_t) * (nb + 1)));
+  LSPCG_HIP(hipMalloc(&m->colind, sizeof(int32_t) * std::max<int64_t>(nnzb, 1)));
+  LSPCG_HIP(hipMalloc(&m->vals, dtype_size(dtype) * std::max<int64_t>(nnzb * bs * bs, 1)));
+  *out = m.release();
+  return LSPCG_OK;
+}
+
+int lspcg_mat_create_bsr(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, const int32_t* indptr,
+                         const int32_t* indices, const void* vals, int dtype, lspcg_mat** out) {
+  LSPCG_CHECK(indptr && (nnzb == 0 || (indices && vals)), LSPCG_ERR_ARG, "mat_create: NULL arrays");
+  lspcg_mat* m = nullptr;
+  int rc = mat_alloc(ctx, nb, nnzb, bs, dtype, &m);
+  if (rc) return rc;
+  hipStream_t st = ctx->stream;
+  hipError_t e = hipMemcpyAsync(m->rowptr, indptr, sizeof(int32_t) * (nb + 1), hipMemcpyDefault, st);
+  if (e == hipSuccess && nnzb)
+    e = hipMemcpyAsync(m->colind, indices, sizeof(int32_t) * nnzb, hipMemcpyDefault, st);
+  if (e == hipSuccess && nnzb)
+    e = hipMemcpyAsync(m->vals, vals, dtype_size(dtype) * nnzb * bs * bs, hipMemcpyDefault, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);  // host sources may be released by the caller
+  if (e != hipSuccess) {
+    set_error(std::string("mat_create copy failed: ") + hipGetErrorString(e));
+    lspcg_mat_destroy(m);
+    return LSPCG_ERR_HIP;
+  }
+  *out = m;
+  return LSPCG_OK;
+}
+
+int lspcg_mat_create_csr(lspcg_ctx* ctx, int64_t n, int64_t nnz, const int32_t* indptr, const int32_t* indices,
+                         const void* vals, int dtype, lspcg_mat** out) {
+  return lspcg_mat_create_bsr(ctx, n, nnz, 1, indptr, indices, vals, dtype, out);
+}
+
+int lspcg_mat_destroy(lspcg_mat* A) {
+  if (!A) return LSPCG_OK;
+  (void)hipSetDevice(A->ctx->device);
+  (void)hipFree(A->rowptr);
+  (void)hipFree(A->colind);
+  (void)hipFree(A->vals);
+  delete A;
+  return LSPCG_OK;
+}
+
+int lspcg_mat_info(const lspcg_mat* A, int64_t* n, int64_t* nnzb, int* bs, int* dtype) {
+  LSPCG_CHECK(A, LSPCG_ERR_ARG, "mat_info: NULL");
+  if (n) *n = A->n;
+  if (nnzb) *nnzb = A->nnzb;
+  if (bs) *bs = A->block_size;
+  if (dtype) *dtype = A->dtype;
+  return LSPCG_OK;
+}
+
+int lspcg_mat_copy_out(const lspcg_mat* A, int32_t* indptr, int32_t* indices, void* vals) {
+  LSPCG_CHECK(A, LSPCG_ERR_ARG, "copy_out: NULL");
+  hipStream_t st = A->ctx->stream;
+  if (indptr) LSPCG_HIP(hipMemcpyAsync(indptr, A->rowptr, sizeof(int32_t) * (A->nb + 1), hipMemcpyDefault, st));
+  if (indices && A->nnzb) LSPCG_HIP(hipMemcpyAsync(indices, A->colind, sizeof(int32_t) * A->nnzb, hipMemcpyDefault, st));
+  if (vals && A->nnzb)
+    LSPCG_HIP(hipMemcpyAsync(vals, A->vals, dtype_size(A->dtype) * A->nnzb * A->block_size * A->block_size,
+                             hipMemcpyDefault, st));
+  LSPCG_HIP(hipStreamSynchronize(st));
+  return LSPCG_OK;
+}
+
+int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out) {
+  LSPCG_CHECK(A && out, LSPCG_ERR_ARG, "transpose: NULL");
+  lspcg_ctx* ctx = A->ctx;
+  hipStream_t st = ctx->stream;
+  lspcg_mat* Tm = nullptr;
+  int rc = mat_alloc(ctx, A->nb, A->nnzb, A->block_size, A->dtype, &Tm);
+  if (rc) return rc;
+  int32_t* cnt = nullptr;
+  int64_t* tsrc = nullptr;
+  auto fail = [&](hipError_t e) {
+    set_error(std::string("transpose: ") + hipGetErrorString(e));
+    (void)hipFree(cnt);
+    (void)hipFree(tsrc);
+    lspcg_mat_destroy(Tm);
+    return LSPCG_ERR_HIP;
+  };
+  hipError_t e = hipMalloc(&cnt, sizeof(int32_t) * (A->nb + 1));
+  if (e == hipSuccess) e = hipMalloc(&tsrc, sizeof(int64_t) * std::max<int64_t>(A->nnzb, 1));
+  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (A->nb + 1), st);
+  if (e != hipSuccess) return fail(e);
+  // counts -> host exclusive scan (nb+1 ints; setup path, not the solve loop)
+  hipLaunchKernelGGL(k_count_cols, dim3(grid_for(A->nnzb)), dim3(kThreads), 0, st, A->nnzb, A->colind, cnt);
+  std::vector<int32_t> h(A->nb + 1);
+  e = hipMemcpyAsync(h.data(), cnt, sizeof(int32_t) * A->nb, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return fail(e);
+  int64_t acc = 0;
+  for (int64_t i = 0; i < A->nb; ++i) {
+    const int32_t c = h[i];
+    h[i] = int32_t(acc);
+    acc += c;
+  }
+  h[A->nb] = int32_t(acc);
+  e = hipMemcpyAsync(Tm->rowptr, h.data(), sizeof(int32_t) * (A->nb + 1), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (A->nb + 1), st);
+  if (e != hipSuccess) return fail(e);
+  if (A->dtype == LSPCG_F64) {
+    if (A->block_size == 1) launch_transpose_fill<double, 1>(A, Tm, cnt, Tm->colind, tsrc, st);
+    else launch_transpose_fill<double, 3>(A, Tm, cnt, Tm->colind, tsrc, st);
+  } else {
+    if (A->block_size == 1) launch_transpose_fill<float, 1>(A, Tm, cnt, Tm->colind, tsrc, st);
+    else launch_transpose_fill<float, 3>(A, Tm, cnt, Tm->colind, tsrc, st);
+  }
+  e = hipStreamSynchronize(st);
+  (void)hipFree(cnt);
+  (void)hipFree(tsrc);
+  cnt = nullptr;
+  tsrc = nullptr;
+  if (e != hipSuccess) return fail(e);
+  *out = Tm;
+  return LSPCG_OK;
+}
+
+int lspcg_mat_diagonal(const lspcg_mat* A, void* d) {
+  LSPCG_CHECK(A && d, LSPCG_ERR_ARG, "diagonal: NULL");
+  hipStream_t st = A->ctx->stream;
+  const int g = grid_for(A->nb);
+  if (A->dtype == LSPCG_F64) {
+    if (A->block_size == 1)
+      hipLaunchKernelGGL((k_diagonal<double, 1>), dim3(g), dim3(kThreads), 0, st, A->nb, A->rowptr, A->colind,
+                         static_cast<const double*>(A->vals), static_cast<double*>(d));
+    else
+      hipLaunchKernelGGL((k_diagonal<double, 3>), dim3(g), dim3(kThreads), 0, st, A->nb, A->rowptr, A->colind,
+                         static_cast<const double*>(A->vals), static_cast<double*>(d));
+  } else {
+    if (A->block_size == 1)
+      hipLaunchKernelGGL((k_diagonal<float, 1>), dim3(g), dim3(kThreads), 0, st, A->nb, A->rowptr, A->colind,
+                         static_cast<const float*>(A->vals), static_cast<float*>(d));
+    else
+      hipLaunchKernelGGL((k_diagonal<float, 3>), dim3(g), dim3(kThreads), 0, st, A->nb, A->rowptr, A->colind,
+                         static_cast<const float*>(A->vals), static_cast<float*>(d));
+  }
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+int lspcg_mat_scale_columns(lspcg_mat* A, const void* d) {
+  LSPCG_CHECK(A && d, LSPCG_ERR_ARG, "scale_columns: NULL");
+  hipStream_t st = A->ctx->stream;
+  const int g = grid_for(A->nnzb * A->block_size * A->block_size);
+  if (A->dtype == LSPCG_F64) {
+    if (A->block_size == 1)
+      hipLaunchKernelGGL((k_scale_columns<double, 1>), dim3(g), dim3(kThreads), 0, st, A->nnzb, A->colind,
+                         static_cast<double*>(A->vals), static_cast<const double*>(d));
+    else
+      hipLaunchKernelGGL((k_scale_columns<double, 3>), dim3(g), dim3(kThreads), 0, st, A->nnzb, A->colind,
+                         static_cast<double*>(A->vals), static_cast<const double*>(d));
+  } else {
+    if (A->block_size == 1)
+      hipLaunchKernelGGL((k_scale_columns<float, 1>), dim3(g), dim3(kThreads), 0, st, A->nnzb, A->colind,
+                         static_cast<float*>(A->vals), static_cast<const float*>(d));
+    else
+      hipLaunchKernelGGL((k_scale_columns<float, 3>), dim3(g), dim3(kThreads), 0, st, A->nnzb, A->colind,
+                         static_cast<float*>(A->vals), static_cast<const float*>(d));
+  }
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y) {
+  LSPCG_CHECK(ctx && A && x && y, LSPCG_ERR_ARG, "spmv: NULL argument");
+  int rc;
+  if (A->dtype == LSPCG_F64)
+    rc = launch_spmv_any<double>(A, static_cast<const double*>(x), ProNone{}, EpiStore<double>{static_cast<double*>(y)},
+                                 ctx->stream);
+  else
+    rc = launch_spmv_any<float>(A, static_cast<const float*>(x), ProNone{}, EpiStore<float>{static_cast<float*>(y)},
+                                ctx->stream);
+  if (rc) return rc;
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y, int reps, double* avg_ms) {
+  LSPCG_CHECK(ctx && A && reps > 0 && avg_ms, LSPCG_ERR_ARG, "spmv_timed: bad argument");
+  hipEvent_t e0, e1;
+  LSPCG_HIP(hipEventCreate(&e0));
+  LSPCG_HIP(hipEventCreate(&e1));
+  LSPCG_HIP(hipEventRecord(e0, ctx->stream));
+  for (int i = 0; i < reps; ++i) {
+    int rc = lspcg_spmv(ctx, A, x, y);
+    if (rc) return rc;
+  }
+  LSPCG_HIP(hipEventRecord(e1, ctx->stream));
+  LSPCG_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  LSPCG_HIP(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *avg_ms = double(ms) / reps;
+  return LSPCG_OK;
+}
+
+int lspcg_dot(lspcg_ctx* ctx, int64_t n, int dtype, const void* x, const void* y, double* out) {
+  LSPCG_CHECK(ctx && x && y && out && n >= 0, LSPCG_ERR_ARG, "dot: bad argument");
+  hipStream_t st = ctx->stream;
+  const int g = grid_for(n);
+  double* buf = nullptr;  // [partials(2*g) | result]
+  unsigned* ticket = nullptr;
+  LSPCG_HIP(hipMalloc(&buf, sizeof(double) * (2 * g + 1)));
+  LSPCG_HIP(hipMalloc(&ticket, sizeof(unsigned)));
+  LSPCG_HIP(hipMemsetAsync(ticket, 0, sizeof(unsigned), st));
+  if (dtype == LSPCG_F64)
+    hipLaunchKernelGGL(k_dot<double>, dim3(g), dim3(kThreads), 0, st, n, static_cast<const double*>(x),
+                       static_cast<const double*>(y), buf, ticket, buf + 2 * g);
+  else
+    hipLaunchKernelGGL(k_dot<float>, dim3(g), dim3(kThreads), 0, st, n, static_cast<const float*>(x),
+                       static_cast<const float*>(y), buf, ticket, buf + 2 * g);
+  LSPCG_HIP(hipGetLastError());
+  LSPCG_HIP(hipMemcpyAsync(out, buf + 2 * g, sizeof(double), hipMemcpyDeviceToHost, st));
+  LSPCG_HIP(hipStreamSynchronize(st));
+  (void)hipFree(buf);
+  (void)hipFree(ticket);
+  return LSPCG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,196 @@
+// Internal declarations shared by the lspcg HIP translation units (gfx950 / CDNA4).
+//
+// Numerics contract (DESIGN.md "Parity"): every translation unit is compiled with
+// -ffp-contract=off so that elementwise updates and the sequential row sums of the
+// SpMV round exactly like scipy's csr_matvec / numpy ufuncs (product rounded, then
+// added).  Dot products use a compensated (Dot2, Ogita-Rump-Oishi) fp64 accumulation
+// reduced in a fixed order, i.e. they are deterministic and almost always equal to
+// the correctly rounded dot.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/lspcg.h"
+
+namespace lspcg {
+
+// ---------------------------------------------------------------------------
+// Error handling
+// ---------------------------------------------------------------------------
+void set_error(const std::string& msg);
+
+#define LSPCG_HIP(call)                                                                    \
+  do {                                                                                     \
+    hipError_t _e = (call);                                                                \
+    if (_e != hipSuccess) {                                                                \
+      ::lspcg::set_error(std::string(#call) + " failed: " + hipGetErrorString(_e) + " at " \
+                         + __FILE__ + ":" + std::to_string(__LINE__));                     \
+      return LSPCG_ERR_HIP;                                                                \
+    }                                                                                      \
+  } while (0)
+
+#define LSPCG_CHECK(cond, code, msg)   \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::lspcg::set_error(msg);         \
+      return (code);                   \
+    }                                  \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Launch geometry
+// ---------------------------------------------------------------------------
+constexpr int kThreads = 256;       // 4 wave64 per workgroup
+constexpr int kSpmvCap = 4096;      // staged scalar entries per chunk (fp64: 32 KiB LDS)
+constexpr int kElemBlocksMax = 2048;  // grid cap for streaming elementwise kernels
+
+// ---------------------------------------------------------------------------
+// Compensated (double-double) accumulation
+// ---------------------------------------------------------------------------
+struct DD {
+  double s, c;
+};
+
+__device__ __forceinline__ DD dd_zero() { return DD{0.0, 0.0}; }
+
+__device__ __forceinline__ DD dd_add(DD a, DD b) {
+  const double s = a.s + b.s;
+  const double bb = s - a.s;
+  const double e = (a.s - (s - bb)) + (b.s - bb);
+  return DD{s, (a.c + b.c) + e};
+}
+
+// a += x*y with an exact product (FMA TwoProduct) and TwoSum.
+__device__ __forceinline__ void dd_fma(DD& a, double x, double y) {
+  const double p = x * y;
+  const double e = __builtin_fma(x, y, -p);
+  const double s = a.s + p;
+  const double bb = s - a.s;
+  const double t = (a.s - (s - bb)) + (p - bb);
+  a.s = s;
+  a.c = a.c + (t + e);
+}
+
+__device__ __forceinline__ double dd_value(DD a) { return a.s + a.c; }
+
+__device__ __forceinline__ DD dd_shfl_xor(DD a, int m) {
+  DD r;
+  r.s = __shfl_xor(a.s, m, 64);
+  r.c = __shfl_xor(a.c, m, 64);
+  return r;
+}
+
+// Fixed-order workgroup reduction of N DD values; the result is valid in thread 0.
+template <int N>
+__device__ __forceinline__ void block_reduce_dd(DD (&v)[N], DD* lds /* >= 4*N */) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) v[j] = dd_add(v[j], dd_shfl_xor(v[j], m));
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) lds[wid * N + j] = v[j];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      DD a = lds[j];
+      for (int w = 1; w < nw; ++w) a = dd_add(a, lds[w * N + j]);
+      v[j] = a;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Agent-scope helpers (MI355X_MICROARCH.md "Valid forms", table row 1): partials are
+// published with sc1 (atomic) stores, drained, then one relaxed ticket add; the last
+// arriver reads every partial with sc1 loads.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void st_agent_f64(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent_f64(const double* p) {
+  unsigned long long u = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __longlong_as_double(static_cast<long long>(u));
+}
+
+// Grid-wide deterministic reduction of N dot products.  Every workgroup of the launch
+// must call it exactly once (uniformly).  The workgroup that arrives last sums all
+// partials in block-index order and calls fin(values) on thread 0.
+template <int N, class Fin>
+__device__ __forceinline__ void grid_reduce_dd(DD (&v)[N], double* partials, unsigned* ticket, Fin fin) {
+  __shared__ DD lds[4 * N];
+  __shared__ int s_last;
+  block_reduce_dd<N>(v, lds);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      st_agent_f64(&partials[(size_t(blockIdx.x) * N + j) * 2 + 0], v[j].s);
+      st_agent_f64(&partials[(size_t(blockIdx.x) * N + j) * 2 + 1], v[j].c);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  DD acc[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) acc[j] = dd_zero();
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      DD p{ld_agent_f64(&partials[(size_t(b) * N + j) * 2 + 0]), ld_agent_f64(&partials[(size_t(b) * N + j) * 2 + 1])};
+      acc[j] = dd_add(acc[j], p);
+    }
+  }
+  __syncthreads();
+  block_reduce_dd<N>(acc, lds);
+  if (threadIdx.x == 0) {
+    double out[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) out[j] = dd_value(acc[j]);
+    fin(out);
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ double round_to(double v) {
+  return static_cast<double>(static_cast<T>(v));
+}
+
+}  // namespace lspcg
+
+// ---------------------------------------------------------------------------
+// Handle structs (opaque in the C ABI)
+// ---------------------------------------------------------------------------
+struct lspcg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+};
+
+struct lspcg_mat {
+  lspcg_ctx* ctx = nullptr;
+  int block_size = 1;   // 1 = scalar CSR, 3 = BSR 3x3
+  int dtype = LSPCG_F64;
+  int64_t n = 0;        // scalar rows (= cols)
+  int64_t nb = 0;       // block rows
+  int64_t nnzb = 0;     // stored blocks (scalar nnz when block_size == 1)
+  int32_t* rowptr = nullptr;  // [nb+1]
+  int32_t* colind = nullptr;  // [nnzb]
+  void* vals = nullptr;       // [nnzb*bs*bs], row-major blocks
+};

@@ -1,0 +1,523 @@
+// Device-resident preconditioned CG (replaces pymathprim.linalg.PreconditionedConjugateGradient,
+// call sites neural_cg/utils/validate.py:54-160; arithmetic order of scipy 1.15
+// iterative.py:359-418, the reference's CPU restatement validate.py:163-341).
+//
+// One iteration (ext_spai) is five kernels, every one predicated on a device `done` flag so
+// that the host can launch graph-captured chunks of iterations and poll once per chunk
+// without changing the iteration count or the iterate:
+//   K1  t = Lᵀ r                 (prologue: convergence test on ‖r‖ -- top of the scipy loop)
+//   K2  z = L t + ε r ; ρ = r·z   (SpMV epilogue + grid dot)
+//   K3  p = p·β + z               (β = ρ/ρ_prev; p = z at iteration 0)
+//   K4  q = A p ; π = p·q          (SpMV epilogue + grid dot)
+//   K5  x += α p ; r -= α q ; ‖r‖² (α = ρ/π; last workgroup advances the iteration)
+// Unpreconditioned CG drops K1/K2 (z = r, ρ = ‖r‖²) and moves the convergence test to K3;
+// diagonal (Jacobi) PCG computes z = r / diag(A) and ρ inside K5.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <memory>
+#include <string>
+
+#include "lspcg_internal.hpp"
+#include "lspcg_spmv.hpp"
+
+namespace lspcg {
+
+struct PcgState {
+  double bb;        // ‖b‖²
+  double rr;        // ‖r_k‖² (rounded to T)
+  double rho;       // r·z of the current iteration (rounded to T)
+  double rho_prev;  // previous iteration's ρ
+  double pq;        // p·q (rounded to T)
+  double atol;      // rtol·‖b‖
+  double rtol;
+  double eps;       // ε of ext_spai
+  double* hist;     // ‖r_k‖ history (nullable)
+  int64_t iter;     // completed iterations
+  int64_t max_iter;
+  int32_t done;     // 0 running, 1 converged, 2 max_iter reached, 3 non-finite residual
+  int32_t pad;
+};
+
+template <typename T>
+__device__ __forceinline__ T tsqrt(T v) { return sqrt(v); }
+
+// Top-of-iteration test of scipy's loop: `for iteration in range(maxiter): if norm(r) < atol`.
+template <typename T>
+struct ProCheck {
+  PcgState* S;
+  __device__ __forceinline__ bool exit() const {
+    if (S->done) return true;
+    int code = 0;
+    if (S->iter >= S->max_iter) {
+      code = 2;
+    } else {
+      const double rn = double(tsqrt<T>(T(S->rr)));
+      if (rn < S->atol) code = 1;
+      else if (!(rn == rn) || rn == INFINITY) code = 3;
+    }
+    if (code && blockIdx.x == 0 && threadIdx.x == 0) S->done = code;
+    return code != 0;
+  }
+};
+
+struct ProDone {
+  const PcgState* S;
+  __device__ __forceinline__ bool exit() const { return S->done != 0; }
+};
+
+// K1: t = Lᵀ r  (scaled variant: t = (Lᵀ r) / d)
+template <typename T, bool SCALED>
+struct EpiT {
+  static constexpr int NDOT = 0;
+  T* t;
+  const T* d;
+  __device__ __forceinline__ void row(int64_t i, T s, DD*) const {
+    if constexpr (SCALED) t[i] = s / d[i];
+    else t[i] = s;
+  }
+  __device__ __forceinline__ void fin(const double*) const {}
+  double* partials = nullptr;
+  unsigned* ticket = nullptr;
+};
+
+// K2: z = L t + ε r  (scaled: z = L t + (ε r)/d);  ρ = r·z
+template <typename T, bool SCALED>
+struct EpiZ {
+  static constexpr int NDOT = 1;
+  T* z;
+  const T* r;
+  const T* d;
+  T eps;
+  PcgState* S;
+  double* partials;
+  unsigned* ticket;
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T ri = r[i];
+    T zi;
+    if constexpr (SCALED) zi = s + (eps * ri) / d[i];
+    else zi = s + eps * ri;
+    z[i] = zi;
+    dd_fma(dots[0], double(ri), double(zi));
+  }
+  __device__ __forceinline__ void fin(const double* v) const { S->rho = round_to<T>(v[0]); }
+};
+
+// K4: q = A p ; π = p·q
+template <typename T>
+struct EpiQ {
+  static constexpr int NDOT = 1;
+  T* q;
+  const T* p;
+  PcgState* S;
+  double* partials;
+  unsigned* ticket;
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    q[i] = s;
+    dd_fma(dots[0], double(p[i]), double(s));
+  }
+  __device__ __forceinline__ void fin(const double* v) const { S->pq = round_to<T>(v[0]); }
+};
+
+// init: r = b - A x0 ; ‖r‖², ‖b‖²  (scipy: r = b - matvec(x) if x.any() else b.copy();
+// with x0 = 0 the subtraction returns b bit-for-bit)
+template <typename T, int PRE>
+struct EpiResid {
+  static constexpr int NDOT = 2;
+  T* r;
+  const T* b;
+  PcgState* S;
+  double* partials;
+  unsigned* ticket;
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T bi = b[i];
+    const T ri = bi - s;
+    r[i] = ri;
+    dd_fma(dots[0], double(ri), double(ri));
+    dd_fma(dots[1], double(bi), double(bi));
+  }
+  __device__ __forceinline__ void fin(const double* v) const {
+    S->rr = round_to<T>(v[0]);
+    S->bb = round_to<T>(v[1]);
+    const double bn = double(tsqrt<T>(T(S->bb)));
+    S->atol = fmax(0.0, S->rtol * bn);
+    if (PRE == LSPCG_PRECOND_NONE) S->rho = S->rr;
+    S->iter = 0;
+    S->done = (bn == 0.0) ? 1 : 0;
+    if (S->hist) S->hist[0] = double(tsqrt<T>(T(S->rr)));
+  }
+};
+
+// K3: p = p*β + z  (iteration 0: p = z)
+template <typename T, class Pro>
+__global__ void __launch_bounds__(kThreads) k_update_p(int64_t n, Pro pro, const PcgState* S, const T* __restrict__ z,
+                                                       T* __restrict__ p) {
+  if (pro.exit()) return;
+  const bool first = S->iter == 0;
+  const T beta = first ? T(0) : T(S->rho) / T(S->rho_prev);
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const T zi = z[i];
+    p[i] = first ? zi : (p[i] * beta) + zi;
+  }
+}
+
+// K5: x += α p ; r -= α q ; ‖r‖²  (+ Jacobi: z = r/d, ρ = r·z)
+template <typename T, int PRE>
+__global__ void __launch_bounds__(kThreads) k_update_xr(int64_t n, PcgState* S, const T* __restrict__ p,
+                                                        const T* __restrict__ q, T* __restrict__ x, T* __restrict__ r,
+                                                        const T* __restrict__ d, T* __restrict__ z, double* partials,
+                                                        unsigned* ticket) {
+  if (S->done) return;
+  constexpr int ND = PRE == LSPCG_PRECOND_DIAGONAL ? 2 : 1;
+  const T alpha = T(S->rho) / T(S->pq);
+  DD dots[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) dots[j] = dd_zero();
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    x[i] = x[i] + alpha * p[i];
+    const T ri = r[i] - alpha * q[i];
+    r[i] = ri;
+    dd_fma(dots[0], double(ri), double(ri));
+    if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) {
+      const T zi = ri / d[i];
+      z[i] = zi;
+      dd_fma(dots[1], double(ri), double(zi));
+    }
+  }
+  grid_reduce_dd<ND>(dots, partials, ticket, [&](const double* v) {
+    const double rr = round_to<T>(v[0]);
+    S->rr = rr;
+    S->rho_prev = S->rho;
+    if constexpr (PRE == LSPCG_PRECOND_NONE) S->rho = rr;
+    if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) S->rho = round_to<T>(v[1]);
+    const int64_t it = S->iter + 1;
+    S->iter = it;
+    if (S->hist) S->hist[it] = double(tsqrt<T>(T(rr)));
+  });
+}
+
+// Jacobi init: z = r / d ; ρ = r·z
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_jacobi_init(int64_t n, PcgState* S, const T* __restrict__ r,
+                                                          const T* __restrict__ d, T* __restrict__ z, double* partials,
+                                                          unsigned* ticket) {
+  DD dots[1] = {dd_zero()};
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const T ri = r[i];
+    const T zi = ri / d[i];
+    z[i] = zi;
+    dd_fma(dots[0], double(ri), double(zi));
+  }
+  grid_reduce_dd<1>(dots, partials, ticket, [&](const double* v) { S->rho = round_to<T>(v[0]); });
+}
+
+static int elem_grid(int64_t n) {
+  const int64_t g = (n + kThreads * 4 - 1) / (kThreads * 4);
+  return int(std::max<int64_t>(1, std::min<int64_t>(g, kElemBlocksMax)));
+}
+
+}  // namespace lspcg
+
+using namespace lspcg;
+
+struct lspcg_solver {
+  lspcg_ctx* ctx = nullptr;
+  const lspcg_mat* A = nullptr;
+  const lspcg_mat* L = nullptr;
+  lspcg_mat* LT = nullptr;  // owned
+  int precond = LSPCG_PRECOND_NONE;
+  int dtype = LSPCG_F64;
+  int64_t n = 0;
+  double eps = 0.0;
+  hipStream_t stream = nullptr;  // solver-owned (capturable) stream
+  void *x = nullptr, *b = nullptr, *r = nullptr, *z = nullptr, *t = nullptr, *p = nullptr, *q = nullptr,
+       *d = nullptr;
+  PcgState* S = nullptr;
+  PcgState* hS = nullptr;  // pinned host mirror
+  double* partials = nullptr;
+  unsigned* ticket = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_poll = nullptr;
+  std::map<int, hipGraphExec_t> graphs;
+  std::map<int, hipGraph_t> graph_defs;
+};
+
+template <typename T>
+static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
+  const int64_t n = s->n;
+  T* x = static_cast<T*>(s->x);
+  T* r = static_cast<T*>(s->r);
+  T* z = static_cast<T*>(s->z);
+  T* t = static_cast<T*>(s->t);
+  T* p = static_cast<T*>(s->p);
+  T* q = static_cast<T*>(s->q);
+  const T* d = static_cast<const T*>(s->d);
+  PcgState* S = s->S;
+  const int eg = elem_grid(n);
+  int rc = LSPCG_OK;
+  switch (s->precond) {
+    case LSPCG_PRECOND_EXT_SPAI:
+    case LSPCG_PRECOND_EXT_SPAI_SCALED: {
+      const bool scaled = s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
+      if (scaled) {
+        rc = launch_spmv_any<T>(s->LT, r, ProCheck<T>{S}, EpiT<T, true>{t, d}, st);
+        if (!rc)
+          rc = launch_spmv_any<T>(s->L, t, ProDone{S}, EpiZ<T, true>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st);
+      } else {
+        rc = launch_spmv_any<T>(s->LT, r, ProCheck<T>{S}, EpiT<T, false>{t, d}, st);
+        if (!rc)
+          rc = launch_spmv_any<T>(s->L, t, ProDone{S}, EpiZ<T, false>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st);
+      }
+      if (rc) return rc;
+      hipLaunchKernelGGL((k_update_p<T, ProDone>), dim3(eg), dim3(kThreads), 0, st, n, ProDone{S}, S, z, p);
+      rc = launch_spmv_any<T>(s->A, p, ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket}, st);
+      if (rc) return rc;
+      hipLaunchKernelGGL((k_update_xr<T, LSPCG_PRECOND_EXT_SPAI>), dim3(eg), dim3(kThreads), 0, st, n, S, p, q, x, r,
+                         d, z, s->partials, s->ticket);
+      break;
+    }
+    case LSPCG_PRECOND_NONE: {
+      hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S, r, p);
+      rc = launch_spmv_any<T>(s->A, p, ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket}, st);
+      if (rc) return rc;
+      hipLaunchKernelGGL((k_update_xr<T, LSPCG_PRECOND_NONE>), dim3(eg), dim3(kThreads), 0, st, n, S, p, q, x, r, d,
+                         z, s->partials, s->ticket);
+      break;
+    }
+    case LSPCG_PRECOND_DIAGONAL: {
+      hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S, z, p);
+      rc = launch_spmv_any<T>(s->A, p, ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket}, st);
+      if (rc) return rc;
+      hipLaunchKernelGGL((k_update_xr<T, LSPCG_PRECOND_DIAGONAL>), dim3(eg), dim3(kThreads), 0, st, n, S, p, q, x, r,
+                         d, z, s->partials, s->ticket);
+      break;
+    }
+    default:
+      set_error("unknown preconditioner");
+      return LSPCG_ERR_ARG;
+  }
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+template <typename T>
+static int enqueue_init(lspcg_solver* s, hipStream_t st) {
+  PcgState* S = s->S;
+  int rc;
+  switch (s->precond) {
+    case LSPCG_PRECOND_NONE:
+      rc = launch_spmv_any<T>(s->A, static_cast<const T*>(s->x), ProNone{},
+                              EpiResid<T, LSPCG_PRECOND_NONE>{static_cast<T*>(s->r), static_cast<const T*>(s->b), S,
+                                                              s->partials, s->ticket},
+                              st);
+      break;
+    default:
+      rc = launch_spmv_any<T>(s->A, static_cast<const T*>(s->x), ProNone{},
+                              EpiResid<T, LSPCG_PRECOND_EXT_SPAI>{static_cast<T*>(s->r), static_cast<const T*>(s->b),
+                                                                  S, s->partials, s->ticket},
+                              st);
+  }
+  if (rc) return rc;
+  if (s->precond == LSPCG_PRECOND_DIAGONAL)
+    hipLaunchKernelGGL(k_jacobi_init<T>, dim3(elem_grid(s->n)), dim3(kThreads), 0, st, s->n, S,
+                       static_cast<const T*>(s->r), static_cast<const T*>(s->d), static_cast<T*>(s->z), s->partials,
+                       s->ticket);
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+static int get_graph(lspcg_solver* s, int chunk, hipGraphExec_t* out) {
+  auto it = s->graphs.find(chunk);
+  if (it != s->graphs.end()) {
+    *out = it->second;
+    return LSPCG_OK;
+  }
+  hipGraph_t g = nullptr;
+  LSPCG_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+  int rc = LSPCG_OK;
+  for (int i = 0; i < chunk && rc == LSPCG_OK; ++i)
+    rc = s->dtype == LSPCG_F64 ? enqueue_iteration<double>(s, s->stream) : enqueue_iteration<float>(s, s->stream);
+  hipError_t e = hipStreamEndCapture(s->stream, &g);
+  if (rc) return rc;
+  LSPCG_HIP(e);
+  hipGraphExec_t ex = nullptr;
+  LSPCG_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  s->graphs[chunk] = ex;
+  s->graph_defs[chunk] = g;
+  *out = ex;
+  return LSPCG_OK;
+}
+
+static size_t esize(int dtype) { return dtype == LSPCG_F32 ? 4 : 8; }
+
+extern "C" {
+
+int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_solver** out) {
+  LSPCG_CHECK(ctx && A && out, LSPCG_ERR_ARG, "solver_create: NULL argument");
+  LSPCG_CHECK(precond >= LSPCG_PRECOND_NONE && precond <= LSPCG_PRECOND_EXT_SPAI_SCALED, LSPCG_ERR_ARG,
+              "solver_create: unknown preconditioner " + std::to_string(precond));
+  LSPCG_HIP(hipSetDevice(ctx->device));
+  std::unique_ptr<lspcg_solver> s(new lspcg_solver());
+  s->ctx = ctx;
+  s->A = A;
+  s->precond = precond;
+  s->dtype = A->dtype;
+  s->n = A->n;
+  const size_t vb = esize(s->dtype) * std::max<int64_t>(s->n, 1);
+  LSPCG_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d}) LSPCG_HIP(hipMalloc(v, vb));
+  LSPCG_HIP(hipMalloc(&s->S, sizeof(PcgState)));
+  LSPCG_HIP(hipHostMalloc(&s->hS, sizeof(PcgState), hipHostMallocDefault));
+  // partial slots: largest grid of any reducing launch (SpMV grid of A / L, element grid) x 2 dots
+  // (n/255 bounds the grid of a CSR (256 rows/WG) and a BSR3 (85 block rows/WG) launch,
+  // so L / Lᵀ in either layout fit too)
+  const int64_t g = std::max<int64_t>((A->n + 254) / 255 + 1, kElemBlocksMax);
+  LSPCG_HIP(hipMalloc(&s->partials, sizeof(double) * 2 * 2 * (g + 1)));
+  LSPCG_HIP(hipMalloc(&s->ticket, sizeof(unsigned) * 4));
+  LSPCG_HIP(hipMemsetAsync(s->ticket, 0, sizeof(unsigned) * 4, s->stream));
+  LSPCG_HIP(hipMemsetAsync(s->S, 0, sizeof(PcgState), s->stream));
+  for (hipEvent_t* e : {&s->ev_in, &s->ev_out, &s->ev_poll}) LSPCG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  LSPCG_HIP(hipEventCreate(&s->ev_t0));
+  LSPCG_HIP(hipEventCreate(&s->ev_t1));
+  if (precond == LSPCG_PRECOND_DIAGONAL) {
+    int rc = lspcg_mat_diagonal(A, s->d);  // issues on ctx stream
+    if (rc) return rc;
+    LSPCG_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  LSPCG_HIP(hipStreamSynchronize(s->stream));
+  *out = s.release();
+  return LSPCG_OK;
+}
+
+int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, double* t_prec_ms) {
+  LSPCG_CHECK(s && L, LSPCG_ERR_ARG, "set_spai: NULL");
+  LSPCG_CHECK(s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED, LSPCG_ERR_ARG,
+              "set_spai: solver was not created with an ext_spai preconditioner");
+  LSPCG_CHECK(L->n == s->n, LSPCG_ERR_ARG, "set_spai: L has a different size than A");
+  LSPCG_CHECK(L->dtype == s->dtype, LSPCG_ERR_ARG, "set_spai: L dtype differs from A dtype");
+  hipStream_t cst = s->ctx->stream;
+  LSPCG_HIP(hipEventRecord(s->ev_t0, cst));
+  if (s->LT) {
+    lspcg_mat_destroy(s->LT);
+    s->LT = nullptr;
+  }
+  int rc = lspcg_mat_transpose(L, &s->LT);
+  if (rc) return rc;
+  if (s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) {
+    rc = lspcg_mat_diagonal(s->A, s->d);
+    if (rc) return rc;
+  }
+  LSPCG_HIP(hipEventRecord(s->ev_t1, cst));
+  LSPCG_HIP(hipEventSynchronize(s->ev_t1));
+  float ms = 0.f;
+  LSPCG_HIP(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1));
+  if (t_prec_ms) *t_prec_ms = ms;
+  s->L = L;
+  s->eps = epsilon;
+  // graphs capture matrix pointers: drop them when the preconditioner changes
+  for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
+  s->graphs.clear();
+  s->graph_defs.clear();
+  return LSPCG_OK;
+}
+
+int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int64_t max_iter, int64_t* iters,
+                       double* res_hist, double* t_solve_ms) {
+  LSPCG_CHECK(s && b && x && iters, LSPCG_ERR_ARG, "solve: NULL argument");
+  LSPCG_CHECK(!(s->precond >= LSPCG_PRECOND_EXT_SPAI) || s->LT, LSPCG_ERR_ARG, "solve: ext_spai not set");
+  LSPCG_HIP(hipSetDevice(s->ctx->device));
+  const int64_t n = s->n;
+  if (max_iter <= 0) max_iter = n;
+  hipStream_t st = s->stream;
+  const size_t vb = esize(s->dtype) * n;
+  double* dhist = nullptr;
+  if (res_hist) LSPCG_HIP(hipMalloc(&dhist, sizeof(double) * (max_iter + 2)));
+
+  LSPCG_HIP(hipEventRecord(s->ev_in, s->ctx->stream));
+  LSPCG_HIP(hipStreamWaitEvent(st, s->ev_in, 0));
+  LSPCG_HIP(hipEventRecord(s->ev_t0, st));
+  if (n) {
+    LSPCG_HIP(hipMemcpyAsync(s->b, b, vb, hipMemcpyDeviceToDevice, st));
+    LSPCG_HIP(hipMemcpyAsync(s->x, x, vb, hipMemcpyDeviceToDevice, st));
+  }
+  PcgState init{};
+  init.rtol = rtol;
+  init.eps = s->eps;
+  init.hist = dhist;
+  init.max_iter = max_iter;
+  *s->hS = init;
+  LSPCG_HIP(hipMemcpyAsync(s->S, s->hS, sizeof(PcgState), hipMemcpyHostToDevice, st));
+  int rc = s->dtype == LSPCG_F64 ? enqueue_init<double>(s, st) : enqueue_init<float>(s, st);
+  if (rc) return rc;
+
+  // Poll loop: chunk sizes follow the observed residual decay so that at most a few
+  // early-exit launches trail the converged iteration.
+  int64_t last_it = 0;
+  double last_rr = -1.0;
+  int chunk = 4;
+  for (;;) {
+    LSPCG_HIP(hipMemcpyAsync(s->hS, s->S, sizeof(PcgState), hipMemcpyDeviceToHost, st));
+    LSPCG_HIP(hipEventRecord(s->ev_poll, st));
+    LSPCG_HIP(hipEventSynchronize(s->ev_poll));
+    const PcgState cur = *s->hS;
+    if (cur.done) break;
+    if (cur.iter >= max_iter) break;  // defensive; ProCheck sets done
+    if (last_rr > 0 && cur.iter > last_it && cur.rr > 0 && cur.rr < last_rr) {
+      const double rate = std::log(cur.rr / last_rr) / double(cur.iter - last_it);  // < 0
+      const double need = std::log((cur.atol * cur.atol) / cur.rr) / rate;
+      int64_t rem = need > 0 ? int64_t(std::ceil(need)) : 1;
+      rem = std::max<int64_t>(1, std::min<int64_t>(rem, max_iter - cur.iter));
+      int c = 1;
+      while (c * 2 <= rem && c < 32) c *= 2;
+      chunk = c;
+    } else if (last_rr > 0) {
+      chunk = std::min(32, chunk * 2);
+    }
+    last_it = cur.iter;
+    last_rr = cur.rr;
+    hipGraphExec_t ex = nullptr;
+    rc = get_graph(s, chunk, &ex);
+    if (rc) return rc;
+    LSPCG_HIP(hipGraphLaunch(ex, st));
+  }
+  const PcgState fin = *s->hS;
+  const void* src = (fin.bb == 0.0) ? s->b : s->x;  // scipy returns b when ‖b‖ = 0
+  if (n) LSPCG_HIP(hipMemcpyAsync(x, src, vb, hipMemcpyDeviceToDevice, st));
+  LSPCG_HIP(hipEventRecord(s->ev_t1, st));
+  LSPCG_HIP(hipEventRecord(s->ev_out, st));
+  LSPCG_HIP(hipStreamWaitEvent(s->ctx->stream, s->ev_out, 0));
+  LSPCG_HIP(hipEventSynchronize(s->ev_t1));
+  float ms = 0.f;
+  LSPCG_HIP(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1));
+  if (t_solve_ms) *t_solve_ms = ms;
+  const int64_t it = (fin.done == 3) ? max_iter : fin.iter;
+  *iters = it;
+  if (res_hist) {
+    const int64_t cnt = std::min<int64_t>(fin.iter, max_iter) + 1;
+    LSPCG_HIP(hipMemcpy(res_hist, dhist, sizeof(double) * cnt, hipMemcpyDeviceToHost));
+    LSPCG_HIP(hipFree(dhist));
+  }
+  return (fin.done == 1) ? LSPCG_OK : LSPCG_NOT_CONVERGED;
+}
+
+int lspcg_solver_destroy(lspcg_solver* s) {
+  if (!s) return LSPCG_OK;
+  (void)hipSetDevice(s->ctx->device);
+  (void)hipStreamSynchronize(s->stream);
+  for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
+  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d}) (void)hipFree(v);
+  (void)hipFree(s->S);
+  (void)hipHostFree(s->hS);
+  (void)hipFree(s->partials);
+  (void)hipFree(s->ticket);
+  for (hipEvent_t e : {s->ev_in, s->ev_out, s->ev_poll, s->ev_t0, s->ev_t1}) (void)hipEventDestroy(e);
+  if (s->LT) lspcg_mat_destroy(s->LT);
+  (void)hipStreamDestroy(s->stream);
+  delete s;
+  return LSPCG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,117 @@
+"""``pymathprim.linalg.PreconditionedConjugateGradient`` on MI355X.
+
+Drop-in for the native solver the reference calls at
+``neural_cg/utils/validate.py:79-80, 116-117, 151-156``::
+
+    solver = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", dtype=np.float64)
+    iters, prec_time_s, solve_time_s = solver(b, x, rtol, max_iter, ext_spai=(L, eps))
+
+Arithmetic follows scipy 1.15 ``cg`` (the reference's own CPU restatement,
+validate.py:163-341): see ``include/lspcg.h`` and DESIGN.md.  ``x`` is updated in place
+with the solution (numpy arrays or device tensors).  Only the HIP path exists:
+``device="cpu"`` raises (the CPU solver is the oracle, which the product never uses).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple, Union
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from . import _lib
+from .sparse import Context, DeviceMatrix, _ptr, lspcg_dtype
+
+GPU_DEVICES = ("cuda", "hip", "gpu", "rocm")
+SUPPORTED = tuple(_lib.PRECOND)
+BASELINE_ONLY = ("ic", "ainv", "fsai")  # pymathprim baselines (infer.py:310-321), SURVEY 8(f) "next"
+
+
+def _as_device_matrix(M, dtype, block_size: int, ctx: Context) -> DeviceMatrix:
+    if isinstance(M, DeviceMatrix):
+        if M.dtype_code != lspcg_dtype(dtype):
+            raise TypeError(f"matrix dtype {M.dtype} differs from solver dtype {dtype}")
+        return M
+    return DeviceMatrix.from_scipy(sp.csr_matrix(M), dtype=dtype, block_size=block_size, ctx=ctx)
+
+
+class PreconditionedConjugateGradient:
+    def __init__(self, matrix, device: str = "cuda", preconditioner: str = "none", dtype=np.float64,
+                 block_size: int = 1, ctx: Optional[Context] = None):
+        if str(device).split(":")[0] not in GPU_DEVICES:
+            raise ValueError(
+                f"device={device!r}: this framework runs PCG on MI355X only (device='cuda'); the CPU "
+                "reference path is not part of the product")
+        if preconditioner in BASELINE_ONLY:
+            raise NotImplementedError(f"preconditioner {preconditioner!r} is a pymathprim baseline that is not "
+                                      "implemented yet (SURVEY.md 8(f) 'next' rank 3)")
+        if preconditioner not in SUPPORTED:
+            raise ValueError(f"unknown preconditioner {preconditioner!r}; expected one of {SUPPORTED}")
+        dev = str(device).split(":")
+        self.ctx = ctx or Context.get(int(dev[1]) if len(dev) > 1 else None)
+        self.dtype = np.dtype(dtype)
+        self.preconditioner = preconditioner
+        self.A = _as_device_matrix(matrix, self.dtype, block_size, self.ctx)
+        self.n = self.A.n
+        h = C.c_void_p()
+        _lib.call("lspcg_solver_create", self.ctx.handle, self.A.handle, _lib.PRECOND[preconditioner], C.byref(h))
+        self.handle = h
+        self._L = None
+        self._spai_key = None
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.lspcg_solver_destroy(h)
+            self.handle = None
+
+    def set_spai(self, L, epsilon: float, block_size: int = 1) -> float:
+        """Install M⁻¹ = L Lᵀ + εI (ext_spai); returns the device setup time in seconds."""
+        Ld = _as_device_matrix(L, self.dtype, block_size, self.ctx)
+        ms = C.c_double()
+        _lib.call("lspcg_solver_set_spai", self.handle, Ld.handle, float(epsilon), C.byref(ms))
+        self._L = Ld  # keep alive: the solver reads it
+        self._spai_key = (id(L), float(epsilon))
+        return ms.value / 1e3
+
+    def solve(self, b: torch.Tensor, x: torch.Tensor, rtol: float = 1e-6, max_iter: int = 0,
+              return_history: bool = False):
+        """Device-tensor form: returns ``(iters, converged, solve_time_s[, res_hist])``."""
+        assert b.numel() == self.n and x.numel() == self.n
+        assert b.is_cuda and x.is_cuda and b.is_contiguous() and x.is_contiguous()
+        mi = int(max_iter) if max_iter and max_iter > 0 else self.n
+        it = C.c_int64()
+        ms = C.c_double()
+        hist = np.empty(mi + 2, dtype=np.float64) if return_history else None
+        rc = _lib.call("lspcg_solver_solve", self.handle, _ptr(b), _ptr(x), float(rtol), mi, C.byref(it),
+                       hist.ctypes.data_as(_lib.p_f64) if hist is not None else None, C.byref(ms),
+                       allow_not_converged=True)
+        out = (it.value, rc == _lib.OK, ms.value / 1e3)
+        if return_history:
+            out = out + (hist[: min(it.value, mi) + 1].copy(),)
+        return out
+
+    def __call__(self, b, x, rtol: float = 1e-6, max_iter: int = 0, ext_spai=None,
+                 return_history: bool = False) -> Tuple:
+        prec = 0.0
+        if self.preconditioner in ("ext_spai", "ext_spai_scaled"):
+            if ext_spai is None and self._L is None:
+                raise ValueError("ext_spai=(L, epsilon) is required for this preconditioner")
+            if ext_spai is not None:
+                L, eps = ext_spai
+                if self._spai_key != (id(L), float(eps)):
+                    prec = self.set_spai(L, eps, block_size=getattr(L, "block_size", 1)
+                                         if isinstance(L, DeviceMatrix) else 1)
+        tdt = torch.float32 if self.dtype == np.float32 else torch.float64
+        dev = self.ctx.torch_device
+        bt = torch.as_tensor(b).to(device=dev, dtype=tdt).contiguous().reshape(-1)
+        xt = torch.as_tensor(x).to(device=dev, dtype=tdt).contiguous().reshape(-1)
+        res = self.solve(bt, xt, rtol, max_iter, return_history)
+        if not (isinstance(x, torch.Tensor) and x.is_cuda and x.data_ptr() == xt.data_ptr()):
+            if isinstance(x, np.ndarray):
+                x[...] = xt.cpu().numpy().reshape(x.shape)
+            elif isinstance(x, torch.Tensor):
+                x.copy_(xt.reshape(x.shape))
+        iters, _conv, solve = res[:3]
+        return (iters, prec, solve) + (tuple(res[3:]) if return_history else ())

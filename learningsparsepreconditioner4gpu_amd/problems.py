@@ -1,0 +1,311 @@
+"""Synthetic SPD systems that feed the PCG hot path (host-side input plumbing).
+
+These are the inputs of the reference's hot path, not part of it.  The
+reference produces its matrices offline with ``datagen/*.py`` (pymathprim,
+tetgen, pyssim -- none of which exist here), so every generator below is
+either an exact restatement (``generate_spd_sparse_matrix``) or a stand-in
+with the same structure, as SURVEY.md section 8(d) specifies:
+
+* ``generate_spd_sparse_matrix``  -- restates ``datagen/synthetic.py:10-27``.
+* ``poisson2d_grid``              -- stand-in for ``datagen/poisson.py:48-84``
+  (cotangent Laplacian of a right-triangle grid, Dirichlet on a random 10 % of
+  the boundary vertices, masked with ``neural_cg/data.py:159-170`` semantics).
+* ``kuhn_laplacian``              -- the roofline target of SURVEY.md 8(d):
+  Freudenthal/Kuhn tet grid, 14 neighbours + self per interior vertex.
+* ``elasticity_box``              -- stand-in for ``datagen/elast_twist.py``:
+  block_size 3 linear-elastic tet stiffness + mass/dt^2, Dirichlet x-ends.
+* ``heat_tet``                    -- stand-in for ``datagen/heat_tetmesh.py``.
+
+All functions return scipy CSR matrices (float64, int32 indices, sorted) and,
+where the reference has one, the Dirichlet mask ``[N, b]``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import numpy as np
+import scipy.sparse as sp
+
+
+# ---------------------------------------------------------------------------
+# datagen/synthetic.py:10-27
+# ---------------------------------------------------------------------------
+def generate_spd_sparse_matrix(n, sparsity=0.01, condition_amplifier=1e-6, random_state=None):
+    """Random SPD ``MᵀM + αI`` exactly as ``datagen/synthetic.py:10-27``.
+
+    ``random_state`` is forwarded to ``np.random.default_rng`` just like the
+    reference (the datagen passes a ``np.random.RandomState``).
+    """
+    rng = np.random.default_rng(random_state)
+    M = sp.random(n, n, density=sparsity, format="csr", random_state=rng)
+    M.data = (M.data - 0.5) * 2
+    scaling = np.linspace(1, condition_amplifier, n)
+    D = sp.diags(scaling)
+    M = D @ M
+    A = M.T @ M
+    A += sp.eye(n) * condition_amplifier
+    return _canon(A)
+
+
+def synthetic_c1(n: int = 10240, seed: int = 42):
+    """BASELINE config 1: synthetic N=10240, sparsity 3e-4, amplifier 1e-5."""
+    return generate_spd_sparse_matrix(n, 3e-4, 1e-5, np.random.RandomState(seed))
+
+
+def _canon(A) -> sp.csr_matrix:
+    A = sp.csr_matrix(A)
+    A.sum_duplicates()
+    A.sort_indices()
+    A.indptr = A.indptr.astype(np.int32)
+    A.indices = A.indices.astype(np.int32)
+    return A
+
+
+# ---------------------------------------------------------------------------
+# Dirichlet masking (neural_cg/data.py:159-170 semantics)
+# ---------------------------------------------------------------------------
+def apply_dbc_masking(mat, mask: np.ndarray) -> sp.csr_matrix:
+    """Zero rows/cols with ``mask == 0`` and put 1 on their diagonal.
+
+    Same result as ``neural_cg/data.py:159-170`` (COO zeroing + ``diags(1-mask)``
+    added through scipy's CSR addition, which drops explicit zeros).
+    """
+    coo = sp.coo_matrix(mat)
+    m = np.asarray(mask, dtype=np.float64).ravel()
+    data = coo.data.copy()
+    data[m[coo.row] == 0] = 0
+    data[m[coo.col] == 0] = 0
+    coo = sp.coo_matrix((data, (coo.row, coo.col)), shape=coo.shape)
+    out = coo.tocsr() + sp.diags(1.0 - m, 0, shape=coo.shape, format="csr")
+    return _canon(out)
+
+
+# ---------------------------------------------------------------------------
+# Meshes
+# ---------------------------------------------------------------------------
+def grid_triangles(nx: int, ny: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Unit right-triangle grid with nx*ny vertices (row-major)."""
+    xs, ys = np.meshgrid(np.arange(nx, dtype=np.float64), np.arange(ny, dtype=np.float64), indexing="xy")
+    nodes = np.stack([xs.ravel(), ys.ravel()], axis=1)
+    i, j = np.meshgrid(np.arange(nx - 1), np.arange(ny - 1), indexing="xy")
+    v00 = (j * nx + i).ravel()
+    v10 = v00 + 1
+    v01 = v00 + nx
+    v11 = v01 + 1
+    tris = np.concatenate([np.stack([v00, v10, v11], 1), np.stack([v00, v11, v01], 1)], 0)
+    return nodes, tris.astype(np.int64)
+
+
+def cotangent_laplacian(nodes: np.ndarray, tris: np.ndarray) -> sp.csr_matrix:
+    """Positive semi-definite cotangent Laplacian (stand-in for pymathprim.geometry.laplacian)."""
+    n = nodes.shape[0]
+    rows, cols, vals = [], [], []
+    for k in range(3):
+        a = tris[:, k]
+        b = tris[:, (k + 1) % 3]
+        c = tris[:, (k + 2) % 3]
+        u = nodes[a] - nodes[c]
+        v = nodes[b] - nodes[c]
+        dot = np.sum(u * v, axis=1)
+        if nodes.shape[1] == 2:
+            cr = np.abs(u[:, 0] * v[:, 1] - u[:, 1] * v[:, 0])
+        else:
+            cr = np.linalg.norm(np.cross(u, v), axis=1)
+        w = 0.5 * dot / cr  # 0.5 * cot(angle at c)
+        rows += [a, b, a, b]
+        cols += [b, a, a, b]
+        vals += [-w, -w, w, w]
+    L = sp.coo_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(n, n)).tocsr()
+    L.sum_duplicates()
+    L.eliminate_zeros()
+    return _canon(L)
+
+
+def boundary_vertices_tri(tris: np.ndarray) -> np.ndarray:
+    e = np.concatenate([tris[:, [0, 1]], tris[:, [1, 2]], tris[:, [2, 0]]], 0)
+    e = np.sort(e, axis=1)
+    uniq, cnt = np.unique(e, axis=0, return_counts=True)
+    return np.unique(uniq[cnt == 1].ravel())
+
+
+def poisson2d_grid(nx: int = 256, ny: int = 256, ratio: float = 0.1, seed: int = 42):
+    """BASELINE config 2 stand-in: Poisson-2D, N = nx*ny (65,536 at 256²), fp64.
+
+    Returns ``(A, mask[N,1], nodes)`` with A already Dirichlet-masked as
+    ``datagen/poisson.py:74-81`` does.
+    """
+    nodes, tris = grid_triangles(nx, ny)
+    L = cotangent_laplacian(nodes, tris)
+    bnd = boundary_vertices_tri(tris)
+    rng = np.random.default_rng(seed)
+    dbc_cnt = int(ratio * len(bnd))
+    dbc = rng.choice(bnd.shape[0], size=dbc_cnt, replace=False)
+    mask = np.ones((L.shape[0], 1), dtype=np.float64)
+    mask[bnd[dbc]] = 0
+    return apply_dbc_masking(L, mask), mask, nodes
+
+
+_KUHN_OFFSETS = np.array(
+    [(1, 0, 0), (0, 1, 0), (0, 0, 1), (1, 1, 0), (1, 0, 1), (0, 1, 1), (1, 1, 1)], dtype=np.int64
+)
+
+
+def kuhn_laplacian(n: int = 101, shift: float = 1e-4, ny: Optional[int] = None, nz: Optional[int] = None):
+    """Weighted graph Laplacian of the Kuhn (Freudenthal) tet grid + ``shift*I``.
+
+    Vertex (i, j, k) -> (i*ny + j)*nz + k.  Every vertex couples to the 14
+    Kuhn neighbours ±(1,0,0) ±(0,1,0) ±(0,0,1) ±(1,1,0) ±(1,0,1) ±(0,1,1)
+    ±(1,1,1) with weight 1/|d|².  At n=101: N=1,030,301, nnz=15,210,901
+    (SURVEY.md 8(d) roofline target).
+    """
+    nx = n
+    ny = n if ny is None else ny
+    nz = n if nz is None else nz
+    N = nx * ny * nz
+    rows, cols, vals = [], [], []
+    idx = np.arange(N, dtype=np.int64).reshape(nx, ny, nz)
+    deg = np.zeros(N, dtype=np.float64)
+    for d in _KUHN_OFFSETS:
+        w = 1.0 / float(np.dot(d, d))
+        a = idx[: nx - d[0], : ny - d[1], : nz - d[2]].ravel()
+        b = idx[d[0]:, d[1]:, d[2]:].ravel()
+        rows += [a, b]
+        cols += [b, a]
+        vals += [np.full(a.size, -w), np.full(a.size, -w)]
+        np.add.at(deg, a, w)
+        np.add.at(deg, b, w)
+    rows.append(np.arange(N))
+    cols.append(np.arange(N))
+    vals.append(deg + shift)
+    A = sp.coo_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(N, N))
+    return _canon(A)
+
+
+def kuhn_tets(nx: int, ny: int, nz: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Vertices and tetrahedra of a Kuhn-split (6 tets / cube) box grid."""
+    g = np.stack(np.meshgrid(np.arange(nx), np.arange(ny), np.arange(nz), indexing="ij"), -1).reshape(-1, 3)
+    nodes = g.astype(np.float64)
+    idx = lambda i, j, k: (i * ny + j) * nz + k
+    ci, cj, ck = np.meshgrid(np.arange(nx - 1), np.arange(ny - 1), np.arange(nz - 1), indexing="ij")
+    ci, cj, ck = ci.ravel(), cj.ravel(), ck.ravel()
+    tets = []
+    import itertools
+
+    for perm in itertools.permutations(range(3)):
+        p = np.zeros((ci.size, 3), dtype=np.int64)
+        v = [idx(ci, cj, ck)]
+        for ax in perm:
+            p[:, ax] += 1
+            v.append(idx(ci + p[:, 0], cj + p[:, 1], ck + p[:, 2]))
+        tets.append(np.stack(v, 1))
+    return nodes, np.concatenate(tets, 0)
+
+
+def _tet_gradients(nodes: np.ndarray, tets: np.ndarray):
+    X = nodes[tets]  # [T,4,3]
+    Dm = np.stack([X[:, 1] - X[:, 0], X[:, 2] - X[:, 0], X[:, 3] - X[:, 0]], -1)  # [T,3,3] columns
+    vol = np.abs(np.linalg.det(Dm)) / 6.0
+    Dinv = np.linalg.inv(Dm)  # rows = grads of barycentric 1..3
+    g123 = Dinv  # [T,3(node),3(xyz)]
+    g0 = -g123.sum(1, keepdims=True)
+    return np.concatenate([g0, g123], 1), vol  # [T,4,3], [T]
+
+
+def p1_stiffness(nodes, tets, kappa=None) -> sp.csr_matrix:
+    G, vol = _tet_gradients(nodes, tets)
+    w = vol if kappa is None else vol * kappa
+    K = np.einsum("tad,tbd->tab", G, G) * w[:, None, None]
+    r = np.repeat(tets, 4, axis=1).ravel()
+    c = np.tile(tets, (1, 4)).ravel()
+    n = nodes.shape[0]
+    return _canon(sp.coo_matrix((K.ravel(), (r, c)), shape=(n, n)))
+
+
+def lumped_mass(nodes, tets) -> np.ndarray:
+    _, vol = _tet_gradients(nodes, tets)
+    m = np.zeros(nodes.shape[0])
+    np.add.at(m, tets.ravel(), np.repeat(vol / 4.0, 4))
+    return m
+
+
+def heat_tet(nx: int, ny: int, nz: int, rho: float = 2e-4, seed: int = 0):
+    """Heat-tetmesh stand-in (``datagen/heat_tetmesh.py:26-56``): ``L + diag(M·ρ)``.
+
+    Returns ``(A, mask[N,1], features[N,3])`` (features = xyz, as
+    ``heat_tetmesh.py:99``).
+    """
+    nodes, tets = kuhn_tets(nx, ny, nz)
+    rng = np.random.default_rng(seed)
+    kappa = rng.uniform(0.01, 1.0, size=tets.shape[0])
+    K = p1_stiffness(nodes, tets, kappa)
+    M = lumped_mass(nodes, tets)
+    A = sp.csr_matrix(K + sp.diags(M * rho))
+    A.eliminate_zeros()
+    A = _canon(A)
+    mask = np.ones((A.shape[0], 1))
+    return A, mask, nodes / max(nx, ny, nz)
+
+
+def elasticity_box(nx: int = 117, ny: int = 30, nz: int = 30, E: float = 3e6, nu: float = 0.4,
+                   density: float = 1.0, dt: float = 0.01):
+    """Elasticity-twist stand-in, block_size 3 (``datagen/elast_twist.py:17-129``).
+
+    Linear-elastic P1 tet stiffness (E, ν) + lumped mass/dt², vertices at
+    both x-ends Dirichlet.  Returns ``(A_bsr_pattern_csr, mask[N,3], nodes)``
+    where A is the *scalar* CSR (n = 3N) before masking and mask is per dof.
+    """
+    nodes, tets = kuhn_tets(nx, ny, nz)
+    nodes = nodes / float(max(ny, nz) - 1)
+    G, vol = _tet_gradients(nodes, tets)
+    lam = E * nu / ((1 + nu) * (1 - 2 * nu))
+    mu = E / (2 * (1 + nu))
+    # K_ab(ij) = vol * (lam * g_a,i g_b,j + mu * (g_a,j g_b,i + δ_ij g_a·g_b))
+    gg = np.einsum("tad,tbd->tab", G, G)
+    Kt = (lam * np.einsum("tai,tbj->tabij", G, G)
+          + mu * np.einsum("taj,tbi->tabij", G, G)
+          + mu * gg[:, :, :, None, None] * np.eye(3)[None, None, None])
+    Kt *= vol[:, None, None, None, None]
+    T = tets.shape[0]
+    ra = (3 * tets[:, :, None, None, None] + np.arange(3)[None, None, None, :, None])
+    cb = (3 * tets[:, None, :, None, None] + np.arange(3)[None, None, None, None, :])
+    ra = np.broadcast_to(ra, (T, 4, 4, 3, 3)).ravel()
+    cb = np.broadcast_to(cb, (T, 4, 4, 3, 3)).ravel()
+    n = 3 * nodes.shape[0]
+    K = sp.coo_matrix((Kt.ravel(), (ra, cb)), shape=(n, n)).tocsr()
+    m = lumped_mass(nodes, tets) * density / dt ** 2
+    A = _canon(K + sp.diags(np.repeat(m, 3)))
+    mask = np.ones((nodes.shape[0], 3))
+    x = nodes[:, 0]
+    mask[(x <= x.min() + 1e-9) | (x >= x.max() - 1e-9)] = 0
+    return A, mask, nodes
+
+
+# ---------------------------------------------------------------------------
+# Block (graph) view of a scalar CSR, the reference's edge_index / block_values
+# ---------------------------------------------------------------------------
+@dataclass
+class BlockGraph:
+    """COO block view of a matrix (``neural_cg/data.py:471-572`` ``load``).
+
+    ``edge_index [2,E]`` int64 row-major sorted, ``block_values [E,b,b]`` f64,
+    ``num_nodes`` = block rows.
+    """
+
+    edge_index: np.ndarray
+    block_values: np.ndarray
+    num_nodes: int
+    block_size: int
+
+
+def to_block_graph(A: sp.csr_matrix, block_size: int = 1) -> BlockGraph:
+    if block_size == 1:
+        coo = sp.coo_matrix(A)
+        return BlockGraph(np.vstack([coo.row, coo.col]).astype(np.int64),
+                          coo.data.astype(np.float64).reshape(-1, 1, 1), A.shape[0], 1)
+    bsr = sp.bsr_matrix(sp.csr_matrix(A), blocksize=(block_size, block_size))
+    bsr.sort_indices()
+    nb = A.shape[0] // block_size
+    rows = np.repeat(np.arange(nb), np.diff(bsr.indptr))
+    return BlockGraph(np.vstack([rows, bsr.indices]).astype(np.int64), bsr.data.astype(np.float64),
+                      nb, block_size)

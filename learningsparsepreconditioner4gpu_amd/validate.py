@@ -1,0 +1,111 @@
+"""Drop-in mirror of ``neural_cg/utils/validate.py``'s hot-path API, backed by HIP.
+
+Same names, arguments, return values and error behaviour as the reference:
+
+* ``to_csr_cpu``                 -- validate.py:22-51 (assembly runs on the GPU, result
+  returned as a sorted scipy CSR like the reference)
+* ``get_cg_iter_time``           -- validate.py:54-86 (raises ``RuntimeError("CG did not
+  converge")`` when ``iter >= max_iter``, as :84-85)
+* ``get_pcg_iter_time``          -- validate.py:89-121 (ext_spai, never raises)
+* ``get_pcg_scaled_iter_time``   -- validate.py:124-160 (ext_spai_scaled)
+
+Matrices may be scipy CSR (uploaded) or :class:`DeviceMatrix` (already in HBM);
+``device`` must be a GPU device -- there is no CPU solver in the product.
+Right-hand sides are formed on the device exactly as ``b = A @ gt`` (bit-identical to
+scipy's csr_matvec).
+"""
+from __future__ import annotations
+
+from typing import Tuple, Union
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from .linalg import PreconditionedConjugateGradient
+from .sparse import Context, DeviceMatrix, assemble, lspcg_dtype
+
+
+def to_numpy(x) -> np.ndarray:
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    if isinstance(x, np.ndarray):
+        return x
+    raise ValueError(f"Unknown type {type(x)}")
+
+
+def to_csr_device(edge_index, edge_attr, n: int, mask, dtype=np.float64, block_output: bool = False) -> DeviceMatrix:
+    """GPU assembly with to_csr_cpu semantics; the result stays in HBM."""
+    ei = torch.as_tensor(edge_index)
+    ea = torch.as_tensor(edge_attr)
+    assert ei.ndim == 2 and ei.shape[0] == 2
+    assert ea.ndim in [1, 3]
+    m = None if mask is None else torch.as_tensor(mask)
+    tdt = torch.float32 if np.dtype(dtype) == np.float32 else torch.float64
+    return assemble(ei, ea, n, m, dtype=tdt, block_output=block_output)
+
+
+def to_csr_cpu(edge_index, edge_attr, n: int, mask, dtype=np.float64) -> sp.csr_matrix:
+    """validate.py:22-51.  Assembled on the GPU, returned as a sorted scipy CSR."""
+    return to_csr_device(edge_index, edge_attr, n, mask, dtype).to_scipy()
+
+
+def _device_rhs(A: DeviceMatrix, gt) -> torch.Tensor:
+    g = torch.as_tensor(np.asarray(to_numpy(gt) if isinstance(gt, torch.Tensor) else gt)).reshape(-1)
+    return A.matvec(g.to(device=A.ctx.torch_device, dtype=A.dtype))
+
+
+def _prepare(A, dtype, block_size=1) -> DeviceMatrix:
+    if isinstance(A, DeviceMatrix):
+        return A
+    return DeviceMatrix.from_scipy(sp.csr_matrix(A), dtype=dtype, block_size=block_size, ctx=Context.get())
+
+
+def get_cg_iter_time(A, gt, rtol=1e-6, max_iter=0, dtype=np.float64, repeat=1, device="cuda",
+                     method="ainv") -> Tuple[float, float, float]:
+    """validate.py:54-86 (method in none / diagonal; ic / ainv / fsai are baselines not built yet)."""
+    Ad = _prepare(A, dtype)
+    rows = Ad.n
+    max_iter = max_iter if max_iter > 0 else rows
+    b = _device_rhs(Ad, gt)
+    iter_cnt, time_prec, time_elp = 0, 0.0, 0.0
+    x = torch.zeros_like(b)
+    for _ in range(repeat):
+        solver = PreconditionedConjugateGradient(Ad, device=device, preconditioner=method, dtype=dtype)
+        this_iter, this_prec, this_solve = solver(b.clone(), x.clone(), rtol, max_iter)
+        iter_cnt += this_iter
+        time_prec += this_prec
+        time_elp += this_solve
+        if this_iter >= max_iter:
+            raise RuntimeError("CG did not converge")
+    return iter_cnt / repeat, time_prec / repeat, time_elp / repeat
+
+
+def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device):
+    Ad = _prepare(A, dtype)
+    Ld = spai if isinstance(spai, DeviceMatrix) else _prepare(spai, dtype)
+    rows = Ad.n
+    max_iter = max_iter if max_iter > 0 else rows
+    b = _device_rhs(Ad, gt)
+    assert repeat > 0
+    iter_cnt, time_elp, time_prec = 0, 0.0, 0.0
+    x = torch.zeros_like(b)
+    for _ in range(repeat):
+        solver = PreconditionedConjugateGradient(Ad, device=device, preconditioner=method, dtype=dtype)
+        this_iter, this_prec, this_solve = solver(b.clone(), x.clone(), rtol, max_iter, ext_spai=(Ld, epsilon))
+        iter_cnt += this_iter
+        time_prec += this_prec
+        time_elp += this_solve
+    return iter_cnt / repeat, time_prec / repeat, time_elp / repeat
+
+
+def get_pcg_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat=1, dtype=np.float64,
+                      device="cuda") -> Tuple[float, float, float]:
+    """validate.py:89-121: ext_spai PCG, M⁻¹ = L Lᵀ + εI."""
+    return _pcg_generic("ext_spai", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device)
+
+
+def get_pcg_scaled_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat=1, dtype=np.float64,
+                             device="cuda") -> Tuple[float, float, float]:
+    """validate.py:124-160: ext_spai_scaled PCG, M⁻¹ r = L((Lᵀr)/d) + εr/d, d = diag(A)."""
+    return _pcg_generic("ext_spai_scaled", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device)

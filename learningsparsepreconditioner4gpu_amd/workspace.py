@@ -1,0 +1,103 @@
+"""Inference workspace: GNN -> L in HBM, the hot half of ``SimpleTrainingWorkspace``.
+
+Mirrors ``neural_cg/workspace.py`` (``forward`` :92-94, ``inference_step`` :195-205) and
+``neural_cg/scaled_workspace.py`` (``inference_step`` :199-212) without Lightning: the
+GNN runs as HIP kernels and L is assembled on the GPU with ``to_csr_cpu`` semantics
+(``lspcg_assemble``), so nothing is copied back to the host.  ``dt`` has the reference's
+meaning: wall time of the GNN forward until its result is available (the reference stops
+the clock after ``.cpu()``, i.e. after a device sync).
+"""
+from __future__ import annotations
+
+from time import time
+from typing import Optional, Tuple, Union
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from .data import GraphSample
+from .nn import NodeEdgeProcessing, build_gnn, default_gnn_config
+from .sparse import DeviceMatrix, assemble
+
+
+class SimpleInferenceWorkspace:
+    def __init__(self, node_features: int, edge_features: int, block_size: int = 1, epsilon: float = 3e-3,
+                 gnn: Optional[dict] = None, seed: Optional[int] = 0, device: Union[str, torch.device] = "cuda"):
+        self.block_size = block_size
+        self.epsilon = float(epsilon)
+        cfg = default_gnn_config() if gnn is None else dict(gnn)
+        if seed is not None:
+            torch.manual_seed(seed)
+        self.gnn = NodeEdgeProcessing(node_in_features=node_features, node_out_features=None,
+                                      edge_in_features=edge_features, edge_out_features=block_size * block_size,
+                                      **cfg)
+        self.device = torch.device(device)
+
+    # ---- checkpoints (workspace.py:52 save_hyperparameters; infer.py:237 load_from_checkpoint)
+    @classmethod
+    def load_from_checkpoint(cls, path: str, device="cuda", trusted: bool = False) -> "SimpleInferenceWorkspace":
+        """Load a Lightning checkpoint of the reference: ``hyper_parameters`` (block_size, epsilon,
+        node_features, edge_features, gnn) and ``state_dict['gnn.*']``.  Loaded with
+        ``weights_only=True`` unless ``trusted=True`` (only for files you produced yourself)."""
+        ck = torch.load(path, map_location="cpu", weights_only=not trusted)
+        hp = ck.get("hyper_parameters", {})
+        gnn_cfg = hp.get("gnn")
+        ws = cls(node_features=int(hp["node_features"]), edge_features=int(hp["edge_features"]),
+                 block_size=int(hp.get("block_size", 1)), epsilon=float(hp.get("epsilon", 3e-3)),
+                 gnn=None if gnn_cfg is None else {k: (dict(v) if hasattr(v, "items") else v)
+                                                    for k, v in dict(gnn_cfg).items()},
+                 seed=None, device=device)
+        sd = {k[len("gnn."):]: v for k, v in ck["state_dict"].items() if k.startswith("gnn.")}
+        ws.gnn.load_state_dict(sd, strict=True)
+        return ws
+
+    def to(self, device) -> "SimpleInferenceWorkspace":
+        self.device = torch.device(device)
+        return self
+
+    def eval(self) -> "SimpleInferenceWorkspace":
+        return self
+
+    # ---- workspace.py:92-94
+    def forward(self, node_attr, edge_index, edge_attr) -> torch.Tensor:
+        _, boo = self.gnn(node_attr, edge_index, edge_attr)
+        return boo.reshape(-1, self.block_size, self.block_size)
+
+    __call__ = forward
+
+    def _assemble(self, sample: GraphSample, boo: torch.Tensor, block_output: Optional[bool]) -> DeviceMatrix:
+        n = sample.num_nodes * self.block_size
+        bo = (self.block_size > 1) if block_output is None else block_output
+        return assemble(sample.edge_index, boo, n, sample.mask, dtype=torch.float64, block_output=bo)
+
+    # ---- workspace.py:195-205
+    def inference_step(self, sample: GraphSample, time_beg: Optional[float] = None, block_output: Optional[bool] = None,
+                       return_scipy: bool = False) -> Tuple[Union[DeviceMatrix, sp.csr_matrix], float]:
+        s = sample if sample.x.is_cuda else sample.to(self.device)
+        time_beg = time()
+        boo = self.forward(s.x, s.edge_index, s.edge_attr)
+        torch.cuda.synchronize(boo.device)
+        dt = time() - time_beg
+        L = self._assemble(s, boo, block_output)
+        return (L.to_scipy().tocsr() if return_scipy else L), dt
+
+    def system_matrix(self, sample: GraphSample, block_output: Optional[bool] = None) -> DeviceMatrix:
+        """``to_csr_cpu(edge_index, matrix_values, n, mask)`` (infer.py:282) on the device."""
+        s = sample if sample.x.is_cuda else sample.to(self.device)
+        return self._assemble(s, s.matrix_values, block_output)
+
+
+class ScaledInferenceWorkspace(SimpleInferenceWorkspace):
+    """scaled_workspace.py:199-212: L <- L · diag(rsqrt(diag(A) + 1e-7)), solved with ext_spai_scaled."""
+
+    def inference_step(self, sample: GraphSample, time_beg: Optional[float] = None, block_output: Optional[bool] = None,
+                       return_scipy: bool = False):
+        s = sample if sample.x.is_cuda else sample.to(self.device)
+        time_beg = time()
+        boo = self.forward(s.x, s.edge_index, s.edge_attr)
+        torch.cuda.synchronize(boo.device)
+        dt = time() - time_beg
+        L = self._assemble(s, boo, block_output)
+        L.scale_columns_(s.rsqrt_diag.reshape(-1).to(torch.float64))
+        return (L.to_scipy().tocsr() if return_scipy else L), dt

@@ -1,0 +1,89 @@
+"""GPU parity: HIP GNN forward (lspcg_gnn_forward) vs the oracle's torch-CPU restatement,
+fp32 within 1e-5 (BASELINE.json north_star), plus the end-to-end inference_step -> PCG."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import gnn as OG
+from oracle import linalg as O
+from learningsparsepreconditioner4gpu_amd import problems as P
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(node_in, edge_in, bs, seed=0):
+    from learningsparsepreconditioner4gpu_amd.nn import build_gnn
+
+    ref = OG.build(node_in, edge_in, bs, seed=seed)
+    gpu = build_gnn(node_in, edge_in, bs, seed=seed)
+    return ref, gpu
+
+
+def _close(a, b, tol=1e-5):
+    scale = max(1.0, float(np.abs(b).max()))
+    err = float(np.abs(a - b).max())
+    assert err <= tol * scale, (err, scale)
+
+
+@pytest.mark.parametrize("case", ["poisson", "synthetic", "elast"])
+def test_gnn_forward_matches_oracle(gpu_ctx, case):
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+
+    if case == "poisson":
+        A, mask, _ = P.poisson2d_grid(23, 19)
+        s = make_sample(A, mask)
+        bs = 1
+    elif case == "synthetic":
+        A = P.generate_spd_sparse_matrix(1500, 4e-3, 1e-5, np.random.RandomState(1))
+        s = make_sample(A, None, use_edge_features_as_node_feature="mean")
+        bs = 1
+    else:
+        A, mask, nodes = P.elasticity_box(7, 4, 4)
+        s = make_sample(A, mask, node_features=np.concatenate([nodes, nodes * 0.5], 1), block_size=3)
+        bs = 3
+    ref, gpu = _pair(s.x.shape[1], s.edge_attr.shape[1], bs, seed=3)
+    with torch.no_grad():
+        _, want = ref(s.x, s.edge_index, s.edge_attr)
+    _, got = gpu(s.x.cuda(), s.edge_index.cuda(), s.edge_attr.cuda())
+    _close(got.cpu().numpy(), want.numpy())
+
+
+def test_gnn_deterministic(gpu_ctx):
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+
+    A, mask, _ = P.poisson2d_grid(30, 30)
+    s = make_sample(A, mask).to("cuda")
+    _, gpu = _pair(s.x.shape[1], s.edge_attr.shape[1], 1, seed=1)
+    a = gpu(s.x, s.edge_index, s.edge_attr)[1]
+    b = gpu(s.x, s.edge_index, s.edge_attr)[1]
+    assert torch.equal(a, b)
+
+
+def test_inference_step_and_pcg_end_to_end(gpu_ctx):
+    """GNN -> device assembly of L (masked) -> ext_spai PCG vs oracle on the same L."""
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+    from learningsparsepreconditioner4gpu_amd.validate import get_pcg_iter_time
+
+    A, mask, _ = P.poisson2d_grid(26, 21)
+    s = make_sample(A, mask)
+    ws = SimpleInferenceWorkspace(node_features=s.x.shape[1], edge_features=s.edge_attr.shape[1], seed=0)
+    L_dev, dt = ws.inference_step(s)
+    assert dt > 0
+    # oracle: same GNN weights on CPU, then to_csr restatement
+    ref = OG.build(s.x.shape[1], s.edge_attr.shape[1], 1, seed=0)
+    with torch.no_grad():
+        boo = ref(s.x, s.edge_index, s.edge_attr)[1].reshape(-1, 1, 1).numpy()
+    n = A.shape[0]
+    L_ref = O.to_csr(s.edge_index.numpy(), boo, n, s.mask.numpy())
+    L_got = L_dev.to_scipy()
+    assert np.array_equal(L_got.indptr, L_ref.indptr) and np.array_equal(L_got.indices, L_ref.indices)
+    _close(L_got.data, L_ref.data)
+    # the solve (A assembled on device from the scaled fp32 matrix values, infer.py:282)
+    A_dev = ws.system_matrix(s)
+    A_ref = O.to_csr(s.edge_index.numpy(), s.matrix_values.numpy(), n, s.mask.numpy())
+    assert abs(A_dev.to_scipy() - A_ref).max() == 0
+    gt = s.mask.numpy().ravel().astype(np.float64)
+    it, prec, solve = get_pcg_iter_time(A_dev, gt, L_dev, ws.epsilon, rtol=1e-8)
+    it_o, _, _ = O.pcg(A_ref, A_ref @ gt, O.spai_operator(L_got, ws.epsilon), rtol=1e-8, dot="exact")
+    assert it == it_o

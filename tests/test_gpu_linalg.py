@@ -1,0 +1,153 @@
+"""GPU parity: HIP SpMV / dot / PCG through the C ABI vs the CPU oracle.
+
+Tolerances (BASELINE.json north_star): SpMV and elementwise updates are bit-identical to
+scipy; PCG iteration counts equal the oracle's exactly; solutions agree within 1e-12
+relative (fp64) / 1e-5 (fp32).
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from oracle import linalg as O
+from tests import _cases
+from learningsparsepreconditioner4gpu_amd import problems as P
+
+pytestmark = pytest.mark.gpu
+
+
+def _dm(A, dtype=np.float64, bs=1):
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    return DeviceMatrix.from_scipy(A, dtype=dtype, block_size=bs)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("which", ["synthetic", "poisson", "kuhn", "ragged"])
+def test_spmv_bitwise_vs_scipy(gpu_ctx, which, dtype):
+    A = {
+        "synthetic": lambda: P.generate_spd_sparse_matrix(3000, 3e-3, 1e-5, np.random.RandomState(0)),
+        "poisson": lambda: P.poisson2d_grid(40, 33)[0],
+        "kuhn": lambda: P.kuhn_laplacian(13),
+        "ragged": lambda: _cases.ragged_matrix(),
+    }[which]().astype(dtype)
+    x = np.random.default_rng(5).normal(size=A.shape[0]).astype(dtype)
+    ref = A @ x
+    y = _dm(A, dtype).matvec(torch.from_numpy(x).cuda()).cpu().numpy()
+    assert np.array_equal(y, ref), np.max(np.abs(y - ref))
+
+
+def test_spmv_bsr3_matches_scalar_csr(gpu_ctx):
+    A, mask, _ = P.elasticity_box(10, 5, 4)
+    x = np.random.default_rng(2).normal(size=A.shape[0])
+    B = sp.bsr_matrix(A, blocksize=(3, 3))
+    ref = B.tocsr() @ x  # scalar CSR incl. in-block zeros: same summation sequence as the BSR kernel
+    y = _dm(A, np.float64, 3).matvec(torch.from_numpy(x).cuda()).cpu().numpy()
+    assert np.array_equal(y, ref)
+    assert np.allclose(y, A @ x, rtol=1e-14, atol=1e-14 * np.abs(A @ x).max())
+
+
+def test_empty_matrix_and_zero_rows(gpu_ctx):
+    A = sp.csr_matrix((5, 5))
+    y = _dm(A).matvec(torch.ones(5, dtype=torch.float64, device="cuda")).cpu().numpy()
+    assert np.array_equal(y, np.zeros(5))
+
+
+def test_dot_is_correctly_rounded(gpu_ctx):
+    from learningsparsepreconditioner4gpu_amd.sparse import dot
+
+    rng = np.random.default_rng(0)
+    for n in [0, 1, 1000, 100_003]:
+        a = rng.normal(size=n) * np.exp(rng.normal(size=n) * 5)
+        b = rng.normal(size=n)
+        got = dot(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda())
+        assert got == O.exact_dot(a, b)
+
+
+def test_transpose_and_diagonal(gpu_ctx):
+    A = _cases.ragged_matrix(800)
+    Ad = _dm(A)
+    T = Ad.transpose().to_scipy()
+    ref = sp.csr_matrix(A.T)
+    ref.sort_indices()
+    assert np.array_equal(T.indptr, ref.indptr) and np.array_equal(T.indices, ref.indices)
+    assert np.array_equal(T.data, ref.data)
+    assert np.array_equal(Ad.diagonal().cpu().numpy(), A.diagonal())
+    Ae, _, _ = P.elasticity_box(6, 4, 3)
+    Bd = _dm(Ae, np.float64, 3)
+    Tb = Bd.transpose().to_scipy().tocsr()
+    assert abs(Tb - sp.csr_matrix(Ae.T)).max() == 0
+    assert np.array_equal(Bd.diagonal().cpu().numpy(), Ae.diagonal())
+
+
+def _solve(A, b, method, L=None, eps=3e-3, rtol=1e-8, dtype=np.float64, max_iter=0):
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=method, dtype=dtype)
+    x = np.zeros(A.shape[0], dtype=dtype)
+    it, prec, solve, hist = s(b.astype(dtype), x, rtol, max_iter,
+                              ext_spai=(L, eps) if L is not None else None, return_history=True)
+    return it, x, hist
+
+
+def _oracle_psolve(method, A, L, eps):
+    if method == "none":
+        return None
+    if method == "diagonal":
+        return O.diagonal_operator(A)
+    if method == "ext_spai":
+        return O.spai_operator(L, eps)
+    return O.spai_scaled_operator(A, L, eps)
+
+
+@pytest.mark.parametrize("method", ["none", "diagonal", "ext_spai", "ext_spai_scaled"])
+@pytest.mark.parametrize("case", range(4))
+def test_pcg_parity_fp64(gpu_ctx, method, case):
+    name, A, mask = _cases.spd_cases()[case]
+    gt = np.ones(A.shape[0]) if mask is None else mask.ravel().astype(np.float64)
+    b = A @ gt
+    L = _cases.spai_like(A, seed=case) if method.startswith("ext_spai") else None
+    eps = 3e-3
+    it_o, x_o, h_o = O.pcg(A, b, _oracle_psolve(method, A, L, eps), rtol=1e-8, dot="exact")
+    it, x, h = _solve(A, b, method, L, eps)
+    assert it == it_o, (name, method, it, it_o)
+    rel = np.linalg.norm(x - x_o) / max(np.linalg.norm(x_o), 1e-300)
+    assert rel <= 1e-12, (name, method, rel)
+    assert len(h) == it + 1
+    np.testing.assert_allclose(h, h_o, rtol=1e-10, atol=0)
+
+
+@pytest.mark.parametrize("method", ["none", "ext_spai"])
+def test_pcg_parity_fp32(gpu_ctx, method):
+    A, mask, _ = P.poisson2d_grid(20, 18)
+    A32 = A.astype(np.float32)
+    gt = mask.ravel().astype(np.float32)
+    b = (A32 @ gt).astype(np.float32)
+    L = _cases.spai_like(A).astype(np.float32) if method == "ext_spai" else None
+    eps = 3e-3
+    psolve = None if L is None else O.spai_operator(L, np.float32(eps))
+    it_o, x_o, _ = O.pcg(A32, b, psolve, rtol=1e-6, dot="exact", dtype=np.float32)
+    it, x, _ = _solve(A32, b, method, L, eps, rtol=1e-6, dtype=np.float32)
+    assert it == it_o
+    assert np.linalg.norm(x - x_o) / np.linalg.norm(x_o) <= 1e-5
+
+
+def test_pcg_max_iter_and_zero_rhs(gpu_ctx):
+    A = P.kuhn_laplacian(7)
+    b = A @ np.ones(A.shape[0])
+    it, x, h = _solve(A, b, "none", max_iter=5)
+    it_o, x_o, _ = O.pcg(A, b, None, rtol=1e-8, max_iter=5, dot="exact")
+    assert it == it_o == 5
+    assert np.linalg.norm(x - x_o) <= 1e-13 * np.linalg.norm(x_o)
+    it, x, _ = _solve(A, np.zeros(A.shape[0]), "none")
+    assert it == 0 and not x.any()
+
+
+def test_validate_api_raises_when_not_converged(gpu_ctx):
+    from learningsparsepreconditioner4gpu_amd.validate import get_cg_iter_time
+
+    A = P.kuhn_laplacian(9)
+    with pytest.raises(RuntimeError, match="CG did not converge"):
+        get_cg_iter_time(A, np.ones(A.shape[0]), rtol=1e-12, max_iter=3, method="none")
+    it, prec, solve = get_cg_iter_time(A, np.ones(A.shape[0]), rtol=1e-8, method="none")
+    assert it == O.pcg(A, A @ np.ones(A.shape[0]), None, rtol=1e-8, dot="exact")[0]
