@@ -309,3 +309,34 @@ def to_block_graph(A: sp.csr_matrix, block_size: int = 1) -> BlockGraph:
     rows = np.repeat(np.arange(nb), np.diff(bsr.indptr))
     return BlockGraph(np.vstack([rows, bsr.indices]).astype(np.int64), bsr.data.astype(np.float64),
                       nb, block_size)
+
+
+def kuhn_dirichlet(n: int = 101, shift: float = 1e-4):
+    """Bench workload: ``kuhn_laplacian(n)`` with Dirichlet vertices on the i = 0 face.
+
+    Returns ``(A_raw, mask[N,1])``; masking is applied by the hot path's own assembly
+    (``to_csr_cpu`` semantics), like ``infer.py:282`` does for every sample.
+    """
+    A = kuhn_laplacian(n, shift)
+    mask = np.ones((A.shape[0], 1), dtype=np.float64)
+    mask[: n * n] = 0.0  # vertex index (i*n + j)*n + k with i = 0
+    return A, mask
+
+
+def workload(name: str):
+    """Named systems: returns ``(A_raw, mask, node_features, block_size, edge_to_node)``."""
+    if name.startswith("kuhn"):
+        n = int(name[4:] or 101)
+        A, mask = kuhn_dirichlet(n)
+        return A, mask, None, 1, "disable"
+    if name.startswith("poisson"):
+        n = int(name[7:] or 256)
+        A, mask, _ = poisson2d_grid(n, n)
+        return A, mask, None, 1, "disable"
+    if name.startswith("synthetic"):
+        n = int(name[9:] or 10240)
+        return synthetic_c1(n), None, None, 1, "mean"
+    if name.startswith("elast"):
+        A, mask, nodes = elasticity_box()
+        return A, mask, np.concatenate([nodes, np.zeros_like(nodes)], 1), 3, "disable"
+    raise KeyError(name)

@@ -181,10 +181,12 @@ class DeviceMatrix:
 
     __matmul__ = matvec
 
-    def spmv_timed(self, x: torch.Tensor, y: torch.Tensor, reps: int) -> float:
-        """Average device milliseconds of one SpMV launch over ``reps`` back-to-back launches."""
+    def spmv_timed(self, x: torch.Tensor, y: torch.Tensor, reps: int, flush_bytes: int = 0) -> float:
+        """Average device ms of one SpMV launch: ``reps`` back-to-back launches (warm), or with
+        ``flush_bytes`` > 0 each launch timed alone after an Infinity-Cache-evicting memset (cold)."""
         ms = C.c_double()
-        _lib.call("lspcg_spmv_timed", self.ctx.handle, self.handle, _ptr(x), _ptr(y), int(reps), C.byref(ms))
+        _lib.call("lspcg_spmv_timed", self.ctx.handle, self.handle, _ptr(x), _ptr(y), int(reps), int(flush_bytes),
+                  C.byref(ms))
         return ms.value
 
 

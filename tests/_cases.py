@@ -32,8 +32,9 @@ def ragged_matrix(n: int = 3000, seed: int = 1) -> sp.csr_matrix:
         c = rng.choice(n, size=k, replace=False)
         rows += [i] * k
         cols += list(c)
-    rows += [7] * 2500  # long row (+ beyond chunk with the neighbours)
-    cols += list(rng.choice(n, size=2500, replace=False))
+    k = min(2500, n)
+    rows += [7] * k  # long row (+ beyond chunk with the neighbours)
+    cols += list(rng.choice(n, size=k, replace=False))
     A = sp.csr_matrix((rng.normal(size=len(rows)), (rows, cols)), shape=(n, n))
     A.sum_duplicates()
     A.sort_indices()
