@@ -47,6 +47,7 @@ SIGNATURES = {
     "lspcg_mat_scale_columns": (C.c_int, [vp, vp]),
     "lspcg_spmv": (C.c_int, [vp, vp, vp, vp]),
     "lspcg_spmv_timed": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int64, p_f64]),
+    "lspcg_spmv_variant_timed": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int64, p_f64]),
     "lspcg_dot": (C.c_int, [vp, C.c_int64, C.c_int, vp, vp, p_f64]),
     "lspcg_solver_create": (C.c_int, [vp, vp, C.c_int, pp]),
     "lspcg_solver_set_spai": (C.c_int, [vp, vp, C.c_double, p_f64]),

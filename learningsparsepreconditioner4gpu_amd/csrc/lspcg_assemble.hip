@@ -180,8 +180,7 @@ static int assemble_t(lspcg_ctx* ctx, int64_t nb, int64_t E, const int64_t* ei, 
     m->n = n;
     m->nnzb = E;
     LSPCG_HIP(hipMalloc(&m->rowptr, sizeof(int32_t) * (nb + 1)));
-    LSPCG_HIP(hipMalloc(&m->colind, sizeof(int32_t) * (E > 0 ? E : 1)));
-    LSPCG_HIP(hipMalloc(&m->vals, sizeof(TO) * (E > 0 ? E * BS * BS : 1)));
+    if (int rc = mat_alloc_entries(m.get(), E)) return rc;
     hipLaunchKernelGGL((k_asm_bsr<TO, TI, TM, BS>), dim3(grid_of(nb)), dim3(kThreads), 0, st, in, m->rowptr,
                        m->colind, static_cast<TO*>(m->vals), flag);
     LSPCG_HIP(hipMemcpyAsync(&hflag, flag, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -214,8 +213,7 @@ static int assemble_t(lspcg_ctx* ctx, int64_t nb, int64_t E, const int64_t* ei, 
   LSPCG_HIP(hipStreamSynchronize(st));
   (void)hipFree(tmp);
   m->nnzb = nnz;
-  LSPCG_HIP(hipMalloc(&m->colind, sizeof(int32_t) * (nnz > 0 ? nnz : 1)));
-  LSPCG_HIP(hipMalloc(&m->vals, sizeof(TO) * (nnz > 0 ? nnz : 1)));
+  if (int rc = mat_alloc_entries(m.get(), nnz)) return rc;
   hipLaunchKernelGGL((k_asm_fill<TO, TI, TM, BS>), dim3(grid_of(n)), dim3(kThreads), 0, st, in, m->rowptr, m->colind,
                      static_cast<TO*>(m->vals));
   LSPCG_HIP(hipGetLastError());

@@ -18,6 +18,17 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 
 static size_t dtype_size(int dtype) { return dtype == LSPCG_F32 ? 4 : 8; }
 
+int mat_alloc_entries(lspcg_mat* m, int64_t nnzb) {
+  const int64_t ne = nnzb * m->block_size * m->block_size;
+  const size_t es = dtype_size(m->dtype);
+  hipStream_t st = m->ctx->stream;
+  LSPCG_HIP(hipMalloc(&m->colind, sizeof(int32_t) * (nnzb + kEntryPad)));
+  LSPCG_HIP(hipMalloc(&m->vals, es * (ne + kEntryPad)));
+  LSPCG_HIP(hipMemsetAsync(m->colind + nnzb, 0, sizeof(int32_t) * kEntryPad, st));
+  LSPCG_HIP(hipMemsetAsync(static_cast<char*>(m->vals) + es * ne, 0, es * kEntryPad, st));
+  return LSPCG_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Transpose: counting sort by column with atomics, then a per-row insertion sort of
 // the (original row, source position) pairs -> deterministic, sorted output.
@@ -103,6 +114,18 @@ __global__ void __launch_bounds__(kThreads) k_dot(int64_t n, const T* __restrict
   grid_reduce_dd<1>(d, partials, ticket, [&](const double* v) { out[0] = v[0]; });
 }
 
+// Reads a large buffer (evicts the Infinity Cache with CLEAN lines; a memset would leave
+// dirty lines whose write-back would be charged to the next kernel).
+using u32x4 = unsigned __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(kThreads) k_flush_read(const u32x4* __restrict__ buf, int64_t n, unsigned* sink) {
+  unsigned acc = 0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const u32x4 v = buf[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9e3779b9u) sink[0] = acc;  // keeps the loads alive
+}
+
 static int grid_for(int64_t n) {
   int64_t g = (n + kThreads - 1) / kThreads;
   return int(std::max<int64_t>(1, std::min<int64_t>(g, kElemBlocksMax)));
@@ -117,6 +140,21 @@ inline void launch_transpose_fill(const lspcg_mat* A, lspcg_mat* Tm, int32_t* fi
   hipLaunchKernelGGL((k_sort_gather_transpose<T, BS>), dim3(g), dim3(kThreads), 0, st, A->nb, Tm->rowptr, trow, tsrc,
                      static_cast<const T*>(A->vals), static_cast<T*>(Tm->vals));
 }
+
+// ---- diagnostic SpMV configurations (fp64, scalar CSR) for on-device A/B tuning
+using SpmvLaunch = void (*)(const lspcg_mat*, const void*, void*, hipStream_t);
+template <int TH, int GPT, bool NT>
+static void spmv_variant(const lspcg_mat* A, const void* x, void* y, hipStream_t st) {
+  launch_spmv_cfg<double, 1, TH, GPT, NT>(A, static_cast<const double*>(x), ProNone{},
+                                          EpiStore<double>{static_cast<double*>(y)}, st);
+}
+static const SpmvLaunch kSpmvVariants[] = {
+    spmv_variant<256, 4, false>, spmv_variant<256, 4, true>,  spmv_variant<256, 2, false>,
+    spmv_variant<256, 2, true>,  spmv_variant<128, 4, false>, spmv_variant<128, 8, false>,
+    spmv_variant<512, 2, false>, spmv_variant<512, 4, false>, spmv_variant<64, 8, false>,
+    spmv_variant<128, 2, false>, spmv_variant<256, 8, false>, spmv_variant<128, 4, true>,
+};
+static constexpr int kNumSpmvVariants = int(sizeof(kSpmvVariants) / sizeof(kSpmvVariants[0]));
 
 }  // namespace lspcg
 
@@ -173,8 +211,8 @@ static int mat_alloc(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, int dtype
   m->n = nb * bs;
   m->nnzb = nnzb;
   LSPCG_HIP(hipMalloc(&m->rowptr, sizeof(int32_t) * (nb + 1)));
-  LSPCG_HIP(hipMalloc(&m->colind, sizeof(int32_t) * std::max<int64_t>(nnzb, 1)));
-  LSPCG_HIP(hipMalloc(&m->vals, dtype_size(dtype) * std::max<int64_t>(nnzb * bs * bs, 1)));
+  int rc = mat_alloc_entries(m.get(), nnzb);
+  if (rc) return rc;
   *out = m.release();
   return LSPCG_OK;
 }
@@ -350,33 +388,43 @@ int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y) {
   return LSPCG_OK;
 }
 
-int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y, int reps, int64_t flush_bytes,
-                     double* avg_ms) {
+static int spmv_timed_impl(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y, int reps, int64_t flush_bytes,
+                           double* avg_ms, SpmvLaunch fn) {
   LSPCG_CHECK(ctx && A && reps > 0 && avg_ms && flush_bytes >= 0, LSPCG_ERR_ARG, "spmv_timed: bad argument");
   hipEvent_t e0, e1;
   LSPCG_HIP(hipEventCreate(&e0));
   LSPCG_HIP(hipEventCreate(&e1));
   void* flush = nullptr;
-  if (flush_bytes > 0) LSPCG_HIP(hipMalloc(&flush, size_t(flush_bytes)));
+  if (flush_bytes > 0) {
+    LSPCG_HIP(hipMalloc(&flush, size_t(flush_bytes) + 64));
+    LSPCG_HIP(hipMemsetAsync(flush, 1, size_t(flush_bytes) + 64, ctx->stream));
+  }
+  auto launch = [&]() -> int {
+    if (fn) {
+      fn(A, x, y, ctx->stream);
+      LSPCG_HIP(hipGetLastError());
+      return LSPCG_OK;
+    }
+    return lspcg_spmv(ctx, A, x, y);
+  };
   double total = 0.0;
   if (!flush) {
+    if (int rc = launch()) return rc;  // untimed first launch
     LSPCG_HIP(hipEventRecord(e0, ctx->stream));
-    for (int i = 0; i < reps; ++i) {
-      int rc = lspcg_spmv(ctx, A, x, y);
-      if (rc) return rc;
-    }
+    for (int i = 0; i < reps; ++i)
+      if (int rc = launch()) return rc;
     LSPCG_HIP(hipEventRecord(e1, ctx->stream));
     LSPCG_HIP(hipEventSynchronize(e1));
     float ms = 0.f;
     LSPCG_HIP(hipEventElapsedTime(&ms, e0, e1));
     total = ms;
   } else {
-    // cold: overwrite an Infinity-Cache-sized buffer between launches, time each launch alone
+    // cold: read an Infinity-Cache-sized buffer between launches, time each launch alone
     for (int i = 0; i < reps; ++i) {
-      LSPCG_HIP(hipMemsetAsync(flush, i & 0xff, size_t(flush_bytes), ctx->stream));
+      hipLaunchKernelGGL(k_flush_read, dim3(4096), dim3(kThreads), 0, ctx->stream, static_cast<const u32x4*>(flush),
+                         flush_bytes / 16, reinterpret_cast<unsigned*>(static_cast<char*>(flush) + flush_bytes));
       LSPCG_HIP(hipEventRecord(e0, ctx->stream));
-      int rc = lspcg_spmv(ctx, A, x, y);
-      if (rc) return rc;
+      if (int rc = launch()) return rc;
       LSPCG_HIP(hipEventRecord(e1, ctx->stream));
       LSPCG_HIP(hipEventSynchronize(e1));
       float ms = 0.f;
@@ -389,6 +437,19 @@ int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y,
   (void)hipEventDestroy(e1);
   *avg_ms = total / reps;
   return LSPCG_OK;
+}
+
+int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y, int reps, int64_t flush_bytes,
+                     double* avg_ms) {
+  return spmv_timed_impl(ctx, A, x, y, reps, flush_bytes, avg_ms, nullptr);
+}
+
+int lspcg_spmv_variant_timed(lspcg_ctx* ctx, const lspcg_mat* A, int variant, const void* x, void* y, int reps,
+                             int64_t flush_bytes, double* avg_ms) {
+  if (variant < 0) return kNumSpmvVariants;
+  LSPCG_CHECK(A && variant < kNumSpmvVariants && A->dtype == LSPCG_F64 && A->block_size == 1, LSPCG_ERR_ARG,
+              "spmv_variant_timed: fp64 scalar CSR and a valid variant id required");
+  return spmv_timed_impl(ctx, A, x, y, reps, flush_bytes, avg_ms, kSpmvVariants[variant]);
 }
 
 int lspcg_dot(lspcg_ctx* ctx, int64_t n, int dtype, const void* x, const void* y, double* out) {

@@ -45,8 +45,8 @@ void set_error(const std::string& msg);
 // Launch geometry
 // ---------------------------------------------------------------------------
 constexpr int kThreads = 256;       // 4 wave64 per workgroup
-constexpr int kSpmvCap = 4096;      // staged scalar entries per chunk (fp64: 32 KiB LDS)
 constexpr int kElemBlocksMax = 2048;  // grid cap for streaming elementwise kernels
+constexpr int kEntryPad = 16;       // zeroed padding entries after colind / vals (branch-free SpMV loads)
 
 // ---------------------------------------------------------------------------
 // Compensated (double-double) accumulation
@@ -86,7 +86,7 @@ __device__ __forceinline__ DD dd_shfl_xor(DD a, int m) {
 
 // Fixed-order workgroup reduction of N DD values; the result is valid in thread 0.
 template <int N>
-__device__ __forceinline__ void block_reduce_dd(DD (&v)[N], DD* lds /* >= 4*N */) {
+__device__ __forceinline__ void block_reduce_dd(DD (&v)[N], DD* lds /* >= waves*N */) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
 #pragma unroll
@@ -131,7 +131,7 @@ __device__ __forceinline__ double ld_agent_f64(const double* p) {
 // partials in block-index order and calls fin(values) on thread 0.
 template <int N, class Fin>
 __device__ __forceinline__ void grid_reduce_dd(DD (&v)[N], double* partials, unsigned* ticket, Fin fin) {
-  __shared__ DD lds[4 * N];
+  __shared__ DD lds[16 * N];  // up to 16 waves (1024 threads)
   __shared__ int s_last;
   block_reduce_dd<N>(v, lds);
   if (threadIdx.x == 0) {
@@ -172,6 +172,12 @@ __device__ __forceinline__ double round_to(double v) {
   return static_cast<double>(static_cast<T>(v));
 }
 
+}  // namespace lspcg
+
+struct lspcg_mat;
+namespace lspcg {
+// (Re)allocate m->colind / m->vals for nnzb stored blocks with zeroed kEntryPad padding.
+int mat_alloc_entries(lspcg_mat* m, int64_t nnzb);
 }  // namespace lspcg
 
 // ---------------------------------------------------------------------------

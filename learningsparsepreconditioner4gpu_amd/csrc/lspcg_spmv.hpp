@@ -27,17 +27,8 @@ struct SpmvArgs {
   const T* x;             // gathered vector
 };
 
-template <int BS>
-__host__ __device__ constexpr int spmv_rows_per_block() { return kThreads / BS; }
-
-template <typename T, int BS>
-__host__ __device__ constexpr int spmv_cap() {
-  // fp32 entries are half the size: stage twice as many per chunk (same 32 KiB LDS).
-  return ((kSpmvCap * (sizeof(T) == 4 ? 2 : 1)) / (BS * BS)) * (BS * BS);
-}
-
-inline int64_t spmv_grid(int64_t nb, int bs) {
-  const int rb = kThreads / bs;
+inline int64_t spmv_grid(int64_t nb, int bs) {  // grid of the production configuration (<= n/255 + 1)
+  const int rb = 256 / bs;
   return (nb + rb - 1) / rb;
 }
 
@@ -57,14 +48,54 @@ struct EpiStore {
   unsigned* ticket = nullptr;
 };
 
-template <typename T, int BS, class Pro, class Epi>
-__global__ void __launch_bounds__(kThreads) k_spmv(SpmvArgs<T, BS> a, Pro pro, Epi epi) {
+// Entries are loaded in groups of 4 consecutive scalar entries (16-B column-index loads,
+// 2x16-B fp64 value loads) with NO per-element predicate: group indices are clamped to the
+// chunk, and the index/value arrays carry kEntryPad padding entries (column 0, value 0),
+// so every load is in bounds and the compiler issues all of them before the first wait.
+using i32x4 = int __attribute__((ext_vector_type(4)));
+using f64x2 = double __attribute__((ext_vector_type(2)));
+using f32x4 = float __attribute__((ext_vector_type(4)));
+
+template <typename T>
+struct Vec4;
+template <>
+struct Vec4<double> {
+  template <bool NT>
+  __device__ static __forceinline__ void load(const double* p, double (&v)[4]) {
+    const f64x2* q = reinterpret_cast<const f64x2*>(p);
+    const f64x2 a = NT ? __builtin_nontemporal_load(q) : q[0];
+    const f64x2 b = NT ? __builtin_nontemporal_load(q + 1) : q[1];
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+  }
+  __device__ static __forceinline__ void store(double* p, const double (&v)[4]) {
+    reinterpret_cast<double2*>(p)[0] = make_double2(v[0], v[1]);
+    reinterpret_cast<double2*>(p)[1] = make_double2(v[2], v[3]);
+  }
+};
+template <>
+struct Vec4<float> {
+  template <bool NT>
+  __device__ static __forceinline__ void load(const float* p, float (&v)[4]) {
+    const f32x4* q = reinterpret_cast<const f32x4*>(p);
+    const f32x4 a = NT ? __builtin_nontemporal_load(q) : q[0];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+  __device__ static __forceinline__ void store(float* p, const float (&v)[4]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+
+// THREADS = workgroup size (one scalar row per thread), GPT = groups of 4 entries each
+// thread stages per chunk (chunk = THREADS*GPT*4 entries), NT = non-temporal matrix loads.
+template <typename T, int BS, int THREADS, int GPT, bool NT, class Pro, class Epi>
+__global__ void __launch_bounds__(THREADS) k_spmv(SpmvArgs<T, BS> a, Pro pro, Epi epi) {
   constexpr int BB = BS * BS;
-  constexpr int CAP = spmv_cap<T, BS>();
-  constexpr int RB = spmv_rows_per_block<BS>();
-  constexpr int PER = (CAP + kThreads - 1) / kThreads;
+  constexpr int CAPG = THREADS * GPT;             // groups of 4 entries per chunk
+  constexpr int RB = THREADS / BS;                // block rows per workgroup
+  constexpr int PERG = GPT;
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
-  __shared__ T prod[CAP];
+  constexpr int kThreads = THREADS;
+  __shared__ __attribute__((aligned(16))) T prod[CAPG * 4];
 
   if (pro.exit()) return;
 
@@ -78,51 +109,78 @@ __global__ void __launch_bounds__(kThreads) k_spmv(SpmvArgs<T, BS> a, Pro pro, E
   const int comp = tid % BS;
   int64_t kb_beg = 0, kb_end = 0;
   if (active) {
-    kb_beg = a.rowptr[I];
-    kb_end = a.rowptr[I + 1];
+    kb_beg = int64_t(a.rowptr[I]) * BB;   // scalar-entry range of this thread's block row
+    kb_end = int64_t(a.rowptr[I + 1]) * BB;
   }
   T acc = T(0);
+  const int64_t G0 = e0 >> 2;
+  const int64_t G1 = (e1 + 3) >> 2;
 
-  for (int64_t c0 = e0; c0 < e1; c0 += CAP) {
-    const int64_t c1 = c0 + CAP < e1 ? c0 + CAP : e1;
-    // ---- stage: coalesced value/index loads, x gather, products -> LDS
-    int cidx[PER];
-    T v[PER];
+  for (int64_t gs = G0; gs < G1; gs += CAPG) {
+    const int64_t ge = gs + CAPG < G1 ? gs + CAPG : G1;
+    // ---- stage: branch-free 16-B loads, x gather, products -> LDS
+    int cidx[PERG][4];
+    T v[PERG][4];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int64_t k = c0 + tid + int64_t(u) * kThreads;
-      if (k < c1) {
-        if constexpr (BS == 1) {
-          cidx[u] = a.colind[k];
-        } else {
+    for (int u = 0; u < PERG; ++u) {
+      int64_t g = gs + tid + int64_t(u) * kThreads;
+      g = g < ge ? g : ge - 1;
+      Vec4<T>::template load<NT>(a.vals + 4 * g, v[u]);
+      if constexpr (BS == 1) {
+        const i32x4 c = NT ? __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(a.colind) + g)
+                           : reinterpret_cast<const i32x4*>(a.colind)[g];
+        cidx[u][0] = c.x; cidx[u][1] = c.y; cidx[u][2] = c.z; cidx[u][3] = c.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t k = 4 * g + j;
           const int64_t kb = k / BB;
           const int w = int(k - kb * BB);
-          cidx[u] = a.colind[kb] * BS + (w % BS);
+          cidx[u][j] = a.colind[kb] * BS + (w % BS);
         }
-        v[u] = a.vals[k];
       }
     }
-    T xv[PER];
+    T xv[PERG][4];
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int64_t k = c0 + tid + int64_t(u) * kThreads;
-      if (k < c1) xv[u] = a.x[cidx[u]];
-    }
+    for (int u = 0; u < PERG; ++u)
 #pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int64_t k = c0 + tid + int64_t(u) * kThreads;
-      if (k < c1) prod[k - c0] = v[u] * xv[u];
+      for (int j = 0; j < 4; ++j) xv[u][j] = a.x[cidx[u][j]];
+#pragma unroll
+    for (int u = 0; u < PERG; ++u) {
+      int64_t g = gs + tid + int64_t(u) * kThreads;
+      g = g < ge ? g : ge - 1;
+      T pr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pr[j] = v[u][j] * xv[u][j];
+      Vec4<T>::store(prod + 4 * (g - gs), pr);
     }
     __syncthreads();
     // ---- per-row sequential accumulation (scipy order)
     if (active) {
-      const int64_t lo = c0 / BB, hi = c1 / BB;
-      const int64_t kbs = kb_beg > lo ? kb_beg : lo;
-      const int64_t kbe = kb_end < hi ? kb_end : hi;
-      const T* pp = prod + (kbs - lo) * BB + comp * BS;
-      for (int64_t kb = kbs; kb < kbe; ++kb, pp += BB) {
+      const int64_t lo = 4 * gs, hi = 4 * ge;
+      const int64_t ks = kb_beg > lo ? kb_beg : lo;
+      const int64_t ke = kb_end < hi ? kb_end : hi;
+      if constexpr (BS == 1) {
+        // 4 LDS reads in flight per step (clamped in-bounds index), adds stay sequential
+        const T* pp = prod - lo;
+        int64_t k = ks;
+        for (; k + 4 <= ke; k += 4) {
+          const T p0 = pp[k], p1 = pp[k + 1], p2 = pp[k + 2], p3 = pp[k + 3];
+          acc = acc + p0;
+          acc = acc + p1;
+          acc = acc + p2;
+          acc = acc + p3;
+        }
+        for (; k < ke; ++k) acc = acc + pp[k];
+      } else {
+        // entries of scalar row (I, comp): k = kb*BB + comp*BS + c, blocks in order
+        for (int64_t kb = kb_beg; kb < kb_end; kb += BB) {
 #pragma unroll
-        for (int cc = 0; cc < BS; ++cc) acc = acc + pp[cc];
+          for (int c = 0; c < BS; ++c) {
+            const int64_t k = kb + comp * BS + c;
+            if (k >= ks && k < ke) acc = acc + prod[k - lo];
+          }
+        }
       }
     }
     __syncthreads();
@@ -137,11 +195,32 @@ __global__ void __launch_bounds__(kThreads) k_spmv(SpmvArgs<T, BS> a, Pro pro, E
   }
 }
 
+// Production configuration (tuned on MI355X, tools/spmv_probe.py): see DESIGN.md "SpMV".
+template <typename T>
+struct SpmvCfg {
+  static constexpr int THREADS = 256;
+  static constexpr int GPT = sizeof(T) == 8 ? 4 : 8;
+  static constexpr bool NT = false;
+};
+
+template <int THREADS, int BS>
+inline int64_t spmv_grid_t(int64_t nb) {
+  const int rb = THREADS / BS;
+  return (nb + rb - 1) / rb;
+}
+
+template <typename T, int BS, int THREADS, int GPT, bool NT, class Pro, class Epi>
+inline void launch_spmv_cfg(const lspcg_mat* A, const T* x, Pro pro, Epi epi, hipStream_t st) {
+  SpmvArgs<T, BS> a{A->nb, A->rowptr, A->colind, static_cast<const T*>(A->vals), x};
+  const int64_t grid = spmv_grid_t<THREADS, BS>(A->nb);
+  if (grid > 0)
+    hipLaunchKernelGGL((k_spmv<T, BS, THREADS, GPT, NT, Pro, Epi>), dim3(unsigned(grid)), dim3(THREADS), 0, st, a,
+                       pro, epi);
+}
+
 template <typename T, int BS, class Pro, class Epi>
 inline void launch_spmv(const lspcg_mat* A, const T* x, Pro pro, Epi epi, hipStream_t st) {
-  SpmvArgs<T, BS> a{A->nb, A->rowptr, A->colind, static_cast<const T*>(A->vals), x};
-  const int64_t grid = spmv_grid(A->nb, BS);
-  if (grid > 0) hipLaunchKernelGGL((k_spmv<T, BS, Pro, Epi>), dim3(unsigned(grid)), dim3(kThreads), 0, st, a, pro, epi);
+  launch_spmv_cfg<T, BS, SpmvCfg<T>::THREADS, SpmvCfg<T>::GPT, SpmvCfg<T>::NT>(A, x, pro, epi, st);
 }
 
 // Dispatch on the matrix block size.
