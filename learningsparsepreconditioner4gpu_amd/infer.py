@@ -1,0 +1,198 @@
+"""Inference driver: GNN -> SPAI -> PCG per sample, Timestat + CSVs (infer.py of the reference).
+
+Mirrors ``/root/reference/infer.py``: warm-up of the GNN (:270-275), per sample the
+preconditioner time averaged over ``repeat`` inference steps (:288-293), rhs = mask /
+random / neighbour (:297-307), the Neural PCG row (:322-331) and the two CSVs with the
+reference schema (:372-384: ``Key, Total Time (ms), Solve Time (ms), Precond Time (ms),
+#Iteration`` and the per-sample ``all_*`` file with ``Matrix Size``).  Differences: the
+PCG runs on the MI355X (key ``Neural+HIP``); the pymathprim baseline rows (:310-321) are
+not produced; ``Precond Time`` is the GNN time (the reference overwrites it with the last
+baseline's setup time).  Samples are sharded one-per-GPU under torchrun
+(``distributed.run_sharded``) with a single all-gather at the end.
+
+    python -m learningsparsepreconditioner4gpu_amd.infer --dataset heat_batch8 --rtol 1e-8
+    torchrun --nproc-per-node 8 -m learningsparsepreconditioner4gpu_amd.infer --dataset heat_batch8
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Dict, List, Sequence
+
+import numpy as np
+import torch
+
+from . import problems as P
+from .data import GraphSample, make_sample
+from .distributed import SolveRecord, run_sharded
+from .validate import get_pcg_iter_time, get_pcg_scaled_iter_time
+from .workspace import ScaledInferenceWorkspace, SimpleInferenceWorkspace
+
+
+@dataclass
+class InferenceTimestat:
+    all_solve_time: List[float] = field(default_factory=list)
+    all_prec_time: List[float] = field(default_factory=list)
+    all_iteration: List[float] = field(default_factory=list)
+    all_matrix_size: List[int] = field(default_factory=list)
+
+
+class Timestat:
+    """infer.py:38-151 (same keys, same CSV columns)."""
+
+    def __init__(self):
+        self.stat_dict: Dict[str, InferenceTimestat] = {}
+
+    def put(self, key: str, solve_time: float, prec_time: float, iteration: float, matrix_size: int):
+        s = self.stat_dict.setdefault(key, InferenceTimestat())
+        s.all_solve_time.append(solve_time)
+        s.all_prec_time.append(prec_time)
+        s.all_iteration.append(iteration)
+        s.all_matrix_size.append(matrix_size)
+
+    def timestat_to_dataframe(self):
+        import pandas as pd
+
+        rows = []
+        for key, st in self.stat_dict.items():
+            sol = np.mean(st.all_solve_time) * 1000
+            pre = np.mean(st.all_prec_time) * 1000
+            rows.append({"Key": key, "Total Time (ms)": sol + pre, "Solve Time (ms)": sol, "Precond Time (ms)": pre,
+                         "#Iteration": np.mean(st.all_iteration)})
+        df = pd.DataFrame(rows)
+        cols = ["Total Time (ms)", "Solve Time (ms)", "Precond Time (ms)", "#Iteration"]
+        if len(df):
+            df[cols] = df[cols].round(4)
+        return df
+
+    def all_time_stat(self):
+        import pandas as pd
+
+        rows = []
+        for key, st in self.stat_dict.items():
+            for s, p, i, m in zip(st.all_solve_time, st.all_prec_time, st.all_iteration, st.all_matrix_size):
+                rows.append({"Key": key, "Solve Time (ms)": s * 1000, "Precond Time (ms)": p * 1000, "#Iteration": i,
+                             "Matrix Size": m})
+        df = pd.DataFrame(rows)
+        cols = ["Solve Time (ms)", "Precond Time (ms)", "#Iteration", "Matrix Size"]
+        if len(df):
+            df[cols] = df[cols].round(4)
+        return df
+
+    def print(self):
+        for key, st in self.stat_dict.items():
+            print(f"{key}: solve {np.mean(st.all_solve_time) * 1e3:.2f} ms, precond "
+                  f"{np.mean(st.all_prec_time) * 1e3:.2f} ms, {np.mean(st.all_iteration):.4f} it/sample")
+
+
+def synthetic_dataset(name: str) -> List[GraphSample]:
+    """Stand-in datasets; the reference's generated/ folders are absent."""
+    if name == "heat_batch8":  # C5: 8 heat-tet systems, 400-32000 vertices, seeds 0-7
+        rng = np.random.default_rng(0)
+        out = []
+        for s in range(8):
+            nv = int(rng.integers(400, 32000))
+            k = max(4, int(round(nv ** (1 / 3))))
+            A, mask, feats = P.heat_tet(k, k, max(4, nv // (k * k)), rho=float(rng.uniform(1e-4, 5e-4)), seed=s)
+            out.append(make_sample(A, mask, node_features=feats))
+        return out
+    if name.startswith("poisson"):
+        A, mask, _ = P.poisson2d_grid(256, 256)
+        return [make_sample(A, mask)]
+    if name.startswith("synthetic"):
+        return [make_sample(P.synthetic_c1(), None, use_edge_features_as_node_feature="mean")]
+    if name.startswith("kuhn"):
+        A, mask = P.kuhn_dirichlet(int(name[4:] or 101))
+        return [make_sample(A, mask)]
+    raise KeyError(name)
+
+
+def rhs_for(rhs: str, mask: np.ndarray, A_full_rowsum=None) -> np.ndarray:
+    m = mask.reshape(-1).astype(np.float64)
+    if rhs in ("mask", "ones"):
+        return m
+    if rhs == "random":
+        return np.random.randn(m.size) * m
+    raise ValueError(f"Unknown rhs type: {rhs}")
+
+
+def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: float = 1e-6, repeat: int = 1,
+        rhs: str = "mask", warmup: int = 20) -> List[SolveRecord]:
+    pcg = get_pcg_scaled_iter_time if isinstance(ws, ScaledInferenceWorkspace) else get_pcg_iter_time
+    dev = torch.device("cuda", torch.cuda.current_device())
+    warmed = set()
+
+    def solve(i: int) -> SolveRecord:
+        s = samples[i].to(dev)
+        if not warmed:
+            for _ in range(warmup):
+                ws.inference_step(s)
+            warmed.add(True)
+        prec = 0.0
+        for _ in range(repeat):
+            _, dt = ws.inference_step(s)
+            prec += dt
+        prec /= repeat
+        L, _ = ws.inference_step(s)
+        A = ws.system_matrix(s)
+        r = rhs_for(rhs, s.mask.cpu().numpy())
+        it, _, sol = pcg(A, r, L, ws.epsilon, rtol=rtol, repeat=repeat)
+        return SolveRecord(index=i, iters=it, rel_res=float("nan"), t_prec=prec, t_solve=sol, n=A.n, nnz=A.nnz,
+                           converged=it < A.n)
+
+    weights = [float(s.edge_index.shape[1]) for s in samples]
+    return run_sharded(len(samples), weights, solve)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dataset", default="heat_batch8")
+    ap.add_argument("--exp-name", default=None)
+    ap.add_argument("--rtol", type=float, default=1e-6)
+    ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--rhs", default="mask")
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workspace", default="simple", choices=["simple", "scaled"])
+    ap.add_argument("--pretrained", default="")
+    ap.add_argument("--epsilon", type=float, default=3e-3)
+    ap.add_argument("--out-dir", default="output")
+    ap.add_argument("--infer-prefix", default="")
+    args = ap.parse_args(argv)
+
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    samples = synthetic_dataset(args.dataset)
+    cls = ScaledInferenceWorkspace if args.workspace == "scaled" else SimpleInferenceWorkspace
+    if args.pretrained:
+        ws = cls.load_from_checkpoint(args.pretrained)
+    else:
+        s0 = samples[0]
+        ws = cls(node_features=s0.x.shape[1], edge_features=s0.edge_attr.shape[1], block_size=s0.block_size,
+                 epsilon=args.epsilon, seed=0)
+    recs = run(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, warmup=args.warmup)
+    if not dist.is_initialized() or dist.get_rank() == 0:
+        stats = Timestat()
+        for r in recs:
+            stats.put("Neural+HIP", r.t_solve, r.t_prec, r.iters, r.n)
+        stats.print()
+        out = Path(args.out_dir)
+        out.mkdir(parents=True, exist_ok=True)
+        exp = args.exp_name or args.dataset
+        log_rtol = -int(math.log10(args.rtol))
+        stats.timestat_to_dataframe().to_csv(out / f"infer_{args.infer_prefix}{exp}_{log_rtol}.csv", index=False)
+        stats.all_time_stat().to_csv(out / f"all_infer_{args.infer_prefix}{exp}_{log_rtol}.csv", index=False)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return recs
+
+
+if __name__ == "__main__":
+    main()

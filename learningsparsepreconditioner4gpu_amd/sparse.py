@@ -49,6 +49,8 @@ class Context:
 
     @classmethod
     def get(cls, device: Optional[Union[int, torch.device, str]] = None) -> "Context":
+        if not torch.cuda.is_available():
+            raise _lib.LspcgUnavailable("no ROCm GPU visible: the lspcg HIP path needs an MI355X (gfx950)")
         if device is None:
             dev = torch.cuda.current_device()
         elif isinstance(device, (torch.device, str)):

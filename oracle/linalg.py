@@ -115,7 +115,26 @@ def exact_dot(a: np.ndarray, b: np.ndarray) -> float:
     return math.fsum(np.concatenate([p, e]))
 
 
-DOTS = {"numpy": np.dot, "exact": exact_dot}
+def pairwise_dot(a: np.ndarray, b: np.ndarray) -> float:
+    """numpy pairwise summation of the products (a different, equally valid rounding order)."""
+    return float(np.sum(np.asarray(a) * np.asarray(b)))
+
+
+def reversed_dot(a: np.ndarray, b: np.ndarray) -> float:
+    return float(np.dot(np.asarray(a)[::-1].copy(), np.asarray(b)[::-1].copy()))
+
+
+DOTS = {"numpy": np.dot, "exact": exact_dot, "pairwise": pairwise_dot, "reversed": reversed_dot}
+
+
+def count_spread(A, b, psolve, rtol, max_iter=0, dtype=np.float64):
+    """Iteration counts of the scipy-ordered PCG under every admissible dot ordering in DOTS.
+
+    On ill-conditioned systems CG's count depends on rounding (e.g. the synthetic κ≈1e10
+    matrices): the reference itself changes count with the BLAS thread count.  Returns
+    (min, max) over the orderings -- the band a faithful implementation must land in."""
+    its = [pcg(A, b, psolve, rtol=rtol, max_iter=max_iter, dot=d, dtype=dtype)[0] for d in DOTS]
+    return min(its), max(its)
 
 
 # ---------------------------------------------------------------------------
@@ -135,7 +154,7 @@ def pcg(A: csr_matrix, b: np.ndarray, psolve: Optional[Callable] = None, rtol: f
     b = np.asarray(b, dtype=dtype)
     n = b.shape[0]
     max_iter = max_iter if max_iter > 0 else n
-    bnrm2 = math.sqrt(d(b, b)) if dot == "exact" else np.linalg.norm(b)
+    bnrm2 = math.sqrt(d(b, b)) if dot != "numpy" else np.linalg.norm(b)
     atol = max(0.0, float(rtol) * float(bnrm2))
     x = np.zeros_like(b) if x0 is None else np.array(x0, dtype=dtype)
     hist = []
@@ -144,7 +163,7 @@ def pcg(A: csr_matrix, b: np.ndarray, psolve: Optional[Callable] = None, rtol: f
     r = b - A @ x if x.any() else b.copy()
     rho_prev, p = None, None
     for iteration in range(max_iter):
-        rn = math.sqrt(d(r, r)) if dot == "exact" else np.linalg.norm(r)
+        rn = math.sqrt(d(r, r)) if dot != "numpy" else np.linalg.norm(r)
         hist.append(float(rn))
         if rn < atol:
             return iteration, x, hist
@@ -162,7 +181,7 @@ def pcg(A: csr_matrix, b: np.ndarray, psolve: Optional[Callable] = None, rtol: f
         x += alpha * p
         r -= alpha * q
         rho_prev = rho_cur
-    hist.append(float(math.sqrt(d(r, r)) if dot == "exact" else np.linalg.norm(r)))
+    hist.append(float(math.sqrt(d(r, r)) if dot != "numpy" else np.linalg.norm(r)))
     return max_iter, x, hist
 
 

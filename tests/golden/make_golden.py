@@ -1,0 +1,203 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
+
+Runs only in the development container, where /root/reference exists (never on the GPU
+box; the committed .npz files are what travels).  The reference targets Python 3.12 with
+loguru / torch_geometric / lightning, so a few import shims are installed first
+(SURVEY.md 8(c)): ``typing.override`` and stub modules for loguru and torch_geometric
+(placeholders only; the functions exercised here do not call into them, except that the
+GNN fixture constructs modules whose PyG base classes are parameter-holder stand-ins).
+
+Fixtures (inputs and the reference's outputs, data only):
+  to_csr.npz       -- neural_cg/utils/validate.py:22-51 to_csr_cpu on 4 masked/unmasked
+                      scalar and 3x3-block COO inputs
+  pcg_counts.npz   -- validate.py get_cg_iter_time_scipy / get_pcg_iter_time_scipy /
+                      get_pcg_diagonal_iter_time_scipy / get_pcg_scaled_iter_time_scipy
+                      iteration counts on small systems (A, L, gt stored)
+  synthetic.npz    -- datagen/synthetic.py generate_spd_sparse_matrix(512, 3e-3, 1e-5, RandomState(7))
+  gnn_init.npz     -- state_dict of neural_cg.nn.gnns.NodeEdgeProcessing (config/gnn.yaml)
+                      constructed after torch.manual_seed(0)
+  make_data.npz    -- neural_cg/data.py make_data outputs for one masked block matrix
+
+    python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import sys
+import types
+import typing
+from pathlib import Path
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+from torch import nn
+
+REF = Path("/root/reference")
+OUT = Path(__file__).resolve().parent
+ROOT = OUT.parents[1]
+
+
+def install_shims():
+    typing.override = lambda f: f
+    lg = types.ModuleType("loguru")
+
+    class _L:
+        def __getattr__(self, _):
+            return lambda *a, **k: None
+
+    lg.logger = _L()
+    sys.modules["loguru"] = lg
+    tg = types.ModuleType("torch_geometric")
+    tgd = types.ModuleType("torch_geometric.data")
+    tgu = types.ModuleType("torch_geometric.utils")
+    tgn = types.ModuleType("torch_geometric.nn")
+
+    class Data:
+        def __init__(self, **kw):
+            self.__dict__.update(kw)
+
+    class Dataset:
+        def __init__(self, *a, **k):
+            pass
+
+    class MessagePassing(nn.Module):  # construction-only stand-in (no propagate)
+        def __init__(self, aggr="add", flow="source_to_target", **kw):
+            super().__init__()
+
+    class MessageNorm(nn.Module):  # parameter holder with PyG's state (scale = 1)
+        def __init__(self, learn_scale=False):
+            super().__init__()
+            self.scale = nn.Parameter(torch.empty(1), requires_grad=learn_scale)
+            self.reset_parameters()
+
+        def reset_parameters(self):
+            self.scale.data.fill_(1.0)
+
+    tgd.Data, tgd.Dataset = Data, Dataset
+    for name in ("scatter", "coalesce", "remove_self_loops", "to_torch_coo_tensor", "to_edge_index"):
+        setattr(tgu, name, None)
+    tgn.MessagePassing, tgn.MessageNorm = MessagePassing, MessageNorm
+    sys.modules.update({"torch_geometric": tg, "torch_geometric.data": tgd, "torch_geometric.utils": tgu,
+                        "torch_geometric.nn": tgn})
+    sys.path.insert(0, str(REF))
+
+
+def reference_synthetic():
+    """datagen/synthetic.py:10-27 executed from the reference's source file."""
+    src = (REF / "datagen" / "synthetic.py").read_text()
+    body = src.split("class SyntheticDatagen")[0]
+    body = "\n".join(l for l in body.splitlines() if not l.startswith(("from typing", "import hydra",
+                                                                         "from neural_cg")))
+    ns = {}
+    exec(compile(body, str(REF / "datagen" / "synthetic.py"), "exec"), ns)
+    return ns["generate_spd_sparse_matrix"]
+
+
+def main():
+    install_shims()
+    from neural_cg import data as rdata
+    from neural_cg.nn import gnns as rgnn
+    from neural_cg.utils import validate as rval
+
+    sys.path.insert(0, str(ROOT))
+    from learningsparsepreconditioner4gpu_amd import problems as P
+
+    rng = np.random.default_rng(2024)
+    # ---------------- to_csr_cpu
+    cases = {}
+    A, mask, _ = P.poisson2d_grid(9, 7)
+    g = P.to_block_graph(A, 1)
+    cases["poisson_masked_f32in"] = (g.edge_index, g.block_values.astype(np.float32), A.shape[0], mask)
+    cases["poisson_nomask"] = (g.edge_index, g.block_values, A.shape[0], None)
+    Ae, me, _ = P.elasticity_box(4, 3, 3)
+    ge = P.to_block_graph(Ae, 3)
+    vals = ge.block_values.copy()
+    vals[rng.random(vals.shape) < 0.1] = 0.0
+    cases["elast_b3_masked"] = (ge.edge_index, vals.astype(np.float32), Ae.shape[0], me)
+    K = P.kuhn_laplacian(4)
+    K = sp.csr_matrix(K - sp.diags(K.diagonal()))
+    K.eliminate_zeros()
+    gk = P.to_block_graph(K, 1)
+    mk = (rng.random((K.shape[0], 1)) > 0.3).astype(np.float64)
+    cases["kuhn_nodiag_masked"] = (gk.edge_index, gk.block_values, K.shape[0], mk)
+    out = {}
+    for name, (ei, ea, n, m) in cases.items():
+        csr = rval.to_csr_cpu(torch.from_numpy(ei), torch.from_numpy(ea), n,
+                              None if m is None else torch.from_numpy(m), dtype=np.float64)
+        out[f"{name}__edge_index"] = ei
+        out[f"{name}__edge_attr"] = ea
+        out[f"{name}__n"] = np.array(n)
+        out[f"{name}__mask"] = np.zeros(0) if m is None else m
+        out[f"{name}__indptr"] = csr.indptr
+        out[f"{name}__indices"] = csr.indices
+        out[f"{name}__data"] = csr.data
+    np.savez_compressed(OUT / "to_csr.npz", **out)
+
+    # ---------------- synthetic generator
+    gen = reference_synthetic()
+    S = sp.csr_matrix(gen(512, 3e-3, 1e-5, np.random.RandomState(7)))
+    S.sort_indices()
+    np.savez_compressed(OUT / "synthetic.npz", indptr=S.indptr, indices=S.indices, data=S.data, n=512,
+                        sparsity=3e-3, amp=1e-5, seed=7)
+
+    # ---------------- PCG iteration counts (scipy restatements in validate.py)
+    pc = {}
+    systems = {
+        "synthetic600": (sp.csr_matrix(gen(600, 8e-3, 1e-3, np.random.RandomState(11))), None),
+        "poisson16": P.poisson2d_grid(16, 16)[:2],
+        "kuhn7": (P.kuhn_laplacian(7), None),
+    }
+    for name, (A, mask) in systems.items():
+        A = sp.csr_matrix(A)
+        A.sort_indices()
+        n = A.shape[0]
+        gt = np.ones(n) if mask is None else mask.ravel().astype(np.float64)
+        Lr = np.random.default_rng(5)
+        L = A.copy()
+        rows = np.repeat(np.arange(n), np.diff(A.indptr))
+        d = np.abs(A.diagonal()) + 1e-12
+        L.data = Lr.normal(size=A.nnz) * 0.05 / np.sqrt(d[rows])
+        dg = rows == A.indices
+        L.data[dg] = 1.0 / np.sqrt(d[rows[dg]])
+        eps = 3e-3
+        pc[f"{name}__indptr"], pc[f"{name}__indices"], pc[f"{name}__data"] = A.indptr, A.indices, A.data
+        pc[f"{name}__L_data"] = L.data
+        pc[f"{name}__gt"] = gt
+        pc[f"{name}__eps"] = np.array(eps)
+        for rtol in (1e-6, 1e-8):
+            tag = f"{name}__rtol{int(-np.log10(rtol))}"
+            pc[f"{tag}__none"] = np.array(rval.get_cg_iter_time_scipy(A, gt, rtol=rtol))
+            pc[f"{tag}__diagonal"] = np.array(rval.get_pcg_diagonal_iter_time_scipy(A, gt, rtol=rtol))
+            pc[f"{tag}__ext_spai"] = np.array(rval.get_pcg_iter_time_scipy(A, gt, L, eps, rtol=rtol))
+            pc[f"{tag}__ext_spai_scaled"] = np.array(rval.get_pcg_scaled_iter_time_scipy(A, gt, L, eps, rtol=rtol))
+    np.savez_compressed(OUT / "pcg_counts.npz", **pc)
+
+    # ---------------- GNN construction / seeded init (config/gnn.yaml)
+    ff = lambda norm: {"pre_norm": norm, "hidden_channels": 16, "num_layers": 2}
+    cfg = dict(node_encoder=ff("none"), edge_encoder=ff("none"), node_decoder=ff("none"), edge_decoder=ff("none"),
+               num_mp_layers=4, node_residual=True, edge_residual=True, node_features=16, edge_features=16,
+               node_mlp=ff("layer"), edge_mlp=ff("layer"), msg_mlp=ff("layer"), msg_norm=True, aggr="add")
+    torch.manual_seed(0)
+    net = rgnn.NodeEdgeProcessing(node_in_features=4, node_out_features=None, edge_in_features=9,
+                                  edge_out_features=9, **cfg)
+    np.savez_compressed(OUT / "gnn_init.npz", **{k: v.detach().numpy() for k, v in net.state_dict().items()})
+
+    # ---------------- make_data (data.py:218-336), 'disable' edge->node aggregation
+    Ab, mb, nodes = P.elasticity_box(4, 3, 3)
+    gb = P.to_block_graph(Ab, 3)
+    raw = rdata.RawData(block_values=gb.block_values, diagonals=Ab.diagonal().reshape(-1, 3),
+                        edge_index=gb.edge_index, node_features=nodes, lhs=None, rhs=None, mask=mb,
+                        num_nodes=gb.num_nodes, block_size=3)
+    dd = rdata.make_data(raw, use_matrix_as_edge_feature=True, use_mask_as_node_feature=True,
+                         use_node_features_as_edge_feature=False, use_edge_features_as_node_feature="disable",
+                         use_random_rhs=True, normalize_matrix="mean", is_inference=True)
+    np.savez_compressed(OUT / "make_data.npz", A_indptr=Ab.indptr, A_indices=Ab.indices, A_data=Ab.data, mask=mb,
+                        nodes=nodes, x=dd.x.numpy(), edge_index=dd.edge_index.numpy(), edge_attr=dd.edge_attr.numpy(),
+                        matrix_values=dd.matrix_values.numpy(), rsqrt_diag=dd.rsqrt_diag.numpy(),
+                        inv_diag=dd.inv_diag.numpy(), mask_out=dd.mask.numpy())
+    for f in sorted(OUT.glob("*.npz")):
+        print(f.name, f.stat().st_size)
+
+
+if __name__ == "__main__":
+    main()

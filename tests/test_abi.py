@@ -1,0 +1,60 @@
+"""CPU: the C-ABI library loads and exports exactly the entry points include/lspcg.h declares
+(no compute calls -- there is no GPU here)."""
+import re
+import subprocess
+
+import pytest
+
+from tests.conftest import ROOT
+
+
+def _header_functions():
+    txt = (ROOT / "include" / "lspcg.h").read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return set(re.findall(r"\b(lspcg_[a-z0-9_]+)\s*\(", txt))
+
+
+def test_header_matches_binding_table():
+    from learningsparsepreconditioner4gpu_amd import _lib
+
+    assert _header_functions() == set(_lib.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    from learningsparsepreconditioner4gpu_amd import _lib
+
+    lib_path = _lib.LIB_PATH
+    if not lib_path.exists():
+        pytest.fail(f"{lib_path} not built (run __graft_entry__.build())")
+    out = subprocess.run(["nm", "-D", "--defined-only", str(lib_path)], capture_output=True, text=True, check=True)
+    exported = set(re.findall(r"\bT (lspcg_[a-z0-9_]+)$", out.stdout, flags=re.M))
+    missing = _header_functions() - exported
+    assert not missing, missing
+    lib = _lib.load()  # resolves and types every symbol via ctypes
+    assert lib.lspcg_version() >= 10000
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from learningsparsepreconditioner4gpu_amd import _lib
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+    from learningsparsepreconditioner4gpu_amd import problems as P
+
+    A = P.kuhn_laplacian(3)
+    with pytest.raises(_lib.LspcgUnavailable):
+        PreconditionedConjugateGradient(A, device="cuda", preconditioner="none")
+    with pytest.raises(ValueError, match="MI355X only"):
+        PreconditionedConjugateGradient(A, device="cpu", preconditioner="none")
+    with pytest.raises(NotImplementedError):
+        PreconditionedConjugateGradient(A, device="cuda", preconditioner="ic")
+
+
+def test_product_never_imports_oracle():
+    """The product package must not import the CPU oracle (it is test infrastructure)."""
+    pkg = ROOT / "learningsparsepreconditioner4gpu_amd"
+    for f in pkg.rglob("*.py"):
+        src = f.read_text()
+        assert not re.search(r"^\s*(from|import)\s+oracle\b", src, flags=re.M), f

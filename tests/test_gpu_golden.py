@@ -1,0 +1,74 @@
+"""GPU vs the reference's own outputs (tests/golden, produced by tests/golden/make_golden.py):
+device to_csr_cpu bit-exact, PCG iteration counts exact (well-conditioned) / inside the
+rounding band (ill-conditioned synthetic), for every preconditioner and both tolerances."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from oracle import linalg as O
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+WELL_CONDITIONED = ("poisson16", "kuhn7")
+
+
+def _load(name):
+    return np.load(GOLDEN / name, allow_pickle=False)
+
+
+def test_device_to_csr_matches_reference(gpu_ctx):
+    from learningsparsepreconditioner4gpu_amd.validate import to_csr_cpu
+
+    z = _load("to_csr.npz")
+    for c in sorted({k.split("__")[0] for k in z.files}):
+        m = z[f"{c}__mask"]
+        got = to_csr_cpu(torch.from_numpy(z[f"{c}__edge_index"]), torch.from_numpy(z[f"{c}__edge_attr"]),
+                         int(z[f"{c}__n"]), None if m.size == 0 else torch.from_numpy(m))
+        assert np.array_equal(got.indptr, z[f"{c}__indptr"]), c
+        assert np.array_equal(got.indices, z[f"{c}__indices"]), c
+        assert np.array_equal(got.data, z[f"{c}__data"]), c
+
+
+@pytest.mark.parametrize("method", ["none", "diagonal", "ext_spai", "ext_spai_scaled"])
+def test_pcg_counts_match_reference(gpu_ctx, method):
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    z = _load("pcg_counts.npz")
+    for name in sorted({k.split("__")[0] for k in z.files}):
+        ip, ix, d = z[f"{name}__indptr"], z[f"{name}__indices"], z[f"{name}__data"]
+        n = ip.size - 1
+        A = sp.csr_matrix((d, ix, ip), shape=(n, n))
+        L = sp.csr_matrix((z[f"{name}__L_data"], ix, ip), shape=(n, n))
+        gt, eps = z[f"{name}__gt"], float(z[f"{name}__eps"])
+        b = A @ gt
+        for rtol in (6, 8):
+            want = int(z[f"{name}__rtol{rtol}__{method}"])
+            s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=method)
+            x = np.zeros(n)
+            it, _, _ = s(b, x, 10.0 ** -rtol, 0, ext_spai=(L, eps) if method.startswith("ext") else None)
+            if name in WELL_CONDITIONED:
+                assert it == want, (name, rtol, method, it, want)
+            else:
+                ps = {"none": None, "diagonal": O.diagonal_operator(A), "ext_spai": O.spai_operator(L, eps),
+                      "ext_spai_scaled": O.spai_scaled_operator(A, L, eps)}[method]
+                lo, hi = O.count_spread(A, b, ps, 10.0 ** -rtol)
+                assert lo <= it <= hi, (name, rtol, method, lo, it, hi, want)
+
+
+def test_infer_driver_end_to_end(gpu_ctx, tmp_path):
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+    from learningsparsepreconditioner4gpu_amd.infer import Timestat, run
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    samples = [make_sample(*P.poisson2d_grid(20 + 3 * i, 17)[:2]) for i in range(3)]
+    ws = SimpleInferenceWorkspace(node_features=1, edge_features=1, seed=0)
+    recs = run(samples, ws, rtol=1e-8, warmup=1)
+    assert [r.index for r in recs] == [0, 1, 2]
+    st = Timestat()
+    for r in recs:
+        assert r.iters > 0 and r.converged
+        st.put("Neural+HIP", r.t_solve, r.t_prec, r.iters, r.n)
+    df = st.timestat_to_dataframe()
+    assert list(df.columns) == ["Key", "Total Time (ms)", "Solve Time (ms)", "Precond Time (ms)", "#Iteration"]

@@ -1,0 +1,87 @@
+"""CPU: host-side logic -- generators, byte models, weight packing, sample building."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from learningsparsepreconditioner4gpu_amd import problems as P
+
+
+def test_kuhn_roofline_target_sizes():
+    # 101^3 -> N = 1,030,301, nnz = 15,210,901 (formula check at small n)
+    for n in (3, 5, 8):
+        A = P.kuhn_laplacian(n)
+        m = n - 1
+        want = n ** 3 + 2 * (3 * m * n * n + 3 * m * m * n + m ** 3)
+        assert A.nnz == want
+        assert (A != A.T).nnz == 0
+        assert np.all(np.linalg.eigvalsh(A.toarray()) > 0)
+
+
+def test_elasticity_is_spd_block3():
+    A, mask, nodes = P.elasticity_box(5, 3, 3)
+    assert A.shape[0] == 3 * nodes.shape[0]
+    assert abs(A - A.T).max() < 1e-6 * abs(A).max()
+    assert mask.shape == (nodes.shape[0], 3) and (mask == 0).any()
+    ev = np.linalg.eigvalsh(A.toarray())
+    assert ev.min() > 0
+
+
+def test_poisson_masking_semantics():
+    A, mask, _ = P.poisson2d_grid(12, 10)
+    m = mask.ravel()
+    dead = np.where(m == 0)[0]
+    assert len(dead) > 0
+    for i in dead:
+        row = A.getrow(i)
+        assert row.nnz == 1 and row[0, i] == 1.0
+        assert A.getcol(i).nnz == 1
+
+
+def test_bench_byte_model():
+    import bench
+
+    n, nnz = 1030301, 15210901
+    assert bench.spmv_bytes(n, nnz) == 12 * nnz + 20 * n + 4 == 203136836
+    assert bench.pcg_bytes_per_iter(n, nnz, nnz) == 3 * 203136836 + 80 * n
+
+
+def test_pack_weights_layout():
+    from learningsparsepreconditioner4gpu_amd.nn import build_gnn
+
+    H = 16
+    ff = lambda i, o: H * i + H + H * H + H + o * H + o
+    for node_in, edge_in, bs in [(2, 1, 1), (4, 1, 1), (9, 9, 3)]:
+        g = build_gnn(node_in, edge_in, bs, seed=0)
+        blob = g.pack_weights()
+        want = ff(node_in, H) + ff(edge_in, H) + 4 * ((2 * H + ff(H, H)) + 2 * (6 * H + ff(3 * H, H))) \
+            + ff(3 * H, bs * bs)
+        assert blob.numel() == want and blob.dtype == torch.float32
+        # first block = node encoder lift weight, row-major [16, node_in]
+        assert torch.equal(blob[: H * node_in], g.node_enc.lift[0].weight.detach().reshape(-1))
+
+
+def test_make_sample_edge_mean_feature():
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+
+    A = P.generate_spd_sparse_matrix(300, 2e-2, 1e-3, np.random.RandomState(0))
+    s = make_sample(A, None, use_edge_features_as_node_feature="mean")
+    assert s.x.shape == (300, 2)  # mask + mean edge feature (training/synthetic.sh)
+    ei = s.edge_index.numpy()
+    tgt = 17
+    sel = ei[1] == tgt
+    assert np.isclose(s.x[tgt, 1].item(), s.edge_attr.numpy()[sel, 0].astype(np.float64).mean(), rtol=1e-6)
+
+
+def test_timestat_csv_schema(tmp_path):
+    from learningsparsepreconditioner4gpu_amd.infer import Timestat
+
+    st = Timestat()
+    st.put("Neural+HIP", 0.010, 0.002, 113, 6276)
+    st.put("Neural+HIP", 0.020, 0.004, 115, 6300)
+    df = st.timestat_to_dataframe()
+    assert list(df.columns) == ["Key", "Total Time (ms)", "Solve Time (ms)", "Precond Time (ms)", "#Iteration"]
+    assert df.iloc[0]["Total Time (ms)"] == 18.0 and df.iloc[0]["#Iteration"] == 114.0
+    al = st.all_time_stat()
+    assert list(al.columns) == ["Key", "Solve Time (ms)", "Precond Time (ms)", "#Iteration", "Matrix Size"]
+    assert len(al) == 2
