@@ -143,9 +143,10 @@ inline void launch_transpose_fill(const lspcg_mat* A, lspcg_mat* Tm, int32_t* fi
 
 // ---- diagnostic SpMV configurations (fp64, scalar CSR) for on-device A/B tuning
 using SpmvLaunch = void (*)(const lspcg_mat*, const void*, void*, hipStream_t);
-template <int TH, int GPT, bool NT>
+template <int TH, int GPT, bool NT, bool LANEC = false, bool XCD = false>
 static void spmv_variant(const lspcg_mat* A, const void* x, void* y, hipStream_t st) {
-  launch_spmv_cfg<double, 1, TH, GPT, NT>(A, static_cast<const double*>(x), ProNone{},
+  launch_spmv_cfg<double, double, 1, TH, GPT, NT, ProNone, GatherVec<double>, EpiStore<double>, LANEC, XCD>(
+      A, GatherVec<double>{static_cast<const double*>(x)}, ProNone{},
                                           EpiStore<double>{static_cast<double*>(y)}, st);
 }
 static const SpmvLaunch kSpmvVariants[] = {
@@ -153,6 +154,9 @@ static const SpmvLaunch kSpmvVariants[] = {
     spmv_variant<256, 2, true>,  spmv_variant<128, 4, false>, spmv_variant<128, 8, false>,
     spmv_variant<512, 2, false>, spmv_variant<512, 4, false>, spmv_variant<64, 8, false>,
     spmv_variant<128, 2, false>, spmv_variant<256, 8, false>, spmv_variant<128, 4, true>,
+    spmv_variant<256, 4, false, true>, spmv_variant<256, 2, false, true>, spmv_variant<128, 4, false, true>,
+    spmv_variant<512, 2, false, true>,  spmv_variant<256, 4, false, false, true>, spmv_variant<256, 4, false, true, true>,
+    spmv_variant<128, 4, false, false, true>,
 };
 static constexpr int kNumSpmvVariants = int(sizeof(kSpmvVariants) / sizeof(kSpmvVariants[0]));
 

@@ -146,14 +146,31 @@ __device__ __forceinline__ void grid_reduce_dd(DD (&v)[N], double* partials, uns
   }
   __syncthreads();
   if (!s_last) return;
+  // Last arriver: every partial is read with sc1 loads, issued in batches of PB per lane
+  // before any of them is consumed (one round trip per batch, not one per partial), and
+  // summed in block-index order -> the result does not depend on which block was last.
+  constexpr int PB = 8;
   DD acc[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) acc[j] = dd_zero();
-  for (unsigned b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+  const unsigned G = gridDim.x;
+  for (unsigned base = 0; base < G; base += blockDim.x * PB) {
+    double ps[PB][N], pc[PB][N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      DD p{ld_agent_f64(&partials[(size_t(b) * N + j) * 2 + 0]), ld_agent_f64(&partials[(size_t(b) * N + j) * 2 + 1])};
-      acc[j] = dd_add(acc[j], p);
+    for (int u = 0; u < PB; ++u) {
+      unsigned b = base + threadIdx.x + u * blockDim.x;
+      b = b < G ? b : G - 1;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        ps[u][j] = ld_agent_f64(&partials[(size_t(b) * N + j) * 2 + 0]);
+        pc[u][j] = ld_agent_f64(&partials[(size_t(b) * N + j) * 2 + 1]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+      const bool ok = base + threadIdx.x + u * blockDim.x < G;
+#pragma unroll
+      for (int j = 0; j < N; ++j) acc[j] = dd_add(acc[j], DD{ok ? ps[u][j] : 0.0, ok ? pc[u][j] : 0.0});
     }
   }
   __syncthreads();
@@ -165,6 +182,20 @@ __device__ __forceinline__ void grid_reduce_dd(DD (&v)[N], double* partials, uns
     fin(out);
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// Explicit global (address space 1) accesses: pointers picked at run time (ping-pong buffers,
+// pointers inside structs) otherwise compile to flat_* instructions, which can only be waited
+// for with vmcnt(0)+lgkmcnt(0) and serialise a gather loop.
+template <typename T>
+using gptr_t = __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ T gld(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)(p);
+}
+template <typename T>
+__device__ __forceinline__ void gst(T* p, T v) {
+  *(__attribute__((address_space(1))) T*)(p) = v;
 }
 
 template <typename T>
@@ -199,4 +230,8 @@ struct lspcg_mat {
   int32_t* rowptr = nullptr;  // [nb+1]
   int32_t* colind = nullptr;  // [nnzb]
   void* vals = nullptr;       // [nnzb*bs*bs], row-major blocks
+  // storage type of vals: equals dtype, or LSPCG_F32 for an fp64 matrix whose values are all
+  // exactly representable in fp32 (compact storage, fp64 arithmetic: bit-identical results)
+  int val_dtype = -1;
+  int storage_dtype() const { return val_dtype < 0 ? dtype : val_dtype; }
 };

@@ -1,24 +1,29 @@
 // Device-resident preconditioned CG (replaces pymathprim.linalg.PreconditionedConjugateGradient,
-// call sites neural_cg/utils/validate.py:54-160; arithmetic order of scipy 1.15
-// iterative.py:359-418, the reference's CPU restatement validate.py:163-341).
+// call sites neural_cg/utils/validate.py:54-160; arithmetic of scipy 1.15 iterative.py:359-418,
+// the reference's CPU restatement validate.py:163-341).
 //
-// One iteration (ext_spai) is five kernels, every one predicated on a device `done` flag so
-// that the host can launch graph-captured chunks of iterations and poll once per chunk
-// without changing the iteration count or the iterate:
-//   K1  t = Lᵀ r                 (prologue: convergence test on ‖r‖ -- top of the scipy loop)
-//   K2  z = L t + ε r ; ρ = r·z   (SpMV epilogue + grid dot)
-//   K3  p = p·β + z               (β = ρ/ρ_prev; p = z at iteration 0)
-//   K4  q = A p ; π = p·q          (SpMV epilogue + grid dot)
-//   K5  x += α p ; r -= α q ; ‖r‖² (α = ρ/π; last workgroup advances the iteration)
-// Unpreconditioned CG drops K1/K2 (z = r, ρ = ‖r‖²) and moves the convergence test to K3;
-// diagonal (Jacobi) PCG computes z = r / diag(A) and ρ inside K5.
+// Schedule (DESIGN.md "PCG"): the AXPY-type updates of scipy's loop are evaluated where their
+// results are consumed, with the exact same floating-point expression, so every vector holds
+// the same bits as in scipy's order while an ext_spai iteration is THREE kernels:
+//   KA  r_k = r_{k-1} - α_{k-1} q_{k-1} (own rows, stored; recomputed in the gather),
+//       ‖r_k‖², t = Lᵀ r_k                                   [SpMV Lᵀ]
+//   KB  (test ‖r_k‖ < atol -- top of scipy's loop) z = L t + ε r_k ; ρ_k = r_k·z   [SpMV L]
+//   KC  p_k = p_{k-1}β + z (own rows stored; recomputed in the gather), x += α_{k-1} p_{k-1},
+//       q = A p_k ; π = p_k·q ; α_k = ρ_k/π                    [SpMV A]
+// Unpreconditioned / diagonal PCG: KA is elementwise (+ z = r/d, ρ) and the test moves to KC.
+// r and p ping-pong between two buffers (a gather must never see a half-updated vector); the
+// last x update is applied by one fix-up kernel after the loop.  Every kernel is predicated on
+// a device `done` flag, so the host replays graph-captured chunks of iterations and polls once
+// per chunk without changing the iteration count or the iterate.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "lspcg_internal.hpp"
 #include "lspcg_spmv.hpp"
@@ -28,9 +33,10 @@ namespace lspcg {
 struct PcgState {
   double bb;        // ‖b‖²
   double rr;        // ‖r_k‖² (rounded to T)
-  double rho;       // r·z of the current iteration (rounded to T)
-  double rho_prev;  // previous iteration's ρ
-  double pq;        // p·q (rounded to T)
+  double rho;       // ρ_k = r_k·z_k (rounded to T)
+  double rho_prev;  // ρ_{k-1}
+  double pq;        // π_k = p_k·q_k (rounded to T)
+  double alpha;     // α_k = ρ_k/π_k computed in T
   double atol;      // rtol·‖b‖
   double rtol;
   double eps;       // ε of ext_spai
@@ -68,62 +74,160 @@ struct ProDone {
   __device__ __forceinline__ bool exit() const { return S->done != 0; }
 };
 
-// K1: t = Lᵀ r  (scaled variant: t = (Lᵀ r) / d)
-template <typename T, bool SCALED>
-struct EpiT {
-  static constexpr int NDOT = 0;
-  T* t;
-  const T* d;
-  __device__ __forceinline__ void row(int64_t i, T s, DD*) const {
-    if constexpr (SCALED) t[i] = s / d[i];
-    else t[i] = s;
-  }
-  __device__ __forceinline__ void fin(const double*) const {}
-  double* partials = nullptr;
-  unsigned* ticket = nullptr;
+// r ping-pong: r_k lives in R[k & 1]; r_0 in R[0].
+template <typename T>
+struct RBuf {
+  T* R0;
+  T* R1;
+  __device__ __forceinline__ T* cur(int64_t k) const { return (k & 1) ? R1 : R0; }
+  __device__ __forceinline__ T* prev(int64_t k) const { return k == 0 ? R0 : cur(k - 1); }
 };
 
-// K2: z = L t + ε r  (scaled: z = L t + (ε r)/d);  ρ = r·z
+// gather of r_k = r_{k-1} - α_{k-1} q_{k-1} (scipy `r -= alpha*q`), identity at k = 0
+template <typename T>
+struct GatherR {
+  RBuf<T> R;
+  const T* q;
+  const PcgState* S;
+  const T* rold = nullptr;
+  T alpha = T(0);
+  bool upd = false;
+  __device__ __forceinline__ void prepare() {
+    const int64_t k = S->iter;
+    upd = k > 0;
+    alpha = T(S->alpha);
+    rold = R.prev(k);
+  }
+  // both loads unconditional, select afterwards: a select between a register and a load on a
+  // runtime flag makes hipcc branch around every load (cdna_hip_programming.md, 4(c))
+  __device__ __forceinline__ T operator()(int64_t j) const {
+    const T a = gld(rold + j);
+    const T b = gld(q + j);
+    const T u = a - alpha * b;
+    return upd ? u : a;
+  }
+};
+
+// gather of p_k = p_{k-1}*β + z_k (scipy `p *= beta; p += z`), p_0 = z_0; p_k in P[k & 1]
+template <typename T>
+struct GatherP {
+  const T* zsrc;  // z, or nullptr for CG (z = r_k)
+  RBuf<T> R;
+  const T* P0;
+  const T* P1;
+  const PcgState* S;
+  const T* z = nullptr;
+  const T* pold = nullptr;
+  T beta = T(0);
+  bool first = true;
+  __device__ __forceinline__ void prepare() {
+    const int64_t k = S->iter;
+    first = k == 0;
+    pold = (k & 1) ? P0 : P1;
+    z = zsrc ? zsrc : R.cur(k);
+    beta = first ? T(0) : T(S->rho) / T(S->rho_prev);
+  }
+  __device__ __forceinline__ T operator()(int64_t j) const {
+    const T a = gld(z + j);
+    const T b = gld(pold + j);
+    const T u = (b * beta) + a;
+    return first ? a : u;
+  }
+};
+
+// KA (ext_spai): own-row r update + ‖r‖², t = Lᵀ r (scaled variant: (Lᵀ r)/d)
+template <typename T, bool SCALED>
+struct EpiRT {
+  static constexpr int NDOT = 1;
+  GatherR<T> g;
+  T* t;
+  const T* d;
+  PcgState* S;
+  double* partials;
+  unsigned* ticket;
+  T* rnew = nullptr;
+  __device__ __forceinline__ void prepare() {
+    g.prepare();
+    rnew = g.R.cur(S->iter);
+  }
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T ri = g(i);
+    if (g.upd) gst(rnew + i, ri);
+    if constexpr (SCALED) gst(t + i, s / gld(d + i));
+    else gst(t + i, s);
+    dd_fma(dots[0], double(ri), double(ri));
+  }
+  __device__ __forceinline__ void fin(const double* v) const {
+    const double rr = round_to<T>(v[0]);
+    S->rr = rr;
+    if (S->hist) S->hist[S->iter] = double(tsqrt<T>(T(rr)));
+  }
+};
+
+// KB: z = L t + ε r  (scaled: z = L t + (ε r)/d);  ρ = r·z
 template <typename T, bool SCALED>
 struct EpiZ {
   static constexpr int NDOT = 1;
   T* z;
-  const T* r;
+  RBuf<T> R;
   const T* d;
   T eps;
   PcgState* S;
   double* partials;
   unsigned* ticket;
+  const T* r = nullptr;
+  __device__ __forceinline__ void prepare() { r = R.cur(S->iter); }
   __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
-    const T ri = r[i];
+    const T ri = gld(r + i);
     T zi;
-    if constexpr (SCALED) zi = s + (eps * ri) / d[i];
+    if constexpr (SCALED) zi = s + (eps * ri) / gld(d + i);
     else zi = s + eps * ri;
-    z[i] = zi;
+    gst(z + i, zi);
     dd_fma(dots[0], double(ri), double(zi));
   }
-  __device__ __forceinline__ void fin(const double* v) const { S->rho = round_to<T>(v[0]); }
+  __device__ __forceinline__ void fin(const double* v) const {
+    S->rho_prev = S->rho;
+    S->rho = round_to<T>(v[0]);
+  }
 };
 
-// K4: q = A p ; π = p·q
+// KC: own-row p_k (stored) and deferred x += α_{k-1} p_{k-1}; q = A p_k ; π = p_k·q ; α_k
 template <typename T>
-struct EpiQ {
+struct EpiPQ {
   static constexpr int NDOT = 1;
+  GatherP<T> g;
+  T* P0;
+  T* P1;
+  T* x;
   T* q;
-  const T* p;
   PcgState* S;
   double* partials;
   unsigned* ticket;
-  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
-    q[i] = s;
-    dd_fma(dots[0], double(p[i]), double(s));
+  T* pnew = nullptr;
+  T alpha_prev = T(0);
+  __device__ __forceinline__ void prepare() {
+    g.prepare();
+    pnew = (S->iter & 1) ? P1 : P0;
+    alpha_prev = T(S->alpha);
   }
-  __device__ __forceinline__ void fin(const double* v) const { S->pq = round_to<T>(v[0]); }
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T pi = g(i);
+    gst(pnew + i, pi);
+    if (!g.first) gst(x + i, gld(x + i) + alpha_prev * gld(g.pold + i));
+    gst(q + i, s);
+    dd_fma(dots[0], double(pi), double(s));
+  }
+  __device__ __forceinline__ void fin(const double* v) const {
+    const double pq = round_to<T>(v[0]);
+    S->pq = pq;
+    S->alpha = double(T(S->rho) / T(pq));
+    S->iter = S->iter + 1;
+  }
 };
 
-// init: r = b - A x0 ; ‖r‖², ‖b‖²  (scipy: r = b - matvec(x) if x.any() else b.copy();
+// init: r_0 = b - A x0 ; ‖r_0‖², ‖b‖²  (scipy: r = b - matvec(x) if x.any() else b.copy();
 // with x0 = 0 the subtraction returns b bit-for-bit)
-template <typename T, int PRE>
+template <typename T>
 struct EpiResid {
   static constexpr int NDOT = 2;
   T* r;
@@ -131,6 +235,7 @@ struct EpiResid {
   PcgState* S;
   double* partials;
   unsigned* ticket;
+  __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
     const T bi = b[i];
     const T ri = bi - s;
@@ -143,79 +248,112 @@ struct EpiResid {
     S->bb = round_to<T>(v[1]);
     const double bn = double(tsqrt<T>(T(S->bb)));
     S->atol = fmax(0.0, S->rtol * bn);
-    if (PRE == LSPCG_PRECOND_NONE) S->rho = S->rr;
+    S->rho = S->rr;
+    S->alpha = 0.0;
     S->iter = 0;
     S->done = (bn == 0.0) ? 1 : 0;
     if (S->hist) S->hist[0] = double(tsqrt<T>(T(S->rr)));
   }
 };
 
-// K3: p = p*β + z  (iteration 0: p = z)
-template <typename T, class Pro>
-__global__ void __launch_bounds__(kThreads) k_update_p(int64_t n, Pro pro, const PcgState* S, const T* __restrict__ z,
-                                                       T* __restrict__ p) {
-  if (pro.exit()) return;
-  const bool first = S->iter == 0;
-  const T beta = first ? T(0) : T(S->rho) / T(S->rho_prev);
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-    const T zi = z[i];
-    p[i] = first ? zi : (p[i] * beta) + zi;
+template <typename T>
+struct V2T;
+template <>
+struct V2T<double> {
+  using type = double __attribute__((ext_vector_type(2)));
+};
+template <>
+struct V2T<float> {
+  using type = float __attribute__((ext_vector_type(2)));
+};
+
+// KA for CG / Jacobi: r_k = r_{k-1} - α q (elementwise, ping-pong), ‖r‖² (+ z = r/d, ρ = r·z)
+template <typename T, int PRE>
+__device__ __forceinline__ void r_elem(bool upd, T alpha, T ro, T qi, T& rn, const T* d, T* z, int64_t i, DD* dots) {
+  rn = upd ? ro - alpha * qi : ro;
+  dd_fma(dots[0], double(rn), double(rn));
+  if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) {
+    const T zi = rn / d[i];
+    z[i] = zi;
+    dd_fma(dots[1], double(rn), double(zi));
   }
 }
 
-// K5: x += α p ; r -= α q ; ‖r‖²  (+ Jacobi: z = r/d, ρ = r·z)
 template <typename T, int PRE>
-__global__ void __launch_bounds__(kThreads) k_update_xr(int64_t n, PcgState* S, const T* __restrict__ p,
-                                                        const T* __restrict__ q, T* __restrict__ x, T* __restrict__ r,
-                                                        const T* __restrict__ d, T* __restrict__ z, double* partials,
-                                                        unsigned* ticket) {
+__global__ void __launch_bounds__(kThreads) k_update_r(int64_t n, PcgState* S, RBuf<T> R, const T* __restrict__ q,
+                                                       const T* __restrict__ d, T* __restrict__ z, double* partials,
+                                                       unsigned* ticket) {
+  using V2 = typename V2T<T>::type;
   if (S->done) return;
   constexpr int ND = PRE == LSPCG_PRECOND_DIAGONAL ? 2 : 1;
-  const T alpha = T(S->rho) / T(S->pq);
+  const int64_t k = S->iter;
+  const bool upd = k > 0;
+  const T alpha = T(S->alpha);
+  const T* ro = R.prev(k);
+  T* rn = R.cur(k);
   DD dots[ND];
 #pragma unroll
   for (int j = 0; j < ND; ++j) dots[j] = dd_zero();
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-    x[i] = x[i] + alpha * p[i];
-    const T ri = r[i] - alpha * q[i];
-    r[i] = ri;
-    dd_fma(dots[0], double(ri), double(ri));
-    if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) {
-      const T zi = ri / d[i];
-      z[i] = zi;
-      dd_fma(dots[1], double(ri), double(zi));
-    }
+  const int64_t np = n >> 1;
+  const int64_t t0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, ts = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t j = t0; j < np; j += ts) {
+    const V2 rr = reinterpret_cast<const V2*>(ro)[j];
+    const V2 qq = reinterpret_cast<const V2*>(q)[j];
+    V2 out;
+    T a0, a1;
+    r_elem<T, PRE>(upd, alpha, rr.x, qq.x, a0, d, z, 2 * j, dots);
+    r_elem<T, PRE>(upd, alpha, rr.y, qq.y, a1, d, z, 2 * j + 1, dots);
+    out.x = a0;
+    out.y = a1;
+    if (upd) reinterpret_cast<V2*>(rn)[j] = out;
+  }
+  if ((n & 1) && t0 == 0) {
+    const int64_t i = n - 1;
+    T a;
+    r_elem<T, PRE>(upd, alpha, ro[i], q[i], a, d, z, i, dots);
+    if (upd) rn[i] = a;
   }
   grid_reduce_dd<ND>(dots, partials, ticket, [&](const double* v) {
-    const double rr = round_to<T>(v[0]);
-    S->rr = rr;
+    const double rr2 = round_to<T>(v[0]);
+    S->rr = rr2;
     S->rho_prev = S->rho;
-    if constexpr (PRE == LSPCG_PRECOND_NONE) S->rho = rr;
-    if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) S->rho = round_to<T>(v[1]);
-    const int64_t it = S->iter + 1;
-    S->iter = it;
-    if (S->hist) S->hist[it] = double(tsqrt<T>(T(rr)));
+    S->rho = (PRE == LSPCG_PRECOND_DIAGONAL) ? round_to<T>(v[ND - 1]) : rr2;
+    if (S->hist) S->hist[S->iter] = double(tsqrt<T>(T(rr2)));
   });
 }
 
-// Jacobi init: z = r / d ; ρ = r·z
+// after the loop: the deferred x += α_{k-1} p_{k-1} of the last completed iteration
 template <typename T>
-__global__ void __launch_bounds__(kThreads) k_jacobi_init(int64_t n, PcgState* S, const T* __restrict__ r,
-                                                          const T* __restrict__ d, T* __restrict__ z, double* partials,
-                                                          unsigned* ticket) {
-  DD dots[1] = {dd_zero()};
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-    const T ri = r[i];
-    const T zi = ri / d[i];
-    z[i] = zi;
-    dd_fma(dots[0], double(ri), double(zi));
-  }
-  grid_reduce_dd<1>(dots, partials, ticket, [&](const double* v) { S->rho = round_to<T>(v[0]); });
+__global__ void __launch_bounds__(kThreads) k_x_fixup(int64_t n, const PcgState* S, const T* __restrict__ P0,
+                                                      const T* __restrict__ P1, T* __restrict__ x) {
+  const int64_t k = S->iter;
+  if (k < 1 || S->bb == 0.0) return;
+  const T alpha = T(S->alpha);
+  const T* p = ((k - 1) & 1) ? P1 : P0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    x[i] = x[i] + alpha * p[i];
 }
 
-static int elem_grid(int64_t n) {
+// ---- storage optimisation helpers (see DESIGN.md "PCG storage")
+__global__ void k_f32_inexact(int64_t n, const double* __restrict__ v, int* __restrict__ flag) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const double a = v[i];
+    if (!(double(float(a)) == a)) atomicOr(flag, 1);  // also true for NaN
+  }
+}
+__global__ void k_to_f32(int64_t n, const double* __restrict__ v, float* __restrict__ out) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = float(v[i]);
+}
+__global__ void k_i32_neq(int64_t n, const int32_t* __restrict__ a, const int32_t* __restrict__ b,
+                          int* __restrict__ flag) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    if (a[i] != b[i]) atomicOr(flag, 1);
+}
+
+static int elem_grid(int64_t n) {  // 2 elements per lane, >= 2 pairs per lane, <= 1024 partials
   const int64_t g = (n + kThreads * 4 - 1) / (kThreads * 4);
-  return int(std::max<int64_t>(1, std::min<int64_t>(g, kElemBlocksMax)));
+  return int(std::max<int64_t>(1, std::min<int64_t>(g, 1024)));
 }
 
 }  // namespace lspcg
@@ -233,7 +371,7 @@ struct lspcg_solver {
   double eps = 0.0;
   hipStream_t stream = nullptr;  // solver-owned (capturable) stream
   void *x = nullptr, *b = nullptr, *r = nullptr, *z = nullptr, *t = nullptr, *p = nullptr, *q = nullptr,
-       *d = nullptr;
+       *d = nullptr, *r1 = nullptr, *p1 = nullptr;
   PcgState* S = nullptr;
   PcgState* hS = nullptr;  // pinned host mirror
   double* partials = nullptr;
@@ -241,88 +379,138 @@ struct lspcg_solver {
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_poll = nullptr;
   std::map<int, hipGraphExec_t> graphs;
   std::map<int, hipGraph_t> graph_defs;
+  // iteration views of A, L, Lᵀ: compact fp32 values when lossless, one shared index
+  // structure when the patterns coincide (non-owning copies of the handles + owned buffers)
+  lspcg_mat Av, Lv, LTv;
+  void* own_A = nullptr;
+  void* own_L = nullptr;
+  void* own_LT = nullptr;
+  int* flag = nullptr;
+  bool compact = true;
 };
+
+static int flag_run(lspcg_solver* s, hipStream_t st, int* out) {
+  int h = 0;
+  LSPCG_HIP(hipMemcpyAsync(&h, s->flag, sizeof(int), hipMemcpyDeviceToHost, st));
+  LSPCG_HIP(hipStreamSynchronize(st));
+  *out = h;
+  return LSPCG_OK;
+}
+
+// view <- M; compact fp64 values to fp32 when exact; share `base`'s index arrays when equal.
+static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const lspcg_mat* base, void** own) {
+  hipStream_t st = s->ctx->stream;
+  if (*own) {
+    LSPCG_HIP(hipStreamSynchronize(s->stream));
+    (void)hipFree(*own);
+    *own = nullptr;
+  }
+  *view = *M;
+  const int64_t ne = M->nnzb * M->block_size * M->block_size;
+  int f = 0;
+  if (s->compact && M->dtype == LSPCG_F64 && M->storage_dtype() == LSPCG_F64 && ne > 0) {
+    LSPCG_HIP(hipMemsetAsync(s->flag, 0, sizeof(int), st));
+    hipLaunchKernelGGL(k_f32_inexact, dim3(elem_grid(ne)), dim3(kThreads), 0, st, ne,
+                       static_cast<const double*>(M->vals), s->flag);
+    if (int rc = flag_run(s, st, &f)) return rc;
+    if (!f) {
+      float* v = nullptr;
+      LSPCG_HIP(hipMalloc(&v, sizeof(float) * (ne + kEntryPad)));
+      *own = v;
+      LSPCG_HIP(hipMemsetAsync(v + ne, 0, sizeof(float) * kEntryPad, st));
+      hipLaunchKernelGGL(k_to_f32, dim3(elem_grid(ne)), dim3(kThreads), 0, st, ne,
+                         static_cast<const double*>(M->vals), v);
+      view->vals = v;
+      view->val_dtype = LSPCG_F32;
+    }
+  }
+  if (base && base != M && base->nb == M->nb && base->nnzb == M->nnzb && base->block_size == M->block_size) {
+    LSPCG_HIP(hipMemsetAsync(s->flag, 0, sizeof(int), st));
+    hipLaunchKernelGGL(k_i32_neq, dim3(elem_grid(M->nb + 1)), dim3(kThreads), 0, st, M->nb + 1, M->rowptr,
+                       base->rowptr, s->flag);
+    if (M->nnzb)
+      hipLaunchKernelGGL(k_i32_neq, dim3(elem_grid(M->nnzb)), dim3(kThreads), 0, st, M->nnzb, M->colind,
+                         base->colind, s->flag);
+    if (int rc = flag_run(s, st, &f)) return rc;
+    if (!f) {
+      view->rowptr = base->rowptr;
+      view->colind = base->colind;
+    }
+  }
+  LSPCG_HIP(hipStreamSynchronize(st));
+  return LSPCG_OK;
+}
 
 template <typename T>
 static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
   const int64_t n = s->n;
   T* x = static_cast<T*>(s->x);
-  T* r = static_cast<T*>(s->r);
   T* z = static_cast<T*>(s->z);
   T* t = static_cast<T*>(s->t);
-  T* p = static_cast<T*>(s->p);
+  T* P0 = static_cast<T*>(s->p);
+  T* P1 = static_cast<T*>(s->p1);
   T* q = static_cast<T*>(s->q);
   const T* d = static_cast<const T*>(s->d);
+  const RBuf<T> R{static_cast<T*>(s->r), static_cast<T*>(s->r1)};
   PcgState* S = s->S;
   const int eg = elem_grid(n);
   int rc = LSPCG_OK;
   switch (s->precond) {
     case LSPCG_PRECOND_EXT_SPAI:
     case LSPCG_PRECOND_EXT_SPAI_SCALED: {
-      const bool scaled = s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
-      if (scaled) {
-        rc = launch_spmv_any<T>(s->LT, r, ProCheck<T>{S}, EpiT<T, true>{t, d}, st);
+      const GatherR<T> gr{R, q, S};
+      if (s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) {
+        rc = launch_spmv_gx<T>(&s->LTv, gr, ProDone{S}, EpiRT<T, true>{gr, t, d, S, s->partials, s->ticket}, st);
         if (!rc)
-          rc = launch_spmv_any<T>(s->L, t, ProDone{S}, EpiZ<T, true>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st);
+          rc = launch_spmv_any<T>(&s->Lv, static_cast<const T*>(t), ProCheck<T>{S},
+                                  EpiZ<T, true>{z, R, d, T(s->eps), S, s->partials, s->ticket}, st);
       } else {
-        rc = launch_spmv_any<T>(s->LT, r, ProCheck<T>{S}, EpiT<T, false>{t, d}, st);
+        rc = launch_spmv_gx<T>(&s->LTv, gr, ProDone{S}, EpiRT<T, false>{gr, t, d, S, s->partials, s->ticket}, st);
         if (!rc)
-          rc = launch_spmv_any<T>(s->L, t, ProDone{S}, EpiZ<T, false>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st);
+          rc = launch_spmv_any<T>(&s->Lv, static_cast<const T*>(t), ProCheck<T>{S},
+                                  EpiZ<T, false>{z, R, d, T(s->eps), S, s->partials, s->ticket}, st);
       }
       if (rc) return rc;
-      hipLaunchKernelGGL((k_update_p<T, ProDone>), dim3(eg), dim3(kThreads), 0, st, n, ProDone{S}, S, z, p);
-      rc = launch_spmv_any<T>(s->A, p, ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket}, st);
-      if (rc) return rc;
-      hipLaunchKernelGGL((k_update_xr<T, LSPCG_PRECOND_EXT_SPAI>), dim3(eg), dim3(kThreads), 0, st, n, S, p, q, x, r,
-                         d, z, s->partials, s->ticket);
+      const GatherP<T> gp{z, R, P0, P1, S};
+      rc = launch_spmv_gx<T>(&s->Av, gp, ProDone{S}, EpiPQ<T>{gp, P0, P1, x, q, S, s->partials, s->ticket}, st);
       break;
     }
-    case LSPCG_PRECOND_NONE: {
-      hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S, r, p);
-      rc = launch_spmv_any<T>(s->A, p, ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket}, st);
-      if (rc) return rc;
-      hipLaunchKernelGGL((k_update_xr<T, LSPCG_PRECOND_NONE>), dim3(eg), dim3(kThreads), 0, st, n, S, p, q, x, r, d,
-                         z, s->partials, s->ticket);
-      break;
-    }
+    case LSPCG_PRECOND_NONE:
     case LSPCG_PRECOND_DIAGONAL: {
-      hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S, z, p);
-      rc = launch_spmv_any<T>(s->A, p, ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket}, st);
-      if (rc) return rc;
-      hipLaunchKernelGGL((k_update_xr<T, LSPCG_PRECOND_DIAGONAL>), dim3(eg), dim3(kThreads), 0, st, n, S, p, q, x, r,
-                         d, z, s->partials, s->ticket);
+      if (s->precond == LSPCG_PRECOND_NONE)
+        hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_NONE>), dim3(eg), dim3(kThreads), 0, st, n, S, R, q, d, z,
+                           s->partials, s->ticket);
+      else
+        hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_DIAGONAL>), dim3(eg), dim3(kThreads), 0, st, n, S, R, q, d, z,
+                           s->partials, s->ticket);
+      const GatherP<T> gp{s->precond == LSPCG_PRECOND_NONE ? nullptr : z, R, P0, P1, S};
+      rc = launch_spmv_gx<T>(&s->Av, gp, ProCheck<T>{S}, EpiPQ<T>{gp, P0, P1, x, q, S, s->partials, s->ticket}, st);
       break;
     }
     default:
       set_error("unknown preconditioner");
       return LSPCG_ERR_ARG;
   }
+  if (rc) return rc;
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
 
 template <typename T>
 static int enqueue_init(lspcg_solver* s, hipStream_t st) {
-  PcgState* S = s->S;
-  int rc;
-  switch (s->precond) {
-    case LSPCG_PRECOND_NONE:
-      rc = launch_spmv_any<T>(s->A, static_cast<const T*>(s->x), ProNone{},
-                              EpiResid<T, LSPCG_PRECOND_NONE>{static_cast<T*>(s->r), static_cast<const T*>(s->b), S,
-                                                              s->partials, s->ticket},
+  int rc = launch_spmv_any<T>(&s->Av, static_cast<const T*>(s->x), ProNone{},
+                              EpiResid<T>{static_cast<T*>(s->r), static_cast<const T*>(s->b), s->S, s->partials,
+                                          s->ticket},
                               st);
-      break;
-    default:
-      rc = launch_spmv_any<T>(s->A, static_cast<const T*>(s->x), ProNone{},
-                              EpiResid<T, LSPCG_PRECOND_EXT_SPAI>{static_cast<T*>(s->r), static_cast<const T*>(s->b),
-                                                                  S, s->partials, s->ticket},
-                              st);
-  }
   if (rc) return rc;
-  if (s->precond == LSPCG_PRECOND_DIAGONAL)
-    hipLaunchKernelGGL(k_jacobi_init<T>, dim3(elem_grid(s->n)), dim3(kThreads), 0, st, s->n, S,
-                       static_cast<const T*>(s->r), static_cast<const T*>(s->d), static_cast<T*>(s->z), s->partials,
-                       s->ticket);
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+template <typename T>
+static int enqueue_fixup(lspcg_solver* s, hipStream_t st) {
+  hipLaunchKernelGGL(k_x_fixup<T>, dim3(elem_grid(s->n)), dim3(kThreads), 0, st, s->n, s->S,
+                     static_cast<const T*>(s->p), static_cast<const T*>(s->p1), static_cast<T*>(s->x));
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
@@ -366,7 +554,10 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   s->n = A->n;
   const size_t vb = esize(s->dtype) * std::max<int64_t>(s->n, 1);
   LSPCG_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d}) LSPCG_HIP(hipMalloc(v, vb));
+  for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d, &s->r1, &s->p1}) {
+    LSPCG_HIP(hipMalloc(v, vb));
+    LSPCG_HIP(hipMemsetAsync(*v, 0, vb, s->stream));
+  }
   LSPCG_HIP(hipMalloc(&s->S, sizeof(PcgState)));
   LSPCG_HIP(hipHostMalloc(&s->hS, sizeof(PcgState), hipHostMallocDefault));
   // partial slots: largest grid of any reducing launch (SpMV grid of A / L, element grid) x 2 dots
@@ -380,6 +571,9 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   for (hipEvent_t* e : {&s->ev_in, &s->ev_out, &s->ev_poll}) LSPCG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   LSPCG_HIP(hipEventCreate(&s->ev_t0));
   LSPCG_HIP(hipEventCreate(&s->ev_t1));
+  LSPCG_HIP(hipMalloc(&s->flag, sizeof(int)));
+  if (const char* e = std::getenv("LSPCG_NO_COMPACT")) s->compact = e[0] == '0';
+  if (int rc = make_view(s.get(), A, &s->Av, nullptr, &s->own_A)) return rc;
   if (precond == LSPCG_PRECOND_DIAGONAL) {
     int rc = lspcg_mat_diagonal(A, s->d);  // issues on ctx stream
     if (rc) return rc;
@@ -408,6 +602,8 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     rc = lspcg_mat_diagonal(s->A, s->d);
     if (rc) return rc;
   }
+  if ((rc = make_view(s, L, &s->Lv, &s->Av, &s->own_L))) return rc;
+  if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT))) return rc;
   LSPCG_HIP(hipEventRecord(s->ev_t1, cst));
   LSPCG_HIP(hipEventSynchronize(s->ev_t1));
   float ms = 0.f;
@@ -462,8 +658,7 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     LSPCG_HIP(hipEventRecord(s->ev_poll, st));
     LSPCG_HIP(hipEventSynchronize(s->ev_poll));
     const PcgState cur = *s->hS;
-    if (cur.done) break;
-    if (cur.iter >= max_iter) break;  // defensive; ProCheck sets done
+    if (cur.done) break;  // ProCheck sets done (convergence, max_iter or a non-finite residual)
     if (last_rr > 0 && cur.iter > last_it && cur.rr > 0 && cur.rr < last_rr) {
       const double rate = std::log(cur.rr / last_rr) / double(cur.iter - last_it);  // < 0
       const double need = std::log((cur.atol * cur.atol) / cur.rr) / rate;
@@ -483,6 +678,8 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     LSPCG_HIP(hipGraphLaunch(ex, st));
   }
   const PcgState fin = *s->hS;
+  rc = s->dtype == LSPCG_F64 ? enqueue_fixup<double>(s, st) : enqueue_fixup<float>(s, st);
+  if (rc) return rc;
   const void* src = (fin.bb == 0.0) ? s->b : s->x;  // scipy returns b when ‖b‖ = 0
   if (n) LSPCG_HIP(hipMemcpyAsync(x, src, vb, hipMemcpyDeviceToDevice, st));
   LSPCG_HIP(hipEventRecord(s->ev_t1, st));
@@ -508,13 +705,15 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipStreamSynchronize(s->stream);
   for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
-  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d}) (void)hipFree(v);
+  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d, s->r1, s->p1}) (void)hipFree(v);
   (void)hipFree(s->S);
   (void)hipHostFree(s->hS);
   (void)hipFree(s->partials);
   (void)hipFree(s->ticket);
   for (hipEvent_t e : {s->ev_in, s->ev_out, s->ev_poll, s->ev_t0, s->ev_t1}) (void)hipEventDestroy(e);
   if (s->LT) lspcg_mat_destroy(s->LT);
+  for (void* p : {s->own_A, s->own_L, s->own_LT}) (void)hipFree(p);
+  (void)hipFree(s->flag);
   (void)hipStreamDestroy(s->stream);
   delete s;
   return LSPCG_OK;

@@ -14,17 +14,27 @@
 // needed for them.
 #pragma once
 
+#include <algorithm>
+
 #include "lspcg_internal.hpp"
 
 namespace lspcg {
 
-template <typename T, int BS>
+template <typename T, typename VT, int BS>
 struct SpmvArgs {
   int64_t nb;             // block rows
   const int32_t* rowptr;  // [nb+1]
   const int32_t* colind;  // [nnzb]
-  const T* vals;          // [nnzb*BS*BS]
-  const T* x;             // gathered vector
+  const VT* vals;         // [nnzb*BS*BS] storage type (VT = float for compact fp64 matrices)
+};
+
+// Gather functors: x_j as seen by the SpMV.  prepare() runs once per workgroup after the
+// prologue (it may read solver state); operator() is evaluated for every gathered column.
+template <typename T>
+struct GatherVec {
+  const T* x;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ T operator()(int64_t j) const { return gld(x + j); }
 };
 
 inline int64_t spmv_grid(int64_t nb, int bs) {  // grid of the production configuration (<= n/255 + 1)
@@ -42,7 +52,8 @@ template <typename T>
 struct EpiStore {
   static constexpr int NDOT = 0;
   T* y;
-  __device__ __forceinline__ void row(int64_t r, T s, DD*) const { y[r] = s; }
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ void row(int64_t r, T s, DD*) const { gst(y + r, s); }
   __device__ __forceinline__ void fin(const double*) const {}
   double* partials = nullptr;
   unsigned* ticket = nullptr;
@@ -87,8 +98,14 @@ struct Vec4<float> {
 
 // THREADS = workgroup size (one scalar row per thread), GPT = groups of 4 entries each
 // thread stages per chunk (chunk = THREADS*GPT*4 entries), NT = non-temporal matrix loads.
-template <typename T, int BS, int THREADS, int GPT, bool NT, class Pro, class Epi>
-__global__ void __launch_bounds__(THREADS) k_spmv(SpmvArgs<T, BS> a, Pro pro, Epi epi) {
+// LANEC: lane-consecutive staging (lane t <-> entry c0 + t + u*THREADS, 4/8-B loads): one
+// gather instruction then covers ~64/15 consecutive rows, i.e. few distinct cache lines.
+// XCD: persistent grid (multiple of 8) whose workgroups b, b+8, ... (one XCD under the observed
+// round-robin dispatch) walk one contiguous eighth of the row tiles, so each XCD's 4 MiB L2
+// only holds the gather window of its own slice.  Placement is a speed hint only.
+template <typename T, typename VT, int BS, int THREADS, int GPT, bool NT, class Pro, class Gx, class Epi,
+          bool LANEC = false, bool XCD = false>
+__global__ void __launch_bounds__(THREADS) k_spmv(SpmvArgs<T, VT, BS> a, Pro pro, Gx gx, Epi epi) {
   constexpr int BB = BS * BS;
   constexpr int CAPG = THREADS * GPT;             // groups of 4 entries per chunk
   constexpr int RB = THREADS / BS;                // block rows per workgroup
@@ -98,9 +115,28 @@ __global__ void __launch_bounds__(THREADS) k_spmv(SpmvArgs<T, BS> a, Pro pro, Ep
   __shared__ __attribute__((aligned(16))) T prod[CAPG * 4];
 
   if (pro.exit()) return;
+  gx.prepare();
+  epi.prepare();
 
   const int tid = threadIdx.x;
-  const int64_t b0 = int64_t(blockIdx.x) * RB;
+  DD d[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) d[j] = dd_zero();
+  const int64_t ntiles = (a.nb + RB - 1) / RB;
+  // Reducing launches are capped at a resident grid (the dot's per-workgroup ticket and
+  // the last arriver's partial sweep then cost once per workgroup, not once per tile);
+  // each workgroup walks tiles blockIdx.x, blockIdx.x + gridDim.x, ... (or its XCD slice)
+  int64_t t_first = blockIdx.x, t_end = ntiles, t_step = gridDim.x;
+  if constexpr (XCD) {
+    const int64_t per = gridDim.x >> 3;
+    const int64_t t8 = (ntiles + 7) >> 3;
+    const int64_t x = blockIdx.x & 7;
+    t_first = x * t8 + (blockIdx.x >> 3);
+    t_end = (x + 1) * t8 < ntiles ? (x + 1) * t8 : ntiles;
+    t_step = per;
+  }
+  for (int64_t tile = t_first; tile < t_end; tile += t_step) {
+  const int64_t b0 = tile * RB;
   const int64_t b1 = b0 + RB < a.nb ? b0 + RB : a.nb;
   const int64_t e0 = int64_t(a.rowptr[b0]) * BB;
   const int64_t e1 = int64_t(a.rowptr[b1]) * BB;
@@ -118,14 +154,46 @@ __global__ void __launch_bounds__(THREADS) k_spmv(SpmvArgs<T, BS> a, Pro pro, Ep
 
   for (int64_t gs = G0; gs < G1; gs += CAPG) {
     const int64_t ge = gs + CAPG < G1 ? gs + CAPG : G1;
+    if constexpr (LANEC) {
+      // entries [4gs, 4ge) clamped to [e0, e1); LDS index = entry - 4gs
+      constexpr int PE = 4 * PERG;
+      const int64_t lo4 = 4 * gs;
+      int64_t hi4 = 4 * ge;
+      hi4 = hi4 < e1 ? hi4 : e1;
+      const int64_t lo = lo4 > e0 ? lo4 : e0;
+      int cidx[PE];
+      VT v[PE];
+#pragma unroll
+      for (int u = 0; u < PE; ++u) {
+        int64_t k = lo + tid + int64_t(u) * kThreads;
+        k = k < hi4 ? k : hi4 - 1;
+        v[u] = gld(a.vals + k);
+        if constexpr (BS == 1) {
+          cidx[u] = gld(a.colind + k);
+        } else {
+          const int64_t kb = k / BB;
+          const int w = int(k - kb * BB);
+          cidx[u] = gld(a.colind + kb) * BS + (w % BS);
+        }
+      }
+      T xv[PE];
+#pragma unroll
+      for (int u = 0; u < PE; ++u) xv[u] = gx(cidx[u]);
+#pragma unroll
+      for (int u = 0; u < PE; ++u) {
+        int64_t k = lo + tid + int64_t(u) * kThreads;
+        k = k < hi4 ? k : hi4 - 1;
+        prod[k - lo4] = T(v[u]) * xv[u];
+      }
+    } else {
     // ---- stage: branch-free 16-B loads, x gather, products -> LDS
     int cidx[PERG][4];
-    T v[PERG][4];
+    VT v[PERG][4];
 #pragma unroll
     for (int u = 0; u < PERG; ++u) {
       int64_t g = gs + tid + int64_t(u) * kThreads;
       g = g < ge ? g : ge - 1;
-      Vec4<T>::template load<NT>(a.vals + 4 * g, v[u]);
+      Vec4<VT>::template load<NT>(a.vals + 4 * g, v[u]);
       if constexpr (BS == 1) {
         const i32x4 c = NT ? __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(a.colind) + g)
                            : reinterpret_cast<const i32x4*>(a.colind)[g];
@@ -144,17 +212,18 @@ __global__ void __launch_bounds__(THREADS) k_spmv(SpmvArgs<T, BS> a, Pro pro, Ep
 #pragma unroll
     for (int u = 0; u < PERG; ++u)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xv[u][j] = a.x[cidx[u][j]];
+      for (int j = 0; j < 4; ++j) xv[u][j] = gx(cidx[u][j]);
 #pragma unroll
     for (int u = 0; u < PERG; ++u) {
       int64_t g = gs + tid + int64_t(u) * kThreads;
       g = g < ge ? g : ge - 1;
       T pr[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) pr[j] = v[u][j] * xv[u][j];
+      for (int j = 0; j < 4; ++j) pr[j] = T(v[u][j]) * xv[u][j];  // exact widening of VT
       Vec4<T>::store(prod + 4 * (g - gs), pr);
     }
     __syncthreads();
+    }
     // ---- per-row sequential accumulation (scipy order)
     if (active) {
       const int64_t lo = 4 * gs, hi = 4 * ge;
@@ -185,17 +254,15 @@ __global__ void __launch_bounds__(THREADS) k_spmv(SpmvArgs<T, BS> a, Pro pro, Ep
     }
     __syncthreads();
   }
-
-  DD d[ND];
-#pragma unroll
-  for (int j = 0; j < ND; ++j) d[j] = dd_zero();
   if (active) epi.row(b0 * BS + tid, acc, d);
+  }  // tiles
+
   if constexpr (Epi::NDOT > 0) {
     grid_reduce_dd<Epi::NDOT>(d, epi.partials, epi.ticket, [&](const double* vals) { epi.fin(vals); });
   }
 }
 
-// Production configuration (tuned on MI355X, tools/spmv_probe.py): see DESIGN.md "SpMV".
+// Production configuration (tuned on MI355X with tools/spmv_probe.py): see DESIGN.md "SpMV".
 template <typename T>
 struct SpmvCfg {
   static constexpr int THREADS = 256;
@@ -209,32 +276,49 @@ inline int64_t spmv_grid_t(int64_t nb) {
   return (nb + rb - 1) / rb;
 }
 
-template <typename T, int BS, int THREADS, int GPT, bool NT, class Pro, class Epi>
-inline void launch_spmv_cfg(const lspcg_mat* A, const T* x, Pro pro, Epi epi, hipStream_t st) {
-  SpmvArgs<T, BS> a{A->nb, A->rowptr, A->colind, static_cast<const T*>(A->vals), x};
-  const int64_t grid = spmv_grid_t<THREADS, BS>(A->nb);
+constexpr int64_t kReduceGridMax = 1024;  // 256 CUs x 4 resident 256-thread workgroups
+
+template <typename T, typename VT, int BS, int THREADS, int GPT, bool NT, class Pro, class Gx, class Epi,
+          bool LANEC = false, bool XCD = false>
+inline void launch_spmv_cfg(const lspcg_mat* A, Gx gx, Pro pro, Epi epi, hipStream_t st) {
+  SpmvArgs<T, VT, BS> a{A->nb, A->rowptr, A->colind, static_cast<const VT*>(A->vals)};
+  int64_t grid = spmv_grid_t<THREADS, BS>(A->nb);
+  const int64_t cap = kReduceGridMax * 256 / THREADS;
+  if (XCD) grid = std::min<int64_t>(((grid + 7) / 8) * 8, cap);
+  else if (Epi::NDOT > 0 && grid > cap) grid = cap;
   if (grid > 0)
-    hipLaunchKernelGGL((k_spmv<T, BS, THREADS, GPT, NT, Pro, Epi>), dim3(unsigned(grid)), dim3(THREADS), 0, st, a,
-                       pro, epi);
+    hipLaunchKernelGGL((k_spmv<T, VT, BS, THREADS, GPT, NT, Pro, Gx, Epi, LANEC, XCD>), dim3(unsigned(grid)),
+                       dim3(THREADS), 0, st, a, pro, gx, epi);
 }
 
-template <typename T, int BS, class Pro, class Epi>
-inline void launch_spmv(const lspcg_mat* A, const T* x, Pro pro, Epi epi, hipStream_t st) {
-  launch_spmv_cfg<T, BS, SpmvCfg<T>::THREADS, SpmvCfg<T>::GPT, SpmvCfg<T>::NT>(A, x, pro, epi, st);
+template <typename T, int BS, class Pro, class Gx, class Epi>
+inline void launch_spmv(const lspcg_mat* A, Gx gx, Pro pro, Epi epi, hipStream_t st) {
+  if constexpr (sizeof(T) == 8) {
+    if (A->storage_dtype() == LSPCG_F32) {
+      launch_spmv_cfg<T, float, BS, SpmvCfg<T>::THREADS, SpmvCfg<T>::GPT, SpmvCfg<T>::NT>(A, gx, pro, epi, st);
+      return;
+    }
+  }
+  launch_spmv_cfg<T, T, BS, SpmvCfg<T>::THREADS, SpmvCfg<T>::GPT, SpmvCfg<T>::NT>(A, gx, pro, epi, st);
 }
 
-// Dispatch on the matrix block size.
-template <typename T, class Pro, class Epi>
-inline int launch_spmv_any(const lspcg_mat* A, const T* x, Pro pro, Epi epi, hipStream_t st) {
+// Dispatch on the matrix block size; `gx` is a gather functor.
+template <typename T, class Pro, class Gx, class Epi>
+inline int launch_spmv_gx(const lspcg_mat* A, Gx gx, Pro pro, Epi epi, hipStream_t st) {
   if (A->block_size == 1) {
-    launch_spmv<T, 1>(A, x, pro, epi, st);
+    launch_spmv<T, 1>(A, gx, pro, epi, st);
   } else if (A->block_size == 3) {
-    launch_spmv<T, 3>(A, x, pro, epi, st);
+    launch_spmv<T, 3>(A, gx, pro, epi, st);
   } else {
     set_error("unsupported block size " + std::to_string(A->block_size));
     return LSPCG_ERR_UNSUPPORTED;
   }
   return LSPCG_OK;
+}
+
+template <typename T, class Pro, class Epi>
+inline int launch_spmv_any(const lspcg_mat* A, const T* x, Pro pro, Epi epi, hipStream_t st) {
+  return launch_spmv_gx<T>(A, GatherVec<T>{x}, pro, epi, st);
 }
 
 }  // namespace lspcg

@@ -5,4 +5,4 @@ tag=${1:-r1}
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/prof_$tag
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_$tag -o bench -- python3 bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof_$tag/bench.json 2> gpurun_out/prof_$tag/bench.err
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o bench -- python3 bench.py --steps 3 --warmup 1 --no-cpu > gpurun_out/prof_$tag/bench.json 2> gpurun_out/prof_$tag/bench.err
