@@ -3,17 +3,27 @@
 // and MPLayer (basic_layers.py:145-225, PyG 2.6.1 source_to_target flow: x_i = x[dst =
 // edge_index[1]], x_j = x[src = edge_index[0]], messages summed at dst).  fp32.
 //
-// Layout (DESIGN.md "GNN"): edges are kept in CSC order (sorted by dst, then by original
-// edge id) for the whole forward.  One message-passing layer is ONE kernel: a 256-thread
-// workgroup owns 256 destination nodes and streams their incoming edges in chunks of 512
-// (coalesced edge-feature reads/writes, x rows gathered).  Per edge a thread computes the
-// shared LayerNorm(48) statistics, the message MLP and the edge MLP, writes the updated
-// edge feature in place and drops the message into LDS; after a barrier every node thread
-// sums its messages in CSC order (deterministic, no atomics), applies LayerNorm(16) + the
-// node MLP + residual and writes the next node state.  Messages never touch HBM.
+// MFMA design (DESIGN.md "GNN"): every MLP runs on v_mfma_f32_16x16x4_f32 (exact fp32
+// FMA chains).  A wave owns a tile of 16 items (edges or nodes); lane l = (item l&15,
+// quarter q = l>>4).  Layers compute H^T = W * IN^T: the weights are the A operand (one f32
+// per lane per 4-deep K step, pre-arranged on the host into per-lane "fragments" held in
+// LDS), the activations the B operand.  The 16x16 accumulator of one layer (lane l: rows
+// 4q..4q+3 of item l&15) is directly the next layer's B operand with K slot q of step s =
+// hidden unit 4q+s -- no data movement between layers.  Input features are laid out so a
+// lane's 4 K-slots of each 16-wide block are 4 contiguous floats: every row read/write is a
+// 16-B access.  LayerNorm affine parameters are folded into the first Linear on the host.
+//
+// One message-passing layer is ONE kernel: a 256-thread workgroup owns 256 destination
+// nodes and streams their incoming edges (kept in CSC order for the whole forward) in
+// chunks of 256; per edge tile it computes the shared LayerNorm(48) statistics, the message
+// MLP and the edge MLP (two interleaved MFMA chains), writes the updated edge feature in
+// place and drops the message into LDS; after a barrier every node lane sums its messages
+// in CSC order (deterministic, no atomics).  The node MLP then runs on 16-node tiles.
+// Messages never touch HBM.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <cmath>
 #include <memory>
 #include <string>
 #include <vector>
@@ -23,77 +33,75 @@
 namespace lspcg {
 
 constexpr int H = 16;        // hidden = node_features = edge_features
-constexpr int CE = 512;      // edges per LDS chunk (512 x 16 x 4 B = 32 KiB)
+constexpr int CE = 256;      // edges per LDS chunk (256 x 16 x 4 B = 16 KiB)
 constexpr int kMaxIn = 32;   // encoder input features supported
 
-// FeedForward(in, out, hidden=16, num_layers=2) parameter block:
+using f4 = float __attribute__((ext_vector_type(4)));
+
+// FeedForward(in, out, hidden=16, num_layers=2) parameter block of the packed blob:
 //   [W1 (16 x in) | b1 (16) | W2 (16 x 16) | b2 (16) | W3 (out x 16) | b3 (out)]
 __host__ __device__ constexpr int ff_size(int in, int out) { return H * in + H + H * H + H + out * H + out; }
 
+// Fragment block of one FeedForward (floats): [A1 (S1 x 64) | C1 (64 x 4) | A2 (4 x 64) |
+// C2 (64 x 4) | A3 (4 x 64) | C3 (64 x 4)]
+__host__ __device__ constexpr int frag_size(int s1) { return s1 * 64 + 5 * 256; }
+
 __device__ __forceinline__ float gelu(float v) { return 0.5f * v * (1.0f + erff(v * 0.7071067811865476f)); }
+__device__ __forceinline__ f4 gelu4(f4 a) { return f4{gelu(a.x), gelu(a.y), gelu(a.z), gelu(a.w)}; }
 
-template <int IN>
-__device__ __forceinline__ void linear16(const float* __restrict__ W, const float* __restrict__ b, const float* in,
-                                         float* out) {
+__device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float comp(f4 v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+
+// layers 2 and 3 of an FF on the layer-1 pre-activation `h` (in accumulator layout)
+__device__ __forceinline__ f4 ff_tail(const float* fr, int s1, f4 h, int lane) {
+  const float* a2 = fr + s1 * 64 + 256;
+  const float* c2 = a2 + 256;
+  const float* a3 = c2 + 256;
+  const float* c3 = a3 + 256;
+  h = gelu4(h);
+  f4 h2 = *reinterpret_cast<const f4*>(c2 + lane * 4);
 #pragma unroll
-  for (int o = 0; o < H; ++o) {
-    float acc = b[o];
+  for (int s = 0; s < 4; ++s) h2 = mfma(a2[s * 64 + lane], comp(h, s), h2);
+  h2 = gelu4(h2);
+  f4 o = *reinterpret_cast<const f4*>(c3 + lane * 4);
 #pragma unroll
-    for (int i = 0; i < IN; ++i) acc = __builtin_fmaf(in[i], W[o * IN + i], acc);
-    out[o] = acc;
-  }
+  for (int s = 0; s < 4; ++s) o = mfma(a3[s * 64 + lane], comp(h2, s), o);
+  return o;
 }
 
-// hidden part of the FF after its first layer: GELU -> Linear16 -> GELU -> Linear(out)
-template <int OUT>
-__device__ __forceinline__ void ff_tail(const float* __restrict__ w2, const float* h1, float* out) {
-  float a[H], h2[H];
+// Two FFs with 48 inputs sharing the same B operand (message + edge MLP of an MPLayer),
+// interleaved so the two dependent MFMA chains overlap.
+__device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const float (&in)[12], int lane, f4& oa,
+                                       f4& ob) {
+  f4 ha = *reinterpret_cast<const f4*>(fa + 12 * 64 + lane * 4);
+  f4 hb = *reinterpret_cast<const f4*>(fb + 12 * 64 + lane * 4);
 #pragma unroll
-  for (int o = 0; o < H; ++o) a[o] = gelu(h1[o]);
-  linear16<H>(w2, w2 + H * H, a, h2);
-#pragma unroll
-  for (int o = 0; o < H; ++o) a[o] = gelu(h2[o]);
-  const float* W3 = w2 + H * H + H;
-  const float* b3 = W3 + OUT * H;
-#pragma unroll
-  for (int o = 0; o < OUT; ++o) {
-    float acc = b3[o];
-#pragma unroll
-    for (int i = 0; i < H; ++i) acc = __builtin_fmaf(a[i], W3[o * H + i], acc);
-    out[o] = acc;
+  for (int s = 0; s < 12; ++s) {
+    ha = mfma(fa[s * 64 + lane], in[s], ha);
+    hb = mfma(fb[s * 64 + lane], in[s], hb);
   }
+  oa = ff_tail(fa, 12, ha, lane);
+  ob = ff_tail(fb, 12, hb, lane);
 }
 
-// Encoder with a runtime input width, input row read straight from global memory
-// (loop over inputs outermost so no runtime-indexed register array is needed).
-__device__ __forceinline__ void ff_encode(const float* __restrict__ w, int in_n, const float* __restrict__ in,
-                                          float* out) {
-  float h1[H];
+template <int S1>
+__device__ __forceinline__ f4 ff_tile(const float* fr, const float (&in)[S1], int lane) {
+  f4 h = *reinterpret_cast<const f4*>(fr + S1 * 64 + lane * 4);
 #pragma unroll
-  for (int o = 0; o < H; ++o) h1[o] = w[H * in_n + o];
-  for (int i = 0; i < in_n; ++i) {
-    const float v = in[i];
-#pragma unroll
-    for (int o = 0; o < H; ++o) h1[o] = __builtin_fmaf(v, w[o * in_n + i], h1[o]);
-  }
-  ff_tail<H>(w + H * in_n + H, h1, out);
+  for (int s = 0; s < S1; ++s) h = mfma(fr[s * 64 + lane], in[s], h);
+  return ff_tail(fr, S1, h, lane);
 }
 
-__device__ __forceinline__ void ld16(const float* __restrict__ p, float* v) {
-  const float4* q = reinterpret_cast<const float4*>(p);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float4 t = q[j];
-    v[4 * j] = t.x;
-    v[4 * j + 1] = t.y;
-    v[4 * j + 2] = t.z;
-    v[4 * j + 3] = t.w;
-  }
-}
-__device__ __forceinline__ void st16(float* __restrict__ p, const float* v) {
-  float4* q = reinterpret_cast<float4*>(p);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) q[j] = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+__device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
+// 48-feature block layout of a lane: in[s], s = 4*block + c  <->  feature 16*block + 4q + c
+__device__ __forceinline__ void pack12(f4 b0, f4 b1, f4 b2, float (&v)[12]) {
+  v[0] = b0.x; v[1] = b0.y; v[2] = b0.z; v[3] = b0.w;
+  v[4] = b1.x; v[5] = b1.y; v[6] = b1.z; v[7] = b1.w;
+  v[8] = b2.x; v[9] = b2.y; v[10] = b2.z; v[11] = b2.w;
 }
 
 // ---------------------------------------------------------------------------
@@ -134,159 +142,152 @@ __global__ void k_csc_sort(int64_t N, const int64_t* __restrict__ ei, int64_t E,
 }
 
 // ---------------------------------------------------------------------------
-// Encoders / decoder
+// Encoders / decoder (16-item MFMA tiles, 4 waves per workgroup, grid-stride over tiles)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_node_enc(int64_t N, int fin, const float* __restrict__ w,
-                                                       const float* __restrict__ x, float* __restrict__ h) {
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < N; i += int64_t(gridDim.x) * blockDim.x) {
-    float out[H];
-    ff_encode(w, fin, x + i * fin, out);
-    st16(h + i * H, out);
-  }
-}
-
-__global__ void __launch_bounds__(kThreads) k_edge_enc(int64_t E, int fe, const float* __restrict__ w,
-                                                       const float* __restrict__ ea, const int32_t* __restrict__ perm,
-                                                       float* __restrict__ ecsc) {
-  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < E; k += int64_t(gridDim.x) * blockDim.x) {
-    float out[H];
-    const int64_t oe = perm[k];
-    ff_encode(w, fe, ea + oe * fe, out);
-    st16(ecsc + k * H, out);
+// Encoder input layout: K slot q of step s = input feature 4s + q (zero past `fin`).
+template <bool EDGE>
+__global__ void __launch_bounds__(256) k_encode(int64_t M, int fin, const float* __restrict__ fr,
+                                               const float* __restrict__ in, const int32_t* __restrict__ perm,
+                                               float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, it = lane & 15, q = lane >> 4;
+  const int s1 = (fin + 3) / 4;
+  const int64_t ntiles = (M + 15) / 16;
+  for (int64_t t = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < ntiles; t += int64_t(gridDim.x) * 4) {
+    const int64_t m = t * 16 + it;
+    const bool valid = m < M;
+    const int64_t mm = valid ? m : M - 1;
+    const int64_t row = EDGE ? int64_t(perm[mm]) : mm;
+    f4 h = ld4(fr + s1 * 64 + lane * 4);
+    for (int s = 0; s < s1; ++s) {
+      const int f = 4 * s + q;
+      const float v = f < fin ? in[row * fin + f] : 0.f;
+      h = mfma(fr[s * 64 + lane], v, h);
+    }
+    const f4 o = ff_tail(fr, s1, h, lane);
+    if (valid) st4(out + mm * H + 4 * q, o);
   }
 }
 
 // out[e] = edge_dec(cat[e_attr, x[src], x[dst]])  (gnns.py:88-95; original edge order)
 template <int OUT>
-__global__ void __launch_bounds__(kThreads) k_edge_dec(int64_t E, const float* __restrict__ w,
-                                                       const int64_t* __restrict__ ei, const int32_t* __restrict__ inv,
-                                                       const float* __restrict__ ecsc, const float* __restrict__ x,
-                                                       float* __restrict__ out) {
-  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += int64_t(gridDim.x) * blockDim.x) {
-    float in[3 * H], h1[H], o[OUT];
-    ld16(ecsc + int64_t(inv[e]) * H, in);
-    ld16(x + ei[e] * H, in + H);
-    ld16(x + ei[E + e] * H, in + 2 * H);
-    linear16<3 * H>(w, w + 3 * H * H, in, h1);
-    ff_tail<OUT>(w + 3 * H * H + H, h1, o);
+__global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __restrict__ fr,
+                                                 const int64_t* __restrict__ ei, const int32_t* __restrict__ inv,
+                                                 const float* __restrict__ ecsc, const float* __restrict__ x,
+                                                 float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, it = lane & 15, q = lane >> 4;
+  const int64_t ntiles = (E + 15) / 16;
+  for (int64_t t = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < ntiles; t += int64_t(gridDim.x) * 4) {
+    const int64_t e = t * 16 + it;
+    const bool valid = e < E;
+    const int64_t ee = valid ? e : E - 1;
+    float in[12];
+    pack12(ld4(ecsc + int64_t(inv[ee]) * H + 4 * q), ld4(x + ei[ee] * H + 4 * q), ld4(x + ei[E + ee] * H + 4 * q), in);
+    const f4 o = ff_tile<12>(fr, in, lane);
+    if (valid) {
 #pragma unroll
-    for (int j = 0; j < OUT; ++j) out[e * OUT + j] = o[j];
+      for (int r = 0; r < 4; ++r)
+        if (4 * q + r < OUT) out[ee * OUT + 4 * q + r] = comp(o, r);
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
 // One MPLayer (basic_layers.py:193-225) as one kernel
 // ---------------------------------------------------------------------------
-struct LayerW {
-  const float* node;  // [ln_g 16 | ln_b 16 | FF(16 -> 16)]
-  const float* edge;  // [ln_g 48 | ln_b 48 | FF(48 -> 16)]
-  const float* msg;   // [ln_g 48 | ln_b 48 | FF(48 -> 16)]
-};
+constexpr int kFrag48 = frag_size(12);
+constexpr int kFrag16 = frag_size(4);
+constexpr int kLayerFrag = 2 * kFrag48 + kFrag16;  // [msg | edge | node]
 
-__device__ __forceinline__ void ln_ff48(const float* __restrict__ p, const float* xn, float* out) {
-  const float* g = p;
-  const float* bb = p + 3 * H;
-  const float* w = p + 6 * H;
-  float in[3 * H], h1[H];
-#pragma unroll
-  for (int i = 0; i < 3 * H; ++i) in[i] = __builtin_fmaf(xn[i], g[i], bb[i]);
-  linear16<3 * H>(w, w + 3 * H * H, in, h1);
-  ff_tail<H>(w + 3 * H * H + H, h1, out);
-}
-
-__global__ void __launch_bounds__(kThreads) k_mp_layer(int64_t N, LayerW lw, int node_res, int edge_res,
-                                                       const int32_t* __restrict__ ptr, const int32_t* __restrict__ src,
-                                                       const int32_t* __restrict__ dst, const float* __restrict__ x,
-                                                       float* __restrict__ e, float* __restrict__ xout) {
-  __shared__ float msg[CE * H];
-  const int tid = threadIdx.x;
-  const int64_t n0 = int64_t(blockIdx.x) * kThreads;
-  const int64_t n1 = n0 + kThreads < N ? n0 + kThreads : N;
+__global__ void __launch_bounds__(256) k_mp_layer(int64_t N, const float* __restrict__ frag, int node_res,
+                                                 int edge_res, const int32_t* __restrict__ ptr,
+                                                 const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
+                                                 const float* __restrict__ x, float* __restrict__ e,
+                                                 float* __restrict__ xout) {
+  __shared__ __attribute__((aligned(16))) float wl[kLayerFrag];
+  __shared__ __attribute__((aligned(16))) float msg[CE * H];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, it = lane & 15, q = lane >> 4;
+  for (int i = tid; i < kLayerFrag / 4; i += 256) reinterpret_cast<f4*>(wl)[i] = ld4(frag + 4 * i);
+  __syncthreads();
+  const float* fmsg = wl;
+  const float* fedge = wl + kFrag48;
+  const float* fnode = wl + 2 * kFrag48;
+  const int64_t n0 = int64_t(blockIdx.x) * 256;
+  const int64_t n1 = n0 + 256 < N ? n0 + 256 : N;
   const int64_t k0 = ptr[n0], k1 = ptr[n1];
-  const int64_t i = n0 + tid;
-  const bool active = i < n1;
-  int64_t my_b = 0, my_e = 0;
-  if (active) {
-    my_b = ptr[i];
-    my_e = ptr[i + 1];
-  }
-  float agg[H];
+  f4 agg[4];
 #pragma unroll
-  for (int o = 0; o < H; ++o) agg[o] = 0.f;
+  for (int j = 0; j < 4; ++j) agg[j] = f4{0.f, 0.f, 0.f, 0.f};
 
   for (int64_t c0 = k0; c0 < k1; c0 += CE) {
     const int64_t c1 = c0 + CE < k1 ? c0 + CE : k1;
-    for (int64_t k = c0 + tid; k < c1; k += kThreads) {
-      float h[3 * H];
-      ld16(x + int64_t(dst[k]) * H, h);          // x_i (target)
-      ld16(x + int64_t(src[k]) * H, h + H);      // x_j (source)
-      ld16(e + k * H, h + 2 * H);                // edge attr
-      float mean = 0.f;
+    const int ntile = int((c1 - c0 + 15) / 16);
+    for (int t = wave; t < ntile; t += 4) {  // wave-uniform: MFMA needs EXEC all ones
+      const int64_t k = c0 + t * 16 + it;
+      const bool valid = k < c1;
+      const int64_t kk = valid ? k : c1 - 1;
+      const f4 xd = ld4(x + int64_t(dst[kk]) * H + 4 * q);  // x_i (target)
+      const f4 xs = ld4(x + int64_t(src[kk]) * H + 4 * q);  // x_j (source)
+      const f4 ea = ld4(e + kk * H + 4 * q);                // edge attr
+      // LayerNorm(48) statistics: 12 values per lane, 4 lanes per edge (xor 16, 32)
+      float sum = (xd.x + xd.y + xd.z + xd.w) + (xs.x + xs.y + xs.z + xs.w) + (ea.x + ea.y + ea.z + ea.w);
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      const float mean = sum * (1.0f / 48.0f);
+      float v[12];
+      pack12(xd, xs, ea, v);
+      float sq = 0.f;
 #pragma unroll
-      for (int q = 0; q < 3 * H; ++q) mean += h[q];
-      mean *= (1.0f / (3 * H));
-      float var = 0.f;
-#pragma unroll
-      for (int q = 0; q < 3 * H; ++q) {
-        const float dv = h[q] - mean;
-        var = __builtin_fmaf(dv, dv, var);
+      for (int i = 0; i < 12; ++i) {
+        v[i] -= mean;
+        sq = __builtin_fmaf(v[i], v[i], sq);
       }
-      var *= (1.0f / (3 * H));
-      const float rstd = 1.0f / sqrtf(var + 1e-5f);
-      float xn[3 * H];
+      sq += __shfl_xor(sq, 16, 64);
+      sq += __shfl_xor(sq, 32, 64);
+      const float rstd = 1.0f / sqrtf(sq * (1.0f / 48.0f) + 1e-5f);
 #pragma unroll
-      for (int q = 0; q < 3 * H; ++q) xn[q] = (h[q] - mean) * rstd;
-      float m[H], u[H];
-      ln_ff48(lw.msg, xn, m);
-      ln_ff48(lw.edge, xn, u);
-      if (edge_res) {
-#pragma unroll
-        for (int o = 0; o < H; ++o) u[o] += h[2 * H + o];
+      for (int i = 0; i < 12; ++i) v[i] *= rstd;
+      f4 m, u;
+      ff2_48(fmsg, fedge, v, lane, m, u);
+      if (edge_res) u += ea;
+      if (valid) {
+        st4(e + k * H + 4 * q, u);
+        st4(msg + (k - c0) * H + 4 * q, m);
       }
-      st16(e + k * H, u);
-      float* ms = msg + (k - c0) * H;
-#pragma unroll
-      for (int o = 0; o < H; ++o) ms[o] = m[o];
     }
     __syncthreads();
-    if (active) {
-      const int64_t kb = my_b > c0 ? my_b : c0;
-      const int64_t ke = my_e < c1 ? my_e : c1;
-      for (int64_t k = kb; k < ke; ++k) {
-        const float* ms = msg + (k - c0) * H;
 #pragma unroll
-        for (int o = 0; o < H; ++o) agg[o] += ms[o];
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = n0 + (wave + 4 * j) * 16 + it;
+      if (i < n1) {
+        const int64_t kb = ptr[i] > c0 ? ptr[i] : c0;
+        const int64_t ke = ptr[i + 1] < c1 ? ptr[i + 1] : c1;
+        for (int64_t kq = kb; kq < ke; ++kq) agg[j] += ld4(msg + (kq - c0) * H + 4 * q);
       }
     }
     __syncthreads();
   }
-  if (!active) return;
   // update(): node_mlp(aggr) with LayerNorm(16) pre-norm; residual (basic_layers.py:203-206, 224-225)
-  float mean = 0.f;
 #pragma unroll
-  for (int o = 0; o < H; ++o) mean += agg[o];
-  mean *= (1.0f / H);
-  float var = 0.f;
+  for (int j = 0; j < 4; ++j) {
+    const int64_t i = n0 + (wave + 4 * j) * 16 + it;
+    const f4 a = agg[j];
+    float sum = a.x + a.y + a.z + a.w;
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float mean = sum * (1.0f / 16.0f);
+    float v[4] = {a.x - mean, a.y - mean, a.z - mean, a.w - mean};
+    float sq = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+    sq += __shfl_xor(sq, 16, 64);
+    sq += __shfl_xor(sq, 32, 64);
+    const float rstd = 1.0f / sqrtf(sq * (1.0f / 16.0f) + 1e-5f);
 #pragma unroll
-  for (int o = 0; o < H; ++o) {
-    const float dv = agg[o] - mean;
-    var = __builtin_fmaf(dv, dv, var);
+    for (int r = 0; r < 4; ++r) v[r] *= rstd;
+    f4 o = ff_tile<4>(fnode, v, lane);
+    if (i < n1) {
+      if (node_res) o += ld4(x + i * H + 4 * q);
+      st4(xout + i * H + 4 * q, o);
+    }
   }
-  var *= (1.0f / H);
-  const float rstd = 1.0f / sqrtf(var + 1e-5f);
-  float in[H], h1[H], out[H];
-#pragma unroll
-  for (int o = 0; o < H; ++o) in[o] = __builtin_fmaf((agg[o] - mean) * rstd, lw.node[o], lw.node[H + o]);
-  const float* w = lw.node + 2 * H;
-  linear16<H>(w, w + H * H, in, h1);
-  ff_tail<H>(w + H * H + H, h1, out);
-  if (node_res) {
-    float xo[H];
-    ld16(x + i * H, xo);
-#pragma unroll
-    for (int o = 0; o < H; ++o) out[o] += xo[o];
-  }
-  st16(xout + i * H, out);
 }
 
 static int egrid(int64_t n) {
@@ -294,18 +295,92 @@ static int egrid(int64_t n) {
   return int(g < 1 ? 1 : (g > 16384 ? 16384 : g));
 }
 
+static int tgrid(int64_t items) {  // 64 items (4 waves x 16) per workgroup
+  int64_t g = (items + 63) / 64;
+  return int(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
 }  // namespace lspcg
 
 using namespace lspcg;
 
+// ---------------------------------------------------------------------------
+// Host-side fragment preparation
+// ---------------------------------------------------------------------------
+namespace {
+
+struct FF {  // views into the packed (reference-layout) blob
+  const float* W1;
+  const float* b1;
+  const float* W2;
+  const float* b2;
+  const float* W3;
+  const float* b3;
+  int in, out;
+};
+
+FF ff_at(const float* w, int in, int out) {
+  FF f;
+  f.in = in;
+  f.out = out;
+  f.W1 = w;
+  f.b1 = w + H * in;
+  f.W2 = f.b1 + H;
+  f.b2 = f.W2 + H * H;
+  f.W3 = f.b2 + H;
+  f.b3 = f.W3 + out * H;
+  return f;
+}
+
+// Append the fragment block of `f` (LayerNorm affine gamma/beta folded into layer 1 when given).
+// feat(s, q) = input feature in K slot q of step s (-1 = zero).
+template <class Feat>
+void emit_frag(std::vector<float>& o, const FF& f, int s1, Feat feat, const float* gamma, const float* beta) {
+  std::vector<double> W1(H * f.in), b1(H);
+  for (int i = 0; i < H; ++i) {
+    double bb = f.b1[i];
+    for (int k = 0; k < f.in; ++k) {
+      const double w = f.W1[i * f.in + k];
+      W1[i * f.in + k] = gamma ? w * gamma[k] : w;
+      if (beta) bb += w * beta[k];
+    }
+    b1[i] = bb;
+  }
+  for (int s = 0; s < s1; ++s)
+    for (int l = 0; l < 64; ++l) {
+      const int fi = feat(s, l >> 4);
+      o.push_back(fi >= 0 && fi < f.in ? float(W1[(l & 15) * f.in + fi]) : 0.f);
+    }
+  for (int l = 0; l < 64; ++l)
+    for (int r = 0; r < 4; ++r) o.push_back(float(b1[4 * (l >> 4) + r]));
+  for (int s = 0; s < 4; ++s)
+    for (int l = 0; l < 64; ++l) o.push_back(f.W2[(l & 15) * H + 4 * (l >> 4) + s]);
+  for (int l = 0; l < 64; ++l)
+    for (int r = 0; r < 4; ++r) o.push_back(f.b2[4 * (l >> 4) + r]);
+  for (int s = 0; s < 4; ++s)
+    for (int l = 0; l < 64; ++l) {
+      const int i = l & 15;
+      o.push_back(i < f.out ? f.W3[i * H + 4 * (l >> 4) + s] : 0.f);
+    }
+  for (int l = 0; l < 64; ++l)
+    for (int r = 0; r < 4; ++r) {
+      const int i = 4 * (l >> 4) + r;
+      o.push_back(i < f.out ? f.b3[i] : 0.f);
+    }
+}
+
+auto feat48 = [](int s, int q) { return (s >> 2) * 16 + 4 * q + (s & 3); };
+auto feat16 = [](int s, int q) { return 4 * q + s; };
+auto featenc = [](int s, int q) { return 4 * s + q; };
+
+}  // namespace
+
 struct lspcg_gnn {
   lspcg_ctx* ctx = nullptr;
   lspcg_gnn_desc d{};
-  float* w = nullptr;
-  int64_t nw = 0;
-  // offsets into w
+  float* frag = nullptr;  // device fragment blob
   int64_t o_node_enc = 0, o_edge_enc = 0, o_dec = 0;
-  std::vector<int64_t> o_layer;  // per layer: node, edge, msg
+  std::vector<int64_t> o_layer;  // per layer: [msg | edge | node] fragment block
   // workspace
   int64_t capN = -1, capE = -1;
   float *xa = nullptr, *xb = nullptr, *ecsc = nullptr;
@@ -372,24 +447,32 @@ int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* we
   std::unique_ptr<lspcg_gnn> g(new lspcg_gnn());
   g->ctx = ctx;
   g->d = d;
-  g->nw = need;
-  LSPCG_HIP(hipMalloc(&g->w, sizeof(float) * need));
-  LSPCG_HIP(hipMemcpyAsync(g->w, weights, sizeof(float) * need, hipMemcpyDefault, ctx->stream));
-  LSPCG_HIP(hipStreamSynchronize(ctx->stream));
+  std::vector<float> w(need);
+  LSPCG_HIP(hipMemcpy(w.data(), weights, sizeof(float) * need, hipMemcpyDefault));  // host or device source
+  std::vector<float> fr;
   int64_t o = 0;
-  g->o_node_enc = o;
+  g->o_node_enc = int64_t(fr.size());
+  emit_frag(fr, ff_at(w.data() + o, d.node_in, H), (d.node_in + 3) / 4, featenc, nullptr, nullptr);
   o += ff_size(d.node_in, H);
-  g->o_edge_enc = o;
+  g->o_edge_enc = int64_t(fr.size());
+  emit_frag(fr, ff_at(w.data() + o, d.edge_in, H), (d.edge_in + 3) / 4, featenc, nullptr, nullptr);
   o += ff_size(d.edge_in, H);
   for (int l = 0; l < d.num_mp_layers; ++l) {
-    g->o_layer.push_back(o);
+    const float* node = w.data() + o;  // [ln_g 16 | ln_b 16 | FF(16->16)]
     o += 2 * H + ff_size(H, H);
-    g->o_layer.push_back(o);
+    const float* edge = w.data() + o;  // [ln_g 48 | ln_b 48 | FF(48->16)]
     o += 6 * H + ff_size(3 * H, H);
-    g->o_layer.push_back(o);
+    const float* msgp = w.data() + o;
     o += 6 * H + ff_size(3 * H, H);
+    g->o_layer.push_back(int64_t(fr.size()));
+    emit_frag(fr, ff_at(msgp + 6 * H, 3 * H, H), 12, feat48, msgp, msgp + 3 * H);
+    emit_frag(fr, ff_at(edge + 6 * H, 3 * H, H), 12, feat48, edge, edge + 3 * H);
+    emit_frag(fr, ff_at(node + 2 * H, H, H), 4, feat16, node, node + H);
   }
-  g->o_dec = o;
+  g->o_dec = int64_t(fr.size());
+  emit_frag(fr, ff_at(w.data() + o, 3 * H, d.edge_out), 12, feat48, nullptr, nullptr);
+  LSPCG_HIP(hipMalloc(&g->frag, sizeof(float) * fr.size()));
+  LSPCG_HIP(hipMemcpy(g->frag, fr.data(), sizeof(float) * fr.size(), hipMemcpyHostToDevice));
   *out = g.release();
   return LSPCG_OK;
 }
@@ -416,27 +499,27 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
   hipLaunchKernelGGL(k_csc_sort, dim3(egrid(N)), dim3(kThreads), 0, st, N, edge_index, E, g->ptr, g->perm, g->inv,
                      g->src, g->dst);
   // encoders
-  hipLaunchKernelGGL(k_node_enc, dim3(egrid(N)), dim3(kThreads), 0, st, N, d.node_in, g->w + g->o_node_enc, x, g->xa);
-  hipLaunchKernelGGL(k_edge_enc, dim3(egrid(E)), dim3(kThreads), 0, st, E, d.edge_in, g->w + g->o_edge_enc,
+  hipLaunchKernelGGL(k_encode<false>, dim3(tgrid(N)), dim3(256), 0, st, N, d.node_in, g->frag + g->o_node_enc, x,
+                     static_cast<const int32_t*>(nullptr), g->xa);
+  hipLaunchKernelGGL(k_encode<true>, dim3(tgrid(E)), dim3(256), 0, st, E, d.edge_in, g->frag + g->o_edge_enc,
                      edge_attr, g->perm, g->ecsc);
   // message passing
   float* xc = g->xa;
   float* xn = g->xb;
-  const unsigned lg = unsigned((N + kThreads - 1) / kThreads);
+  const unsigned lg = unsigned((N + 255) / 256);
   for (int l = 0; l < d.num_mp_layers; ++l) {
-    LayerW lw{g->w + g->o_layer[3 * l], g->w + g->o_layer[3 * l + 1], g->w + g->o_layer[3 * l + 2]};
-    hipLaunchKernelGGL(k_mp_layer, dim3(lg), dim3(kThreads), 0, st, N, lw, d.node_residual, d.edge_residual, g->ptr,
-                       g->src, g->dst, xc, g->ecsc, xn);
+    hipLaunchKernelGGL(k_mp_layer, dim3(lg), dim3(256), 0, st, N, g->frag + g->o_layer[l], d.node_residual,
+                       d.edge_residual, g->ptr, g->src, g->dst, xc, g->ecsc, xn);
     std::swap(xc, xn);
   }
   // decoder
-  const float* wd = g->w + g->o_dec;
+  const float* fd = g->frag + g->o_dec;
   if (d.edge_out == 1)
-    hipLaunchKernelGGL(k_edge_dec<1>, dim3(egrid(E)), dim3(kThreads), 0, st, E, wd, edge_index, g->inv, g->ecsc, xc, out);
+    hipLaunchKernelGGL(k_edge_dec<1>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, g->inv, g->ecsc, xc, out);
   else if (d.edge_out == 4)
-    hipLaunchKernelGGL(k_edge_dec<4>, dim3(egrid(E)), dim3(kThreads), 0, st, E, wd, edge_index, g->inv, g->ecsc, xc, out);
+    hipLaunchKernelGGL(k_edge_dec<4>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, g->inv, g->ecsc, xc, out);
   else
-    hipLaunchKernelGGL(k_edge_dec<9>, dim3(egrid(E)), dim3(kThreads), 0, st, E, wd, edge_index, g->inv, g->ecsc, xc, out);
+    hipLaunchKernelGGL(k_edge_dec<9>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, g->inv, g->ecsc, xc, out);
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
@@ -445,7 +528,7 @@ int lspcg_gnn_destroy(lspcg_gnn* g) {
   if (!g) return LSPCG_OK;
   (void)hipSetDevice(g->ctx->device);
   gnn_free_ws(g);
-  (void)hipFree(g->w);
+  (void)hipFree(g->frag);
   delete g;
   return LSPCG_OK;
 }

@@ -74,94 +74,18 @@ struct ProDone {
   __device__ __forceinline__ bool exit() const { return S->done != 0; }
 };
 
-// r ping-pong: r_k lives in R[k & 1]; r_0 in R[0].
-template <typename T>
-struct RBuf {
-  T* R0;
-  T* R1;
-  __device__ __forceinline__ T* cur(int64_t k) const { return (k & 1) ? R1 : R0; }
-  __device__ __forceinline__ T* prev(int64_t k) const { return k == 0 ? R0 : cur(k - 1); }
-};
-
-// gather of r_k = r_{k-1} - α_{k-1} q_{k-1} (scipy `r -= alpha*q`), identity at k = 0
-template <typename T>
-struct GatherR {
-  RBuf<T> R;
-  const T* q;
-  const PcgState* S;
-  const T* rold = nullptr;
-  T alpha = T(0);
-  bool upd = false;
-  __device__ __forceinline__ void prepare() {
-    const int64_t k = S->iter;
-    upd = k > 0;
-    alpha = T(S->alpha);
-    rold = R.prev(k);
-  }
-  // both loads unconditional, select afterwards: a select between a register and a load on a
-  // runtime flag makes hipcc branch around every load (cdna_hip_programming.md, 4(c))
-  __device__ __forceinline__ T operator()(int64_t j) const {
-    const T a = gld(rold + j);
-    const T b = gld(q + j);
-    const T u = a - alpha * b;
-    return upd ? u : a;
-  }
-};
-
-// gather of p_k = p_{k-1}*β + z_k (scipy `p *= beta; p += z`), p_0 = z_0; p_k in P[k & 1]
-template <typename T>
-struct GatherP {
-  const T* zsrc;  // z, or nullptr for CG (z = r_k)
-  RBuf<T> R;
-  const T* P0;
-  const T* P1;
-  const PcgState* S;
-  const T* z = nullptr;
-  const T* pold = nullptr;
-  T beta = T(0);
-  bool first = true;
-  __device__ __forceinline__ void prepare() {
-    const int64_t k = S->iter;
-    first = k == 0;
-    pold = (k & 1) ? P0 : P1;
-    z = zsrc ? zsrc : R.cur(k);
-    beta = first ? T(0) : T(S->rho) / T(S->rho_prev);
-  }
-  __device__ __forceinline__ T operator()(int64_t j) const {
-    const T a = gld(z + j);
-    const T b = gld(pold + j);
-    const T u = (b * beta) + a;
-    return first ? a : u;
-  }
-};
-
-// KA (ext_spai): own-row r update + ‖r‖², t = Lᵀ r (scaled variant: (Lᵀ r)/d)
+// KA (ext_spai): t = Lᵀ r  (scaled variant: t = (Lᵀ r)/d)
 template <typename T, bool SCALED>
-struct EpiRT {
-  static constexpr int NDOT = 1;
-  GatherR<T> g;
+struct EpiT {
+  static constexpr int NDOT = 0;
   T* t;
   const T* d;
-  PcgState* S;
-  double* partials;
-  unsigned* ticket;
-  T* rnew = nullptr;
-  __device__ __forceinline__ void prepare() {
-    g.prepare();
-    rnew = g.R.cur(S->iter);
-  }
-  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
-    const T ri = g(i);
-    if (g.upd) gst(rnew + i, ri);
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ void row(int64_t i, T s, DD*) const {
     if constexpr (SCALED) gst(t + i, s / gld(d + i));
     else gst(t + i, s);
-    dd_fma(dots[0], double(ri), double(ri));
   }
-  __device__ __forceinline__ void fin(const double* v) const {
-    const double rr = round_to<T>(v[0]);
-    S->rr = rr;
-    if (S->hist) S->hist[S->iter] = double(tsqrt<T>(T(rr)));
-  }
+  __device__ __forceinline__ void fin(const double*) const {}
 };
 
 // KB: z = L t + ε r  (scaled: z = L t + (ε r)/d);  ρ = r·z
@@ -169,14 +93,13 @@ template <typename T, bool SCALED>
 struct EpiZ {
   static constexpr int NDOT = 1;
   T* z;
-  RBuf<T> R;
+  const T* r;
   const T* d;
   T eps;
   PcgState* S;
   double* partials;
   unsigned* ticket;
-  const T* r = nullptr;
-  __device__ __forceinline__ void prepare() { r = R.cur(S->iter); }
+  __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
     const T ri = gld(r + i);
     T zi;
@@ -191,47 +114,36 @@ struct EpiZ {
   }
 };
 
-// KC: own-row p_k (stored) and deferred x += α_{k-1} p_{k-1}; q = A p_k ; π = p_k·q ; α_k
+// KD: q = A p ; π = p·q ; α = ρ/π
 template <typename T>
-struct EpiPQ {
+struct EpiQ {
   static constexpr int NDOT = 1;
-  GatherP<T> g;
-  T* P0;
-  T* P1;
-  T* x;
   T* q;
+  const T* p;
   PcgState* S;
   double* partials;
   unsigned* ticket;
-  T* pnew = nullptr;
-  T alpha_prev = T(0);
-  __device__ __forceinline__ void prepare() {
-    g.prepare();
-    pnew = (S->iter & 1) ? P1 : P0;
-    alpha_prev = T(S->alpha);
-  }
+  __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
-    const T pi = g(i);
-    gst(pnew + i, pi);
-    if (!g.first) gst(x + i, gld(x + i) + alpha_prev * gld(g.pold + i));
     gst(q + i, s);
-    dd_fma(dots[0], double(pi), double(s));
+    dd_fma(dots[0], double(gld(p + i)), double(s));
   }
   __device__ __forceinline__ void fin(const double* v) const {
     const double pq = round_to<T>(v[0]);
     S->pq = pq;
     S->alpha = double(T(S->rho) / T(pq));
-    S->iter = S->iter + 1;
   }
 };
 
-// init: r_0 = b - A x0 ; ‖r_0‖², ‖b‖²  (scipy: r = b - matvec(x) if x.any() else b.copy();
-// with x0 = 0 the subtraction returns b bit-for-bit)
-template <typename T>
+// init: r_0 = b - A x0 ; ‖r_0‖², ‖b‖² (+ z_0 = r_0/d, ρ_0 = r_0·z_0 for Jacobi)
+// (scipy: r = b - matvec(x) if x.any() else b.copy(); with x0 = 0 the subtraction returns b)
+template <typename T, int PRE>
 struct EpiResid {
-  static constexpr int NDOT = 2;
+  static constexpr int NDOT = PRE == LSPCG_PRECOND_DIAGONAL ? 3 : 2;
   T* r;
   const T* b;
+  const T* d;
+  T* z;
   PcgState* S;
   double* partials;
   unsigned* ticket;
@@ -242,13 +154,18 @@ struct EpiResid {
     r[i] = ri;
     dd_fma(dots[0], double(ri), double(ri));
     dd_fma(dots[1], double(bi), double(bi));
+    if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) {
+      const T zi = ri / d[i];
+      z[i] = zi;
+      dd_fma(dots[2], double(ri), double(zi));
+    }
   }
   __device__ __forceinline__ void fin(const double* v) const {
     S->rr = round_to<T>(v[0]);
     S->bb = round_to<T>(v[1]);
     const double bn = double(tsqrt<T>(T(S->bb)));
     S->atol = fmax(0.0, S->rtol * bn);
-    S->rho = S->rr;
+    S->rho = PRE == LSPCG_PRECOND_DIAGONAL ? round_to<T>(v[2]) : S->rr;
     S->alpha = 0.0;
     S->iter = 0;
     S->done = (bn == 0.0) ? 1 : 0;
@@ -256,80 +173,130 @@ struct EpiResid {
   }
 };
 
+// ---- elementwise kernels: 16-B vectors, 2 vectors per lane, grid <= kReduceGridMax
 template <typename T>
-struct V2T;
-template <>
-struct V2T<double> {
-  using type = double __attribute__((ext_vector_type(2)));
+struct VecT {
+  static constexpr int W = 16 / sizeof(T);
+  using type = T __attribute__((ext_vector_type(W)));
 };
-template <>
-struct V2T<float> {
-  using type = float __attribute__((ext_vector_type(2)));
-};
+constexpr int kElemUnroll = 2;
 
-// KA for CG / Jacobi: r_k = r_{k-1} - α q (elementwise, ping-pong), ‖r‖² (+ z = r/d, ρ = r·z)
-template <typename T, int PRE>
-__device__ __forceinline__ void r_elem(bool upd, T alpha, T ro, T qi, T& rn, const T* d, T* z, int64_t i, DD* dots) {
-  rn = upd ? ro - alpha * qi : ro;
-  dd_fma(dots[0], double(rn), double(rn));
-  if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) {
-    const T zi = rn / d[i];
-    z[i] = zi;
-    dd_fma(dots[1], double(rn), double(zi));
+template <typename T>
+static int elem_vec_grid(int64_t n) {
+  const int64_t nv = n / VecT<T>::W;
+  const int64_t g = (nv + int64_t(kThreads) * kElemUnroll - 1) / (int64_t(kThreads) * kElemUnroll);
+  return int(std::max<int64_t>(1, std::min<int64_t>(g, kReduceGridMax)));
+}
+
+// KC: x += α_{k-1} p_{k-1} (deferred, k > 0) ; p_k = p_{k-1}β + z (scipy `p *= beta; p += z`),
+// p_0 = z.  `Pro` = ProCheck for CG / Jacobi (top-of-loop test), ProDone for ext_spai.
+template <typename T, typename Pro>
+__global__ void __launch_bounds__(kThreads) k_update_p(int64_t n, Pro pro, const PcgState* S,
+                                                       const T* __restrict__ z, T* __restrict__ p,
+                                                       T* __restrict__ x) {
+  using V = typename VecT<T>::type;
+  constexpr int W = VecT<T>::W;
+  if (pro.exit()) return;
+  const bool first = S->iter == 0;
+  const T beta = first ? T(0) : T(S->rho) / T(S->rho_prev);
+  const T alpha = T(S->alpha);
+  const int64_t nv = n / W;
+  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t j0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j0 < nv; j0 += ts * kElemUnroll) {
+    V zz[kElemUnroll], pp[kElemUnroll], xx[kElemUnroll];
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        zz[u] = reinterpret_cast<const V*>(z)[j];
+        pp[u] = reinterpret_cast<const V*>(p)[j];
+        xx[u] = reinterpret_cast<const V*>(x)[j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        if (!first) reinterpret_cast<V*>(x)[j] = xx[u] + alpha * pp[u];
+        reinterpret_cast<V*>(p)[j] = first ? zz[u] : (pp[u] * beta) + zz[u];
+      }
+    }
+  }
+  for (int64_t i = nv * W + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += ts) {
+    const T pi = p[i];
+    if (!first) x[i] = x[i] + alpha * pi;
+    p[i] = first ? z[i] : (pi * beta) + z[i];
   }
 }
 
+// KE: r -= α q ; ‖r‖² (+ Jacobi z = r/d, ρ = r·z) ; iteration count
 template <typename T, int PRE>
-__global__ void __launch_bounds__(kThreads) k_update_r(int64_t n, PcgState* S, RBuf<T> R, const T* __restrict__ q,
-                                                       const T* __restrict__ d, T* __restrict__ z, double* partials,
-                                                       unsigned* ticket) {
-  using V2 = typename V2T<T>::type;
-  if (S->done) return;
+__global__ void __launch_bounds__(kThreads) k_update_r(int64_t n, PcgState* S, const T* __restrict__ q,
+                                                       T* __restrict__ r, const T* __restrict__ d, T* __restrict__ z,
+                                                       double* partials, unsigned* ticket) {
+  using V = typename VecT<T>::type;
+  constexpr int W = VecT<T>::W;
   constexpr int ND = PRE == LSPCG_PRECOND_DIAGONAL ? 2 : 1;
-  const int64_t k = S->iter;
-  const bool upd = k > 0;
+  if (S->done) return;
   const T alpha = T(S->alpha);
-  const T* ro = R.prev(k);
-  T* rn = R.cur(k);
   DD dots[ND];
 #pragma unroll
   for (int j = 0; j < ND; ++j) dots[j] = dd_zero();
-  const int64_t np = n >> 1;
-  const int64_t t0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, ts = int64_t(gridDim.x) * blockDim.x;
-  for (int64_t j = t0; j < np; j += ts) {
-    const V2 rr = reinterpret_cast<const V2*>(ro)[j];
-    const V2 qq = reinterpret_cast<const V2*>(q)[j];
-    V2 out;
-    T a0, a1;
-    r_elem<T, PRE>(upd, alpha, rr.x, qq.x, a0, d, z, 2 * j, dots);
-    r_elem<T, PRE>(upd, alpha, rr.y, qq.y, a1, d, z, 2 * j + 1, dots);
-    out.x = a0;
-    out.y = a1;
-    if (upd) reinterpret_cast<V2*>(rn)[j] = out;
+  const int64_t nv = n / W;
+  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
+  auto elem = [&](T ri, int64_t i) {
+    dd_fma(dots[0], double(ri), double(ri));
+    if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) {
+      const T zi = ri / d[i];
+      z[i] = zi;
+      dd_fma(dots[1], double(ri), double(zi));
+    }
+  };
+  for (int64_t j0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j0 < nv; j0 += ts * kElemUnroll) {
+    V rr[kElemUnroll], qq[kElemUnroll];
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        rr[u] = reinterpret_cast<const V*>(r)[j];
+        qq[u] = reinterpret_cast<const V*>(q)[j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        const V rn = rr[u] - alpha * qq[u];
+        reinterpret_cast<V*>(r)[j] = rn;
+#pragma unroll
+        for (int w = 0; w < W; ++w) elem(rn[w], j * W + w);
+      }
+    }
   }
-  if ((n & 1) && t0 == 0) {
-    const int64_t i = n - 1;
-    T a;
-    r_elem<T, PRE>(upd, alpha, ro[i], q[i], a, d, z, i, dots);
-    if (upd) rn[i] = a;
+  for (int64_t i = nv * W + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += ts) {
+    const T ri = r[i] - alpha * q[i];
+    r[i] = ri;
+    elem(ri, i);
   }
   grid_reduce_dd<ND>(dots, partials, ticket, [&](const double* v) {
     const double rr2 = round_to<T>(v[0]);
     S->rr = rr2;
-    S->rho_prev = S->rho;
-    S->rho = (PRE == LSPCG_PRECOND_DIAGONAL) ? round_to<T>(v[ND - 1]) : rr2;
-    if (S->hist) S->hist[S->iter] = double(tsqrt<T>(T(rr2)));
+    if constexpr (PRE != LSPCG_PRECOND_EXT_SPAI && PRE != LSPCG_PRECOND_EXT_SPAI_SCALED) {
+      S->rho_prev = S->rho;
+      S->rho = (PRE == LSPCG_PRECOND_DIAGONAL) ? round_to<T>(v[ND - 1]) : rr2;
+    }
+    const int64_t it = S->iter + 1;
+    S->iter = it;
+    if (S->hist) S->hist[it] = double(tsqrt<T>(T(rr2)));
   });
 }
 
 // after the loop: the deferred x += α_{k-1} p_{k-1} of the last completed iteration
 template <typename T>
-__global__ void __launch_bounds__(kThreads) k_x_fixup(int64_t n, const PcgState* S, const T* __restrict__ P0,
-                                                      const T* __restrict__ P1, T* __restrict__ x) {
-  const int64_t k = S->iter;
-  if (k < 1 || S->bb == 0.0) return;
+__global__ void __launch_bounds__(kThreads) k_x_fixup(int64_t n, const PcgState* S, const T* __restrict__ p,
+                                                      T* __restrict__ x) {
+  if (S->iter < 1 || S->bb == 0.0) return;
   const T alpha = T(S->alpha);
-  const T* p = ((k - 1) & 1) ? P1 : P0;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
     x[i] = x[i] + alpha * p[i];
 }
@@ -371,7 +338,7 @@ struct lspcg_solver {
   double eps = 0.0;
   hipStream_t stream = nullptr;  // solver-owned (capturable) stream
   void *x = nullptr, *b = nullptr, *r = nullptr, *z = nullptr, *t = nullptr, *p = nullptr, *q = nullptr,
-       *d = nullptr, *r1 = nullptr, *p1 = nullptr;
+       *d = nullptr;
   PcgState* S = nullptr;
   PcgState* hS = nullptr;  // pinned host mirror
   double* partials = nullptr;
@@ -445,63 +412,74 @@ template <typename T>
 static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
   const int64_t n = s->n;
   T* x = static_cast<T*>(s->x);
+  T* r = static_cast<T*>(s->r);
   T* z = static_cast<T*>(s->z);
   T* t = static_cast<T*>(s->t);
-  T* P0 = static_cast<T*>(s->p);
-  T* P1 = static_cast<T*>(s->p1);
+  T* p = static_cast<T*>(s->p);
   T* q = static_cast<T*>(s->q);
   const T* d = static_cast<const T*>(s->d);
-  const RBuf<T> R{static_cast<T*>(s->r), static_cast<T*>(s->r1)};
   PcgState* S = s->S;
-  const int eg = elem_grid(n);
+  const int eg = elem_vec_grid<T>(n);
   int rc = LSPCG_OK;
   switch (s->precond) {
     case LSPCG_PRECOND_EXT_SPAI:
     case LSPCG_PRECOND_EXT_SPAI_SCALED: {
-      const GatherR<T> gr{R, q, S};
-      if (s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) {
-        rc = launch_spmv_gx<T>(&s->LTv, gr, ProDone{S}, EpiRT<T, true>{gr, t, d, S, s->partials, s->ticket}, st);
-        if (!rc)
-          rc = launch_spmv_any<T>(&s->Lv, static_cast<const T*>(t), ProCheck<T>{S},
-                                  EpiZ<T, true>{z, R, d, T(s->eps), S, s->partials, s->ticket}, st);
-      } else {
-        rc = launch_spmv_gx<T>(&s->LTv, gr, ProDone{S}, EpiRT<T, false>{gr, t, d, S, s->partials, s->ticket}, st);
-        if (!rc)
-          rc = launch_spmv_any<T>(&s->Lv, static_cast<const T*>(t), ProCheck<T>{S},
-                                  EpiZ<T, false>{z, R, d, T(s->eps), S, s->partials, s->ticket}, st);
-      }
+      const bool sc = s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
+      rc = sc ? launch_spmv_any<T>(&s->LTv, static_cast<const T*>(r), ProCheck<T>{S}, EpiT<T, true>{t, d}, st)
+              : launch_spmv_any<T>(&s->LTv, static_cast<const T*>(r), ProCheck<T>{S}, EpiT<T, false>{t, d}, st);
       if (rc) return rc;
-      const GatherP<T> gp{z, R, P0, P1, S};
-      rc = launch_spmv_gx<T>(&s->Av, gp, ProDone{S}, EpiPQ<T>{gp, P0, P1, x, q, S, s->partials, s->ticket}, st);
+      rc = sc ? launch_spmv_any<T>(&s->Lv, static_cast<const T*>(t), ProDone{S},
+                                   EpiZ<T, true>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st)
+              : launch_spmv_any<T>(&s->Lv, static_cast<const T*>(t), ProDone{S},
+                                   EpiZ<T, false>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st);
+      if (rc) return rc;
+      hipLaunchKernelGGL((k_update_p<T, ProDone>), dim3(eg), dim3(kThreads), 0, st, n, ProDone{S}, S,
+                         static_cast<const T*>(z), p, x);
       break;
     }
     case LSPCG_PRECOND_NONE:
-    case LSPCG_PRECOND_DIAGONAL: {
-      if (s->precond == LSPCG_PRECOND_NONE)
-        hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_NONE>), dim3(eg), dim3(kThreads), 0, st, n, S, R, q, d, z,
-                           s->partials, s->ticket);
-      else
-        hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_DIAGONAL>), dim3(eg), dim3(kThreads), 0, st, n, S, R, q, d, z,
-                           s->partials, s->ticket);
-      const GatherP<T> gp{s->precond == LSPCG_PRECOND_NONE ? nullptr : z, R, P0, P1, S};
-      rc = launch_spmv_gx<T>(&s->Av, gp, ProCheck<T>{S}, EpiPQ<T>{gp, P0, P1, x, q, S, s->partials, s->ticket}, st);
+    case LSPCG_PRECOND_DIAGONAL:
+      hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S,
+                         static_cast<const T*>(s->precond == LSPCG_PRECOND_NONE ? r : z), p, x);
       break;
-    }
     default:
       set_error("unknown preconditioner");
       return LSPCG_ERR_ARG;
   }
+  rc = launch_spmv_any<T>(&s->Av, static_cast<const T*>(p), ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket},
+                          st);
   if (rc) return rc;
+  switch (s->precond) {
+    case LSPCG_PRECOND_NONE:
+      hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_NONE>), dim3(eg), dim3(kThreads), 0, st, n, S, q, r, d, z,
+                         s->partials, s->ticket);
+      break;
+    case LSPCG_PRECOND_DIAGONAL:
+      hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_DIAGONAL>), dim3(eg), dim3(kThreads), 0, st, n, S, q, r, d, z,
+                         s->partials, s->ticket);
+      break;
+    default:
+      hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_EXT_SPAI>), dim3(eg), dim3(kThreads), 0, st, n, S, q, r, d, z,
+                         s->partials, s->ticket);
+  }
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
 
 template <typename T>
 static int enqueue_init(lspcg_solver* s, hipStream_t st) {
-  int rc = launch_spmv_any<T>(&s->Av, static_cast<const T*>(s->x), ProNone{},
-                              EpiResid<T>{static_cast<T*>(s->r), static_cast<const T*>(s->b), s->S, s->partials,
-                                          s->ticket},
-                              st);
+  T* r = static_cast<T*>(s->r);
+  const T* b = static_cast<const T*>(s->b);
+  const T* d = static_cast<const T*>(s->d);
+  T* z = static_cast<T*>(s->z);
+  const T* x = static_cast<const T*>(s->x);
+  const int rc = s->precond == LSPCG_PRECOND_DIAGONAL
+                     ? launch_spmv_any<T>(&s->Av, x, ProNone{},
+                                          EpiResid<T, LSPCG_PRECOND_DIAGONAL>{r, b, d, z, s->S, s->partials, s->ticket},
+                                          st)
+                     : launch_spmv_any<T>(&s->Av, x, ProNone{},
+                                          EpiResid<T, LSPCG_PRECOND_NONE>{r, b, d, z, s->S, s->partials, s->ticket},
+                                          st);
   if (rc) return rc;
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
@@ -510,7 +488,7 @@ static int enqueue_init(lspcg_solver* s, hipStream_t st) {
 template <typename T>
 static int enqueue_fixup(lspcg_solver* s, hipStream_t st) {
   hipLaunchKernelGGL(k_x_fixup<T>, dim3(elem_grid(s->n)), dim3(kThreads), 0, st, s->n, s->S,
-                     static_cast<const T*>(s->p), static_cast<const T*>(s->p1), static_cast<T*>(s->x));
+                     static_cast<const T*>(s->p), static_cast<T*>(s->x));
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
@@ -554,7 +532,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   s->n = A->n;
   const size_t vb = esize(s->dtype) * std::max<int64_t>(s->n, 1);
   LSPCG_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d, &s->r1, &s->p1}) {
+  for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d}) {
     LSPCG_HIP(hipMalloc(v, vb));
     LSPCG_HIP(hipMemsetAsync(*v, 0, vb, s->stream));
   }
@@ -705,7 +683,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipStreamSynchronize(s->stream);
   for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
-  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d, s->r1, s->p1}) (void)hipFree(v);
+  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d}) (void)hipFree(v);
   (void)hipFree(s->S);
   (void)hipHostFree(s->hS);
   (void)hipFree(s->partials);
