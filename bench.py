@@ -164,6 +164,15 @@ def main():
     t_iter = float(np.median(solve_times)) / max(it_per_solve, 1)
     pcg_gbs = pcg_bytes_per_iter(n, nnz_a, nnz_l) / t_iter / 1e9
 
+    # HBM bytes per launch of the same kernel on the same matrix from the committed PMC passes
+    # (tools/spmv_traffic.sh: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), if they match
+    traffic = None
+    tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "spmv_traffic.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        if tj.get("n") == n and tj.get("nnz") == nnz_a:
+            traffic = tj["traffic_bytes"]
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
@@ -212,10 +221,11 @@ def main():
             "roofline": {
                 "kernel": "k_spmv<double,1> scalar CSR SpMV of A (staged, bit-exact scipy order)",
                 "bound": "hbm", "achieved": gbs_cold, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": gbs_cold / HBM_PEAK_GBS, "traffic": None,
+                "frac": gbs_cold / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_unit": "bytes per launch (profiles/spmv_traffic.json)",
                 "alg_bytes_per_launch": alg, "avg_launch_ms_cold": ms_cold, "avg_launch_ms_warm": ms_warm,
                 "achieved_warm": gbs_warm,
-                "method": "HIP events on the ctx stream; cold = 512 MiB memset between launches",
+                "method": "HIP events on the ctx stream; cold = a 512 MiB read before every launch, launch time = (R x (flush+SpMV) - R x flush)/R",
             },
             "cpu_baseline": cpu,
         }

@@ -84,8 +84,9 @@ int lspcg_mat_scale_columns(lspcg_mat* A, const void* d);
 /* y = A x (scipy csr_matvec bit pattern: per-row sequential sum in index order) */
 int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y);
 /* average device ms of one SpMV launch, HIP events on the ctx stream.  flush_bytes == 0:
- * reps back-to-back launches (warm caches); > 0: before every launch an untimed read of a
- * flush_bytes buffer evicts the 256 MiB Infinity Cache and each launch is timed alone (cold). */
+ * reps back-to-back launches (warm caches); > 0: before every launch a read of a flush_bytes
+ * buffer evicts the 256 MiB Infinity Cache (cold); the launch time is (reps x (flush + SpMV)
+ * - reps x flush) / reps, i.e. the in-stream duration without per-event overhead. */
 int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y, int reps,
                      int64_t flush_bytes, double* avg_ms);
 /* diagnostics: time SpMV launch configuration `variant` (fp64 scalar CSR; see csrc/lspcg_core.hip

@@ -46,6 +46,10 @@ void set_error(const std::string& msg);
 // ---------------------------------------------------------------------------
 constexpr int kThreads = 256;       // 4 wave64 per workgroup
 constexpr int kElemBlocksMax = 2048;  // grid cap for streaming elementwise kernels
+// grid_reduce_dd ticket buffer: [top | group 0 | group 1 | ...], one 128-B line each
+constexpr int kTicketGroup = 32;
+constexpr int kTicketStride = 32;
+constexpr int kTicketWords = kTicketStride * (1 + kElemBlocksMax / kTicketGroup);
 constexpr int kEntryPad = 16;       // zeroed padding entries after colind / vals (branch-free SpMV loads)
 
 // ---------------------------------------------------------------------------
@@ -141,8 +145,20 @@ __device__ __forceinline__ void grid_reduce_dd(DD (&v)[N], double* partials, uns
       st_agent_f64(&partials[(size_t(blockIdx.x) * N + j) * 2 + 1], v[j].c);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (t == gridDim.x - 1);
+    // two-level ticket: same-address device-scope atomics serialise at the memory side, so
+    // each group of kTicketGroup workgroups counts on its own cache line and only the group's
+    // last arriver touches the top-level ticket (<= G/32 + 32 serialised atomics, not G)
+    const unsigned G = gridDim.x;
+    const unsigned g = blockIdx.x / kTicketGroup;
+    const unsigned gsize = min(unsigned(kTicketGroup), G - g * kTicketGroup);
+    const unsigned ng = (G + kTicketGroup - 1) / kTicketGroup;
+    unsigned* gt = ticket + kTicketStride * (1 + g);
+    int last = 0;
+    if (__hip_atomic_fetch_add(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      __hip_atomic_store(gt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+    }
+    s_last = last;
   }
   __syncthreads();
   if (!s_last) return;

@@ -543,8 +543,8 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   // so L / Lᵀ in either layout fit too)
   const int64_t g = std::max<int64_t>((A->n + 254) / 255 + 1, kElemBlocksMax);
   LSPCG_HIP(hipMalloc(&s->partials, sizeof(double) * 2 * 2 * (g + 1)));
-  LSPCG_HIP(hipMalloc(&s->ticket, sizeof(unsigned) * 4));
-  LSPCG_HIP(hipMemsetAsync(s->ticket, 0, sizeof(unsigned) * 4, s->stream));
+  LSPCG_HIP(hipMalloc(&s->ticket, sizeof(unsigned) * kTicketWords));
+  LSPCG_HIP(hipMemsetAsync(s->ticket, 0, sizeof(unsigned) * kTicketWords, s->stream));
   LSPCG_HIP(hipMemsetAsync(s->S, 0, sizeof(PcgState), s->stream));
   for (hipEvent_t* e : {&s->ev_in, &s->ev_out, &s->ev_poll}) LSPCG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   LSPCG_HIP(hipEventCreate(&s->ev_t0));

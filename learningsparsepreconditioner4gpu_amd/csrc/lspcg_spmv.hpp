@@ -283,7 +283,7 @@ template <typename T, typename VT, int BS, int THREADS, int GPT, bool NT, class 
 inline void launch_spmv_cfg(const lspcg_mat* A, Gx gx, Pro pro, Epi epi, hipStream_t st) {
   SpmvArgs<T, VT, BS> a{A->nb, A->rowptr, A->colind, static_cast<const VT*>(A->vals)};
   int64_t grid = spmv_grid_t<THREADS, BS>(A->nb);
-  const int64_t cap = kReduceGridMax * 256 / THREADS;
+  const int64_t cap = std::min<int64_t>(kReduceGridMax * 256 / THREADS, kElemBlocksMax);  // ticket buffer bound
   if (XCD) grid = std::min<int64_t>(((grid + 7) / 8) * 8, cap);
   else if (Epi::NDOT > 0 && grid > cap) grid = cap;
   if (grid > 0)
