@@ -46,7 +46,26 @@ __host__ __device__ constexpr int ff_size(int in, int out) { return H * in + H +
 // C2 (64 x 4) | A3 (4 x 64) | C3 (64 x 4)]
 __host__ __device__ constexpr int frag_size(int s1) { return s1 * 64 + 5 * 256; }
 
-__device__ __forceinline__ float gelu(float v) { return 0.5f * v * (1.0f + erff(v * 0.7071067811865476f)); }
+// GELU(v) = 0.5 v erfc(-v/sqrt2).  erfc by the Chebyshev-fitted form of Numerical Recipes
+// (erfcc: fractional error < 1.2e-7 for every argument), branch-free: one rcp, one exp and 10
+// FMAs instead of ocml's two-branch erff -- the per-edge MLPs are VALU-bound on GELU.
+// Relative (not only absolute) accuracy also holds in the negative tail, where GELU -> 0.
+__device__ __forceinline__ float gelu(float v) {
+  const float z = fabsf(v) * 0.7071067811865476f;
+  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.5f, z, 1.0f));
+  float p = 0.17087277f;
+  p = __builtin_fmaf(t, p, -0.82215223f);
+  p = __builtin_fmaf(t, p, 1.48851587f);
+  p = __builtin_fmaf(t, p, -1.13520398f);
+  p = __builtin_fmaf(t, p, 0.27886807f);
+  p = __builtin_fmaf(t, p, -0.18628806f);
+  p = __builtin_fmaf(t, p, 0.09678418f);
+  p = __builtin_fmaf(t, p, 0.37409196f);
+  p = __builtin_fmaf(t, p, 1.00002368f);
+  p = __builtin_fmaf(t, p, -1.26551223f);
+  const float ec = t * __expf(__builtin_fmaf(-z, z, p));  // erfc(|v|/sqrt2)
+  return 0.5f * v * (v >= 0.f ? 2.0f - ec : ec);
+}
 __device__ __forceinline__ f4 gelu4(f4 a) { return f4{gelu(a.x), gelu(a.y), gelu(a.z), gelu(a.w)}; }
 
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
@@ -218,16 +237,48 @@ __global__ void __launch_bounds__(256) k_mp_layer(int64_t N, const float* __rest
 #pragma unroll
   for (int j = 0; j < 4; ++j) agg[j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  for (int64_t c0 = k0; c0 < k1; c0 += CE) {
+  // Edge tiles T = 0..NT-1 of this workgroup (16 CSC edges each); wave w takes T = w, w+4, ...
+  // Software pipeline: while tile T is computed, the gathers of tile T+4 and the index
+  // loads of tile T+8 are in flight (registers carry across the chunk barriers).
+  const int NT = int((k1 - k0 + 15) / 16);
+  const int64_t klast = k1 - 1;
+  auto edge_of = [&](int T) { const int64_t k = k0 + int64_t(T) * 16 + it; return k < k1 ? k : klast; };
+  int qd = 0, qs = 0;
+  f4 pxd{}, pxs{}, pea{};
+  if (wave < NT) {
+    const int64_t kk = edge_of(wave);
+    qd = dst[kk];
+    qs = src[kk];
+    pxd = ld4(x + int64_t(qd) * H + 4 * q);
+    pxs = ld4(x + int64_t(qs) * H + 4 * q);
+    pea = ld4(e + kk * H + 4 * q);
+    if (wave + 4 < NT) {
+      const int64_t kn = edge_of(wave + 4);
+      qd = dst[kn];
+      qs = src[kn];
+    }
+  }
+  const int nchunk = (NT + 15) / 16;
+  for (int c = 0; c < nchunk; ++c) {
+    const int64_t c0 = k0 + int64_t(c) * CE;
     const int64_t c1 = c0 + CE < k1 ? c0 + CE : k1;
-    const int ntile = int((c1 - c0 + 15) / 16);
-    for (int t = wave; t < ntile; t += 4) {  // wave-uniform: MFMA needs EXEC all ones
-      const int64_t k = c0 + t * 16 + it;
-      const bool valid = k < c1;
-      const int64_t kk = valid ? k : c1 - 1;
-      const f4 xd = ld4(x + int64_t(dst[kk]) * H + 4 * q);  // x_i (target)
-      const f4 xs = ld4(x + int64_t(src[kk]) * H + 4 * q);  // x_j (source)
-      const f4 ea = ld4(e + kk * H + 4 * q);                // edge attr
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+      const int T = c * 16 + wave + 4 * i;
+      if (T >= NT) break;  // wave-uniform: MFMA needs EXEC all ones
+      const int64_t k = k0 + int64_t(T) * 16 + it;
+      const bool valid = k < k1;
+      const f4 xd = pxd, xs = pxs, ea = pea;  // x_i (target), x_j (source), edge attr
+      if (T + 4 < NT) {
+        pxd = ld4(x + int64_t(qd) * H + 4 * q);
+        pxs = ld4(x + int64_t(qs) * H + 4 * q);
+        pea = ld4(e + edge_of(T + 4) * H + 4 * q);
+        if (T + 8 < NT) {
+          const int64_t kn = edge_of(T + 8);
+          qd = dst[kn];
+          qs = src[kn];
+        }
+      }
       // LayerNorm(48) statistics: 12 values per lane, 4 lanes per edge (xor 16, 32)
       float sum = (xd.x + xd.y + xd.z + xd.w) + (xs.x + xs.y + xs.z + xs.w) + (ea.x + ea.y + ea.z + ea.w);
       sum += __shfl_xor(sum, 16, 64);
@@ -237,15 +288,15 @@ __global__ void __launch_bounds__(256) k_mp_layer(int64_t N, const float* __rest
       pack12(xd, xs, ea, v);
       float sq = 0.f;
 #pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        v[i] -= mean;
-        sq = __builtin_fmaf(v[i], v[i], sq);
+      for (int j = 0; j < 12; ++j) {
+        v[j] -= mean;
+        sq = __builtin_fmaf(v[j], v[j], sq);
       }
       sq += __shfl_xor(sq, 16, 64);
       sq += __shfl_xor(sq, 32, 64);
       const float rstd = 1.0f / sqrtf(sq * (1.0f / 48.0f) + 1e-5f);
 #pragma unroll
-      for (int i = 0; i < 12; ++i) v[i] *= rstd;
+      for (int j = 0; j < 12; ++j) v[j] *= rstd;
       f4 m, u;
       ff2_48(fmsg, fedge, v, lane, m, u);
       if (edge_res) u += ea;
