@@ -24,13 +24,15 @@ class GraphSample:
     edge_index: torch.Tensor      # [2, E] int64, row-major sorted
     edge_attr: torch.Tensor       # [E, F_e] fp32
     mask: torch.Tensor            # [N, b] fp32
-    matrix_values: torch.Tensor   # [E, b, b] fp32 (scaled matrix)
+    matrix_values: Optional[torch.Tensor]  # [E, b, b] fp32 (scaled matrix)
     diagonal: Optional[torch.Tensor] = None
     inv_diag: Optional[torch.Tensor] = None
     rsqrt_diag: Optional[torch.Tensor] = None
     block_size: int = 1
     matrix_scale: float = 1.0
     ptr: torch.Tensor = field(default=None)
+    gt: Optional[torch.Tensor] = None        # lhs / matrix_scale (training samples with a stored lhs)
+    residual: Optional[torch.Tensor] = None  # rhs * mask (training samples)
 
     def __post_init__(self):
         if self.ptr is None:

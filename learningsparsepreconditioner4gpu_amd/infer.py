@@ -20,7 +20,7 @@ import math
 import os
 from dataclasses import dataclass, field
 from pathlib import Path
-from typing import Dict, List, Sequence
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -110,12 +110,34 @@ def synthetic_dataset(name: str) -> List[GraphSample]:
     raise KeyError(name)
 
 
-def rhs_for(rhs: str, mask: np.ndarray, A_full_rowsum=None) -> np.ndarray:
+def folder_dataset(prefix: str, block_size: int = 1, fixed_topology: bool = False, shared_features: bool = False,
+                   node_features: bool = True, edge_to_node: str = "disable", normalize="mean") -> List[GraphSample]:
+    """Samples of an on-disk dataset (dataset.FolderDataset, data.py:339-640; config/data.yaml
+    defaults), one per rhs column like the reference's dataloader."""
+    from .dataset import FolderDataset
+
+    ds = FolderDataset(is_fixed_topology=fixed_topology, load_into_memory=False, block_size=block_size,
+                       has_shared_features=shared_features, use_node_features=node_features,
+                       use_matrix_as_edge_feature=True, use_mask_as_node_feature=True,
+                       use_node_features_as_edge_feature=False, use_edge_features_as_node_feature=edge_to_node,
+                       use_random_rhs=True, normalize_matrix=normalize, prefix=prefix)
+    return [ds.get(i, is_inference=True) for i in range(ds.len())]
+
+
+def rhs_for(rhs: str, mask: np.ndarray, sample: Optional[GraphSample] = None) -> np.ndarray:
+    """infer.py:297-309: mask / ones, random (masked), neighbour (A_full (1-m) + 0.1 m, masked)."""
     m = mask.reshape(-1).astype(np.float64)
     if rhs in ("mask", "ones"):
         return m
     if rhs == "random":
         return np.random.randn(m.size) * m
+    if rhs == "neighbour":
+        from .validate import to_csr_cpu
+
+        n = m.size
+        A_full = to_csr_cpu(sample.edge_index, sample.matrix_values, n, None)
+        A_full.data.fill(1.0)
+        return (A_full @ (1 - m) + 0.1 * m) * m
     raise ValueError(f"Unknown rhs type: {rhs}")
 
 
@@ -138,7 +160,7 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
         prec /= repeat
         L, _ = ws.inference_step(s)
         A = ws.system_matrix(s)
-        r = rhs_for(rhs, s.mask.cpu().numpy())
+        r = rhs_for(rhs, s.mask.cpu().numpy(), s)
         it, _, sol = pcg(A, r, L, ws.epsilon, rtol=rtol, repeat=repeat)
         return SolveRecord(index=i, iters=it, rel_res=float("nan"), t_prec=prec, t_solve=sol, n=A.n, nnz=A.nnz,
                            converged=it < A.n)
@@ -150,6 +172,13 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--dataset", default="heat_batch8")
+    ap.add_argument("--folder", default="", help="on-disk dataset (datagen folder format); overrides --dataset")
+    ap.add_argument("--block-size", type=int, default=1)
+    ap.add_argument("--fixed-topology", action="store_true")
+    ap.add_argument("--shared-features", action="store_true")
+    ap.add_argument("--no-node-features", action="store_true")
+    ap.add_argument("--edge-to-node", default="disable", choices=["disable", "sum", "mean", "max", "min"])
+    ap.add_argument("--normalize", default="mean")
     ap.add_argument("--exp-name", default=None)
     ap.add_argument("--rtol", type=float, default=1e-6)
     ap.add_argument("--repeat", type=int, default=1)
@@ -169,7 +198,11 @@ def main(argv=None):
     torch.cuda.set_device(local)
     if world > 1 and not dist.is_initialized():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    samples = synthetic_dataset(args.dataset)
+    if args.folder:
+        samples = folder_dataset(args.folder, args.block_size, args.fixed_topology, args.shared_features,
+                                 not args.no_node_features, args.edge_to_node, args.normalize)
+    else:
+        samples = synthetic_dataset(args.dataset)
     cls = ScaledInferenceWorkspace if args.workspace == "scaled" else SimpleInferenceWorkspace
     if args.pretrained:
         ws = cls.load_from_checkpoint(args.pretrained)
@@ -185,7 +218,7 @@ def main(argv=None):
         stats.print()
         out = Path(args.out_dir)
         out.mkdir(parents=True, exist_ok=True)
-        exp = args.exp_name or args.dataset
+        exp = args.exp_name or (Path(args.folder).name if args.folder else args.dataset)
         log_rtol = -int(math.log10(args.rtol))
         stats.timestat_to_dataframe().to_csv(out / f"infer_{args.infer_prefix}{exp}_{log_rtol}.csv", index=False)
         stats.all_time_stat().to_csv(out / f"all_infer_{args.infer_prefix}{exp}_{log_rtol}.csv", index=False)

@@ -17,6 +17,11 @@ Fixtures (inputs and the reference's outputs, data only):
   gnn_init.npz     -- state_dict of neural_cg.nn.gnns.NodeEdgeProcessing (config/gnn.yaml)
                       constructed after torch.manual_seed(0)
   make_data.npz    -- neural_cg/data.py make_data outputs for one masked block matrix
+  folder_free/, folder_fixed/ + folder.npz
+                   -- two on-disk datasets in the datagen_helper.py folder format (written by
+                      dataset.FolderWriter: .mtx + features/mask/rhs/lhs; fixed-topology 3x3
+                      blocks with demo.mtx + value vectors + shared features) and the outputs of
+                      the reference's FolderDataset.get(i) for every sample
 
     python tests/golden/make_golden.py
 """
@@ -56,9 +61,18 @@ def install_shims():
         def __init__(self, **kw):
             self.__dict__.update(kw)
 
-    class Dataset:
+        def to_dict(self):
+            return dict(self.__dict__)
+
+    class Dataset:  # PyG Dataset: len() / get() hooks behind __len__ / __getitem__
         def __init__(self, *a, **k):
             pass
+
+        def __len__(self):
+            return self.len()
+
+        def __getitem__(self, i):
+            return self.get(i)
 
     class MessagePassing(nn.Module):  # construction-only stand-in (no propagate)
         def __init__(self, aggr="add", flow="source_to_target", **kw):
@@ -195,6 +209,56 @@ def main():
                         nodes=nodes, x=dd.x.numpy(), edge_index=dd.edge_index.numpy(), edge_attr=dd.edge_attr.numpy(),
                         matrix_values=dd.matrix_values.numpy(), rsqrt_diag=dd.rsqrt_diag.numpy(),
                         inv_diag=dd.inv_diag.numpy(), mask_out=dd.mask.numpy())
+    # ---------------- FolderDataset (data.py:339-640) on two folders written in the datagen format
+    import shutil
+
+    from learningsparsepreconditioner4gpu_amd.dataset import FolderWriter
+
+    fx = {}
+    free, fixed = OUT / "folder_free", OUT / "folder_fixed"
+    for d in (free, fixed):
+        shutil.rmtree(d, ignore_errors=True)
+    w = FolderWriter(str(free), block_size=1, save_rhs=2, save_lhs=True, seed=3)
+    for k in range(2):
+        Af, mf, _ = P.poisson2d_grid(6 + k, 5)
+        w.append(Af * (1.0 + k), mf, rng.random((Af.shape[0], 2)))
+    Ab, mb, nodes = P.elasticity_box(3, 2, 2)
+    # (bs > 1: the reference's rhs files hold one entry per block row and no lhs can be solved
+    # for them -- datagen_helper.py:300-321 -- so this folder samples a random rhs instead)
+    w = FolderWriter(str(fixed), block_size=3, is_fixed_topology=True, save_rhs=1, save_lhs=False, seed=4)
+    w.write_topology(Ab)
+    w.write_shared(nodes)
+    for k in range(2):
+        Ak = sp.csr_matrix(Ab * (1.0 + 0.5 * k))
+        w.append(Ak, mb, rng.random((Ab.shape[0] // 3, 2)), rhs=rng.standard_normal(Ab.shape[0] // 3))
+    configs = {
+        "free": dict(is_fixed_topology=False, load_into_memory=True, block_size=1, has_shared_features=False,
+                     use_node_features=True, use_matrix_as_edge_feature=True, use_mask_as_node_feature=True,
+                     use_node_features_as_edge_feature=False, use_edge_features_as_node_feature="disable",
+                     use_random_rhs=False, normalize_matrix="mean", prefix=str(free)),
+        "fixed": dict(is_fixed_topology=True, load_into_memory=False, block_size=3, has_shared_features=True,
+                      use_node_features=True, use_matrix_as_edge_feature=True, use_mask_as_node_feature=True,
+                      use_node_features_as_edge_feature=True, use_edge_features_as_node_feature="disable",
+                      use_random_rhs=True, normalize_matrix="frob", prefix=str(fixed)),
+        "free_l1": dict(is_fixed_topology=False, load_into_memory=False, block_size=1, has_shared_features=False,
+                        use_node_features=True, use_matrix_as_edge_feature=True, use_mask_as_node_feature=False,
+                        use_node_features_as_edge_feature=True, use_edge_features_as_node_feature="disable",
+                        use_random_rhs=False, normalize_matrix="l1", prefix=str(free)),
+    }
+    for name, cfg in configs.items():
+        ds = rdata.FolderDataset(**cfg)
+        fx[f"{name}__len"] = np.array(ds.len())
+        fx[f"{name}__nnf"] = np.array(ds.num_node_features)
+        fx[f"{name}__nef"] = np.array(ds.num_edge_features)
+        for i in range(ds.len()):
+            torch.manual_seed(100 + i)  # the random rhs (data.py:318) draws from torch's generator
+            dd = ds.get(i)
+            for key in ("x", "edge_index", "edge_attr", "mask", "matrix_values", "diagonal", "inv_diag",
+                        "rsqrt_diag", "gt", "residual"):
+                if hasattr(dd, key):
+                    fx[f"{name}__{i}__{key}"] = getattr(dd, key).numpy()
+    np.savez_compressed(OUT / "folder.npz", **fx)
+
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)
 

@@ -72,3 +72,27 @@ def test_infer_driver_end_to_end(gpu_ctx, tmp_path):
         st.put("Neural+HIP", r.t_solve, r.t_prec, r.iters, r.n)
     df = st.timestat_to_dataframe()
     assert list(df.columns) == ["Key", "Total Time (ms)", "Solve Time (ms)", "Precond Time (ms)", "#Iteration"]
+
+
+@pytest.mark.parametrize("rhs", ["mask", "neighbour"])
+def test_folder_dataset_through_hot_path(gpu_ctx, rhs):
+    """On-disk dataset (reference folder format, golden folder_free) -> GNN -> L -> PCG through
+    the infer driver; iteration counts equal the oracle's on the same A, L, rhs."""
+    import numpy as np
+
+    from learningsparsepreconditioner4gpu_amd.infer import folder_dataset, rhs_for, run
+    from learningsparsepreconditioner4gpu_amd.validate import to_csr_cpu
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    samples = folder_dataset(str(GOLDEN / "folder_free"))
+    assert len(samples) == 4  # 2 matrices x 2 rhs columns
+    s0 = samples[0]
+    ws = SimpleInferenceWorkspace(node_features=s0.x.shape[1], edge_features=s0.edge_attr.shape[1], seed=0)
+    recs = run(samples, ws, rtol=1e-8, warmup=1, rhs=rhs)
+    for rec, s in zip(recs, samples):
+        d = s.to("cuda")
+        L, _ = ws.inference_step(d)
+        A = to_csr_cpu(d.edge_index, d.matrix_values, s.num_nodes, d.mask)
+        r = rhs_for(rhs, s.mask.numpy(), d)
+        it_o, _, _ = O.pcg(A, A @ r, O.spai_operator(L.to_scipy(), ws.epsilon), rtol=1e-8, dot="exact")
+        assert rec.converged and rec.iters == it_o, (rec.index, rec.iters, it_o)
