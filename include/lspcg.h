@@ -38,6 +38,7 @@ extern "C" {
 #define LSPCG_ERR_HIP (-2)
 #define LSPCG_ERR_UNSUPPORTED (-3)
 #define LSPCG_ERR_FORMAT (-4)
+#define LSPCG_ERR_BREAKDOWN (-5) /* incomplete factorization hit a non-positive pivot */
 
 #define LSPCG_F32 0
 #define LSPCG_F64 1
@@ -47,6 +48,8 @@ extern "C" {
 #define LSPCG_PRECOND_DIAGONAL 1
 #define LSPCG_PRECOND_EXT_SPAI 2
 #define LSPCG_PRECOND_EXT_SPAI_SCALED 3
+/* IC(0) of A, applied by two level-scheduled triangular solves (pymathprim "ic") */
+#define LSPCG_PRECOND_IC 4
 
 typedef struct lspcg_ctx lspcg_ctx;
 typedef struct lspcg_mat lspcg_mat;
@@ -93,6 +96,16 @@ int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y,
  * kSpmvVariants) exactly like lspcg_spmv_timed; variant < 0 returns the number of variants */
 int lspcg_spmv_variant_timed(lspcg_ctx* ctx, const lspcg_mat* A, int variant, const void* x, void* y,
                              int reps, int64_t flush_bytes, double* avg_ms);
+/* ---- baseline preconditioners (pymathprim "ic" / "ainv", infer.py:310-321; algorithms and
+ * operation order: oracle/precond.py; scalar CSR, sorted rows, stored diagonal) ---- */
+/* IC(0): *L = lower-triangular factor with the pattern of tril(A), A ~ L L^T */
+int lspcg_ic0(const lspcg_mat* A, lspcg_mat** L, double* t_ms);
+/* AINV(0): *L = Z D^{-1/2} (Z unit upper, pattern triu(A)) so that L L^T = Z D^{-1} Z^T ~ A^{-1};
+ * use it as an ext_spai factor with epsilon = 0 */
+int lspcg_ainv0(const lspcg_mat* A, lspcg_mat** L, double* t_ms);
+/* x = T^{-1} b, T triangular (lower != 0: diagonal stored last in each row; else first),
+ * level-scheduled; b, x device vectors of T's dtype */
+int lspcg_trsv(const lspcg_mat* T, int lower, const void* b, void* x);
 /* compensated, deterministic dot product of two device vectors; result to host */
 int lspcg_dot(lspcg_ctx* ctx, int64_t n, int dtype, const void* x, const void* y, double* out);
 
@@ -101,6 +114,9 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
 /* ext_spai=(L, eps): builds Lᵀ (and diag(A) for the scaled variant) on device.
  * t_prec_ms (nullable) receives the device time of that setup. L must outlive solves. */
 int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, double* t_prec_ms);
+/* LSPCG_PRECOND_IC solvers: IC(0) factorization of A on the device (pymathprim "ic" setup;
+ * the reference's scipy twin is validate.py:344-429); t_prec_ms = setup time */
+int lspcg_solver_set_ic(lspcg_solver* s, double* t_prec_ms);
 /* Solve A x = b from x (x0, in/out).  Semantics of scipy.sparse.linalg.cg (iterative.py
  * 359-418): atol = rtol*||b||, ||r|| checked at the top of each iteration, iters = number
  * of completed iterations, max_iter <= 0 means n.  res_hist (host, nullable, length

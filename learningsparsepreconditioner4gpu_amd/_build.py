@@ -14,8 +14,8 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 LIB = PKG / "liblspcg_hip.so"
-SOURCES = ["lspcg_core.hip", "lspcg_pcg.hip", "lspcg_assemble.hip", "lspcg_gnn.hip"]
-HEADERS = ["lspcg_internal.hpp", "lspcg_spmv.hpp"]
+SOURCES = ["lspcg_core.hip", "lspcg_pcg.hip", "lspcg_assemble.hip", "lspcg_gnn.hip", "lspcg_factor.hip"]
+HEADERS = ["lspcg_internal.hpp", "lspcg_spmv.hpp", "lspcg_factor.hpp"]
 ARCH = os.environ.get("LSPCG_ARCH", "gfx950")
 
 # -ffp-contract=off: products are rounded before they are added, exactly like

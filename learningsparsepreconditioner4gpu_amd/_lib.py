@@ -14,9 +14,9 @@ PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("LSPCG_LIB", PKG / "liblspcg_hip.so"))
 
 OK, NOT_CONVERGED = 0, 1
-ERR_ARG, ERR_HIP, ERR_UNSUPPORTED, ERR_FORMAT = -1, -2, -3, -4
+ERR_ARG, ERR_HIP, ERR_UNSUPPORTED, ERR_FORMAT, ERR_BREAKDOWN = -1, -2, -3, -4, -5
 F32, F64 = 0, 1
-PRECOND = {"none": 0, "diagonal": 1, "ext_spai": 2, "ext_spai_scaled": 3}
+PRECOND = {"none": 0, "diagonal": 1, "ext_spai": 2, "ext_spai_scaled": 3, "ic": 4}
 
 p_i32 = C.POINTER(C.c_int32)
 p_i64 = C.POINTER(C.c_int64)
@@ -48,9 +48,13 @@ SIGNATURES = {
     "lspcg_spmv": (C.c_int, [vp, vp, vp, vp]),
     "lspcg_spmv_timed": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int64, p_f64]),
     "lspcg_spmv_variant_timed": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int64, p_f64]),
+    "lspcg_ic0": (C.c_int, [vp, pp, p_f64]),
+    "lspcg_ainv0": (C.c_int, [vp, pp, p_f64]),
+    "lspcg_trsv": (C.c_int, [vp, C.c_int, vp, vp]),
     "lspcg_dot": (C.c_int, [vp, C.c_int64, C.c_int, vp, vp, p_f64]),
     "lspcg_solver_create": (C.c_int, [vp, vp, C.c_int, pp]),
     "lspcg_solver_set_spai": (C.c_int, [vp, vp, C.c_double, p_f64]),
+    "lspcg_solver_set_ic": (C.c_int, [vp, p_f64]),
     "lspcg_solver_solve": (C.c_int, [vp, vp, vp, C.c_double, C.c_int64, p_i64, p_f64, p_f64]),
     "lspcg_solver_destroy": (C.c_int, [vp]),
     "lspcg_assemble": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int, vp, vp, C.c_int, vp, C.c_int, C.c_int,

@@ -200,7 +200,10 @@ int lspcg_ctx_synchronize(lspcg_ctx* ctx) {
   return LSPCG_OK;
 }
 
-static int mat_alloc(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, int dtype, lspcg_mat** out) {
+}  // extern "C"
+
+namespace lspcg {
+int mat_alloc(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, int dtype, lspcg_mat** out) {
   LSPCG_CHECK(ctx && out, LSPCG_ERR_ARG, "mat: NULL ctx/out");
   LSPCG_CHECK(bs == 1 || bs == 3, LSPCG_ERR_UNSUPPORTED, "mat: block size must be 1 or 3");
   LSPCG_CHECK(dtype == LSPCG_F32 || dtype == LSPCG_F64, LSPCG_ERR_ARG, "mat: bad dtype");
@@ -220,6 +223,9 @@ static int mat_alloc(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, int dtype
   *out = m.release();
   return LSPCG_OK;
 }
+}  // namespace lspcg
+
+extern "C" {
 
 int lspcg_mat_create_bsr(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, const int32_t* indptr,
                          const int32_t* indices, const void* vals, int dtype, lspcg_mat** out) {

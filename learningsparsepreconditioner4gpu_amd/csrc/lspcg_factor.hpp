@@ -1,0 +1,33 @@
+// Level-scheduled sparse factorizations / triangular solves shared by lspcg_factor.hip and the
+// PCG solver (lspcg_pcg.hip).  See lspcg_factor.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "lspcg.h"
+
+namespace lspcg {
+
+// Rows grouped by dependency level: rows order[ptr[l] .. ptr[l+1]) form level l (ascending row
+// index inside a level); hptr is the host copy of ptr used to size the per-level launches.
+struct Levels {
+  int nlev = 0;
+  int32_t* ptr = nullptr;
+  int32_t* order = nullptr;
+  std::vector<int32_t> hptr;
+  void release();
+};
+
+// lower: row i depends on the columns j < i of its row; upper: on the columns j > i.
+int build_levels(lspcg_ctx* ctx, int64_t n, const int32_t* rp, const int32_t* ci, bool lower, Levels* out);
+// x = T⁻¹ b by levels (lower: diagonal stored last in each row, upper: first); `done` (nullable)
+// is the solver's device done flag -- every launch returns at once when it is set.
+int enqueue_trsv(const lspcg_mat* T, const Levels& lv, bool lower, const void* b, void* x, const int32_t* done,
+                 hipStream_t st);
+int ic0_factor(const lspcg_mat* A, lspcg_mat** L);
+int ainv0_factor(const lspcg_mat* A, lspcg_mat** L);
+
+}  // namespace lspcg

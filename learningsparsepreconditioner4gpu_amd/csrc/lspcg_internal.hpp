@@ -225,6 +225,8 @@ struct lspcg_mat;
 namespace lspcg {
 // (Re)allocate m->colind / m->vals for nnzb stored blocks with zeroed kEntryPad padding.
 int mat_alloc_entries(lspcg_mat* m, int64_t nnzb);
+// New handle with rowptr[nb+1] and padded entry arrays (contents uninitialised).
+int mat_alloc(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, int dtype, lspcg_mat** out);
 }  // namespace lspcg
 
 // ---------------------------------------------------------------------------

@@ -25,6 +25,7 @@
 #include <string>
 #include <vector>
 
+#include "lspcg_factor.hpp"
 #include "lspcg_internal.hpp"
 #include "lspcg_spmv.hpp"
 
@@ -281,13 +282,27 @@ __global__ void __launch_bounds__(kThreads) k_update_r(int64_t n, PcgState* S, c
   grid_reduce_dd<ND>(dots, partials, ticket, [&](const double* v) {
     const double rr2 = round_to<T>(v[0]);
     S->rr = rr2;
-    if constexpr (PRE != LSPCG_PRECOND_EXT_SPAI && PRE != LSPCG_PRECOND_EXT_SPAI_SCALED) {
+    if constexpr (PRE == LSPCG_PRECOND_NONE || PRE == LSPCG_PRECOND_DIAGONAL) {
       S->rho_prev = S->rho;
       S->rho = (PRE == LSPCG_PRECOND_DIAGONAL) ? round_to<T>(v[ND - 1]) : rr2;
     }
     const int64_t it = S->iter + 1;
     S->iter = it;
     if (S->hist) S->hist[it] = double(tsqrt<T>(T(rr2)));
+  });
+}
+
+// IC: ρ = r·z after the two triangular solves
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_dot_rho(int64_t n, PcgState* S, const T* __restrict__ r,
+                                                      const T* __restrict__ z, double* partials, unsigned* ticket) {
+  if (S->done) return;
+  DD dots[1] = {dd_zero()};
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    dd_fma(dots[0], double(r[i]), double(z[i]));
+  grid_reduce_dd<1>(dots, partials, ticket, [&](const double* v) {
+    S->rho_prev = S->rho;
+    S->rho = round_to<T>(v[0]);
   });
 }
 
@@ -354,6 +369,10 @@ struct lspcg_solver {
   void* own_LT = nullptr;
   int* flag = nullptr;
   bool compact = true;
+  // IC(0): factor, its explicit transpose and their level sets
+  lspcg_mat* icL = nullptr;
+  lspcg_mat* icU = nullptr;
+  Levels levL, levU;
 };
 
 static int flag_run(lspcg_solver* s, hipStream_t st, int* out) {
@@ -442,6 +461,17 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
       hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S,
                          static_cast<const T*>(s->precond == LSPCG_PRECOND_NONE ? r : z), p, x);
       break;
+    case LSPCG_PRECOND_IC: {
+      // z = L⁻ᵀ L⁻¹ r (t holds L⁻¹ r), ρ = r·z; then the top-of-loop test in the p update
+      const int32_t* done = &S->done;
+      if ((rc = enqueue_trsv(s->icL, s->levL, true, r, t, done, st))) return rc;
+      if ((rc = enqueue_trsv(s->icU, s->levU, false, t, z, done, st))) return rc;
+      hipLaunchKernelGGL(k_dot_rho<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const T*>(r),
+                         static_cast<const T*>(z), s->partials, s->ticket);
+      hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S,
+                         static_cast<const T*>(z), p, x);
+      break;
+    }
     default:
       set_error("unknown preconditioner");
       return LSPCG_ERR_ARG;
@@ -521,7 +551,7 @@ extern "C" {
 
 int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_solver** out) {
   LSPCG_CHECK(ctx && A && out, LSPCG_ERR_ARG, "solver_create: NULL argument");
-  LSPCG_CHECK(precond >= LSPCG_PRECOND_NONE && precond <= LSPCG_PRECOND_EXT_SPAI_SCALED, LSPCG_ERR_ARG,
+  LSPCG_CHECK(precond >= LSPCG_PRECOND_NONE && precond <= LSPCG_PRECOND_IC, LSPCG_ERR_ARG,
               "solver_create: unknown preconditioner " + std::to_string(precond));
   LSPCG_HIP(hipSetDevice(ctx->device));
   std::unique_ptr<lspcg_solver> s(new lspcg_solver());
@@ -597,10 +627,40 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   return LSPCG_OK;
 }
 
+int lspcg_solver_set_ic(lspcg_solver* s, double* t_prec_ms) {
+  LSPCG_CHECK(s, LSPCG_ERR_ARG, "set_ic: NULL");
+  LSPCG_CHECK(s->precond == LSPCG_PRECOND_IC, LSPCG_ERR_ARG, "set_ic: solver was not created with LSPCG_PRECOND_IC");
+  LSPCG_HIP(hipSetDevice(s->ctx->device));
+  LSPCG_HIP(hipStreamSynchronize(s->stream));
+  hipStream_t cst = s->ctx->stream;
+  LSPCG_HIP(hipEventRecord(s->ev_t0, cst));
+  for (lspcg_mat** m : {&s->icL, &s->icU}) {
+    if (*m) lspcg_mat_destroy(*m);
+    *m = nullptr;
+  }
+  int rc = ic0_factor(s->A, &s->icL);
+  if (!rc) rc = lspcg_mat_transpose(s->icL, &s->icU);
+  if (!rc) rc = build_levels(s->ctx, s->n, s->icL->rowptr, s->icL->colind, true, &s->levL);
+  if (!rc) rc = build_levels(s->ctx, s->n, s->icU->rowptr, s->icU->colind, false, &s->levU);
+  if (rc) return rc;
+  LSPCG_HIP(hipEventRecord(s->ev_t1, cst));
+  LSPCG_HIP(hipEventSynchronize(s->ev_t1));
+  float ms = 0.f;
+  LSPCG_HIP(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1));
+  if (t_prec_ms) *t_prec_ms = ms;
+  for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
+  s->graphs.clear();
+  s->graph_defs.clear();
+  return LSPCG_OK;
+}
+
 int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int64_t max_iter, int64_t* iters,
                        double* res_hist, double* t_solve_ms) {
   LSPCG_CHECK(s && b && x && iters, LSPCG_ERR_ARG, "solve: NULL argument");
-  LSPCG_CHECK(!(s->precond >= LSPCG_PRECOND_EXT_SPAI) || s->LT, LSPCG_ERR_ARG, "solve: ext_spai not set");
+  LSPCG_CHECK(!(s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) || s->LT,
+              LSPCG_ERR_ARG, "solve: ext_spai not set");
+  LSPCG_CHECK(s->precond != LSPCG_PRECOND_IC || s->icL, LSPCG_ERR_ARG, "solve: IC factor not set (lspcg_solver_set_ic)");
   LSPCG_HIP(hipSetDevice(s->ctx->device));
   const int64_t n = s->n;
   if (max_iter <= 0) max_iter = n;
@@ -630,7 +690,10 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   // early-exit launches trail the converged iteration.
   int64_t last_it = 0;
   double last_rr = -1.0;
-  int chunk = 4;
+  // graphs hold <= ~4096 nodes (IC: one launch per level of each triangular solve)
+  const int kpi = s->precond == LSPCG_PRECOND_IC ? s->levL.nlev + s->levU.nlev + 4 : 5;
+  const int max_chunk = std::max(1, std::min(32, 4096 / kpi));
+  int chunk = std::min(4, max_chunk);
   for (;;) {
     LSPCG_HIP(hipMemcpyAsync(s->hS, s->S, sizeof(PcgState), hipMemcpyDeviceToHost, st));
     LSPCG_HIP(hipEventRecord(s->ev_poll, st));
@@ -643,11 +706,12 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
       int64_t rem = need > 0 ? int64_t(std::ceil(need)) : 1;
       rem = std::max<int64_t>(1, std::min<int64_t>(rem, max_iter - cur.iter));
       int c = 1;
-      while (c * 2 <= rem && c < 32) c *= 2;
+      while (c * 2 <= rem && c < max_chunk) c *= 2;
       chunk = c;
     } else if (last_rr > 0) {
-      chunk = std::min(32, chunk * 2);
+      chunk = std::min(max_chunk, chunk * 2);
     }
+    chunk = std::min(chunk, max_chunk);
     last_it = cur.iter;
     last_rr = cur.rr;
     hipGraphExec_t ex = nullptr;
@@ -690,6 +754,10 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipFree(s->ticket);
   for (hipEvent_t e : {s->ev_in, s->ev_out, s->ev_poll, s->ev_t0, s->ev_t1}) (void)hipEventDestroy(e);
   if (s->LT) lspcg_mat_destroy(s->LT);
+  if (s->icL) lspcg_mat_destroy(s->icL);
+  if (s->icU) lspcg_mat_destroy(s->icU);
+  s->levL.release();
+  s->levU.release();
   for (void* p : {s->own_A, s->own_L, s->own_LT}) (void)hipFree(p);
   (void)hipFree(s->flag);
   (void)hipStreamDestroy(s->stream);

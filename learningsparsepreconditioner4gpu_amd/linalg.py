@@ -24,8 +24,8 @@ from . import _lib
 from .sparse import Context, DeviceMatrix, _ptr, lspcg_dtype
 
 GPU_DEVICES = ("cuda", "hip", "gpu", "rocm")
-SUPPORTED = tuple(_lib.PRECOND)
-BASELINE_ONLY = ("ic", "ainv", "fsai")  # pymathprim baselines (infer.py:310-321), SURVEY 8(f) "next"
+SUPPORTED = tuple(_lib.PRECOND) + ("ainv",)
+NOT_BUILT = ("fsai",)  # commented out of the reference's baseline rows (infer.py:315)
 
 
 def _as_device_matrix(M, dtype, block_size: int, ctx: Context) -> DeviceMatrix:
@@ -43,9 +43,9 @@ class PreconditionedConjugateGradient:
             raise ValueError(
                 f"device={device!r}: this framework runs PCG on MI355X only (device='cuda'); the CPU "
                 "reference path is not part of the product")
-        if preconditioner in BASELINE_ONLY:
-            raise NotImplementedError(f"preconditioner {preconditioner!r} is a pymathprim baseline that is not "
-                                      "implemented yet (SURVEY.md 8(f) 'next' rank 3)")
+        if preconditioner in NOT_BUILT:
+            raise NotImplementedError(f"preconditioner {preconditioner!r} is not built (the reference's baseline "
+                                      "rows use none / diagonal / ainv / ic, infer.py:310-315)")
         if preconditioner not in SUPPORTED:
             raise ValueError(f"unknown preconditioner {preconditioner!r}; expected one of {SUPPORTED}")
         dev = str(device).split(":")
@@ -54,11 +54,22 @@ class PreconditionedConjugateGradient:
         self.preconditioner = preconditioner
         self.A = _as_device_matrix(matrix, self.dtype, block_size, self.ctx)
         self.n = self.A.n
+        # "ainv" runs as the ext_spai operator L Lᵀ + 0·I with L = Z D^{-1/2} (lspcg_ainv0)
+        kind = "ext_spai" if preconditioner == "ainv" else preconditioner
         h = C.c_void_p()
-        _lib.call("lspcg_solver_create", self.ctx.handle, self.A.handle, _lib.PRECOND[preconditioner], C.byref(h))
+        _lib.call("lspcg_solver_create", self.ctx.handle, self.A.handle, _lib.PRECOND[kind], C.byref(h))
         self.handle = h
         self._L = None
         self._spai_key = None
+        self.setup_time = 0.0  # device setup of the ic / ainv preconditioner (seconds)
+        if preconditioner == "ic":
+            ms = C.c_double()
+            _lib.call("lspcg_solver_set_ic", self.handle, C.byref(ms))
+            self.setup_time = ms.value / 1e3
+        elif preconditioner == "ainv":
+            L, t = self.A.ainv0()
+            self.setup_time = t + self.set_spai(L, 0.0)
+            self._spai_key = ("ainv",)
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -94,7 +105,7 @@ class PreconditionedConjugateGradient:
 
     def __call__(self, b, x, rtol: float = 1e-6, max_iter: int = 0, ext_spai=None,
                  return_history: bool = False) -> Tuple:
-        prec = 0.0
+        prec = self.setup_time
         if self.preconditioner in ("ext_spai", "ext_spai_scaled"):
             if ext_spai is None and self._L is None:
                 raise ValueError("ext_spai=(L, epsilon) is required for this preconditioner")

@@ -6,7 +6,7 @@ stream the library issues on (the default stream, shared with PyTorch).
 from __future__ import annotations
 
 import ctypes as C
-from typing import Optional, Union
+from typing import Tuple, Optional, Union
 
 import numpy as np
 import scipy.sparse as sp
@@ -162,6 +162,25 @@ class DeviceMatrix:
     @property
     def T(self) -> "DeviceMatrix":
         return self.transpose()
+
+    def ic0(self) -> Tuple["DeviceMatrix", float]:
+        """IC(0) factor L (tril pattern, A ≈ L Lᵀ) on the device; returns (L, setup seconds)."""
+        h, ms = C.c_void_p(), C.c_double()
+        _lib.call("lspcg_ic0", self.handle, C.byref(h), C.byref(ms))
+        return DeviceMatrix(h, self.ctx), ms.value / 1e3
+
+    def ainv0(self) -> Tuple["DeviceMatrix", float]:
+        """AINV(0) factor L = Z D^{-1/2} (L Lᵀ ≈ A⁻¹) on the device; returns (L, setup seconds)."""
+        h, ms = C.c_void_p(), C.c_double()
+        _lib.call("lspcg_ainv0", self.handle, C.byref(h), C.byref(ms))
+        return DeviceMatrix(h, self.ctx), ms.value / 1e3
+
+    def trsv(self, b: torch.Tensor, lower: bool = True, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """x = T⁻¹ b for a triangular matrix (lower: diagonal last per row; upper: first)."""
+        b = b.to(device=self.ctx.torch_device, dtype=self.dtype).contiguous()
+        x = self.empty_vector() if out is None else out
+        _lib.call("lspcg_trsv", self.handle, int(bool(lower)), _ptr(b), _ptr(x))
+        return x
 
     def diagonal(self) -> torch.Tensor:
         d = self.empty_vector()

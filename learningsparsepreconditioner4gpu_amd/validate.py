@@ -63,7 +63,8 @@ def _prepare(A, dtype, block_size=1) -> DeviceMatrix:
 
 def get_cg_iter_time(A, gt, rtol=1e-6, max_iter=0, dtype=np.float64, repeat=1, device="cuda",
                      method="ainv") -> Tuple[float, float, float]:
-    """validate.py:54-86 (method in none / diagonal; ic / ainv / fsai are baselines not built yet)."""
+    """validate.py:54-86: method none / diagonal / ic (IC(0), level-scheduled triangular solves) /
+    ainv (AINV(0) as L Lᵀ); the prec time is the device setup of the preconditioner."""
     Ad = _prepare(A, dtype)
     rows = Ad.n
     max_iter = max_iter if max_iter > 0 else rows

@@ -49,7 +49,7 @@ def test_no_gpu_fails_loudly():
     with pytest.raises(ValueError, match="MI355X only"):
         PreconditionedConjugateGradient(A, device="cpu", preconditioner="none")
     with pytest.raises(NotImplementedError):
-        PreconditionedConjugateGradient(A, device="cuda", preconditioner="ic")
+        PreconditionedConjugateGradient(A, device="cuda", preconditioner="fsai")
 
 
 def test_product_never_imports_oracle():

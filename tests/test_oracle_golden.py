@@ -137,3 +137,26 @@ def test_oracle_gnn_forward_shapes_and_message_direction():
     # through node 0, only through node 1 (2 hops after 4 layers both move) -- check determinism
     _, out2 = net(x, ei, ea)
     assert torch.equal(out, out2)
+
+
+def test_oracle_ic_operator_matches_scipy_triangular_solves():
+    """oracle.precond.ic_operator vs the reference's own IncompleteCholeskyPreconditioner
+    arithmetic (validate.py:344-369: two scipy spsolve_triangular calls)."""
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import spsolve_triangular
+
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from oracle import precond as OP
+
+    A = sp.csr_matrix(P.kuhn_laplacian(5, 1e-2))
+    L = OP.ic0(A)
+    r = np.random.default_rng(0).normal(size=A.shape[0])
+    ref = spsolve_triangular(sp.csc_matrix(L.T), spsolve_triangular(sp.csc_matrix(L), r, lower=True), lower=False)
+    np.testing.assert_allclose(OP.ic_operator(L)(r), ref, rtol=1e-12, atol=1e-14)
+    # IC(0) reproduces A on its pattern; AINV(0) is exact when the inverse factor's pattern fits
+    # triu(A) (2x2 diagonal blocks)
+    R = (L @ L.T - A).multiply(sp.csr_matrix(A != 0))
+    assert abs(R).max() < 1e-12
+    T = sp.csr_matrix(sp.block_diag([np.array([[2.0 + k, -1.0], [-1.0, 3.0]]) for k in range(15)]))
+    Lai = OP.ainv_spai_factor(T)
+    np.testing.assert_allclose((Lai @ Lai.T).toarray() @ T.toarray(), np.eye(30), atol=1e-12)
