@@ -160,13 +160,59 @@ __global__ void k_csc_sort(int64_t N, const int64_t* __restrict__ ei, int64_t E,
   }
 }
 
+// Fast path for row-major sorted edges with a symmetric pattern (every matrix graph of the
+// reference: edge_index comes from a CSR, data.py:471-536): the incoming edges of node c, in
+// ascending source order, are exactly the outgoing edges of c, so edge e = (r -> c) takes CSC slot
+// p = position of r in row c -- a binary search, no atomics and no sort.  flag bit 1: edges
+// not row-major strictly sorted, bit 2: pattern not symmetric (-> generic path).
+__global__ void k_csc_rowstart(int64_t N, int64_t E, const int64_t* __restrict__ ei, int32_t* __restrict__ ptr,
+                               int* flag) {
+  for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r <= N; r += int64_t(gridDim.x) * blockDim.x) {
+    int64_t lo = 0, hi = E;  // first edge with src >= r
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ei[mid] < r) lo = mid + 1;
+      else hi = mid;
+    }
+    ptr[r] = int32_t(lo);
+  }
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e + 1 < E; e += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t r0 = ei[e], r1 = ei[e + 1];
+    if (r0 > r1 || (r0 == r1 && ei[E + e] >= ei[E + e + 1])) atomicOr(flag, 1);
+  }
+}
+
+__global__ void k_csc_sym(int64_t E, const int64_t* __restrict__ ei, const int32_t* __restrict__ ptr,
+                          int32_t* __restrict__ perm, int32_t* __restrict__ inv, int32_t* __restrict__ src,
+                          int32_t* __restrict__ dst, int* flag) {
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t r = ei[e], c = ei[E + e];
+    int64_t lo = ptr[c], hi = ptr[c + 1];
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (ei[E + mid] < r) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo >= ptr[c + 1] || ei[E + lo] != r) {
+      atomicOr(flag, 2);
+      continue;
+    }
+    perm[lo] = int32_t(e);
+    inv[e] = int32_t(lo);
+    src[lo] = int32_t(r);
+    dst[lo] = int32_t(c);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Encoders / decoder (16-item MFMA tiles, 4 waves per workgroup, grid-stride over tiles)
 // ---------------------------------------------------------------------------
-// Encoder input layout: K slot q of step s = input feature 4s + q (zero past `fin`).
+// Encoder input layout: K slot q of step s = input feature 4s + q (zero past `fin`).  Inputs
+// are read in their own (coalesced) order; EDGE: the 64-B output row of edge e goes to its CSC
+// slot outidx[e].
 template <bool EDGE>
 __global__ void __launch_bounds__(256) k_encode(int64_t M, int fin, const float* __restrict__ fr,
-                                               const float* __restrict__ in, const int32_t* __restrict__ perm,
+                                               const float* __restrict__ in, const int32_t* __restrict__ outidx,
                                                float* __restrict__ out) {
   const int lane = threadIdx.x & 63, it = lane & 15, q = lane >> 4;
   const int s1 = (fin + 3) / 4;
@@ -175,15 +221,15 @@ __global__ void __launch_bounds__(256) k_encode(int64_t M, int fin, const float*
     const int64_t m = t * 16 + it;
     const bool valid = m < M;
     const int64_t mm = valid ? m : M - 1;
-    const int64_t row = EDGE ? int64_t(perm[mm]) : mm;
     f4 h = ld4(fr + s1 * 64 + lane * 4);
     for (int s = 0; s < s1; ++s) {
       const int f = 4 * s + q;
-      const float v = f < fin ? in[row * fin + f] : 0.f;
+      const float v = f < fin ? in[mm * fin + f] : 0.f;
       h = mfma(fr[s * 64 + lane], v, h);
     }
     const f4 o = ff_tail(fr, s1, h, lane);
-    if (valid) st4(out + mm * H + 4 * q, o);
+    const int64_t orow = EDGE ? int64_t(outidx[mm]) : mm;
+    if (valid) st4(out + orow * H + 4 * q, o);
   }
 }
 
@@ -436,6 +482,7 @@ struct lspcg_gnn {
   int64_t capN = -1, capE = -1;
   float *xa = nullptr, *xb = nullptr, *ecsc = nullptr;
   int32_t *ptr = nullptr, *cnt = nullptr, *perm = nullptr, *inv = nullptr, *src = nullptr, *dst = nullptr;
+  int* flag = nullptr;
   void* scan_tmp = nullptr;
   size_t scan_bytes = 0;
 };
@@ -453,6 +500,8 @@ static void gnn_free_ws(lspcg_gnn* g) {
     (void)hipFree(p);
   g->xa = g->xb = g->ecsc = nullptr;
   g->ptr = g->cnt = g->perm = g->inv = g->src = g->dst = nullptr;
+  (void)hipFree(g->flag);
+  g->flag = nullptr;
   g->scan_tmp = nullptr;
   g->capN = g->capE = -1;
 }
@@ -470,6 +519,7 @@ static int gnn_reserve(lspcg_gnn* g, int64_t N, int64_t E) {
   LSPCG_HIP(hipMalloc(&g->inv, sizeof(int32_t) * e));
   LSPCG_HIP(hipMalloc(&g->src, sizeof(int32_t) * e));
   LSPCG_HIP(hipMalloc(&g->dst, sizeof(int32_t) * e));
+  LSPCG_HIP(hipMalloc(&g->flag, sizeof(int)));
   g->scan_bytes = 0;
   LSPCG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, g->scan_bytes, g->cnt, g->ptr, int(n + 1), g->ctx->stream));
   LSPCG_HIP(hipMalloc(&g->scan_tmp, g->scan_bytes ? g->scan_bytes : 1));
@@ -542,18 +592,29 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
   const lspcg_gnn_desc& d = g->d;
   // CSC of the edges by destination
   LSPCG_HIP(hipMemsetAsync(g->cnt, 0, sizeof(int32_t) * (N + 1), st));
-  hipLaunchKernelGGL(k_csc_count, dim3(egrid(E)), dim3(kThreads), 0, st, E, edge_index, g->cnt);
-  size_t tb = g->scan_bytes;
-  LSPCG_HIP(hipcub::DeviceScan::ExclusiveSum(g->scan_tmp, tb, g->cnt, g->ptr, int(N + 1), st));
-  LSPCG_HIP(hipMemsetAsync(g->cnt, 0, sizeof(int32_t) * (N + 1), st));
-  hipLaunchKernelGGL(k_csc_fill, dim3(egrid(E)), dim3(kThreads), 0, st, E, edge_index, g->ptr, g->cnt, g->perm);
-  hipLaunchKernelGGL(k_csc_sort, dim3(egrid(N)), dim3(kThreads), 0, st, N, edge_index, E, g->ptr, g->perm, g->inv,
-                     g->src, g->dst);
+  LSPCG_HIP(hipMemsetAsync(g->flag, 0, sizeof(int), st));
+  hipLaunchKernelGGL(k_csc_rowstart, dim3(egrid(std::max(N + 1, E))), dim3(kThreads), 0, st, N, E, edge_index, g->ptr,
+                     g->flag);
+  hipLaunchKernelGGL(k_csc_sym, dim3(egrid(E)), dim3(kThreads), 0, st, E, edge_index, g->ptr, g->perm, g->inv, g->src,
+                     g->dst, g->flag);
+  int hflag = 0;
+  LSPCG_HIP(hipMemcpyAsync(&hflag, g->flag, sizeof(int), hipMemcpyDeviceToHost, st));
+  LSPCG_HIP(hipStreamSynchronize(st));
+  if (hflag) {  // generic: count by dst, scan, slot fill, per-node sort by edge id
+    LSPCG_HIP(hipMemsetAsync(g->cnt, 0, sizeof(int32_t) * (N + 1), st));
+    hipLaunchKernelGGL(k_csc_count, dim3(egrid(E)), dim3(kThreads), 0, st, E, edge_index, g->cnt);
+    size_t tb = g->scan_bytes;
+    LSPCG_HIP(hipcub::DeviceScan::ExclusiveSum(g->scan_tmp, tb, g->cnt, g->ptr, int(N + 1), st));
+    LSPCG_HIP(hipMemsetAsync(g->cnt, 0, sizeof(int32_t) * (N + 1), st));
+    hipLaunchKernelGGL(k_csc_fill, dim3(egrid(E)), dim3(kThreads), 0, st, E, edge_index, g->ptr, g->cnt, g->perm);
+    hipLaunchKernelGGL(k_csc_sort, dim3(egrid(N)), dim3(kThreads), 0, st, N, edge_index, E, g->ptr, g->perm, g->inv,
+                       g->src, g->dst);
+  }
   // encoders
   hipLaunchKernelGGL(k_encode<false>, dim3(tgrid(N)), dim3(256), 0, st, N, d.node_in, g->frag + g->o_node_enc, x,
                      static_cast<const int32_t*>(nullptr), g->xa);
   hipLaunchKernelGGL(k_encode<true>, dim3(tgrid(E)), dim3(256), 0, st, E, d.edge_in, g->frag + g->o_edge_enc,
-                     edge_attr, g->perm, g->ecsc);
+                     edge_attr, g->inv, g->ecsc);
   // message passing
   float* xc = g->xa;
   float* xn = g->xb;

@@ -5,8 +5,9 @@ preconditioner time averaged over ``repeat`` inference steps (:288-293), rhs = m
 random / neighbour (:297-307), the Neural PCG row (:322-331) and the two CSVs with the
 reference schema (:372-384: ``Key, Total Time (ms), Solve Time (ms), Precond Time (ms),
 #Iteration`` and the per-sample ``all_*`` file with ``Matrix Size``).  Differences: the
-PCG runs on the MI355X (key ``Neural+HIP``); the pymathprim baseline rows (:310-321) are
-not produced; ``Precond Time`` is the GNN time (the reference overwrites it with the last
+PCG runs on the MI355X (key ``Neural+HIP``); the pymathprim baseline rows (:310-321) are the
+``PCG-{none,diagonal,ainv,ic}-cuda`` rows of this framework's own GPU baselines (no ``-cpu``
+rows); ``Precond Time`` is the GNN time (the reference overwrites it with the last
 baseline's setup time).  Samples are sharded one-per-GPU under torchrun
 (``distributed.run_sharded``) with a single all-gather at the end.
 
@@ -28,7 +29,7 @@ import torch
 from . import problems as P
 from .data import GraphSample, make_sample
 from .distributed import SolveRecord, run_sharded
-from .validate import get_pcg_iter_time, get_pcg_scaled_iter_time
+from .validate import get_cg_iter_time, get_pcg_iter_time, get_pcg_scaled_iter_time
 from .workspace import ScaledInferenceWorkspace, SimpleInferenceWorkspace
 
 
@@ -169,6 +170,28 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
     return run_sharded(len(samples), weights, solve)
 
 
+def run_baseline(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, method: str, rtol: float = 1e-6,
+                 repeat: int = 1, rhs: str = "mask") -> List[SolveRecord]:
+    """The ``PCG-{method}-cuda`` rows (infer.py:310-321: get_cg_iter_time with method none /
+    diagonal / ainv / ic on the same A and rhs).  A non-converged solve raises RuntimeError in
+    the reference (caught at :363); here its row is NaN and left out of the statistics."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    def solve(i: int) -> SolveRecord:
+        s = samples[i].to(dev)
+        A = ws.system_matrix(s)
+        r = rhs_for(rhs, s.mask.cpu().numpy(), s)
+        try:
+            it, prec, sol = get_cg_iter_time(A, r, rtol=rtol, repeat=repeat, method=method)
+        except RuntimeError:
+            return SolveRecord(index=i, iters=float("nan"), rel_res=float("nan"), t_prec=float("nan"),
+                               t_solve=float("nan"), n=A.n, nnz=A.nnz, converged=False)
+        return SolveRecord(index=i, iters=it, rel_res=float("nan"), t_prec=prec, t_solve=sol, n=A.n, nnz=A.nnz)
+
+    weights = [float(s.edge_index.shape[1]) for s in samples]
+    return run_sharded(len(samples), weights, solve)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--dataset", default="heat_batch8")
@@ -189,6 +212,8 @@ def main(argv=None):
     ap.add_argument("--epsilon", type=float, default=3e-3)
     ap.add_argument("--out-dir", default="output")
     ap.add_argument("--infer-prefix", default="")
+    ap.add_argument("--baselines", default="none,diagonal,ainv,ic",
+                    help="comma list of PCG-{method}-cuda rows (infer.py:310-321); '' for none")
     args = ap.parse_args(argv)
 
     import torch.distributed as dist
@@ -210,11 +235,17 @@ def main(argv=None):
         s0 = samples[0]
         ws = cls(node_features=s0.x.shape[1], edge_features=s0.edge_attr.shape[1], block_size=s0.block_size,
                  epsilon=args.epsilon, seed=0)
-    recs = run(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, warmup=args.warmup)
+    rows = {}
+    for m in [b for b in args.baselines.split(",") if b]:
+        rows[f"PCG-{m}-cuda"] = run_baseline(samples, ws, m, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs)
+    rows["Neural+HIP"] = run(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, warmup=args.warmup)
+    recs = rows["Neural+HIP"]
     if not dist.is_initialized() or dist.get_rank() == 0:
         stats = Timestat()
-        for r in recs:
-            stats.put("Neural+HIP", r.t_solve, r.t_prec, r.iters, r.n)
+        for key, rs in rows.items():
+            for r in rs:
+                if r.iters == r.iters:  # NaN = not converged (reference: RuntimeError, row skipped)
+                    stats.put(key, r.t_solve, r.t_prec, r.iters, r.n)
         stats.print()
         out = Path(args.out_dir)
         out.mkdir(parents=True, exist_ok=True)

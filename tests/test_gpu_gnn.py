@@ -87,3 +87,26 @@ def test_inference_step_and_pcg_end_to_end(gpu_ctx):
     it, prec, solve = get_pcg_iter_time(A_dev, gt, L_dev, ws.epsilon, rtol=1e-8)
     it_o, _, _ = O.pcg(A_ref, A_ref @ gt, O.spai_operator(L_got, ws.epsilon), rtol=1e-8, dot="exact")
     assert it == it_o
+
+
+@pytest.mark.parametrize("graph", ["asymmetric", "unsorted", "isolated"])
+def test_gnn_generic_graphs(gpu_ctx, graph):
+    """Edge lists outside the CSR fast path (asymmetric pattern, unsorted order, nodes without
+    edges) go through the generic CSC build; results equal the oracle."""
+    rng = np.random.default_rng(7)
+    N, E = 300, 2400
+    src = rng.integers(0, N - 10, E)  # the last 10 nodes have no out-edges
+    dst = rng.integers(0, N - 10, E)
+    ei = np.unique(np.stack([src, dst]), axis=1)  # row-major sorted, duplicate free, asymmetric
+    if graph == "unsorted":
+        ei = ei[:, rng.permutation(ei.shape[1])]
+    elif graph == "isolated":
+        ei = ei[:, ei[0] < N // 2]
+    x = torch.from_numpy(rng.normal(size=(N, 3)).astype(np.float32))
+    ea = torch.from_numpy(rng.normal(size=(ei.shape[1], 1)).astype(np.float32))
+    eit = torch.from_numpy(ei.astype(np.int64))
+    ref, gpu = _pair(3, 1, 1, seed=11)
+    with torch.no_grad():
+        _, want = ref(x, eit, ea)
+    _, got = gpu(x.cuda(), eit.cuda(), ea.cuda())
+    _close(got.cpu().numpy(), want.numpy())

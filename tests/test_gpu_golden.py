@@ -96,3 +96,18 @@ def test_folder_dataset_through_hot_path(gpu_ctx, rhs):
         r = rhs_for(rhs, s.mask.numpy(), d)
         it_o, _, _ = O.pcg(A, A @ r, O.spai_operator(L.to_scipy(), ws.epsilon), rtol=1e-8, dot="exact")
         assert rec.iters == it_o, (rec.index, rec.iters, it_o)  # (tiny systems may need n iterations)
+
+
+def test_infer_main_writes_baseline_rows(gpu_ctx, tmp_path):
+    """infer CLI on an on-disk dataset: Neural+HIP and PCG-{none,diagonal,ainv,ic}-cuda rows."""
+    import pandas as pd
+
+    from learningsparsepreconditioner4gpu_amd.infer import main
+
+    main(["--folder", str(GOLDEN / "folder_free"), "--rtol", "1e-8", "--warmup", "1", "--out-dir", str(tmp_path)])
+    df = pd.read_csv(tmp_path / "infer_folder_free_8.csv")
+    keys = set(df["Key"])  # (a row whose every solve hit max_iter = n is left out, like the reference)
+    assert {"Neural+HIP", "PCG-ainv-cuda", "PCG-ic-cuda"} <= keys
+    assert keys <= {"Neural+HIP", "PCG-none-cuda", "PCG-diagonal-cuda", "PCG-ainv-cuda", "PCG-ic-cuda"}
+    alls = pd.read_csv(tmp_path / "all_infer_folder_free_8.csv")
+    assert list(alls.columns) == ["Key", "Solve Time (ms)", "Precond Time (ms)", "#Iteration", "Matrix Size"]
