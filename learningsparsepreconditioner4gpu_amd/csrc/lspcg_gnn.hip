@@ -47,26 +47,51 @@ __host__ __device__ constexpr int ff_size(int in, int out) { return H * in + H +
 __host__ __device__ constexpr int frag_size(int s1) { return s1 * 64 + 5 * 256; }
 
 // GELU(v) = 0.5 v erfc(-v/sqrt2).  erfc by the Chebyshev-fitted form of Numerical Recipes
-// (erfcc: fractional error < 1.2e-7 for every argument), branch-free: one rcp, one exp and 10
-// FMAs instead of ocml's two-branch erff -- the per-edge MLPs are VALU-bound on GELU.
-// Relative (not only absolute) accuracy also holds in the negative tail, where GELU -> 0.
-__device__ __forceinline__ float gelu(float v) {
-  const float z = fabsf(v) * 0.7071067811865476f;
-  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.5f, z, 1.0f));
-  float p = 0.17087277f;
-  p = __builtin_fmaf(t, p, -0.82215223f);
-  p = __builtin_fmaf(t, p, 1.48851587f);
-  p = __builtin_fmaf(t, p, -1.13520398f);
-  p = __builtin_fmaf(t, p, 0.27886807f);
-  p = __builtin_fmaf(t, p, -0.18628806f);
-  p = __builtin_fmaf(t, p, 0.09678418f);
-  p = __builtin_fmaf(t, p, 0.37409196f);
-  p = __builtin_fmaf(t, p, 1.00002368f);
-  p = __builtin_fmaf(t, p, -1.26551223f);
-  const float ec = t * __expf(__builtin_fmaf(-z, z, p));  // erfc(|v|/sqrt2)
-  return 0.5f * v * (v >= 0.f ? 2.0f - ec : ec);
+// (erfcc: fractional error < 1.2e-7 for every argument), branch-free: one rcp, one exp2 and 11
+// FMAs instead of ocml's two-branch erff -- the per-edge MLPs are VALU-bound on GELU.  Two
+// values at a time in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32) halve the polynomial's issue
+// cost.  Relative accuracy also holds in the negative tail, where GELU -> 0.
+using f2 = float __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, float c) { return __builtin_elementwise_fma(a, b, (f2)(c)); }
+// K independent pairs, every step interleaved across them: a dependent packed op needs a wait
+// state on gfx950, so one chain alone would issue an s_nop between every Horner step.
+template <int K>
+__device__ __forceinline__ void gelu_n(f2 (&v)[K]) {
+  f2 z[K], t[K], p[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) z[k] = __builtin_elementwise_abs(v[k]) * (f2)(0.7071067811865476f);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const f2 u = pfma(z[k], (f2)(0.5f), 1.0f);
+    t[k] = (f2){__builtin_amdgcn_rcpf(u.x), __builtin_amdgcn_rcpf(u.y)};
+  }
+  constexpr float C[10] = {0.17087277f, -0.82215223f, 1.48851587f, -1.13520398f, 0.27886807f,
+                           -0.18628806f, 0.09678418f, 0.37409196f, 1.00002368f, -1.26551223f};
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = pfma(t[k], (f2)(C[0]), C[1]);
+#pragma unroll
+  for (int c = 2; c < 10; ++c)
+#pragma unroll
+    for (int k = 0; k < K; ++k) p[k] = pfma(t[k], p[k], C[c]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const f2 arg = __builtin_elementwise_fma(-z[k], z[k], p[k]) * (f2)(1.4426950408889634f);  // log2(e) x
+    const f2 ec = t[k] * (f2){__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};  // erfc(|v|/sqrt2)
+    const f2 phi = {v[k].x >= 0.f ? 2.0f - ec.x : ec.x, v[k].y >= 0.f ? 2.0f - ec.y : ec.y};
+    v[k] = (f2)(0.5f) * v[k] * phi;
+  }
 }
-__device__ __forceinline__ f4 gelu4(f4 a) { return f4{gelu(a.x), gelu(a.y), gelu(a.z), gelu(a.w)}; }
+__device__ __forceinline__ f4 gelu4(f4 a) {
+  f2 v[2] = {(f2){a.x, a.y}, (f2){a.z, a.w}};
+  gelu_n<2>(v);
+  return f4{v[0].x, v[0].y, v[1].x, v[1].y};
+}
+__device__ __forceinline__ void gelu4x2(f4& a, f4& b) {
+  f2 v[4] = {(f2){a.x, a.y}, (f2){a.z, a.w}, (f2){b.x, b.y}, (f2){b.z, b.w}};
+  gelu_n<4>(v);
+  a = f4{v[0].x, v[0].y, v[1].x, v[1].y};
+  b = f4{v[2].x, v[2].y, v[3].x, v[3].y};
+}
 
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -90,8 +115,8 @@ __device__ __forceinline__ f4 ff_tail(const float* fr, int s1, f4 h, int lane) {
   return o;
 }
 
-// Two FFs with 48 inputs sharing the same B operand (message + edge MLP of an MPLayer),
-// interleaved so the two dependent MFMA chains overlap.
+// Two FFs with 48 inputs sharing the same B operand (message + edge MLP of an MPLayer): the
+// two dependent MFMA chains and the two GELU blocks are interleaved so they overlap.
 __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const float (&in)[12], int lane, f4& oa,
                                        f4& ob) {
   f4 ha = *reinterpret_cast<const f4*>(fa + 12 * 64 + lane * 4);
@@ -101,8 +126,26 @@ __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const f
     ha = mfma(fa[s * 64 + lane], in[s], ha);
     hb = mfma(fb[s * 64 + lane], in[s], hb);
   }
-  oa = ff_tail(fa, 12, ha, lane);
-  ob = ff_tail(fb, 12, hb, lane);
+  const float* a2 = fa + 12 * 64 + 256;
+  const float* b2 = fb + 12 * 64 + 256;
+  gelu4x2(ha, hb);
+  f4 h2a = *reinterpret_cast<const f4*>(a2 + 256 + lane * 4);
+  f4 h2b = *reinterpret_cast<const f4*>(b2 + 256 + lane * 4);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    h2a = mfma(a2[s * 64 + lane], comp(ha, s), h2a);
+    h2b = mfma(b2[s * 64 + lane], comp(hb, s), h2b);
+  }
+  gelu4x2(h2a, h2b);
+  const float* a3 = a2 + 512;
+  const float* b3 = b2 + 512;
+  oa = *reinterpret_cast<const f4*>(a3 + 256 + lane * 4);
+  ob = *reinterpret_cast<const f4*>(b3 + 256 + lane * 4);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    oa = mfma(a3[s * 64 + lane], comp(h2a, s), oa);
+    ob = mfma(b3[s * 64 + lane], comp(h2b, s), ob);
+  }
 }
 
 template <int S1>
@@ -340,7 +383,7 @@ __global__ void __launch_bounds__(256) k_mp_layer(int64_t N, const float* __rest
       }
       sq += __shfl_xor(sq, 16, 64);
       sq += __shfl_xor(sq, 32, 64);
-      const float rstd = 1.0f / sqrtf(sq * (1.0f / 48.0f) + 1e-5f);
+      const float rstd = __builtin_amdgcn_rsqf(sq * (1.0f / 48.0f) + 1e-5f);
 #pragma unroll
       for (int j = 0; j < 12; ++j) v[j] *= rstd;
       f4 m, u;
@@ -376,7 +419,7 @@ __global__ void __launch_bounds__(256) k_mp_layer(int64_t N, const float* __rest
     float sq = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
     sq += __shfl_xor(sq, 16, 64);
     sq += __shfl_xor(sq, 32, 64);
-    const float rstd = 1.0f / sqrtf(sq * (1.0f / 16.0f) + 1e-5f);
+    const float rstd = __builtin_amdgcn_rsqf(sq * (1.0f / 16.0f) + 1e-5f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] *= rstd;
     f4 o = ff_tile<4>(fnode, v, lane);
