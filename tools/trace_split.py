@@ -1,0 +1,32 @@
+"""Split the roofline SpMV's rocprofv3 kernel-trace durations into cold (dispatch right after the
+L3-evicting k_flush_read) and warm (right after another SpMV) launches, so the profile's average
+can be compared with bench.py's HIP-event cold / warm figures.
+
+    python tools/trace_split.py gpurun_out/prof_<tag>/bench_kernel_trace.csv
+"""
+import csv
+import json
+import sys
+
+KEY = "EpiStore<double>"  # standalone k_spmv<double, double, 1, ...> of A (bench.py roofline launches)
+
+
+def main(path):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    cold, warm = [], []
+    prev = ""
+    for r in rows:
+        name = r["Kernel_Name"]
+        if KEY in name and "k_spmv<double, double, 1," in name:
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
+            (cold if "k_flush_read" in prev else warm).append(dur)
+        prev = name
+    med = lambda v: sorted(v)[len(v) // 2] if v else None
+    avg = lambda v: sum(v) / len(v) if v else None
+    print(json.dumps({"kernel": "k_spmv<double,double,1,...,EpiStore<double>>", "cold_n": len(cold),
+                      "cold_avg_us": avg(cold), "cold_median_us": med(cold), "warm_n": len(warm),
+                      "warm_avg_us": avg(warm), "warm_median_us": med(warm)}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
