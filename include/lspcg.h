@@ -96,6 +96,11 @@ int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y,
  * kSpmvVariants) exactly like lspcg_spmv_timed; variant < 0 returns the number of variants */
 int lspcg_spmv_variant_timed(lspcg_ctx* ctx, const lspcg_mat* A, int variant, const void* x, void* y,
                              int reps, int64_t flush_bytes, double* avg_ms);
+/* diagnostics: the same timing for the SELL-64 kernel the PCG loop uses (csrc/lspcg_sell.hpp) on a
+ * SELL copy of A built inside the call (fp64 scalar CSR; compact != 0 stores the values as fp32,
+ * which is lossless only when every value is fp32-representable); y = A x, same bits */
+int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int compact, const void* x, void* y,
+                          int reps, int64_t flush_bytes, double* avg_ms);
 /* ---- baseline preconditioners (pymathprim "ic" / "ainv", infer.py:310-321; algorithms and
  * operation order: oracle/precond.py; scalar CSR, sorted rows, stored diagonal) ---- */
 /* IC(0): *L = lower-triangular factor with the pattern of tril(A), A ~ L L^T */

@@ -48,6 +48,7 @@ SIGNATURES = {
     "lspcg_spmv": (C.c_int, [vp, vp, vp, vp]),
     "lspcg_spmv_timed": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int64, p_f64]),
     "lspcg_spmv_variant_timed": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int64, p_f64]),
+    "lspcg_spmv_sell_timed": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int64, p_f64]),
     "lspcg_ic0": (C.c_int, [vp, pp, p_f64]),
     "lspcg_ainv0": (C.c_int, [vp, pp, p_f64]),
     "lspcg_trsv": (C.c_int, [vp, C.c_int, vp, vp]),

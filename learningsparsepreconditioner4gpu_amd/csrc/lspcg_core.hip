@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "lspcg_internal.hpp"
+#include "lspcg_sell.hpp"
 #include "lspcg_spmv.hpp"
 
 namespace lspcg {
@@ -398,8 +399,11 @@ int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y) {
   return LSPCG_OK;
 }
 
-static int spmv_timed_impl(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y, int reps, int64_t flush_bytes,
-                           double* avg_ms, SpmvLaunch fn) {
+}  // extern "C"
+
+template <class Launch>
+static int spmv_timed_impl(lspcg_ctx* ctx, const lspcg_mat* A, int reps, int64_t flush_bytes, double* avg_ms,
+                           Launch launch) {
   LSPCG_CHECK(ctx && A && reps > 0 && avg_ms && flush_bytes >= 0, LSPCG_ERR_ARG, "spmv_timed: bad argument");
   hipEvent_t e0, e1;
   LSPCG_HIP(hipEventCreate(&e0));
@@ -409,14 +413,6 @@ static int spmv_timed_impl(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, vo
     LSPCG_HIP(hipMalloc(&flush, size_t(flush_bytes) + 64));
     LSPCG_HIP(hipMemsetAsync(flush, 1, size_t(flush_bytes) + 64, ctx->stream));
   }
-  auto launch = [&]() -> int {
-    if (fn) {
-      fn(A, x, y, ctx->stream);
-      LSPCG_HIP(hipGetLastError());
-      return LSPCG_OK;
-    }
-    return lspcg_spmv(ctx, A, x, y);
-  };
   double total = 0.0;
   if (!flush) {
     if (int rc = launch()) return rc;  // untimed first launch
@@ -463,9 +459,11 @@ static int spmv_timed_impl(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, vo
   return LSPCG_OK;
 }
 
+extern "C" {
+
 int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y, int reps, int64_t flush_bytes,
                      double* avg_ms) {
-  return spmv_timed_impl(ctx, A, x, y, reps, flush_bytes, avg_ms, nullptr);
+  return spmv_timed_impl(ctx, A, reps, flush_bytes, avg_ms, [&]() -> int { return lspcg_spmv(ctx, A, x, y); });
 }
 
 int lspcg_spmv_variant_timed(lspcg_ctx* ctx, const lspcg_mat* A, int variant, const void* x, void* y, int reps,
@@ -473,7 +471,37 @@ int lspcg_spmv_variant_timed(lspcg_ctx* ctx, const lspcg_mat* A, int variant, co
   if (variant < 0) return kNumSpmvVariants;
   LSPCG_CHECK(A && variant < kNumSpmvVariants && A->dtype == LSPCG_F64 && A->block_size == 1, LSPCG_ERR_ARG,
               "spmv_variant_timed: fp64 scalar CSR and a valid variant id required");
-  return spmv_timed_impl(ctx, A, x, y, reps, flush_bytes, avg_ms, kSpmvVariants[variant]);
+  return spmv_timed_impl(ctx, A, reps, flush_bytes, avg_ms, [&]() -> int {
+    kSpmvVariants[variant](A, x, y, ctx->stream);
+    LSPCG_HIP(hipGetLastError());
+    return LSPCG_OK;
+  });
+}
+
+int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int compact, const void* x, void* y, int reps,
+                          int64_t flush_bytes, double* avg_ms) {
+  LSPCG_CHECK(ctx && A && x && y && A->dtype == LSPCG_F64 && A->block_size == 1 && A->storage_dtype() == LSPCG_F64,
+              LSPCG_ERR_ARG, "spmv_sell_timed: fp64 scalar CSR required");
+  hipStream_t st = ctx->stream;
+  SellPattern P;
+  int rc = sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, 1e30, st, &P);  // any padding
+  if (rc) return rc;
+  void* v = nullptr;
+  rc = sell_fill_values(P, A->colind, A->vals, LSPCG_F64, compact ? LSPCG_F32 : LSPCG_F64, st, &v);
+  if (!rc) {
+    const GatherVec<double> gx{static_cast<const double*>(x)};
+    const EpiStore<double> epi{static_cast<double*>(y)};
+    rc = spmv_timed_impl(ctx, A, reps, flush_bytes, avg_ms, [&]() -> int {
+      if (compact) launch_spmv_sell_cfg<double, float>(P, v, gx, ProNone{}, epi, st);
+      else launch_spmv_sell_cfg<double, double>(P, v, gx, ProNone{}, epi, st);
+      LSPCG_HIP(hipGetLastError());
+      return LSPCG_OK;
+    });
+  }
+  (void)hipStreamSynchronize(st);
+  (void)hipFree(v);
+  P.release();
+  return rc;
 }
 
 int lspcg_dot(lspcg_ctx* ctx, int64_t n, int dtype, const void* x, const void* y, double* out) {

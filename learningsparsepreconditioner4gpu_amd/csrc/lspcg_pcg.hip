@@ -27,6 +27,7 @@
 
 #include "lspcg_factor.hpp"
 #include "lspcg_internal.hpp"
+#include "lspcg_sell.hpp"
 #include "lspcg_spmv.hpp"
 
 namespace lspcg {
@@ -373,7 +374,58 @@ struct lspcg_solver {
   lspcg_mat* icL = nullptr;
   lspcg_mat* icU = nullptr;
   Levels levL, levU;
+  // SELL-64 copies of the scalar iteration views A (0), L (1), Lᵀ (2) (lspcg_sell.hpp); sp[w]
+  // is null where the CSR kernel is used (block size 3, irregular rows, LSPCG_NO_SELL=1)
+  bool use_sell = true;
+  SellPattern spat[3];
+  const SellPattern* sp[3] = {nullptr, nullptr, nullptr};
+  void* sv[3] = {nullptr, nullptr, nullptr};
+  int svd[3] = {0, 0, 0};
 };
+
+// (Re)build the SELL copy of iteration view w (0 = A, 1 = L, 2 = Lᵀ); L and Lᵀ reuse A's
+// pattern when make_view found the same index arrays.
+static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
+  hipStream_t st = s->ctx->stream;
+  LSPCG_HIP(hipStreamSynchronize(s->stream));
+  (void)hipFree(s->sv[w]);
+  s->sv[w] = nullptr;
+  s->spat[w].release();
+  s->sp[w] = nullptr;
+  if (!s->use_sell || view->block_size != 1 || view->n == 0 || view->nnzb == 0) return LSPCG_OK;
+  const SellPattern* P = nullptr;
+  if (w > 0 && s->sp[0] && view->rowptr == s->Av.rowptr && view->colind == s->Av.colind) {
+    P = s->sp[0];
+  } else {
+    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, 1.5, st, &s->spat[w]);
+    if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: CSR kernel
+    if (rc) return rc;
+    P = &s->spat[w];
+  }
+  const int vd = view->storage_dtype();
+  if (int rc = sell_fill_values(*P, view->colind, view->vals, vd, vd, st, &s->sv[w])) return rc;
+  LSPCG_HIP(hipStreamSynchronize(st));
+  s->svd[w] = vd;
+  s->sp[w] = P;
+  return LSPCG_OK;
+}
+
+// SpMV of iteration view w with the fused prologue / epilogue, SELL when available.
+template <typename T, class Pro, class Epi>
+static int launch_it(lspcg_solver* s, int w, const T* x, Pro pro, Epi epi, hipStream_t st) {
+  if (const SellPattern* P = s->sp[w]) {
+    if constexpr (sizeof(T) == 8) {
+      if (s->svd[w] == LSPCG_F32) {
+        launch_spmv_sell_cfg<T, float>(*P, s->sv[w], GatherVec<T>{x}, pro, epi, st);
+        return LSPCG_OK;
+      }
+    }
+    launch_spmv_sell_cfg<T, T>(*P, s->sv[w], GatherVec<T>{x}, pro, epi, st);
+    return LSPCG_OK;
+  }
+  const lspcg_mat* V = w == 0 ? &s->Av : (w == 1 ? &s->Lv : &s->LTv);
+  return launch_spmv_any<T>(V, x, pro, epi, st);
+}
 
 static int flag_run(lspcg_solver* s, hipStream_t st, int* out) {
   int h = 0;
@@ -444,12 +496,12 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
     case LSPCG_PRECOND_EXT_SPAI:
     case LSPCG_PRECOND_EXT_SPAI_SCALED: {
       const bool sc = s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
-      rc = sc ? launch_spmv_any<T>(&s->LTv, static_cast<const T*>(r), ProCheck<T>{S}, EpiT<T, true>{t, d}, st)
-              : launch_spmv_any<T>(&s->LTv, static_cast<const T*>(r), ProCheck<T>{S}, EpiT<T, false>{t, d}, st);
+      rc = sc ? launch_it<T>(s, 2, static_cast<const T*>(r), ProCheck<T>{S}, EpiT<T, true>{t, d}, st)
+              : launch_it<T>(s, 2, static_cast<const T*>(r), ProCheck<T>{S}, EpiT<T, false>{t, d}, st);
       if (rc) return rc;
-      rc = sc ? launch_spmv_any<T>(&s->Lv, static_cast<const T*>(t), ProDone{S},
+      rc = sc ? launch_it<T>(s, 1, static_cast<const T*>(t), ProDone{S},
                                    EpiZ<T, true>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st)
-              : launch_spmv_any<T>(&s->Lv, static_cast<const T*>(t), ProDone{S},
+              : launch_it<T>(s, 1, static_cast<const T*>(t), ProDone{S},
                                    EpiZ<T, false>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st);
       if (rc) return rc;
       hipLaunchKernelGGL((k_update_p<T, ProDone>), dim3(eg), dim3(kThreads), 0, st, n, ProDone{S}, S,
@@ -476,7 +528,7 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
       set_error("unknown preconditioner");
       return LSPCG_ERR_ARG;
   }
-  rc = launch_spmv_any<T>(&s->Av, static_cast<const T*>(p), ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket},
+  rc = launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket},
                           st);
   if (rc) return rc;
   switch (s->precond) {
@@ -504,10 +556,10 @@ static int enqueue_init(lspcg_solver* s, hipStream_t st) {
   T* z = static_cast<T*>(s->z);
   const T* x = static_cast<const T*>(s->x);
   const int rc = s->precond == LSPCG_PRECOND_DIAGONAL
-                     ? launch_spmv_any<T>(&s->Av, x, ProNone{},
+                     ? launch_it<T>(s, 0, x, ProNone{},
                                           EpiResid<T, LSPCG_PRECOND_DIAGONAL>{r, b, d, z, s->S, s->partials, s->ticket},
                                           st)
-                     : launch_spmv_any<T>(&s->Av, x, ProNone{},
+                     : launch_it<T>(s, 0, x, ProNone{},
                                           EpiResid<T, LSPCG_PRECOND_NONE>{r, b, d, z, s->S, s->partials, s->ticket},
                                           st);
   if (rc) return rc;
@@ -581,7 +633,9 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   LSPCG_HIP(hipEventCreate(&s->ev_t1));
   LSPCG_HIP(hipMalloc(&s->flag, sizeof(int)));
   if (const char* e = std::getenv("LSPCG_NO_COMPACT")) s->compact = e[0] == '0';
+  if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
   if (int rc = make_view(s.get(), A, &s->Av, nullptr, &s->own_A)) return rc;
+  if (int rc = build_sell(s.get(), 0, &s->Av)) return rc;
   if (precond == LSPCG_PRECOND_DIAGONAL) {
     int rc = lspcg_mat_diagonal(A, s->d);  // issues on ctx stream
     if (rc) return rc;
@@ -612,6 +666,8 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   }
   if ((rc = make_view(s, L, &s->Lv, &s->Av, &s->own_L))) return rc;
   if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT))) return rc;
+  if ((rc = build_sell(s, 1, &s->Lv))) return rc;
+  if ((rc = build_sell(s, 2, &s->LTv))) return rc;
   LSPCG_HIP(hipEventRecord(s->ev_t1, cst));
   LSPCG_HIP(hipEventSynchronize(s->ev_t1));
   float ms = 0.f;
@@ -759,6 +815,10 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   s->levL.release();
   s->levU.release();
   for (void* p : {s->own_A, s->own_L, s->own_LT}) (void)hipFree(p);
+  for (int w = 0; w < 3; ++w) {
+    (void)hipFree(s->sv[w]);
+    s->spat[w].release();
+  }
   (void)hipFree(s->flag);
   (void)hipStreamDestroy(s->stream);
   delete s;

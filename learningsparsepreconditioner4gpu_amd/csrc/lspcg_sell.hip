@@ -1,0 +1,131 @@
+// SELL-64 view construction (layout and rationale: lspcg_sell.hpp).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+#include "lspcg_sell.hpp"
+
+namespace lspcg {
+
+// ---- construction kernels --------------------------------------------------
+// groups-per-row of each slice = ceil(max row length / 4)
+__global__ void k_sell_len(int64_t n, int64_t ns, const int32_t* __restrict__ rowptr, int32_t* __restrict__ cnt) {
+  const int64_t s = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= ns) return;
+  const int64_t i = s * kSellC + lane;
+  int len = i < n ? rowptr[i + 1] - rowptr[i] : 0;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) len = max(len, __shfl_xor(len, m, 64));
+  if (lane == 0) cnt[s] = (len + 3) >> 2;
+}
+
+// one thread per row: scatter the row's columns (and, if src != nullptr, values) into the
+// slice layout; padding slots get column = row, value = 0
+template <typename VS, typename VD>
+__global__ void k_sell_fill(int64_t n, const int32_t* __restrict__ gp, const int32_t* __restrict__ rowptr,
+                            const int32_t* __restrict__ colind, const VS* __restrict__ src, int32_t* __restrict__ col,
+                            VD* __restrict__ dst) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t s = i / kSellC;
+    const int r = int(i % kSellC);
+    const int32_t b = rowptr[i], len = rowptr[i + 1] - b;
+    const int32_t slots = 4 * (gp[s + 1] - gp[s]);
+    const int64_t base = 256 * int64_t(gp[s]) + 4 * r;
+    for (int32_t k = 0; k < slots; ++k) {
+      const int64_t pos = base + 256 * int64_t(k >> 2) + (k & 3);
+      if (col) col[pos] = k < len ? colind[b + k] : int32_t(i);
+      if (dst) dst[pos] = k < len ? VD(src[b + k]) : VD(0);
+    }
+  }
+}
+
+static int fill_grid(int64_t n) {
+  return int(std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, kElemBlocksMax)));
+}
+
+int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
+                       hipStream_t st, SellPattern* out) {
+  SellPattern P;
+  P.n = n;
+  P.ns = (n + kSellC - 1) / kSellC;
+  P.rowptr = rowptr;
+  int32_t* cnt = nullptr;
+  void* tmp = nullptr;
+  auto fail = [&](hipError_t e) {
+    set_error(std::string("sell_build_pattern: ") + hipGetErrorString(e));
+    (void)hipFree(cnt);
+    (void)hipFree(tmp);
+    P.release();
+    return LSPCG_ERR_HIP;
+  };
+  hipError_t e = hipMalloc(&cnt, sizeof(int32_t) * (P.ns + 1));
+  if (e == hipSuccess) e = hipMalloc(&P.gp, sizeof(int32_t) * (P.ns + 1));
+  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (P.ns + 1), st);
+  if (e != hipSuccess) return fail(e);
+  if (P.ns) hipLaunchKernelGGL(k_sell_len, dim3(unsigned((P.ns + 3) / 4)), dim3(256), 0, st, n, P.ns, rowptr, cnt);
+  size_t tb = 0;
+  e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, P.gp, int(P.ns + 1), st);
+  if (e == hipSuccess) e = hipMalloc(&tmp, tb);
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, P.gp, int(P.ns + 1), st);
+  int32_t groups = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&groups, P.gp + P.ns, sizeof(int32_t), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return fail(e);
+  (void)hipFree(cnt);
+  (void)hipFree(tmp);
+  cnt = nullptr;
+  tmp = nullptr;
+  P.groups = groups;
+  if (double(256) * double(groups) > max_pad * double(std::max<int64_t>(nnz, 1))) {
+    P.release();
+    set_error("sell: padding exceeds the limit (irregular row lengths)");
+    return LSPCG_ERR_UNSUPPORTED;
+  }
+  // zero first: slots of the lanes past row n-1 in the last slice are never written by the
+  // fill and would otherwise hold garbage columns (the kernel gathers them, masked at the add)
+  e = hipMalloc(&P.col, sizeof(int32_t) * std::max<int64_t>(256 * P.groups, 1));
+  if (e == hipSuccess) e = hipMemsetAsync(P.col, 0, sizeof(int32_t) * std::max<int64_t>(256 * P.groups, 1), st);
+  if (e != hipSuccess) return fail(e);
+  if (n)
+    hipLaunchKernelGGL((k_sell_fill<float, float>), dim3(fill_grid(n)), dim3(kThreads), 0, st, n, P.gp, rowptr, colind,
+                       static_cast<const float*>(nullptr), P.col, static_cast<float*>(nullptr));
+  e = hipGetLastError();
+  if (e != hipSuccess) return fail(e);
+  *out = P;
+  return LSPCG_OK;
+}
+
+int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* src, int src_dtype, int dst_dtype,
+                     hipStream_t st, void** out) {
+  const size_t es = dst_dtype == LSPCG_F32 ? 4 : 8;
+  void* v = nullptr;
+  LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(256 * P.groups, 1)));
+  LSPCG_HIP(hipMemsetAsync(v, 0, es * std::max<int64_t>(256 * P.groups, 1), st));
+  const dim3 g(fill_grid(P.n)), b(kThreads);
+  if (P.n) {
+    if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F64)
+      hipLaunchKernelGGL((k_sell_fill<double, double>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
+                         static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<double*>(v));
+    else if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F32)
+      hipLaunchKernelGGL((k_sell_fill<double, float>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
+                         static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<float*>(v));
+    else if (src_dtype == LSPCG_F32 && dst_dtype == LSPCG_F32)
+      hipLaunchKernelGGL((k_sell_fill<float, float>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
+                         static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<float*>(v));
+    else
+      hipLaunchKernelGGL((k_sell_fill<float, double>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
+                         static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<double*>(v));
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    (void)hipFree(v);
+    set_error(std::string("sell_fill_values: ") + hipGetErrorString(e));
+    return LSPCG_ERR_HIP;
+  }
+  *out = v;
+  return LSPCG_OK;
+}
+
+}  // namespace lspcg

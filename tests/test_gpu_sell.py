@@ -1,0 +1,94 @@
+"""GPU parity of the SELL-64 iteration views (csrc/lspcg_sell.hpp) the PCG loop uses.
+
+The SELL kernel must give the CSR kernel's (= scipy csr_matvec's) exact bits on every
+matrix shape, and the PCG with SELL views the same iterate / residual history as with the
+CSR views (LSPCG_NO_SELL=1) -- bit for bit, not within a tolerance.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from tests import _cases
+from learningsparsepreconditioner4gpu_amd import problems as P
+
+pytestmark = pytest.mark.gpu
+
+
+def _dm(A, dtype=np.float64):
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    return DeviceMatrix.from_scipy(A, dtype=dtype)
+
+
+def _sell_spmv(Ad, x, compact):
+    from learningsparsepreconditioner4gpu_amd import _lib
+
+    y = torch.full_like(x, float("nan"))
+    ms = C.c_double()
+    _lib.call("lspcg_spmv_sell_timed", Ad.ctx.handle, Ad.handle, int(compact), C.c_void_p(x.data_ptr()),
+              C.c_void_p(y.data_ptr()), 1, 0, C.byref(ms))
+    return y.cpu().numpy()
+
+
+MATS = {
+    "synthetic": lambda: P.generate_spd_sparse_matrix(3000, 3e-3, 1e-5, np.random.RandomState(0)),
+    "kuhn": lambda: P.kuhn_laplacian(13),
+    "ragged": lambda: _cases.ragged_matrix(),  # empty rows, a 5000-entry row
+    "n1": lambda: sp.csr_matrix(np.array([[2.5]])),
+    "n65": lambda: sp.random(65, 65, density=0.2, random_state=3, format="csr") + sp.eye(65, format="csr"),
+    "zero-rows": lambda: sp.csr_matrix((sp.eye(130, format="csr").toarray() * (np.arange(130) % 3 == 0))),
+}
+
+
+@pytest.mark.parametrize("which", list(MATS))
+def test_sell_spmv_bitwise_vs_scipy(gpu_ctx, which):
+    A = sp.csr_matrix(MATS[which]()).astype(np.float64)
+    A.sort_indices()
+    # fp32-representable values so that the compact (fp32-stored) variant is lossless too
+    A.data = A.data.astype(np.float32).astype(np.float64)
+    x = np.random.default_rng(5).normal(size=A.shape[0])
+    x[::17] = -0.0
+    ref = A @ x
+    Ad = _dm(A)
+    xt = torch.from_numpy(x).cuda()
+    for compact in (0, 1):
+        y = _sell_spmv(Ad, xt, compact)
+        assert np.array_equal(y, ref), (which, compact, np.nanmax(np.abs(y - ref)))
+
+
+def test_sell_skips_padding_with_inf(gpu_ctx):
+    # a short row next to long ones: padded slots must not add 0*inf (NaN) into the sum
+    A = sp.csr_matrix(np.triu(np.ones((70, 70))))
+    x = np.ones(70)
+    x[0] = np.inf
+    ref = A @ x
+    y = _sell_spmv(_dm(A), torch.from_numpy(x).cuda(), 0)
+    assert np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])
+
+
+@pytest.mark.parametrize("precond", ["none", "diagonal", "ext_spai"])
+@pytest.mark.parametrize("case", [0, 1, 2, 3])
+def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    name, A, mask = _cases.spd_cases()[case]
+    A = sp.csr_matrix(A).astype(np.float64)
+    n = A.shape[0]
+    b = torch.from_numpy(A @ np.ones(n)).cuda()
+    out = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("LSPCG_NO_SELL", env)
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
+        if precond == "ext_spai":
+            s.set_spai(_cases.spai_like(A), 1e-3)
+        x = torch.zeros(n, dtype=torch.float64, device="cuda")
+        it, conv, _, hist = s.solve(b, x, rtol=1e-8, return_history=True)
+        out.append((it, x.cpu().numpy(), hist))
+        del s
+    assert out[0][0] == out[1][0], (name, out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1]), name
+    assert np.array_equal(out[0][2], out[1][2]), name
