@@ -97,9 +97,10 @@ int lspcg_spmv_timed(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y,
 int lspcg_spmv_variant_timed(lspcg_ctx* ctx, const lspcg_mat* A, int variant, const void* x, void* y,
                              int reps, int64_t flush_bytes, double* avg_ms);
 /* diagnostics: the same timing for the SELL-64 kernel the PCG loop uses (csrc/lspcg_sell.hpp) on a
- * SELL copy of A built inside the call (fp64 scalar CSR; compact != 0 stores the values as fp32,
- * which is lossless only when every value is fp32-representable); y = A x, same bits */
-int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int compact, const void* x, void* y,
+ * SELL copy of A built inside the call (fp64 scalar CSR).  flags bit 0: store the values as fp32
+ * (lossless only when every value is fp32-representable); bit 1: 16-bit column offsets where they
+ * fit.  y = A x, same bits as lspcg_spmv */
+int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int flags, const void* x, void* y,
                           int reps, int64_t flush_bytes, double* avg_ms);
 /* ---- baseline preconditioners (pymathprim "ic" / "ainv", infer.py:310-321; algorithms and
  * operation order: oracle/precond.py; scalar CSR, sorted rows, stored diagonal) ---- */

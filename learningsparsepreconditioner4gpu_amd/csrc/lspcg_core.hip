@@ -484,15 +484,15 @@ int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int compact, const
               LSPCG_ERR_ARG, "spmv_sell_timed: fp64 scalar CSR required");
   hipStream_t st = ctx->stream;
   SellPattern P;
-  int rc = sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, 1e30, st, &P);  // any padding
+  int rc = sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, 1e30, (compact & 2) != 0, st, &P);  // any padding
   if (rc) return rc;
   void* v = nullptr;
-  rc = sell_fill_values(P, A->colind, A->vals, LSPCG_F64, compact ? LSPCG_F32 : LSPCG_F64, st, &v);
+  rc = sell_fill_values(P, A->colind, A->vals, LSPCG_F64, (compact & 1) ? LSPCG_F32 : LSPCG_F64, st, &v);
   if (!rc) {
     const GatherVec<double> gx{static_cast<const double*>(x)};
     const EpiStore<double> epi{static_cast<double*>(y)};
     rc = spmv_timed_impl(ctx, A, reps, flush_bytes, avg_ms, [&]() -> int {
-      if (compact) launch_spmv_sell_cfg<double, float>(P, v, gx, ProNone{}, epi, st);
+      if (compact & 1) launch_spmv_sell_cfg<double, float>(P, v, gx, ProNone{}, epi, st);
       else launch_spmv_sell_cfg<double, double>(P, v, gx, ProNone{}, epi, st);
       LSPCG_HIP(hipGetLastError());
       return LSPCG_OK;

@@ -377,6 +377,7 @@ struct lspcg_solver {
   // SELL-64 copies of the scalar iteration views A (0), L (1), Lᵀ (2) (lspcg_sell.hpp); sp[w]
   // is null where the CSR kernel is used (block size 3, irregular rows, LSPCG_NO_SELL=1)
   bool use_sell = true;
+  bool sell16 = true;  // 16-bit column offsets where they fit (LSPCG_SELL32=1 disables)
   SellPattern spat[3];
   const SellPattern* sp[3] = {nullptr, nullptr, nullptr};
   void* sv[3] = {nullptr, nullptr, nullptr};
@@ -397,7 +398,8 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   if (w > 0 && s->sp[0] && view->rowptr == s->Av.rowptr && view->colind == s->Av.colind) {
     P = s->sp[0];
   } else {
-    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, 1.5, st, &s->spat[w]);
+    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, 1.5, s->sell16, st,
+                                      &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: CSR kernel
     if (rc) return rc;
     P = &s->spat[w];
@@ -634,6 +636,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   LSPCG_HIP(hipMalloc(&s->flag, sizeof(int)));
   if (const char* e = std::getenv("LSPCG_NO_COMPACT")) s->compact = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
+  if (const char* e = std::getenv("LSPCG_SELL32")) s->sell16 = e[0] == '0';
   if (int rc = make_view(s.get(), A, &s->Av, nullptr, &s->own_A)) return rc;
   if (int rc = build_sell(s.get(), 0, &s->Av)) return rc;
   if (precond == LSPCG_PRECOND_DIAGONAL) {

@@ -21,12 +21,13 @@ __global__ void k_sell_len(int64_t n, int64_t ns, const int32_t* __restrict__ ro
   if (lane == 0) cnt[s] = (len + 3) >> 2;
 }
 
-// one thread per row: scatter the row's columns (and, if src != nullptr, values) into the
-// slice layout; padding slots get column = row, value = 0
+// one thread per row: scatter the row's columns (col32 / col16, whichever is non-null) and,
+// if src != nullptr, values into the slice layout; padding slots get value 0 and column = the
+// row (col32) or kSellPad16 (col16)
 template <typename VS, typename VD>
 __global__ void k_sell_fill(int64_t n, const int32_t* __restrict__ gp, const int32_t* __restrict__ rowptr,
-                            const int32_t* __restrict__ colind, const VS* __restrict__ src, int32_t* __restrict__ col,
-                            VD* __restrict__ dst) {
+                            const int32_t* __restrict__ colind, const VS* __restrict__ src,
+                            int32_t* __restrict__ col32, int16_t* __restrict__ col16, VD* __restrict__ dst) {
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     const int64_t s = i / kSellC;
     const int r = int(i % kSellC);
@@ -35,8 +36,22 @@ __global__ void k_sell_fill(int64_t n, const int32_t* __restrict__ gp, const int
     const int64_t base = 256 * int64_t(gp[s]) + 4 * r;
     for (int32_t k = 0; k < slots; ++k) {
       const int64_t pos = base + 256 * int64_t(k >> 2) + (k & 3);
-      if (col) col[pos] = k < len ? colind[b + k] : int32_t(i);
+      if (col32) col32[pos] = k < len ? colind[b + k] : int32_t(i);
+      if (col16) col16[pos] = k < len ? int16_t(colind[b + k] - int32_t(s * kSellC)) : kSellPad16;
       if (dst) dst[pos] = k < len ? VD(src[b + k]) : VD(0);
+    }
+  }
+}
+
+// flag |= some column is more than 32767 away from its slice's first row
+__global__ void k_sell_fit16(int64_t n, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                             int* __restrict__ flag) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t base = int32_t((i / kSellC) * kSellC);
+    const int32_t b = rowptr[i], e = rowptr[i + 1];
+    if (e > b) {  // sorted columns: the extremes are the first and last entries
+      const int32_t lo = colind[b] - base, hi = colind[e - 1] - base;
+      if (lo < -32767 || hi > 32767) atomicOr(flag, 1);
     }
   }
 }
@@ -46,7 +61,7 @@ static int fill_grid(int64_t n) {
 }
 
 int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
-                       hipStream_t st, SellPattern* out) {
+                       bool allow16, hipStream_t st, SellPattern* out) {
   SellPattern P;
   P.n = n;
   P.ns = (n + kSellC - 1) / kSellC;
@@ -83,14 +98,29 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
     set_error("sell: padding exceeds the limit (irregular row lengths)");
     return LSPCG_ERR_UNSUPPORTED;
   }
+  int fit = 1;  // 0 = 16-bit offsets fit
+  if (allow16 && n) {
+    int* flag = nullptr;
+    e = hipMalloc(&flag, sizeof(int));
+    if (e == hipSuccess) e = hipMemsetAsync(flag, 0, sizeof(int), st);
+    if (e == hipSuccess)
+      hipLaunchKernelGGL(k_sell_fit16, dim3(fill_grid(n)), dim3(kThreads), 0, st, n, rowptr, colind, flag);
+    if (e == hipSuccess) e = hipMemcpyAsync(&fit, flag, sizeof(int), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(flag);
+    if (e != hipSuccess) return fail(e);
+  }
+  P.col_bits = fit == 0 ? 16 : 32;
   // zero first: slots of the lanes past row n-1 in the last slice are never written by the
   // fill and would otherwise hold garbage columns (the kernel gathers them, masked at the add)
-  e = hipMalloc(&P.col, sizeof(int32_t) * std::max<int64_t>(256 * P.groups, 1));
-  if (e == hipSuccess) e = hipMemsetAsync(P.col, 0, sizeof(int32_t) * std::max<int64_t>(256 * P.groups, 1), st);
+  const size_t cbytes = size_t(P.col_bits / 8) * size_t(std::max<int64_t>(256 * P.groups, 1));
+  e = hipMalloc(&P.col, cbytes);
+  if (e == hipSuccess) e = hipMemsetAsync(P.col, 0, cbytes, st);
   if (e != hipSuccess) return fail(e);
   if (n)
     hipLaunchKernelGGL((k_sell_fill<float, float>), dim3(fill_grid(n)), dim3(kThreads), 0, st, n, P.gp, rowptr, colind,
-                       static_cast<const float*>(nullptr), P.col, static_cast<float*>(nullptr));
+                       static_cast<const float*>(nullptr), P.col_bits == 32 ? static_cast<int32_t*>(P.col) : nullptr,
+                       P.col_bits == 16 ? static_cast<int16_t*>(P.col) : nullptr, static_cast<float*>(nullptr));
   e = hipGetLastError();
   if (e != hipSuccess) return fail(e);
   *out = P;
@@ -107,16 +137,16 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
   if (P.n) {
     if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F64)
       hipLaunchKernelGGL((k_sell_fill<double, double>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
-                         static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<double*>(v));
+                         static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr), static_cast<double*>(v));
     else if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F32)
       hipLaunchKernelGGL((k_sell_fill<double, float>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
-                         static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<float*>(v));
+                         static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr), static_cast<float*>(v));
     else if (src_dtype == LSPCG_F32 && dst_dtype == LSPCG_F32)
       hipLaunchKernelGGL((k_sell_fill<float, float>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
-                         static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<float*>(v));
+                         static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr), static_cast<float*>(v));
     else
       hipLaunchKernelGGL((k_sell_fill<float, double>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
-                         static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<double*>(v));
+                         static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr), static_cast<double*>(v));
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

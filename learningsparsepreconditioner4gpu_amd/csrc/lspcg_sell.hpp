@@ -20,13 +20,20 @@ namespace lspcg {
 
 constexpr int kSellC = 64;  // rows per slice = one wave64
 
+// Column storage: 16-bit offsets from the slice's first row when every |col - 64*slice| <=
+// 32767 (banded FEM orderings: 6 instead of 8 B per fp32-valued entry), padding marked by the
+// sentinel kSellPad16 (row lengths then need no rowptr loads); otherwise int32 columns, padding =
+// the row itself, masked with the row length from rowptr.
+constexpr int16_t kSellPad16 = -32768;
+
 // Pattern shared by every matrix with the same CSR (rowptr, colind).
 struct SellPattern {
   int64_t n = 0;
   int64_t ns = 0;                  // slices
   int64_t groups = 0;              // gp[ns]: 4-entry groups per lane, summed over slices
   int32_t* gp = nullptr;           // [ns+1] exclusive prefix of per-slice groups-per-row
-  int32_t* col = nullptr;          // [256*groups] column (padding: the row itself, in bounds)
+  void* col = nullptr;             // [256*groups] int32 columns or int16 offsets (col_bits)
+  int col_bits = 32;
   const int32_t* rowptr = nullptr; // CSR row pointer (row lengths), not owned
   void release() {
     (void)hipFree(gp);
@@ -36,12 +43,12 @@ struct SellPattern {
   }
 };
 
-template <typename VT>
+template <typename VT, typename CT>
 struct SellArgs {
   int64_t n;
   int64_t ns;
   const int32_t* gp;
-  const int32_t* col;
+  const CT* col;
   const int32_t* rowptr;
   const VT* vals;
 };
@@ -65,13 +72,16 @@ struct Vec4Ld<double> {
   }
 };
 
+using i16x4 = short __attribute__((ext_vector_type(4)));
+
 // 256-thread workgroups = 4 slices = one 256-row tile (the same row tiles as k_spmv, so the
 // prologue / epilogue functors and the dot-product reduction are shared).  QB groups of 4
 // entries are loaded per lane before the first gather (branch-free: the group index is
 // clamped, the surplus is masked at the add).
-template <typename T, typename VT, int QB, class Pro, class Gx, class Epi>
-__global__ void __launch_bounds__(256) k_spmv_sell(SellArgs<VT> a, Pro pro, Gx gx, Epi epi) {
+template <typename T, typename VT, typename CT, int QB, class Pro, class Gx, class Epi>
+__global__ void __launch_bounds__(256) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
+  constexpr bool C16 = sizeof(CT) == 2;
   if (pro.exit()) return;
   gx.prepare();
   epi.prepare();
@@ -87,19 +97,34 @@ __global__ void __launch_bounds__(256) k_spmv_sell(SellArgs<VT> a, Pro pro, Gx g
     if (s < a.ns) {  // wave-uniform
       const int32_t g0 = a.gp[s];
       const int nq = a.gp[s + 1] - g0;
-      const int len = i < a.n ? gld(a.rowptr + i + 1) - gld(a.rowptr + i) : 0;
+      int len = 0;
+      if constexpr (!C16) len = i < a.n ? gld(a.rowptr + i + 1) - gld(a.rowptr + i) : 0;
+      const int32_t base = int32_t(s * kSellC);
       const VT* vp = a.vals + 256 * int64_t(g0) + 4 * lane;
-      const int32_t* cp = a.col + 256 * int64_t(g0) + 4 * lane;
+      const CT* cp = a.col + 256 * int64_t(g0) + 4 * lane;
       T acc = T(0);
       for (int q0 = 0; q0 < nq; q0 += QB) {
         VT v[QB][4];
         int c[QB][4];
+        bool m[QB][4];
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
           const int q = min(q0 + u, nq - 1);
           Vec4Ld<VT>::load(vp + 256 * q, v[u]);
-          const i32x4 cc = *(const __attribute__((address_space(1))) i32x4*)(cp + 256 * q);
-          c[u][0] = cc.x; c[u][1] = cc.y; c[u][2] = cc.z; c[u][3] = cc.w;
+          if constexpr (C16) {
+            const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(cp + 256 * q);
+            const int o[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              m[u][j] = (o[j] != kSellPad16) && (q0 + u < nq);
+              c[u][j] = base + (o[j] != kSellPad16 ? o[j] : 0);
+            }
+          } else {
+            const i32x4 cc = *(const __attribute__((address_space(1))) i32x4*)(cp + 256 * q);
+            c[u][0] = cc.x; c[u][1] = cc.y; c[u][2] = cc.z; c[u][3] = cc.w;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) m[u][j] = 4 * (q0 + u) + j < len;
+          }
         }
         T xv[QB][4];
 #pragma unroll
@@ -110,7 +135,7 @@ __global__ void __launch_bounds__(256) k_spmv_sell(SellArgs<VT> a, Pro pro, Gx g
         for (int u = 0; u < QB; ++u)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (4 * (q0 + u) + j < len) acc = acc + T(v[u][j]) * xv[u][j];
+            if (m[u][j]) acc = acc + T(v[u][j]) * xv[u][j];
       }
       if (i < a.n) epi.row(i, acc, d);
     }
@@ -124,11 +149,20 @@ constexpr int64_t kSellReduceGridMax = 2048;  // <= kElemBlocksMax partial slots
 
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
-  SellArgs<VT> a{P.n, P.ns, P.gp, P.col, P.rowptr, static_cast<const VT*>(vals)};
   int64_t grid = (P.n + 255) / 256;
   if (Epi::NDOT > 0 && grid > kSellReduceGridMax) grid = kSellReduceGridMax;
-  if (grid > 0)
-    hipLaunchKernelGGL((k_spmv_sell<T, VT, 4, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(256), 0, st, a, pro, gx, epi);
+  if (grid <= 0) return;
+  if (P.col_bits == 16) {
+    SellArgs<VT, int16_t> a{P.n, P.ns, P.gp, static_cast<const int16_t*>(P.col), P.rowptr,
+                            static_cast<const VT*>(vals)};
+    hipLaunchKernelGGL((k_spmv_sell<T, VT, int16_t, 4, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(256), 0, st, a, pro,
+                       gx, epi);
+  } else {
+    SellArgs<VT, int32_t> a{P.n, P.ns, P.gp, static_cast<const int32_t*>(P.col), P.rowptr,
+                            static_cast<const VT*>(vals)};
+    hipLaunchKernelGGL((k_spmv_sell<T, VT, int32_t, 4, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(256), 0, st, a, pro,
+                       gx, epi);
+  }
 }
 
 }  // namespace lspcg
@@ -137,8 +171,9 @@ namespace lspcg {
 // Host-side construction (lspcg_sell.hip), enqueued on `st`.
 // Builds the SELL-64 pattern of a scalar CSR (n rows); fails with LSPCG_ERR_UNSUPPORTED when the
 // padded size exceeds max_pad x nnz (irregular row lengths: the CSR kernel is used instead).
+// allow16: store 16-bit column offsets when they fit.
 int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
-                       hipStream_t st, SellPattern* out);
+                       bool allow16, hipStream_t st, SellPattern* out);
 // Allocates and fills the SELL value array of a CSR with the same pattern.  src_dtype /
 // dst_dtype: LSPCG_F32 or LSPCG_F64 (fp64 -> fp32 only for exactly representable values).
 int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* src, int src_dtype, int dst_dtype,

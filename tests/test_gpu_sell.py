@@ -40,6 +40,9 @@ MATS = {
     "ragged": lambda: _cases.ragged_matrix(),  # empty rows, a 5000-entry row
     "n1": lambda: sp.csr_matrix(np.array([[2.5]])),
     "n65": lambda: sp.random(65, 65, density=0.2, random_state=3, format="csr") + sp.eye(65, format="csr"),
+    # columns up to 70k rows away from the slice: 16-bit offsets do not fit -> int32 columns
+    "wide": lambda: sp.eye(70000, format="csr") + sp.csr_matrix(
+        (np.full(70000, 0.5), (np.arange(70000), 69999 - np.arange(70000))), shape=(70000, 70000)),
     "zero-rows": lambda: sp.csr_matrix((sp.eye(130, format="csr").toarray() * (np.arange(130) % 3 == 0))),
 }
 
@@ -55,9 +58,9 @@ def test_sell_spmv_bitwise_vs_scipy(gpu_ctx, which):
     ref = A @ x
     Ad = _dm(A)
     xt = torch.from_numpy(x).cuda()
-    for compact in (0, 1):
-        y = _sell_spmv(Ad, xt, compact)
-        assert np.array_equal(y, ref), (which, compact, np.nanmax(np.abs(y - ref)))
+    for flags in (0, 1, 2, 3):  # fp32 values x 16-bit column offsets
+        y = _sell_spmv(Ad, xt, flags)
+        assert np.array_equal(y, ref), (which, flags, np.nanmax(np.abs(y - ref)))
 
 
 def test_sell_skips_padding_with_inf(gpu_ctx):
@@ -66,8 +69,9 @@ def test_sell_skips_padding_with_inf(gpu_ctx):
     x = np.ones(70)
     x[0] = np.inf
     ref = A @ x
-    y = _sell_spmv(_dm(A), torch.from_numpy(x).cuda(), 0)
-    assert np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])
+    for flags in (0, 2):
+        y = _sell_spmv(_dm(A), torch.from_numpy(x).cuda(), flags)
+        assert np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])
 
 
 @pytest.mark.parametrize("precond", ["none", "diagonal", "ext_spai"])
@@ -80,8 +84,9 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
     n = A.shape[0]
     b = torch.from_numpy(A @ np.ones(n)).cuda()
     out = []
-    for env in ("1", "0"):
+    for env, env32 in (("1", "0"), ("0", "1"), ("0", "0")):  # CSR, SELL int32 cols, SELL 16-bit offsets
         monkeypatch.setenv("LSPCG_NO_SELL", env)
+        monkeypatch.setenv("LSPCG_SELL32", env32)
         s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
         if precond == "ext_spai":
             s.set_spai(_cases.spai_like(A), 1e-3)
@@ -89,6 +94,7 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
         it, conv, _, hist = s.solve(b, x, rtol=1e-8, return_history=True)
         out.append((it, x.cpu().numpy(), hist))
         del s
-    assert out[0][0] == out[1][0], (name, out[0][0], out[1][0])
-    assert np.array_equal(out[0][1], out[1][1]), name
-    assert np.array_equal(out[0][2], out[1][2]), name
+    for o in out[1:]:
+        assert out[0][0] == o[0], (name, out[0][0], o[0])
+        assert np.array_equal(out[0][1], o[1]), name
+        assert np.array_equal(out[0][2], o[2]), name

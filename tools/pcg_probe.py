@@ -34,7 +34,8 @@ gt = ds.mask.reshape(-1).to(torch.float64)
 b = A.matvec(gt)
 print(f"{wl}: n={A.n} nnz={A.nnz}", flush=True)
 
-VARIANTS = [("csr", {"LSPCG_NO_SELL": "1"}), ("sell", {"LSPCG_NO_SELL": "0"})]
+VARIANTS = [("csr", {"LSPCG_NO_SELL": "1"}), ("sell32", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "1"}),
+            ("sell16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0"})]
 ref = None
 for name, env in VARIANTS:
     os.environ.update(env)
@@ -63,10 +64,10 @@ for label, flush in (("cold", 512 << 20), ("warm", 0)):
     r = 30 if flush else 90
     ms0 = A.spmv_timed(x, y0, r, flush_bytes=flush)
     out = [f"csr {ms0*1e3:.1f} us ({alg/ms0/1e6:.0f} GB/s)"]
-    for compact in (0, 1):
+    for compact in (0, 1, 3):
         ms = C.c_double()
         _lib.check(lib.lspcg_spmv_sell_timed(A.ctx.handle, A.handle, compact, C.c_void_p(x.data_ptr()),
                                              C.c_void_p(y1.data_ptr()), r, flush, C.byref(ms)))
-        out.append(f"sell{'-f32val' if compact else ''} {ms.value*1e3:.1f} us ({alg/ms.value/1e6:.0f} GB/s) "
+        out.append(f"sell{['', '-f32val', '', '-f32val-c16'][compact]} {ms.value*1e3:.1f} us ({alg/ms.value/1e6:.0f} GB/s) "
                    f"bitexact={torch.equal(y0, y1)}")
     print(f"SpMV {label}: " + " | ".join(out), flush=True)
