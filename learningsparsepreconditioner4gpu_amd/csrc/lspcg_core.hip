@@ -80,6 +80,34 @@ __global__ void k_sort_gather_transpose(int64_t nb, const int32_t* __restrict__ 
   }
 }
 
+// Symmetric-pattern transpose: Aᵀ has A's pattern, and the entry (r, j) of Aᵀ is A's entry
+// (j, r), found by binary search in row j.  One thread per row, deterministic, no atomics;
+// flag <- 1 if some (j, r) is missing (pattern not symmetric: the general path runs instead).
+template <typename T, int BS>
+__global__ void k_transpose_sym(int64_t nb, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                                const T* __restrict__ vals, T* __restrict__ tvals, int* __restrict__ flag) {
+  for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < nb; r += int64_t(gridDim.x) * blockDim.x) {
+    for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+      const int32_t j = colind[k];
+      int32_t lo = rowptr[j], hi = rowptr[j + 1];
+      while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (colind[mid] < r) lo = mid + 1; else hi = mid;
+      }
+      if (lo >= rowptr[j + 1] || colind[lo] != r) {
+        atomicOr(flag, 1);
+        continue;
+      }
+      const T* src = vals + int64_t(lo) * BS * BS;
+      T* dst = tvals + int64_t(k) * BS * BS;
+#pragma unroll
+      for (int a = 0; a < BS; ++a)
+#pragma unroll
+        for (int b = 0; b < BS; ++b) dst[a * BS + b] = src[b * BS + a];
+    }
+  }
+}
+
 template <typename T, int BS>
 __global__ void k_diagonal(int64_t nb, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
                            const T* __restrict__ vals, T* __restrict__ d) {
@@ -293,6 +321,46 @@ int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out) {
   lspcg_mat* Tm = nullptr;
   int rc = mat_alloc(ctx, A->nb, A->nnzb, A->block_size, A->dtype, &Tm);
   if (rc) return rc;
+  {  // symmetric pattern (the ext_spai factor always has A's pattern): value permutation only
+    int* flag = nullptr;
+    int h = 1;
+    hipError_t e = hipMalloc(&flag, sizeof(int));
+    if (e == hipSuccess) e = hipMemsetAsync(flag, 0, sizeof(int), st);
+    if (e == hipSuccess) e = hipMemcpyAsync(Tm->rowptr, A->rowptr, sizeof(int32_t) * (A->nb + 1), hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && A->nnzb)
+      e = hipMemcpyAsync(Tm->colind, A->colind, sizeof(int32_t) * A->nnzb, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && A->nb) {
+      const dim3 g(grid_for(A->nb)), b(kThreads);
+      if (A->dtype == LSPCG_F64) {
+        if (A->block_size == 1)
+          hipLaunchKernelGGL((k_transpose_sym<double, 1>), g, b, 0, st, A->nb, A->rowptr, A->colind,
+                             static_cast<const double*>(A->vals), static_cast<double*>(Tm->vals), flag);
+        else
+          hipLaunchKernelGGL((k_transpose_sym<double, 3>), g, b, 0, st, A->nb, A->rowptr, A->colind,
+                             static_cast<const double*>(A->vals), static_cast<double*>(Tm->vals), flag);
+      } else {
+        if (A->block_size == 1)
+          hipLaunchKernelGGL((k_transpose_sym<float, 1>), g, b, 0, st, A->nb, A->rowptr, A->colind,
+                             static_cast<const float*>(A->vals), static_cast<float*>(Tm->vals), flag);
+        else
+          hipLaunchKernelGGL((k_transpose_sym<float, 3>), g, b, 0, st, A->nb, A->rowptr, A->colind,
+                             static_cast<const float*>(A->vals), static_cast<float*>(Tm->vals), flag);
+      }
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(flag);
+    if (e != hipSuccess) {
+      set_error(std::string("transpose: ") + hipGetErrorString(e));
+      lspcg_mat_destroy(Tm);
+      return LSPCG_ERR_HIP;
+    }
+    if (h == 0) {
+      *out = Tm;
+      return LSPCG_OK;
+    }
+  }
   int32_t* cnt = nullptr;
   int64_t* tsrc = nullptr;
   auto fail = [&](hipError_t e) {

@@ -49,7 +49,8 @@ constexpr int kElemBlocksMax = 2048;  // grid cap for streaming elementwise kern
 // grid_reduce_dd ticket buffer: [top | group 0 | group 1 | ...], one 128-B line each
 constexpr int kTicketGroup = 32;
 constexpr int kTicketStride = 32;
-constexpr int kTicketWords = kTicketStride * (1 + kElemBlocksMax / kTicketGroup);
+constexpr int kReduceBlocksMax = 8192;  // largest grid of a reducing launch (ticket buffer bound)
+constexpr int kTicketWords = kTicketStride * (1 + kReduceBlocksMax / kTicketGroup);
 constexpr int kEntryPad = 16;       // zeroed padding entries after colind / vals (branch-free SpMV loads)
 
 // ---------------------------------------------------------------------------

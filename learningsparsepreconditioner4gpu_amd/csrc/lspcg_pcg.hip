@@ -137,6 +137,170 @@ struct EpiQ {
   }
 };
 
+// ---- fused 3-kernel ext_spai schedule (SELL views; DESIGN.md "PCG schedule") ----------------
+// The AXPY updates are evaluated where they are consumed, with scipy's exact expressions:
+//   KA  r_k = r_{k-1} - α_{k-1} q_{k-1} (gathered, own rows stored), ‖r_k‖², t = Lᵀ r_k
+//   KB  top-of-loop test on ‖r_k‖ ; z = L t + ε r_k ; ρ_k = r_k·z
+//   KC  p_k = p_{k-1}β + z (gathered, own rows stored), x += α_{k-1} p_{k-1}, q = A p_k, π, α_k
+// r_k lives in R[k & 1] and p_k in P[k & 1]: a gather never reads a buffer being written.
+// (base + parity * offset: a select between two struct members would become a dynamically
+// indexed private array, which the compiler moves to scratch / LDS)
+template <typename T>
+struct Pair {
+  T* B0;
+  int64_t delta;  // B1 - B0 in elements
+  __host__ __device__ static Pair make(T* b0, T* b1) { return Pair{b0, int64_t(b1 - b0)}; }
+  __device__ __forceinline__ T* at(int64_t k) const { return B0 + (k & 1) * delta; }
+};
+
+// gather of r_k = r_{k-1} - α_{k-1} q_{k-1} (scipy `r -= alpha*q`); r_0 itself at k = 0
+template <typename T>
+struct GatherR {
+  Pair<T> R;
+  const T* q;
+  const PcgState* S;
+  const T* rold = nullptr;
+  T alpha = T(0);
+  bool upd = false;
+  __device__ __forceinline__ void prepare() {
+    const int64_t k = S->iter;
+    upd = k > 0;
+    alpha = T(S->alpha);
+    rold = R.at(upd ? k - 1 : 0);
+  }
+  // both loads unconditional, select afterwards (no branch around the loads)
+  __device__ __forceinline__ T operator()(int64_t j) const {
+    const T a = gld(rold + j);
+    const T b = gld(q + j);
+    const T u = a - alpha * b;
+    return upd ? u : a;
+  }
+};
+
+// gather of p_k = p_{k-1}β + z_k (scipy `p *= beta; p += z`), p_0 = z_0
+template <typename T>
+struct GatherP {
+  Pair<T> P;
+  const T* z;
+  const PcgState* S;
+  const T* pold = nullptr;
+  T beta = T(0);
+  bool first = true;
+  __device__ __forceinline__ void prepare() {
+    const int64_t k = S->iter;
+    first = k == 0;
+    pold = P.at(k + 1);  // = P[(k-1) & 1]
+    beta = first ? T(0) : T(S->rho) / T(S->rho_prev);
+  }
+  __device__ __forceinline__ T operator()(int64_t j) const {
+    const T a = gld(z + j);
+    const T b = gld(pold + j);
+    const T u = (b * beta) + a;
+    return first ? a : u;
+  }
+};
+
+// KA epilogue: own-row r_k stored, t = Lᵀ r_k (scaled: (Lᵀ r_k)/d), ‖r_k‖²
+template <typename T, bool SCALED>
+struct EpiRT {
+  static constexpr int NDOT = 1;
+  GatherR<T> g;
+  T* t;
+  const T* d;
+  PcgState* S;
+  double* partials;
+  unsigned* ticket;
+  T* rnew = nullptr;
+  __device__ __forceinline__ void prepare() {
+    g.prepare();  // the epilogue's own copy of the gather (own-row r_k)
+    rnew = g.R.at(S->iter);
+  }
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T ri = g(i);
+    if (g.upd) gst(rnew + i, ri);
+    if constexpr (SCALED) gst(t + i, s / gld(d + i));
+    else gst(t + i, s);
+    dd_fma(dots[0], double(ri), double(ri));
+  }
+  __device__ __forceinline__ void fin(const double* v) const {
+    if (!g.upd) return;  // ‖r_0‖ comes from the init launch
+    const double rr = round_to<T>(v[0]);
+    S->rr = rr;
+    if (S->hist) S->hist[S->iter] = double(tsqrt<T>(T(rr)));
+  }
+};
+
+// KB epilogue: z = L t + ε r_k (scaled: + (ε r_k)/d) ; ρ_k = r_k·z
+template <typename T, bool SCALED>
+struct EpiZF {
+  static constexpr int NDOT = 1;
+  T* z;
+  Pair<T> R;
+  const T* d;
+  T eps;
+  PcgState* S;
+  double* partials;
+  unsigned* ticket;
+  const T* r = nullptr;
+  __device__ __forceinline__ void prepare() { r = R.at(S->iter); }
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T ri = gld(r + i);
+    T zi;
+    if constexpr (SCALED) zi = s + (eps * ri) / gld(d + i);
+    else zi = s + eps * ri;
+    gst(z + i, zi);
+    dd_fma(dots[0], double(ri), double(zi));
+  }
+  __device__ __forceinline__ void fin(const double* v) const {
+    S->rho_prev = S->rho;
+    S->rho = round_to<T>(v[0]);
+  }
+};
+
+// KC epilogue: own-row p_k stored, deferred x += α_{k-1} p_{k-1}, q = A p_k ; π = p_k·q ;
+// α_k = ρ_k/π ; iteration k completed
+template <typename T>
+struct EpiPQ {
+  static constexpr int NDOT = 1;
+  GatherP<T> g;
+  T* x;
+  T* q;
+  PcgState* S;
+  double* partials;
+  unsigned* ticket;
+  T* pnew = nullptr;
+  T alpha_prev = T(0);
+  __device__ __forceinline__ void prepare() {
+    g.prepare();  // the epilogue's own copy of the gather (own-row p_k)
+    pnew = g.P.at(S->iter);
+    alpha_prev = T(S->alpha);
+  }
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T pi = g(i);
+    gst(pnew + i, pi);
+    if (!g.first) gst(x + i, gld(x + i) + alpha_prev * gld(g.pold + i));
+    gst(q + i, s);
+    dd_fma(dots[0], double(pi), double(s));
+  }
+  __device__ __forceinline__ void fin(const double* v) const {
+    const double pq = round_to<T>(v[0]);
+    S->pq = pq;
+    S->alpha = double(T(S->rho) / T(pq));
+    S->iter = S->iter + 1;
+  }
+};
+
+// after the fused loop: the deferred x += α_{k-1} p_{k-1}, p_{k-1} = P[(iter-1) & 1]
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_x_fixup_pair(int64_t n, const PcgState* S, Pair<T> P,
+                                                           T* __restrict__ x) {
+  if (S->iter < 1 || S->bb == 0.0) return;
+  const T alpha = T(S->alpha);
+  const T* p = P.at(S->iter - 1);
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    x[i] = x[i] + alpha * gld(p + i);
+}
+
 // init: r_0 = b - A x0 ; ‖r_0‖², ‖b‖² (+ z_0 = r_0/d, ρ_0 = r_0·z_0 for Jacobi)
 // (scipy: r = b - matvec(x) if x.any() else b.copy(); with x0 = 0 the subtraction returns b)
 template <typename T, int PRE>
@@ -354,7 +518,9 @@ struct lspcg_solver {
   double eps = 0.0;
   hipStream_t stream = nullptr;  // solver-owned (capturable) stream
   void *x = nullptr, *b = nullptr, *r = nullptr, *z = nullptr, *t = nullptr, *p = nullptr, *q = nullptr,
-       *d = nullptr;
+       *d = nullptr, *r2 = nullptr, *p2 = nullptr;  // r2 / p2: second halves of the fused ping-pong pairs
+  bool fused = false;   // current ext_spai schedule is the fused 3-kernel one (set_spai decides)
+  bool allow_fused = false;  // LSPCG_PCG_FUSED=1 selects it (measured slower: two gathers per entry)
   PcgState* S = nullptr;
   PcgState* hS = nullptr;  // pinned host mirror
   double* partials = nullptr;
@@ -412,21 +578,50 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   return LSPCG_OK;
 }
 
-// SpMV of iteration view w with the fused prologue / epilogue, SELL when available.
-template <typename T, class Pro, class Epi>
-static int launch_it(lspcg_solver* s, int w, const T* x, Pro pro, Epi epi, hipStream_t st) {
+// SpMV of iteration view w with the fused prologue / gather / epilogue, SELL when available.
+template <typename T, class Gx, class Pro, class Epi>
+static int launch_it_gx(lspcg_solver* s, int w, Gx gx, Pro pro, Epi epi, hipStream_t st) {
   if (const SellPattern* P = s->sp[w]) {
     if constexpr (sizeof(T) == 8) {
       if (s->svd[w] == LSPCG_F32) {
-        launch_spmv_sell_cfg<T, float>(*P, s->sv[w], GatherVec<T>{x}, pro, epi, st);
+        launch_spmv_sell_cfg<T, float>(*P, s->sv[w], gx, pro, epi, st);
         return LSPCG_OK;
       }
     }
-    launch_spmv_sell_cfg<T, T>(*P, s->sv[w], GatherVec<T>{x}, pro, epi, st);
+    launch_spmv_sell_cfg<T, T>(*P, s->sv[w], gx, pro, epi, st);
     return LSPCG_OK;
   }
   const lspcg_mat* V = w == 0 ? &s->Av : (w == 1 ? &s->Lv : &s->LTv);
-  return launch_spmv_any<T>(V, x, pro, epi, st);
+  return launch_spmv_gx<T>(V, gx, pro, epi, st);
+}
+
+template <typename T, class Pro, class Epi>
+static int launch_it(lspcg_solver* s, int w, const T* x, Pro pro, Epi epi, hipStream_t st) {
+  return launch_it_gx<T>(s, w, GatherVec<T>{x}, pro, epi, st);
+}
+
+// fused 3-kernel ext_spai iteration (SELL views only)
+template <typename T, bool SC>
+static int enqueue_iteration_fused(lspcg_solver* s, hipStream_t st) {
+  PcgState* S = s->S;
+  const Pair<T> R = Pair<T>::make(static_cast<T*>(s->r), static_cast<T*>(s->r2));
+  const Pair<T> P = Pair<T>::make(static_cast<T*>(s->p), static_cast<T*>(s->p2));
+  T* t = static_cast<T*>(s->t);
+  T* z = static_cast<T*>(s->z);
+  T* q = static_cast<T*>(s->q);
+  T* x = static_cast<T*>(s->x);
+  const T* d = static_cast<const T*>(s->d);
+  const GatherR<T> gr{R, q, S};
+  int rc = launch_it_gx<T>(s, 2, gr, ProDone{S}, EpiRT<T, SC>{gr, t, d, S, s->partials, s->ticket}, st);
+  if (rc) return rc;
+  rc = launch_it<T>(s, 1, static_cast<const T*>(t), ProCheck<T>{S},
+                    EpiZF<T, SC>{z, R, d, T(s->eps), S, s->partials, s->ticket}, st);
+  if (rc) return rc;
+  const GatherP<T> gp{P, z, S};
+  rc = launch_it_gx<T>(s, 0, gp, ProDone{S}, EpiPQ<T>{gp, x, q, S, s->partials, s->ticket}, st);
+  if (rc) return rc;
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
 }
 
 static int flag_run(lspcg_solver* s, hipStream_t st, int* out) {
@@ -483,6 +678,9 @@ static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const
 
 template <typename T>
 static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
+  if (s->fused)
+    return s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED ? enqueue_iteration_fused<T, true>(s, st)
+                                                       : enqueue_iteration_fused<T, false>(s, st);
   const int64_t n = s->n;
   T* x = static_cast<T*>(s->x);
   T* r = static_cast<T*>(s->r);
@@ -571,6 +769,12 @@ static int enqueue_init(lspcg_solver* s, hipStream_t st) {
 
 template <typename T>
 static int enqueue_fixup(lspcg_solver* s, hipStream_t st) {
+  if (s->fused) {
+    hipLaunchKernelGGL(k_x_fixup_pair<T>, dim3(elem_grid(s->n)), dim3(kThreads), 0, st, s->n, s->S,
+                       Pair<T>::make(static_cast<T*>(s->p), static_cast<T*>(s->p2)), static_cast<T*>(s->x));
+    LSPCG_HIP(hipGetLastError());
+    return LSPCG_OK;
+  }
   hipLaunchKernelGGL(k_x_fixup<T>, dim3(elem_grid(s->n)), dim3(kThreads), 0, st, s->n, s->S,
                      static_cast<const T*>(s->p), static_cast<T*>(s->x));
   LSPCG_HIP(hipGetLastError());
@@ -616,7 +820,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   s->n = A->n;
   const size_t vb = esize(s->dtype) * std::max<int64_t>(s->n, 1);
   LSPCG_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d}) {
+  for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d, &s->r2, &s->p2}) {
     LSPCG_HIP(hipMalloc(v, vb));
     LSPCG_HIP(hipMemsetAsync(*v, 0, vb, s->stream));
   }
@@ -625,7 +829,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   // partial slots: largest grid of any reducing launch (SpMV grid of A / L, element grid) x 2 dots
   // (n/255 bounds the grid of a CSR (256 rows/WG) and a BSR3 (85 block rows/WG) launch,
   // so L / Lᵀ in either layout fit too)
-  const int64_t g = std::max<int64_t>((A->n + 254) / 255 + 1, kElemBlocksMax);
+  const int64_t g = std::max<int64_t>((A->n + 254) / 255 + 1, 4096);
   LSPCG_HIP(hipMalloc(&s->partials, sizeof(double) * 2 * 2 * (g + 1)));
   LSPCG_HIP(hipMalloc(&s->ticket, sizeof(unsigned) * kTicketWords));
   LSPCG_HIP(hipMemsetAsync(s->ticket, 0, sizeof(unsigned) * kTicketWords, s->stream));
@@ -637,6 +841,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   if (const char* e = std::getenv("LSPCG_NO_COMPACT")) s->compact = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SELL32")) s->sell16 = e[0] == '0';
+  if (const char* e = std::getenv("LSPCG_PCG_FUSED")) s->allow_fused = e[0] == '1';
   if (int rc = make_view(s.get(), A, &s->Av, nullptr, &s->own_A)) return rc;
   if (int rc = build_sell(s.get(), 0, &s->Av)) return rc;
   if (precond == LSPCG_PRECOND_DIAGONAL) {
@@ -671,6 +876,9 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT))) return rc;
   if ((rc = build_sell(s, 1, &s->Lv))) return rc;
   if ((rc = build_sell(s, 2, &s->LTv))) return rc;
+  // the fused schedule needs SELL views; it gathers twice per entry, which costs more than the two
+  // elementwise passes it saves (DESIGN.md "PCG schedule"), so it is opt-in
+  s->fused = s->allow_fused && s->sp[0] && s->sp[1] && s->sp[2];
   LSPCG_HIP(hipEventRecord(s->ev_t1, cst));
   LSPCG_HIP(hipEventSynchronize(s->ev_t1));
   float ms = 0.f;
@@ -806,7 +1014,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipStreamSynchronize(s->stream);
   for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
-  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d}) (void)hipFree(v);
+  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d, s->r2, s->p2}) (void)hipFree(v);
   (void)hipFree(s->S);
   (void)hipHostFree(s->hS);
   (void)hipFree(s->partials);

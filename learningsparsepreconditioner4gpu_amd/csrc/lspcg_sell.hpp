@@ -16,6 +16,9 @@
 #include "lspcg_internal.hpp"
 #include "lspcg_spmv.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace lspcg {
 
 constexpr int kSellC = 64;  // rows per slice = one wave64
@@ -145,12 +148,26 @@ __global__ void __launch_bounds__(256) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, 
   }
 }
 
-constexpr int64_t kSellReduceGridMax = 2048;  // <= kElemBlocksMax partial slots
+constexpr int64_t kSellReduceGridMax = 2048;  // <= the solver's partial slots (>= 4096)
+
+// grid caps (experiment knobs LSPCG_SELL_RCAP / LSPCG_SELL_NCAP, read once)
+inline int64_t sell_cap(bool reducing) {
+  static const int64_t rcap = [] {
+    const char* e = std::getenv("LSPCG_SELL_RCAP");
+    const int64_t v = e ? std::atoll(e) : kSellReduceGridMax;
+    return std::max<int64_t>(1, std::min<int64_t>(v, 4096));
+  }();
+  static const int64_t ncap = [] {
+    const char* e = std::getenv("LSPCG_SELL_NCAP");
+    return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1) << 40;
+  }();
+  return reducing ? rcap : ncap;
+}
 
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
   int64_t grid = (P.n + 255) / 256;
-  if (Epi::NDOT > 0 && grid > kSellReduceGridMax) grid = kSellReduceGridMax;
+  grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
   if (P.col_bits == 16) {
     SellArgs<VT, int16_t> a{P.n, P.ns, P.gp, static_cast<const int16_t*>(P.col), P.rowptr,

@@ -80,6 +80,28 @@ def test_transpose_and_diagonal(gpu_ctx):
     assert np.array_equal(Bd.diagonal().cpu().numpy(), Ae.diagonal())
 
 
+@pytest.mark.parametrize("bs", [1, 3])
+def test_transpose_symmetric_pattern_fast_path(gpu_ctx, bs):
+    # symmetric pattern, nonsymmetric values (the ext_spai factor's case): value permutation path
+    B = P.kuhn_laplacian(6).tocsr()
+    if bs == 3:
+        B = sp.kron(B, np.ones((3, 3))).tocsr()
+    A = B.copy()
+    A.data = np.random.default_rng(1).normal(size=A.nnz)
+    A.sort_indices()
+    T = _dm(A, np.float64, bs).transpose().to_scipy()
+    T = sp.csr_matrix(T)
+    ref = sp.csr_matrix(A.T)
+    assert abs(T - ref).max() == 0
+    # one entry without its mirror -> the general path must take over
+    A2 = A.tolil()
+    A2[0, A.shape[0] - 1] = 5.0
+    A2 = sp.csr_matrix(A2)
+    A2.sort_indices()
+    T2 = sp.csr_matrix(_dm(A2, np.float64, 1).transpose().to_scipy())
+    assert abs(T2 - sp.csr_matrix(A2.T)).max() == 0
+
+
 def _solve(A, b, method, L=None, eps=3e-3, rtol=1e-8, dtype=np.float64, max_iter=0):
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
 

@@ -74,7 +74,7 @@ def test_sell_skips_padding_with_inf(gpu_ctx):
         assert np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])
 
 
-@pytest.mark.parametrize("precond", ["none", "diagonal", "ext_spai"])
+@pytest.mark.parametrize("precond", ["none", "diagonal", "ext_spai", "ext_spai_scaled"])
 @pytest.mark.parametrize("case", [0, 1, 2, 3])
 def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
@@ -84,11 +84,13 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
     n = A.shape[0]
     b = torch.from_numpy(A @ np.ones(n)).cuda()
     out = []
-    for env, env32 in (("1", "0"), ("0", "1"), ("0", "0")):  # CSR, SELL int32 cols, SELL 16-bit offsets
+    # CSR views (5 kernels); SELL int32 columns / 16-bit offsets, 5-kernel and fused 3-kernel schedules
+    for env, env32, fused in (("1", "0", "0"), ("0", "1", "0"), ("0", "0", "0"), ("0", "1", "1"), ("0", "0", "1")):
         monkeypatch.setenv("LSPCG_NO_SELL", env)
         monkeypatch.setenv("LSPCG_SELL32", env32)
+        monkeypatch.setenv("LSPCG_PCG_FUSED", fused)
         s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
-        if precond == "ext_spai":
+        if precond.startswith("ext_spai"):
             s.set_spai(_cases.spai_like(A), 1e-3)
         x = torch.zeros(n, dtype=torch.float64, device="cuda")
         it, conv, _, hist = s.solve(b, x, rtol=1e-8, return_history=True)

@@ -35,7 +35,10 @@ b = A.matvec(gt)
 print(f"{wl}: n={A.n} nnz={A.nnz}", flush=True)
 
 VARIANTS = [("csr", {"LSPCG_NO_SELL": "1"}), ("sell32", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "1"}),
-            ("sell16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0"})]
+            ("sell16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_PCG_FUSED": "0"}),
+            ("fused16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_PCG_FUSED": "1"})]
+if os.environ.get("PROBE_VARIANTS") == "cap":
+    VARIANTS = [("sell16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0"})]
 ref = None
 for name, env in VARIANTS:
     os.environ.update(env)
@@ -55,6 +58,8 @@ for name, env in VARIANTS:
     print(f"{name:6s}: iters={it} conv={conv} solve {t*1e3:.3f} ms  {t/it*1e6:.2f} us/iter  {it/t:.0f} it/s{same}", flush=True)
     del solver
 
+if os.environ.get("PROBE_VARIANTS") == "cap":
+    sys.exit(0)
 lib = _lib.load()
 x = torch.randn(A.n, dtype=torch.float64, device="cuda")
 y0 = torch.empty_like(x)
