@@ -152,11 +152,19 @@ def main():
         dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
         elapsed, total_iters = float(mx[0]), float(tt[1])
 
-    # ---- dominant kernel (scalar CSR SpMV of A) against the HBM roofline
+    # ---- the SpMV of A (fp64, the reference's scalar CSR) against the HBM roofline: first the
+    # staged CSR kernel, then after the analysis step (SELL-64 copy, fp64 values, 16-bit column
+    # offsets) -- the product's lspcg_spmv path, which the roofline line reports
     p = torch.randn(n, dtype=torch.float64, device="cuda")
     q = torch.empty_like(p)
+    csr_cold = A.spmv_timed(p, q, args.spmv_reps, flush_bytes=FLUSH_BYTES)
+    csr_warm = A.spmv_timed(p, q, args.spmv_reps * 3)
+    kind = A.prepare_spmv()
     ms_cold = A.spmv_timed(p, q, args.spmv_reps, flush_bytes=FLUSH_BYTES)
     ms_warm = A.spmv_timed(p, q, args.spmv_reps * 3)
+    kernel = (f"k_spmv_sell<double,double,int{kind}> SELL-64 copy of the fp64 CSR A ({kind}-bit column offsets, "
+              "fp64 values), bit-exact scipy order" if kind else
+              "k_spmv<double,1> staged scalar CSR SpMV of A, bit-exact scipy order")
     alg = spmv_bytes(n, nnz_a)
     gbs_cold = alg / (ms_cold * 1e-3) / 1e9
     gbs_warm = alg / (ms_warm * 1e-3) / 1e9
@@ -170,7 +178,7 @@ def main():
     tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "spmv_traffic.json")
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
-        if tj.get("n") == n and tj.get("nnz") == nnz_a:
+        if tj.get("n") == n and tj.get("nnz") == nnz_a and tj.get("kernel_kind") == kind:
             traffic = tj["traffic_bytes"]
 
     cpu = None
@@ -219,12 +227,14 @@ def main():
             "pcg_iter_us": t_iter * 1e6,
             "pcg_alg_GBs": pcg_gbs,
             "roofline": {
-                "kernel": "k_spmv<double,1> scalar CSR SpMV of A (staged, bit-exact scipy order)",
+                "kernel": kernel,
                 "bound": "hbm", "achieved": gbs_cold, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gbs_cold / HBM_PEAK_GBS, "traffic": traffic,
                 "traffic_unit": "bytes per launch (profiles/spmv_traffic.json)",
                 "alg_bytes_per_launch": alg, "avg_launch_ms_cold": ms_cold, "avg_launch_ms_warm": ms_warm,
                 "achieved_warm": gbs_warm,
+                "csr_staged_ms_cold": csr_cold, "csr_staged_ms_warm": csr_warm,
+                "csr_staged_achieved": alg / (csr_cold * 1e-3) / 1e9,
                 "method": "HIP events on the ctx stream; cold = a 512 MiB read before every launch, launch time = (R x (flush+SpMV) - R x flush)/R",
             },
             "cpu_baseline": cpu,

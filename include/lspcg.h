@@ -86,6 +86,11 @@ int lspcg_mat_scale_columns(lspcg_mat* A, const void* d);
 /* ---- kernels ---- */
 /* y = A x (scipy csr_matvec bit pattern: per-row sequential sum in index order) */
 int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y);
+/* analysis step (cf. rocSPARSE csrmv_analysis): attach a SELL-64 copy of a scalar CSR matrix
+ * (same values and dtype; 16-bit column offsets where they fit) that lspcg_spmv then uses -- the
+ * results keep the same bits.  *kind (nullable) = 16 or 32 (column width) or 0 when the matrix
+ * stays on the CSR kernel (block size 3, irregular row lengths).  lspcg_mat_scale_columns drops it. */
+int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind);
 /* average device ms of one SpMV launch, HIP events on the ctx stream.  flush_bytes == 0:
  * reps back-to-back launches (warm caches); > 0: before every launch a read of a flush_bytes
  * buffer evicts the 256 MiB Infinity Cache (cold); the launch time is (reps x (flush + SpMV)
@@ -102,6 +107,9 @@ int lspcg_spmv_variant_timed(lspcg_ctx* ctx, const lspcg_mat* A, int variant, co
  * fit.  y = A x, same bits as lspcg_spmv */
 int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int flags, const void* x, void* y,
                           int reps, int64_t flush_bytes, double* avg_ms);
+/* calibration: the same cold / warm timing for a plain streaming read of `bytes` (16-B loads, 8
+ * workgroups per CU): the achievable bandwidth an SpMV of that many bytes is compared against */
+int lspcg_read_timed(lspcg_ctx* ctx, int64_t bytes, int reps, int64_t flush_bytes, double* avg_ms);
 /* ---- baseline preconditioners (pymathprim "ic" / "ainv", infer.py:310-321; algorithms and
  * operation order: oracle/precond.py; scalar CSR, sorted rows, stored diagonal) ---- */
 /* IC(0): *L = lower-triangular factor with the pattern of tril(A), A ~ L L^T */

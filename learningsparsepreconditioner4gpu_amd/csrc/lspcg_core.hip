@@ -283,9 +283,18 @@ int lspcg_mat_create_csr(lspcg_ctx* ctx, int64_t n, int64_t nnz, const int32_t* 
   return lspcg_mat_create_bsr(ctx, n, nnz, 1, indptr, indices, vals, dtype, out);
 }
 
+static void drop_sell(lspcg_mat* A) {
+  if (!A->sell) return;
+  (void)hipStreamSynchronize(A->ctx->stream);
+  A->sell->release();
+  delete A->sell;
+  A->sell = nullptr;
+}
+
 int lspcg_mat_destroy(lspcg_mat* A) {
   if (!A) return LSPCG_OK;
   (void)hipSetDevice(A->ctx->device);
+  drop_sell(A);
   (void)hipFree(A->rowptr);
   (void)hipFree(A->colind);
   (void)hipFree(A->vals);
@@ -430,8 +439,32 @@ int lspcg_mat_diagonal(const lspcg_mat* A, void* d) {
   return LSPCG_OK;
 }
 
+int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind) {
+  LSPCG_CHECK(A, LSPCG_ERR_ARG, "prepare_spmv: NULL");
+  LSPCG_HIP(hipSetDevice(A->ctx->device));
+  drop_sell(A);
+  if (kind) *kind = 0;
+  if (A->block_size != 1 || A->n == 0 || A->nnzb == 0) return LSPCG_OK;
+  hipStream_t st = A->ctx->stream;
+  std::unique_ptr<SellCopy> c(new SellCopy());
+  int rc = sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, 1.5, true, st, &c->P);
+  if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // irregular rows: the CSR kernel stays
+  if (rc) return rc;
+  const int vd = A->storage_dtype();
+  rc = sell_fill_values(c->P, A->colind, A->vals, vd, vd, st, &c->vals);
+  if (rc) {
+    c->release();
+    return rc;
+  }
+  LSPCG_HIP(hipStreamSynchronize(st));
+  if (kind) *kind = c->P.col_bits;
+  A->sell = c.release();
+  return LSPCG_OK;
+}
+
 int lspcg_mat_scale_columns(lspcg_mat* A, const void* d) {
   LSPCG_CHECK(A && d, LSPCG_ERR_ARG, "scale_columns: NULL");
+  drop_sell(A);  // values change: the SELL copy would be stale
   hipStream_t st = A->ctx->stream;
   const int g = grid_for(A->nnzb * A->block_size * A->block_size);
   if (A->dtype == LSPCG_F64) {
@@ -455,6 +488,16 @@ int lspcg_mat_scale_columns(lspcg_mat* A, const void* d) {
 
 int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y) {
   LSPCG_CHECK(ctx && A && x && y, LSPCG_ERR_ARG, "spmv: NULL argument");
+  if (const SellCopy* c = A->sell) {
+    if (A->dtype == LSPCG_F64)
+      launch_spmv_sell_cfg<double, double>(c->P, c->vals, GatherVec<double>{static_cast<const double*>(x)}, ProNone{},
+                                           EpiStore<double>{static_cast<double*>(y)}, ctx->stream);
+    else
+      launch_spmv_sell_cfg<float, float>(c->P, c->vals, GatherVec<float>{static_cast<const float*>(x)}, ProNone{},
+                                         EpiStore<float>{static_cast<float*>(y)}, ctx->stream);
+    LSPCG_HIP(hipGetLastError());
+    return LSPCG_OK;
+  }
   int rc;
   if (A->dtype == LSPCG_F64)
     rc = launch_spmv_any<double>(A, static_cast<const double*>(x), ProNone{}, EpiStore<double>{static_cast<double*>(y)},
@@ -472,7 +515,7 @@ int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y) {
 template <class Launch>
 static int spmv_timed_impl(lspcg_ctx* ctx, const lspcg_mat* A, int reps, int64_t flush_bytes, double* avg_ms,
                            Launch launch) {
-  LSPCG_CHECK(ctx && A && reps > 0 && avg_ms && flush_bytes >= 0, LSPCG_ERR_ARG, "spmv_timed: bad argument");
+  LSPCG_CHECK(ctx && reps > 0 && avg_ms && flush_bytes >= 0, LSPCG_ERR_ARG, "spmv_timed: bad argument");
   hipEvent_t e0, e1;
   LSPCG_HIP(hipEventCreate(&e0));
   LSPCG_HIP(hipEventCreate(&e1));
@@ -569,6 +612,25 @@ int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int compact, const
   (void)hipStreamSynchronize(st);
   (void)hipFree(v);
   P.release();
+  return rc;
+}
+
+int lspcg_read_timed(lspcg_ctx* ctx, int64_t bytes, int reps, int64_t flush_bytes, double* avg_ms) {
+  LSPCG_CHECK(ctx && bytes >= 16 && reps > 0 && avg_ms, LSPCG_ERR_ARG, "read_timed: bad argument");
+  void* buf = nullptr;
+  LSPCG_HIP(hipMalloc(&buf, size_t(bytes) + 64));
+  LSPCG_HIP(hipMemsetAsync(buf, 2, size_t(bytes) + 64, ctx->stream));
+  int g = 0;
+  LSPCG_HIP(hipDeviceGetAttribute(&g, hipDeviceAttributeMultiprocessorCount, ctx->device));
+  const int rc = spmv_timed_impl(ctx, nullptr, reps, flush_bytes, avg_ms, [&]() -> int {
+    hipLaunchKernelGGL(k_flush_read, dim3(unsigned(g * 8)), dim3(kThreads), 0, ctx->stream,
+                       static_cast<const u32x4*>(buf), bytes / 16,
+                       reinterpret_cast<unsigned*>(static_cast<char*>(buf) + bytes));
+    LSPCG_HIP(hipGetLastError());
+    return LSPCG_OK;
+  });
+  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipFree(buf);
   return rc;
 }
 

@@ -253,4 +253,6 @@ struct lspcg_mat {
   // exactly representable in fp32 (compact storage, fp64 arithmetic: bit-identical results)
   int val_dtype = -1;
   int storage_dtype() const { return val_dtype < 0 ? dtype : val_dtype; }
+  // optional SELL-64 copy for lspcg_spmv (lspcg_mat_prepare_spmv; lspcg_sell.hpp), owned
+  struct SellCopy* sell = nullptr;
 };

@@ -23,7 +23,7 @@ __global__ void k_sell_len(int64_t n, int64_t ns, const int32_t* __restrict__ ro
 
 // one thread per row: scatter the row's columns (col32 / col16, whichever is non-null) and,
 // if src != nullptr, values into the slice layout; padding slots get value 0 and column = the
-// row (col32) or kSellPad16 (col16)
+// -1 (col32) or kSellPad16 (col16)
 template <typename VS, typename VD>
 __global__ void k_sell_fill(int64_t n, const int32_t* __restrict__ gp, const int32_t* __restrict__ rowptr,
                             const int32_t* __restrict__ colind, const VS* __restrict__ src,
@@ -36,7 +36,7 @@ __global__ void k_sell_fill(int64_t n, const int32_t* __restrict__ gp, const int
     const int64_t base = 256 * int64_t(gp[s]) + 4 * r;
     for (int32_t k = 0; k < slots; ++k) {
       const int64_t pos = base + 256 * int64_t(k >> 2) + (k & 3);
-      if (col32) col32[pos] = k < len ? colind[b + k] : int32_t(i);
+      if (col32) col32[pos] = k < len ? colind[b + k] : int32_t(-1);
       if (col16) col16[pos] = k < len ? int16_t(colind[b + k] - int32_t(s * kSellC)) : kSellPad16;
       if (dst) dst[pos] = k < len ? VD(src[b + k]) : VD(0);
     }

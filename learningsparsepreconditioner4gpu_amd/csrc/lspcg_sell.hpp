@@ -25,8 +25,8 @@ constexpr int kSellC = 64;  // rows per slice = one wave64
 
 // Column storage: 16-bit offsets from the slice's first row when every |col - 64*slice| <=
 // 32767 (banded FEM orderings: 6 instead of 8 B per fp32-valued entry), padding marked by the
-// sentinel kSellPad16 (row lengths then need no rowptr loads); otherwise int32 columns, padding =
-// the row itself, masked with the row length from rowptr.
+// sentinel kSellPad16; otherwise int32 columns with padding sentinel -1.  Either way the kernel
+// needs no row lengths (no dependent rowptr load before the entry loads).
 constexpr int16_t kSellPad16 = -32768;
 
 // Pattern shared by every matrix with the same CSR (rowptr, colind).
@@ -81,8 +81,8 @@ using i16x4 = short __attribute__((ext_vector_type(4)));
 // prologue / epilogue functors and the dot-product reduction are shared).  QB groups of 4
 // entries are loaded per lane before the first gather (branch-free: the group index is
 // clamped, the surplus is masked at the add).
-template <typename T, typename VT, typename CT, int QB, class Pro, class Gx, class Epi>
-__global__ void __launch_bounds__(256) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
+template <typename T, typename VT, typename CT, int QB, int TH, class Pro, class Gx, class Epi>
+__global__ void __launch_bounds__(TH) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
   constexpr bool C16 = sizeof(CT) == 2;
   if (pro.exit()) return;
@@ -93,15 +93,13 @@ __global__ void __launch_bounds__(256) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, 
   for (int j = 0; j < ND; ++j) d[j] = dd_zero();
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
-  const int64_t ntiles = (a.n + 255) / 256;
+  const int64_t ntiles = (a.n + TH - 1) / TH;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t s = tile * 4 + w;
-    const int64_t i = tile * 256 + threadIdx.x;
+    const int64_t s = tile * (TH / 64) + w;
+    const int64_t i = tile * TH + threadIdx.x;
     if (s < a.ns) {  // wave-uniform
       const int32_t g0 = a.gp[s];
       const int nq = a.gp[s + 1] - g0;
-      int len = 0;
-      if constexpr (!C16) len = i < a.n ? gld(a.rowptr + i + 1) - gld(a.rowptr + i) : 0;
       const int32_t base = int32_t(s * kSellC);
       const VT* vp = a.vals + 256 * int64_t(g0) + 4 * lane;
       const CT* cp = a.col + 256 * int64_t(g0) + 4 * lane;
@@ -124,9 +122,12 @@ __global__ void __launch_bounds__(256) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, 
             }
           } else {
             const i32x4 cc = *(const __attribute__((address_space(1))) i32x4*)(cp + 256 * q);
-            c[u][0] = cc.x; c[u][1] = cc.y; c[u][2] = cc.z; c[u][3] = cc.w;
+            const int o[4] = {cc.x, cc.y, cc.z, cc.w};
 #pragma unroll
-            for (int j = 0; j < 4; ++j) m[u][j] = 4 * (q0 + u) + j < len;
+            for (int j = 0; j < 4; ++j) {
+              m[u][j] = (o[j] >= 0) && (q0 + u < nq);
+              c[u][j] = o[j] >= 0 ? o[j] : base;
+            }
           }
         }
         T xv[QB][4];
@@ -164,25 +165,52 @@ inline int64_t sell_cap(bool reducing) {
   return reducing ? rcap : ncap;
 }
 
-template <typename T, typename VT, class Pro, class Gx, class Epi>
-inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
-  int64_t grid = (P.n + 255) / 256;
+inline int sell_wg() {  // workgroup size knob LSPCG_SELL_WG (256 / 512 / 1024), read once
+  static const int wg = [] {
+    const char* e = std::getenv("LSPCG_SELL_WG");
+    const int v = e ? std::atoi(e) : 256;
+    return (v == 512 || v == 1024) ? v : 256;
+  }();
+  return wg;
+}
+
+template <typename T, typename VT, typename CT, int TH, class Pro, class Gx, class Epi>
+inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
+  int64_t grid = (P.n + TH - 1) / TH;
   grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
-  if (P.col_bits == 16) {
-    SellArgs<VT, int16_t> a{P.n, P.ns, P.gp, static_cast<const int16_t*>(P.col), P.rowptr,
-                            static_cast<const VT*>(vals)};
-    hipLaunchKernelGGL((k_spmv_sell<T, VT, int16_t, 4, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(256), 0, st, a, pro,
-                       gx, epi);
-  } else {
-    SellArgs<VT, int32_t> a{P.n, P.ns, P.gp, static_cast<const int32_t*>(P.col), P.rowptr,
-                            static_cast<const VT*>(vals)};
-    hipLaunchKernelGGL((k_spmv_sell<T, VT, int32_t, 4, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(256), 0, st, a, pro,
-                       gx, epi);
+  SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
+  hipLaunchKernelGGL((k_spmv_sell<T, VT, CT, 4, TH, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a, pro, gx,
+                     epi);
+}
+
+template <typename T, typename VT, typename CT, class Pro, class Gx, class Epi>
+inline void launch_spmv_sell_ct(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
+  switch (sell_wg()) {
+    case 1024: launch_spmv_sell_th<T, VT, CT, 1024>(P, vals, gx, pro, epi, st); break;
+    case 512: launch_spmv_sell_th<T, VT, CT, 512>(P, vals, gx, pro, epi, st); break;
+    default: launch_spmv_sell_th<T, VT, CT, 256>(P, vals, gx, pro, epi, st);
   }
 }
 
+template <typename T, typename VT, class Pro, class Gx, class Epi>
+inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
+  if (P.col_bits == 16) launch_spmv_sell_ct<T, VT, int16_t>(P, vals, gx, pro, epi, st);
+  else launch_spmv_sell_ct<T, VT, int32_t>(P, vals, gx, pro, epi, st);
+}
+
 }  // namespace lspcg
+
+// SELL copy attached to a matrix handle for the standalone SpMV (same values, same dtype)
+struct SellCopy {
+  lspcg::SellPattern P;
+  void* vals = nullptr;
+  void release() {
+    P.release();
+    (void)hipFree(vals);
+    vals = nullptr;
+  }
+};
 
 namespace lspcg {
 // Host-side construction (lspcg_sell.hip), enqueued on `st`.

@@ -202,6 +202,13 @@ class DeviceMatrix:
 
     __matmul__ = matvec
 
+    def prepare_spmv(self) -> int:
+        """Analysis step: attach a SELL-64 copy that :meth:`matvec` then uses (same bits).
+        Returns the column width (16 / 32) or 0 when the CSR kernel stays in use."""
+        kind = C.c_int()
+        _lib.call("lspcg_mat_prepare_spmv", self.handle, C.byref(kind))
+        return kind.value
+
     def spmv_timed(self, x: torch.Tensor, y: torch.Tensor, reps: int, flush_bytes: int = 0) -> float:
         """Average device ms of one SpMV launch: ``reps`` back-to-back launches (warm), or with
         ``flush_bytes`` > 0 each launch timed alone after an Infinity-Cache-evicting memset (cold)."""

@@ -41,8 +41,9 @@ MATS = {
     "n1": lambda: sp.csr_matrix(np.array([[2.5]])),
     "n65": lambda: sp.random(65, 65, density=0.2, random_state=3, format="csr") + sp.eye(65, format="csr"),
     # columns up to 70k rows away from the slice: 16-bit offsets do not fit -> int32 columns
-    "wide": lambda: sp.eye(70000, format="csr") + sp.csr_matrix(
-        (np.full(70000, 0.5), (np.arange(70000), 69999 - np.arange(70000))), shape=(70000, 70000)),
+    "wide": lambda: sum(sp.csr_matrix((np.full(70000, 0.5 + k), (np.arange(70000), (np.arange(70000) * (k + 1)
+                                                                                  + 9000 * k) % 70000)),
+                                      shape=(70000, 70000)) for k in range(4)).tocsr(),
     "zero-rows": lambda: sp.csr_matrix((sp.eye(130, format="csr").toarray() * (np.arange(130) % 3 == 0))),
 }
 
@@ -100,3 +101,48 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
         assert out[0][0] == o[0], (name, out[0][0], o[0])
         assert np.array_equal(out[0][1], o[1]), name
         assert np.array_equal(out[0][2], o[2]), name
+
+
+def _expected_kind(A, max_pad=1.5):
+    """lspcg_mat_prepare_spmv's rule: SELL-64 if the padded slots stay <= max_pad * nnz, with
+    16-bit column offsets if every |col - 64*slice| <= 32767."""
+    n = A.shape[0]
+    lens = np.diff(A.indptr)
+    if n == 0 or A.nnz == 0:
+        return 0
+    ns = (n + 63) // 64
+    pad = np.zeros(ns * 64, dtype=np.int64)
+    pad[:n] = lens
+    slots = 256 * ((pad.reshape(ns, 64).max(axis=1) + 3) // 4).sum()
+    if slots > max_pad * A.nnz:
+        return 0
+    rows = np.repeat(np.arange(n), lens)
+    off = A.indices - (rows // 64) * 64
+    return 16 if np.all(np.abs(off) <= 32767) else 32
+
+
+@pytest.mark.parametrize("which", list(MATS))
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_prepare_spmv_keeps_bits(gpu_ctx, which, dtype):
+    A = sp.csr_matrix(MATS[which]()).astype(dtype)
+    A.sort_indices()
+    x = np.random.default_rng(7).normal(size=A.shape[0]).astype(dtype)
+    ref = A @ x
+    Ad = _dm(A, dtype)
+    xt = torch.from_numpy(x).cuda()
+    kind = Ad.prepare_spmv()
+    assert kind == _expected_kind(A), which
+    assert np.array_equal(Ad.matvec(xt).cpu().numpy(), ref), (which, kind)
+
+
+def test_prepare_spmv_dropped_by_scale_columns(gpu_ctx):
+    A = sp.csr_matrix(P.kuhn_laplacian(7))
+    Ad = _dm(A)
+    assert Ad.prepare_spmv() == 16
+    d = np.random.default_rng(0).uniform(0.5, 2.0, size=A.shape[0])
+    Ad.scale_columns_(torch.from_numpy(d).cuda())
+    x = np.random.default_rng(1).normal(size=A.shape[0])
+    B = A.copy()
+    B.data = B.data * d[B.indices]  # lspcg_mat_scale_columns: vals[k] * d[col[k]]
+    ref = B @ x
+    assert np.array_equal(Ad.matvec(torch.from_numpy(x).cuda()).cpu().numpy(), ref)

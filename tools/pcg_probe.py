@@ -69,10 +69,16 @@ for label, flush in (("cold", 512 << 20), ("warm", 0)):
     r = 30 if flush else 90
     ms0 = A.spmv_timed(x, y0, r, flush_bytes=flush)
     out = [f"csr {ms0*1e3:.1f} us ({alg/ms0/1e6:.0f} GB/s)"]
-    for compact in (0, 1, 3):
+    for compact in (0, 2, 1, 3):
         ms = C.c_double()
         _lib.check(lib.lspcg_spmv_sell_timed(A.ctx.handle, A.handle, compact, C.c_void_p(x.data_ptr()),
                                              C.c_void_p(y1.data_ptr()), r, flush, C.byref(ms)))
-        out.append(f"sell{['', '-f32val', '', '-f32val-c16'][compact]} {ms.value*1e3:.1f} us ({alg/ms.value/1e6:.0f} GB/s) "
+        out.append(f"sell{['', '-f32val', '-c16', '-f32val-c16'][compact]} {ms.value*1e3:.1f} us ({alg/ms.value/1e6:.0f} GB/s) "
                    f"bitexact={torch.equal(y0, y1)}")
     print(f"SpMV {label}: " + " | ".join(out), flush=True)
+    rd = []
+    for nbytes in (alg, 115 << 20):
+        ms = C.c_double()
+        _lib.check(lib.lspcg_read_timed(A.ctx.handle, int(nbytes), r, flush, C.byref(ms)))
+        rd.append(f"read {nbytes/1e6:.0f} MB {ms.value*1e3:.1f} us ({nbytes/ms.value/1e6:.0f} GB/s)")
+    print(f"stream {label}: " + " | ".join(rd), flush=True)

@@ -1,4 +1,5 @@
-"""Run only the bench's roofline SpMV (fp64 scalar CSR of the kuhn101 system, cold launches).
+"""Run only the bench's roofline SpMV (fp64 A of the kuhn101 system after the SELL analysis step,
+or the staged CSR kernel with --csr; cold launches).
 
 Used under rocprofv3 --pmc by tools/spmv_traffic.sh so that the counter rows of the SpMV
 dispatches are exactly the launches bench.py times (same matrix, same flush)."""
@@ -14,6 +15,7 @@ def main():
     ap.add_argument("--workload", default="kuhn101")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--warm", action="store_true", help="back-to-back launches instead of cold ones")
+    ap.add_argument("--csr", action="store_true", help="staged CSR kernel (skip the SELL analysis step)")
     args = ap.parse_args()
     sys.path.insert(0, ".")
     from bench import FLUSH_BYTES, spmv_bytes
@@ -28,9 +30,10 @@ def main():
     A = ws.system_matrix(s.to("cuda"))
     x = torch.randn(A.n, dtype=torch.float64, device="cuda")
     y = torch.empty_like(x)
+    kind = 0 if args.csr else A.prepare_spmv()
     ms = A.spmv_timed(x, y, args.reps, flush_bytes=0 if args.warm else FLUSH_BYTES)
     print(json.dumps({"workload": args.workload, "n": A.n, "nnz": A.nnz, "alg_bytes": spmv_bytes(A.n, A.nnz),
-                      "avg_ms": ms, "mode": "warm" if args.warm else "cold"}))
+                      "avg_ms": ms, "mode": "warm" if args.warm else "cold", "kernel_kind": kind}))
 
 
 if __name__ == "__main__":

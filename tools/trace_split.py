@@ -8,24 +8,27 @@ import csv
 import json
 import sys
 
-KEY = "EpiStore<double>"  # standalone k_spmv<double, double, 1, ...> of A (bench.py roofline launches)
+KEY = "EpiStore<double>"  # standalone SpMV of A (bench.py roofline launches: staged CSR, then SELL)
 
 
 def main(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    cold, warm = [], []
+    out = {}
     prev = ""
     for r in rows:
         name = r["Kernel_Name"]
-        if KEY in name and "k_spmv<double, double, 1," in name:
+        if KEY in name and ("k_spmv<double, double, 1," in name or "k_spmv_sell<double, double," in name):
+            kern = "sell" if "k_spmv_sell" in name else "csr"
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
-            (cold if "k_flush_read" in prev else warm).append(dur)
+            out.setdefault(kern, ([], []))[0 if "k_flush_read" in prev else 1].append(dur)
         prev = name
     med = lambda v: sorted(v)[len(v) // 2] if v else None
     avg = lambda v: sum(v) / len(v) if v else None
-    print(json.dumps({"kernel": "k_spmv<double,double,1,...,EpiStore<double>>", "cold_n": len(cold),
-                      "cold_avg_us": avg(cold), "cold_median_us": med(cold), "warm_n": len(warm),
-                      "warm_avg_us": avg(warm), "warm_median_us": med(warm)}, indent=1))
+    res = {}
+    for kern, (cold, warm) in out.items():
+        res[kern] = {"cold_n": len(cold), "cold_avg_us": avg(cold), "cold_median_us": med(cold), "warm_n": len(warm),
+                     "warm_avg_us": avg(warm), "warm_median_us": med(warm)}
+    print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
