@@ -166,7 +166,7 @@ __device__ __forceinline__ void grid_reduce_dd(DD (&v)[N], double* partials, uns
   // Last arriver: every partial is read with sc1 loads, issued in batches of PB per lane
   // before any of them is consumed (one round trip per batch, not one per partial), and
   // summed in block-index order -> the result does not depend on which block was last.
-  constexpr int PB = 8;
+  constexpr int PB = N >= 2 ? 4 : 8;  // <= 16 doubles in flight per thread (VGPR budget of the host kernel)
   DD acc[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) acc[j] = dd_zero();

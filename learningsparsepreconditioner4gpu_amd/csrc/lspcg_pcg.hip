@@ -90,10 +90,11 @@ struct EpiT {
   __device__ __forceinline__ void fin(const double*) const {}
 };
 
-// KB: z = L t + ε r  (scaled: z = L t + (ε r)/d);  ρ = r·z
+// KB: z = L t + ε r  (scaled: z = L t + (ε r)/d);  ρ = r·z and ‖r‖² in the same reduction
+// (the top-of-loop test on ‖r_k‖ then runs in the p update; r_0's norm comes from the init)
 template <typename T, bool SCALED>
 struct EpiZ {
-  static constexpr int NDOT = 1;
+  static constexpr int NDOT = 2;
   T* z;
   const T* r;
   const T* d;
@@ -109,15 +110,23 @@ struct EpiZ {
     else zi = s + eps * ri;
     gst(z + i, zi);
     dd_fma(dots[0], double(ri), double(zi));
+    dd_fma(dots[1], double(ri), double(ri));
   }
   __device__ __forceinline__ void fin(const double* v) const {
     S->rho_prev = S->rho;
     S->rho = round_to<T>(v[0]);
+    const int64_t k = S->iter;
+    if (k > 0) {
+      const double rr = round_to<T>(v[1]);
+      S->rr = rr;
+      if (S->hist) S->hist[k] = double(tsqrt<T>(T(rr)));
+    }
   }
 };
 
-// KD: q = A p ; π = p·q ; α = ρ/π
-template <typename T>
+// KD: q = A p ; π = p·q ; α = ρ/π  (INC: this launch also completes the iteration -- ext_spai,
+// whose r update carries no reduction)
+template <typename T, bool INC = false>
 struct EpiQ {
   static constexpr int NDOT = 1;
   T* q;
@@ -134,6 +143,7 @@ struct EpiQ {
     const double pq = round_to<T>(v[0]);
     S->pq = pq;
     S->alpha = double(T(S->rho) / T(pq));
+    if constexpr (INC) S->iter = S->iter + 1;
   }
 };
 
@@ -457,6 +467,35 @@ __global__ void __launch_bounds__(kThreads) k_update_r(int64_t n, PcgState* S, c
   });
 }
 
+// ext_spai: r -= α q only (‖r‖² is reduced by the next L SpMV, the iteration count by KC)
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_update_r_nodot(int64_t n, const PcgState* S, const T* __restrict__ q,
+                                                             T* __restrict__ r) {
+  using V = typename VecT<T>::type;
+  constexpr int W = VecT<T>::W;
+  if (S->done) return;
+  const T alpha = T(S->alpha);
+  const int64_t nv = n / W;
+  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t j0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j0 < nv; j0 += ts * kElemUnroll) {
+    V rr[kElemUnroll], qq[kElemUnroll];
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        rr[u] = reinterpret_cast<const V*>(r)[j];
+        qq[u] = reinterpret_cast<const V*>(q)[j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) reinterpret_cast<V*>(r)[j] = rr[u] - alpha * qq[u];
+    }
+  }
+  for (int64_t i = nv * W + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += ts) r[i] = r[i] - alpha * q[i];
+}
+
 // IC: ρ = r·z after the two triangular solves
 template <typename T>
 __global__ void __launch_bounds__(kThreads) k_dot_rho(int64_t n, PcgState* S, const T* __restrict__ r,
@@ -696,15 +735,16 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
     case LSPCG_PRECOND_EXT_SPAI:
     case LSPCG_PRECOND_EXT_SPAI_SCALED: {
       const bool sc = s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
-      rc = sc ? launch_it<T>(s, 2, static_cast<const T*>(r), ProCheck<T>{S}, EpiT<T, true>{t, d}, st)
-              : launch_it<T>(s, 2, static_cast<const T*>(r), ProCheck<T>{S}, EpiT<T, false>{t, d}, st);
+      rc = sc ? launch_it<T>(s, 2, static_cast<const T*>(r), ProDone{S}, EpiT<T, true>{t, d}, st)
+              : launch_it<T>(s, 2, static_cast<const T*>(r), ProDone{S}, EpiT<T, false>{t, d}, st);
       if (rc) return rc;
       rc = sc ? launch_it<T>(s, 1, static_cast<const T*>(t), ProDone{S},
                                    EpiZ<T, true>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st)
               : launch_it<T>(s, 1, static_cast<const T*>(t), ProDone{S},
                                    EpiZ<T, false>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st);
       if (rc) return rc;
-      hipLaunchKernelGGL((k_update_p<T, ProDone>), dim3(eg), dim3(kThreads), 0, st, n, ProDone{S}, S,
+      // top-of-loop test on ‖r_k‖ (reduced by KB) before the first update of iteration k
+      hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S,
                          static_cast<const T*>(z), p, x);
       break;
     }
@@ -728,10 +768,16 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
       set_error("unknown preconditioner");
       return LSPCG_ERR_ARG;
   }
-  rc = launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket},
-                          st);
+  const bool spai = s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  rc = spai ? launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQ<T, true>{q, p, S, s->partials, s->ticket},
+                           st)
+            : launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket}, st);
   if (rc) return rc;
   switch (s->precond) {
+    case LSPCG_PRECOND_EXT_SPAI:
+    case LSPCG_PRECOND_EXT_SPAI_SCALED:
+      hipLaunchKernelGGL(k_update_r_nodot<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const T*>(q), r);
+      break;
     case LSPCG_PRECOND_NONE:
       hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_NONE>), dim3(eg), dim3(kThreads), 0, st, n, S, q, r, d, z,
                          s->partials, s->ticket);

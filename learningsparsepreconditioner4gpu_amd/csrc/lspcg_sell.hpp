@@ -82,7 +82,7 @@ using i16x4 = short __attribute__((ext_vector_type(4)));
 // entries are loaded per lane before the first gather (branch-free: the group index is
 // clamped, the surplus is masked at the add).
 template <typename T, typename VT, typename CT, int QB, int TH, class Pro, class Gx, class Epi>
-__global__ void __launch_bounds__(TH) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
+__global__ void __launch_bounds__(TH, 1536 / TH) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
   constexpr bool C16 = sizeof(CT) == 2;
   if (pro.exit()) return;
@@ -149,13 +149,18 @@ __global__ void __launch_bounds__(TH) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, G
   }
 }
 
-constexpr int64_t kSellReduceGridMax = 2048;  // <= the solver's partial slots (>= 4096)
-
-// grid caps (experiment knobs LSPCG_SELL_RCAP / LSPCG_SELL_NCAP, read once)
+// Reducing launches use a resident grid: 6 workgroups per CU (the kernel's __launch_bounds__
+// guarantee), i.e. 1536 on MI355X -- one wave of workgroups, each walking its row tiles, so no
+// straggler round delays the ticket (measured best of 768..3072).  Capped by the solver's 4096
+// partial slots.  Knobs LSPCG_SELL_RCAP / LSPCG_SELL_NCAP (read once) for experiments.
 inline int64_t sell_cap(bool reducing) {
   static const int64_t rcap = [] {
     const char* e = std::getenv("LSPCG_SELL_RCAP");
-    const int64_t v = e ? std::atoll(e) : kSellReduceGridMax;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    const int64_t v = e ? std::atoll(e) : int64_t(6) * cus;
     return std::max<int64_t>(1, std::min<int64_t>(v, 4096));
   }();
   static const int64_t ncap = [] {
