@@ -150,11 +150,15 @@ def pcg(A: csr_matrix, b: np.ndarray, psolve: Optional[Callable] = None, rtol: f
     ``dot='numpy'`` reproduces scipy bit-for-bit; ``dot='exact'`` replaces every
     dot/norm with the correctly rounded one (the HIP path's reductions).
     """
-    d = DOTS[dot]
+    dt = np.dtype(dtype).type
+    d0 = DOTS[dot]
+    # scipy's scalars have the vectors' dtype (np.dot of float32 arrays is a float32): ρ, π, α, β
+    # and ‖r‖ are rounded to it before they are used (a no-op for fp64)
+    d = (lambda u, v: dt(d0(u, v))) if dot != "numpy" else d0
     b = np.asarray(b, dtype=dtype)
     n = b.shape[0]
     max_iter = max_iter if max_iter > 0 else n
-    bnrm2 = math.sqrt(d(b, b)) if dot != "numpy" else np.linalg.norm(b)
+    bnrm2 = np.sqrt(d(b, b)) if dot != "numpy" else np.linalg.norm(b)
     atol = max(0.0, float(rtol) * float(bnrm2))
     x = np.zeros_like(b) if x0 is None else np.array(x0, dtype=dtype)
     hist = []
@@ -163,7 +167,7 @@ def pcg(A: csr_matrix, b: np.ndarray, psolve: Optional[Callable] = None, rtol: f
     r = b - A @ x if x.any() else b.copy()
     rho_prev, p = None, None
     for iteration in range(max_iter):
-        rn = math.sqrt(d(r, r)) if dot != "numpy" else np.linalg.norm(r)
+        rn = np.sqrt(d(r, r)) if dot != "numpy" else np.linalg.norm(r)
         hist.append(float(rn))
         if rn < atol:
             return iteration, x, hist
@@ -181,7 +185,7 @@ def pcg(A: csr_matrix, b: np.ndarray, psolve: Optional[Callable] = None, rtol: f
         x += alpha * p
         r -= alpha * q
         rho_prev = rho_cur
-    hist.append(float(math.sqrt(d(r, r)) if dot != "numpy" else np.linalg.norm(r)))
+    hist.append(float(np.sqrt(d(r, r)) if dot != "numpy" else np.linalg.norm(r)))
     return max_iter, x, hist
 
 
