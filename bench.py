@@ -45,6 +45,19 @@ def pcg_bytes_per_iter(n: int, nnz_a: int, nnz_l: int) -> int:
     return spmv_bytes(n, nnz_a) + 2 * spmv_bytes(n, nnz_l) + 8 * n * 10
 
 
+def reduce_timing(elapsed: float, iters: float, device) -> tuple:
+    """Whole-job numbers of a multi-rank run: wall time = MAX over ranks, iterations = SUM
+    (one all-reduce each; RCCL on the GPU, gloo in the CPU test)."""
+    import torch
+    import torch.distributed as dist
+
+    mx = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    sm = torch.tensor([iters], dtype=torch.float64, device=device)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    return float(mx[0]), float(sm[0])
+
+
 def cpu_baseline(A, L, eps, gt, max_iter: int):
     """The reference's CPU restatement (validate.py:163-201: scipy cg + explicit-Lᵀ SPAI
     operator), timed like validate.py:196-198, on a bounded number of iterations."""
@@ -147,11 +160,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     total_iters = float(sum(iters))
     if world > 1:
-        tt = torch.tensor([elapsed, total_iters], dtype=torch.float64, device="cuda")
-        mx = tt.clone()
-        dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-        elapsed, total_iters = float(mx[0]), float(tt[1])
+        elapsed, total_iters = reduce_timing(elapsed, total_iters, torch.device("cuda", local))
 
     # ---- the SpMV of A (fp64, the reference's scalar CSR) against the HBM roofline: first the
     # staged CSR kernel, then after the analysis step (SELL-64 copy, fp64 values, 16-bit column

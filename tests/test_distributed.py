@@ -70,3 +70,30 @@ def test_gloo_sharded_gather(world):
 def test_gather_without_process_group_is_local():
     recs = [SolveRecord(2, 1, 0, 0, 0, 1, 1), SolveRecord(0, 1, 0, 0, 0, 1, 1)]
     assert [r.index for r in gather_records(recs, 3)] == [0, 2]
+
+
+def _bench_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    elapsed, iters = bench.reduce_timing(0.5 + rank, 212.0 * (rank + 1), torch.device("cpu"))
+    q.put((rank, elapsed, iters))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_reduce_timing_max_and_sum(world):
+    """bench.py's N>1 aggregation: value = iterations of ALL ranks / MAX-over-ranks wall time."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for _, elapsed, iters in out:
+        assert elapsed == 0.5 + world - 1
+        assert iters == 212.0 * world * (world + 1) / 2
