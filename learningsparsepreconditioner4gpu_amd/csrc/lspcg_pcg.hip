@@ -496,6 +496,169 @@ __global__ void __launch_bounds__(kThreads) k_update_r_nodot(int64_t n, const Pc
   for (int64_t i = nv * W + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += ts) r[i] = r[i] - alpha * q[i];
 }
 
+// ---- split-reduction ext_spai schedule (SELL views; DESIGN.md "PCG schedule") --------------
+// KB and KC only pre-reduce their dot partials per group of workgroups (grid_partial_groups);
+// the elementwise launches that consume the scalars sum the <= 64 group totals themselves:
+//   KA  t = Lᵀ r_k
+//   KB  z = L t + ε r_k ; groups of ρ_k = r_k·z and ‖r_k‖²                 -> GZ
+//   UP  ρ_k, ‖r_k‖ from GZ ; top-of-loop test ; x += α_{k-1} p_{k-1} ; p_k = p_{k-1}β + z
+//   KC  q = A p_k ; groups of π_k = p_k·q                                  -> GQ
+//   UR  α_k = ρ_k/π_k from GZ, GQ ; r_{k+1} = r_k - α_k q ; persists ρ_k, α_k, iteration k+1
+// Workgroup 0 of UP / UR is the only writer of the persistent state, which only later launches
+// read; every workgroup computes the same scalars (same group totals, same summation tree).
+struct GroupDots {
+  unsigned* ticket;
+  double* partials;
+  double* group_out;
+  int gsz;
+};
+
+template <typename T, bool SCALED>
+struct EpiZG {
+  static constexpr int NDOT = 2;
+  static constexpr bool GROUPS = true;
+  T* z;
+  const T* r;
+  const T* d;
+  T eps;
+  double* partials;
+  unsigned* ticket;
+  double* group_out;
+  int gsz;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T ri = gld(r + i);
+    T zi;
+    if constexpr (SCALED) zi = s + (eps * ri) / gld(d + i);
+    else zi = s + eps * ri;
+    gst(z + i, zi);
+    dd_fma(dots[0], double(ri), double(zi));
+    dd_fma(dots[1], double(ri), double(ri));
+  }
+  __device__ __forceinline__ void fin(const double*) const {}
+};
+
+template <typename T>
+struct EpiQG {
+  static constexpr int NDOT = 1;
+  static constexpr bool GROUPS = true;
+  T* q;
+  const T* p;
+  double* partials;
+  unsigned* ticket;
+  double* group_out;
+  int gsz;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    gst(q + i, s);
+    dd_fma(dots[0], double(gld(p + i)), double(s));
+  }
+  __device__ __forceinline__ void fin(const double*) const {}
+};
+
+// UP
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S, const double* __restrict__ gz, int ngz,
+                                                         const T* __restrict__ z, T* __restrict__ p,
+                                                         T* __restrict__ x) {
+  using V = typename VecT<T>::type;
+  constexpr int W = VecT<T>::W;
+  if (S->done) return;
+  const int64_t k = S->iter;
+  double v[2];
+  group_sum_dd<2>(gz, ngz, v);
+  const double rho = round_to<T>(v[0]);
+  const double rr = k > 0 ? round_to<T>(v[1]) : S->rr;  // ‖r_0‖² from the init launch
+  int code = 0;  // scipy's top-of-loop test (ProCheck)
+  if (k >= S->max_iter) {
+    code = 2;
+  } else {
+    const double rn = double(tsqrt<T>(T(rr)));
+    if (rn < S->atol) code = 1;
+    else if (!(rn == rn) || rn == INFINITY) code = 3;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (k > 0) {
+      S->rr = rr;
+      if (S->hist) S->hist[k] = double(tsqrt<T>(T(rr)));
+    }
+    if (code) S->done = code;
+  }
+  if (code) return;
+  const bool first = k == 0;
+  const T beta = first ? T(0) : T(rho) / T(S->rho);  // S->rho = ρ_{k-1}
+  const T alpha = T(S->alpha);                        // α_{k-1}
+  const int64_t nv = n / W;
+  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t j0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j0 < nv; j0 += ts * kElemUnroll) {
+    V zz[kElemUnroll], pp[kElemUnroll], xx[kElemUnroll];
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        zz[u] = reinterpret_cast<const V*>(z)[j];
+        pp[u] = reinterpret_cast<const V*>(p)[j];
+        xx[u] = reinterpret_cast<const V*>(x)[j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        if (!first) reinterpret_cast<V*>(x)[j] = xx[u] + alpha * pp[u];
+        reinterpret_cast<V*>(p)[j] = first ? zz[u] : (pp[u] * beta) + zz[u];
+      }
+    }
+  }
+  for (int64_t i = nv * W + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += ts) {
+    const T pi = p[i];
+    if (!first) x[i] = x[i] + alpha * pi;
+    p[i] = first ? z[i] : (pi * beta) + z[i];
+  }
+}
+
+// UR
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S, const double* __restrict__ gz, int ngz,
+                                                         const double* __restrict__ gq, int ngq,
+                                                         const T* __restrict__ q, T* __restrict__ r) {
+  using V = typename VecT<T>::type;
+  constexpr int W = VecT<T>::W;
+  if (S->done) return;
+  double vz[2], vq[1];
+  group_sum_dd<2>(gz, ngz, vz);
+  group_sum_dd<1>(gq, ngq, vq);
+  const double rho = round_to<T>(vz[0]);
+  const double pq = round_to<T>(vq[0]);
+  const T alpha = T(rho) / T(pq);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    S->rho_prev = S->rho;
+    S->rho = rho;
+    S->pq = pq;
+    S->alpha = double(alpha);
+    S->iter = S->iter + 1;
+  }
+  const int64_t nv = n / W;
+  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t j0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j0 < nv; j0 += ts * kElemUnroll) {
+    V rr[kElemUnroll], qq[kElemUnroll];
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        rr[u] = reinterpret_cast<const V*>(r)[j];
+        qq[u] = reinterpret_cast<const V*>(q)[j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) reinterpret_cast<V*>(r)[j] = rr[u] - alpha * qq[u];
+    }
+  }
+  for (int64_t i = nv * W + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += ts) r[i] = r[i] - alpha * q[i];
+}
+
 // IC: ρ = r·z after the two triangular solves
 template <typename T>
 __global__ void __launch_bounds__(kThreads) k_dot_rho(int64_t n, PcgState* S, const T* __restrict__ r,
@@ -559,6 +722,11 @@ struct lspcg_solver {
   void *x = nullptr, *b = nullptr, *r = nullptr, *z = nullptr, *t = nullptr, *p = nullptr, *q = nullptr,
        *d = nullptr, *r2 = nullptr, *p2 = nullptr;  // r2 / p2: second halves of the fused ping-pong pairs
   bool fused = false;   // current ext_spai schedule is the fused 3-kernel one (set_spai decides)
+  bool split = false;   // current ext_spai schedule uses the split reductions (set_spai decides)
+  bool allow_split = true;  // LSPCG_SPLIT_REDUCE=0 keeps the last-arriver reductions
+  int split_mode = 1;
+  double* groups = nullptr;  // [GZ: <= 4096 x 2 dots x DD | GQ: <= 4096 x DD]
+  int gsz_l = 1, ng_l = 1, gsz_a = 1, ng_a = 1;  // group size / count of the KB and KC launches
   bool allow_fused = false;  // LSPCG_PCG_FUSED=1 selects it (measured slower: two gathers per entry)
   PcgState* S = nullptr;
   PcgState* hS = nullptr;  // pinned host mirror
@@ -715,8 +883,41 @@ static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const
   return LSPCG_OK;
 }
 
+template <typename T, bool SC>
+static int enqueue_iteration_split(lspcg_solver* s, hipStream_t st) {
+  const int64_t n = s->n;
+  PcgState* S = s->S;
+  T* x = static_cast<T*>(s->x);
+  T* r = static_cast<T*>(s->r);
+  T* z = static_cast<T*>(s->z);
+  T* t = static_cast<T*>(s->t);
+  T* p = static_cast<T*>(s->p);
+  T* q = static_cast<T*>(s->q);
+  const T* d = static_cast<const T*>(s->d);
+  double* gz = s->groups;
+  double* gq = s->groups + 4096 * 2 * 2;
+  const int eg = elem_vec_grid<T>(n);
+  int rc = launch_it<T>(s, 2, static_cast<const T*>(r), ProDone{S}, EpiT<T, SC>{t, d}, st);
+  if (rc) return rc;
+  rc = launch_it<T>(s, 1, static_cast<const T*>(t), ProDone{S},
+                    EpiZG<T, SC>{z, r, d, T(s->eps), s->partials, s->ticket, gz, s->gsz_l}, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_update_p_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
+                     static_cast<const T*>(z), p, x);
+  rc = launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQG<T>{q, p, s->partials, s->ticket, gq, s->gsz_a},
+                    st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_update_r_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
+                     static_cast<const double*>(gq), s->ng_a, static_cast<const T*>(q), r);
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
 template <typename T>
 static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
+  if (s->split)
+    return s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED ? enqueue_iteration_split<T, true>(s, st)
+                                                       : enqueue_iteration_split<T, false>(s, st);
   if (s->fused)
     return s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED ? enqueue_iteration_fused<T, true>(s, st)
                                                        : enqueue_iteration_fused<T, false>(s, st);
@@ -879,6 +1080,8 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   LSPCG_HIP(hipMalloc(&s->partials, sizeof(double) * 2 * 2 * (g + 1)));
   LSPCG_HIP(hipMalloc(&s->ticket, sizeof(unsigned) * kTicketWords));
   LSPCG_HIP(hipMemsetAsync(s->ticket, 0, sizeof(unsigned) * kTicketWords, s->stream));
+  LSPCG_HIP(hipMalloc(&s->groups, sizeof(double) * 4096 * 2 * 3));
+  LSPCG_HIP(hipMemsetAsync(s->groups, 0, sizeof(double) * 4096 * 2 * 3, s->stream));
   LSPCG_HIP(hipMemsetAsync(s->S, 0, sizeof(PcgState), s->stream));
   for (hipEvent_t* e : {&s->ev_in, &s->ev_out, &s->ev_poll}) LSPCG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   LSPCG_HIP(hipEventCreate(&s->ev_t0));
@@ -888,6 +1091,10 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SELL32")) s->sell16 = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_PCG_FUSED")) s->allow_fused = e[0] == '1';
+  if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
+    s->allow_split = e[0] != '0';
+    s->split_mode = std::atoi(e);
+  }
   if (int rc = make_view(s.get(), A, &s->Av, nullptr, &s->own_A)) return rc;
   if (int rc = build_sell(s.get(), 0, &s->Av)) return rc;
   if (precond == LSPCG_PRECOND_DIAGONAL) {
@@ -925,6 +1132,16 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   // the fused schedule needs SELL views; it gathers twice per entry, which costs more than the two
   // elementwise passes it saves (DESIGN.md "PCG schedule"), so it is opt-in
   s->fused = s->allow_fused && s->sp[0] && s->sp[1] && s->sp[2];
+  s->split = !s->fused && s->allow_split && s->sp[0] && s->sp[1] && s->sp[2];
+  if (s->split) {  // <= 64 groups per reducing launch (or, LSPCG_SPLIT_REDUCE=2, no groups at all)
+    const bool nogroups = s->split_mode == 2;
+    auto groups = [nogroups](int64_t grid, int* gsz, int* ng) {
+      *gsz = nogroups ? 1 : int((grid + kMaxGroups - 1) / kMaxGroups);
+      *ng = int((grid + *gsz - 1) / *gsz);
+    };
+    groups(sell_grid(*s->sp[1], true), &s->gsz_l, &s->ng_l);
+    groups(sell_grid(*s->sp[0], true), &s->gsz_a, &s->ng_a);
+  }
   LSPCG_HIP(hipEventRecord(s->ev_t1, cst));
   LSPCG_HIP(hipEventSynchronize(s->ev_t1));
   float ms = 0.f;
@@ -1065,6 +1282,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipHostFree(s->hS);
   (void)hipFree(s->partials);
   (void)hipFree(s->ticket);
+  (void)hipFree(s->groups);
   for (hipEvent_t e : {s->ev_in, s->ev_out, s->ev_poll, s->ev_t0, s->ev_t1}) (void)hipEventDestroy(e);
   if (s->LT) lspcg_mat_destroy(s->LT);
   if (s->icL) lspcg_mat_destroy(s->icL);

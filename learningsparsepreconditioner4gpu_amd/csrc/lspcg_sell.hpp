@@ -144,9 +144,7 @@ __global__ void __launch_bounds__(TH, 1536 / TH) k_spmv_sell(SellArgs<VT, CT> a,
       if (i < a.n) epi.row(i, acc, d);
     }
   }
-  if constexpr (Epi::NDOT > 0) {
-    grid_reduce_dd<Epi::NDOT>(d, epi.partials, epi.ticket, [&](const double* vals) { epi.fin(vals); });
-  }
+  finish_epi_dots<Epi>(d, epi);
 }
 
 // Reducing launches use a resident grid: 6 workgroups per CU (the kernel's __launch_bounds__
@@ -177,6 +175,12 @@ inline int sell_wg() {  // workgroup size knob LSPCG_SELL_WG (256 / 512 / 1024),
     return (v == 512 || v == 1024) ? v : 256;
   }();
   return wg;
+}
+
+// grid of a SELL launch (the solver sizes the split-reduction groups from it)
+inline int64_t sell_grid(const SellPattern& P, bool reducing) {
+  const int64_t th = sell_wg();
+  return std::min<int64_t>((P.n + th - 1) / th, sell_cap(reducing));
 }
 
 template <typename T, typename VT, typename CT, int TH, class Pro, class Gx, class Epi>

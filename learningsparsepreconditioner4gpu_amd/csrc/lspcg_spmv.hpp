@@ -15,6 +15,7 @@
 #pragma once
 
 #include <algorithm>
+#include <type_traits>
 
 #include "lspcg_internal.hpp"
 
@@ -95,6 +96,23 @@ struct Vec4<float> {
     reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
   }
 };
+
+// Epilogues with GROUPS = true finish their dots with grid_partial_groups (the consumers sum the
+// group totals), the others with the last-arriver grid_reduce_dd + fin().
+template <class E, class = void>
+struct epi_groups : std::false_type {};
+template <class E>
+struct epi_groups<E, std::void_t<decltype(E::GROUPS)>> : std::bool_constant<E::GROUPS> {};
+
+template <class Epi>
+__device__ __forceinline__ void finish_epi_dots(DD (&d)[Epi::NDOT > 0 ? Epi::NDOT : 1], Epi& epi) {
+  if constexpr (Epi::NDOT > 0) {
+    if constexpr (epi_groups<Epi>::value)
+      grid_partial_groups<Epi::NDOT>(d, epi.partials, epi.ticket, epi.gsz, epi.group_out);
+    else
+      grid_reduce_dd<Epi::NDOT>(d, epi.partials, epi.ticket, [&](const double* vals) { epi.fin(vals); });
+  }
+}
 
 // THREADS = workgroup size (one scalar row per thread), GPT = groups of 4 entries each
 // thread stages per chunk (chunk = THREADS*GPT*4 entries), NT = non-temporal matrix loads.
@@ -257,9 +275,7 @@ __global__ void __launch_bounds__(THREADS) k_spmv(SpmvArgs<T, VT, BS> a, Pro pro
   if (active) epi.row(b0 * BS + tid, acc, d);
   }  // tiles
 
-  if constexpr (Epi::NDOT > 0) {
-    grid_reduce_dd<Epi::NDOT>(d, epi.partials, epi.ticket, [&](const double* vals) { epi.fin(vals); });
-  }
+  finish_epi_dots<Epi>(d, epi);
 }
 
 // Production configuration (tuned on MI355X with tools/spmv_probe.py): see DESIGN.md "SpMV".

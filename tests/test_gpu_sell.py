@@ -86,10 +86,13 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
     b = torch.from_numpy(A @ np.ones(n)).cuda()
     out = []
     # CSR views (5 kernels); SELL int32 columns / 16-bit offsets, 5-kernel and fused 3-kernel schedules
-    for env, env32, fused in (("1", "0", "0"), ("0", "1", "0"), ("0", "0", "0"), ("0", "1", "1"), ("0", "0", "1")):
+    # (+ split group reductions vs last-arriver reductions on the SELL 16-bit views)
+    for env, env32, fused, split in (("1", "0", "0", "1"), ("0", "1", "0", "1"), ("0", "0", "0", "1"),
+                                     ("0", "0", "0", "0"), ("0", "1", "1", "1"), ("0", "0", "1", "1")):
         monkeypatch.setenv("LSPCG_NO_SELL", env)
         monkeypatch.setenv("LSPCG_SELL32", env32)
         monkeypatch.setenv("LSPCG_PCG_FUSED", fused)
+        monkeypatch.setenv("LSPCG_SPLIT_REDUCE", split)
         s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
         if precond.startswith("ext_spai"):
             s.set_spai(_cases.spai_like(A), 1e-3)

@@ -36,9 +36,13 @@ print(f"{wl}: n={A.n} nnz={A.nnz}", flush=True)
 
 VARIANTS = [("csr", {"LSPCG_NO_SELL": "1"}), ("sell32", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "1"}),
             ("sell16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_PCG_FUSED": "0"}),
-            ("fused16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_PCG_FUSED": "1"})]
+            ("fused16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_PCG_FUSED": "1"}),
+            ("ticket16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_PCG_FUSED": "0", "LSPCG_SPLIT_REDUCE": "0"}),
+            ("split16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_PCG_FUSED": "0", "LSPCG_SPLIT_REDUCE": "1"})]
 if os.environ.get("PROBE_VARIANTS") == "cap":
-    VARIANTS = [("sell16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0"})]
+    VARIANTS = [("ticket16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "0"}),
+                ("split16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "1"}),
+                ("nogroup16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "2"})]
 ref = None
 for name, env in VARIANTS:
     os.environ.update(env)
@@ -47,7 +51,8 @@ for name, env in VARIANTS:
     ts = []
     for _ in range(reps):
         x = torch.zeros_like(b)
-        it, conv, sec, hist = solver.solve(b, x, rtol=1e-8, return_history=True)
+        it, conv, sec, hist = solver.solve(b, x, rtol=1e-8, max_iter=int(os.environ.get("PROBE_MAXIT", "0")),
+                                           return_history=True)
         ts.append(sec)
     t = float(np.median(ts))
     same = ""
