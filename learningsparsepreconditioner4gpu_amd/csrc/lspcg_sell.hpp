@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace lspcg {
 
@@ -81,8 +82,11 @@ using i16x4 = short __attribute__((ext_vector_type(4)));
 // prologue / epilogue functors and the dot-product reduction are shared).  QB groups of 4
 // entries are loaded per lane before the first gather (branch-free: the group index is
 // clamped, the surplus is masked at the add).
-template <typename T, typename VT, typename CT, int QB, int TH, class Pro, class Gx, class Epi>
-__global__ void __launch_bounds__(TH, 1536 / TH) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
+// MINW: minimum workgroups per CU the register allocation must allow (6 x 256 threads for the
+// compact-value PCG kernels, whose reducing launches use a resident 6-per-CU grid; 1 for fp64
+// values and the double-gather fused epilogues, which need more registers than 6/CU leaves).
+template <typename T, typename VT, typename CT, int QB, int TH, int MINW, class Pro, class Gx, class Epi>
+__global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
   constexpr bool C16 = sizeof(CT) == 2;
   if (pro.exit()) return;
@@ -189,8 +193,9 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
   grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
   SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
-  hipLaunchKernelGGL((k_spmv_sell<T, VT, CT, 4, TH, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a, pro, gx,
-                     epi);
+  constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? (TH <= 1536 ? 1536 / TH : 1) : 1;
+  hipLaunchKernelGGL((k_spmv_sell<T, VT, CT, 4, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a,
+                     pro, gx, epi);
 }
 
 template <typename T, typename VT, typename CT, class Pro, class Gx, class Epi>
