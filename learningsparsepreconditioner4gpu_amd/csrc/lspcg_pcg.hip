@@ -556,7 +556,8 @@ struct EpiQG {
   __device__ __forceinline__ void fin(const double*) const {}
 };
 
-// UP
+// UP.  The first chunk's vector loads are issued before the group sums, so their latency overlaps
+// the scalar reduction instead of following it.
 template <typename T>
 __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S, const double* __restrict__ gz, int ngz,
                                                          const T* __restrict__ z, T* __restrict__ p,
@@ -564,6 +565,22 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
   using V = typename VecT<T>::type;
   constexpr int W = VecT<T>::W;
   if (S->done) return;
+  const int64_t nv = n / W;
+  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
+  const int64_t jt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  V zz[kElemUnroll], pp[kElemUnroll], xx[kElemUnroll];
+  auto load = [&](int64_t j0) {
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        zz[u] = reinterpret_cast<const V*>(z)[j];
+        pp[u] = reinterpret_cast<const V*>(p)[j];
+        xx[u] = reinterpret_cast<const V*>(x)[j];
+      }
+    }
+  };
+  load(jt);
   const int64_t k = S->iter;
   double v[2];
   group_sum_dd<2>(gz, ngz, v);
@@ -588,19 +605,8 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
   const bool first = k == 0;
   const T beta = first ? T(0) : T(rho) / T(S->rho);  // S->rho = ρ_{k-1}
   const T alpha = T(S->alpha);                        // α_{k-1}
-  const int64_t nv = n / W;
-  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
-  for (int64_t j0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j0 < nv; j0 += ts * kElemUnroll) {
-    V zz[kElemUnroll], pp[kElemUnroll], xx[kElemUnroll];
-#pragma unroll
-    for (int u = 0; u < kElemUnroll; ++u) {
-      const int64_t j = j0 + u * ts;
-      if (j < nv) {
-        zz[u] = reinterpret_cast<const V*>(z)[j];
-        pp[u] = reinterpret_cast<const V*>(p)[j];
-        xx[u] = reinterpret_cast<const V*>(x)[j];
-      }
-    }
+  for (int64_t j0 = jt; j0 < nv; j0 += ts * kElemUnroll) {
+    if (j0 != jt) load(j0);
 #pragma unroll
     for (int u = 0; u < kElemUnroll; ++u) {
       const int64_t j = j0 + u * ts;
@@ -610,14 +616,14 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
       }
     }
   }
-  for (int64_t i = nv * W + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += ts) {
+  for (int64_t i = nv * W + jt; i < n; i += ts) {
     const T pi = p[i];
     if (!first) x[i] = x[i] + alpha * pi;
     p[i] = first ? z[i] : (pi * beta) + z[i];
   }
 }
 
-// UR
+// UR (first chunk loaded before the group sums, as in UP)
 template <typename T>
 __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S, const double* __restrict__ gz, int ngz,
                                                          const double* __restrict__ gq, int ngq,
@@ -625,6 +631,21 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
   using V = typename VecT<T>::type;
   constexpr int W = VecT<T>::W;
   if (S->done) return;
+  const int64_t nv = n / W;
+  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
+  const int64_t jt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  V rr[kElemUnroll], qq[kElemUnroll];
+  auto load = [&](int64_t j0) {
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        rr[u] = reinterpret_cast<const V*>(r)[j];
+        qq[u] = reinterpret_cast<const V*>(q)[j];
+      }
+    }
+  };
+  load(jt);
   double vz[2], vq[1];
   group_sum_dd<2>(gz, ngz, vz);
   group_sum_dd<1>(gq, ngq, vq);
@@ -638,25 +659,15 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
     S->alpha = double(alpha);
     S->iter = S->iter + 1;
   }
-  const int64_t nv = n / W;
-  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
-  for (int64_t j0 = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; j0 < nv; j0 += ts * kElemUnroll) {
-    V rr[kElemUnroll], qq[kElemUnroll];
-#pragma unroll
-    for (int u = 0; u < kElemUnroll; ++u) {
-      const int64_t j = j0 + u * ts;
-      if (j < nv) {
-        rr[u] = reinterpret_cast<const V*>(r)[j];
-        qq[u] = reinterpret_cast<const V*>(q)[j];
-      }
-    }
+  for (int64_t j0 = jt; j0 < nv; j0 += ts * kElemUnroll) {
+    if (j0 != jt) load(j0);
 #pragma unroll
     for (int u = 0; u < kElemUnroll; ++u) {
       const int64_t j = j0 + u * ts;
       if (j < nv) reinterpret_cast<V*>(r)[j] = rr[u] - alpha * qq[u];
     }
   }
-  for (int64_t i = nv * W + int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += ts) r[i] = r[i] - alpha * q[i];
+  for (int64_t i = nv * W + jt; i < n; i += ts) r[i] = r[i] - alpha * q[i];
 }
 
 // IC: ρ = r·z after the two triangular solves
