@@ -447,7 +447,7 @@ int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind) {
   if (A->block_size != 1 || A->n == 0 || A->nnzb == 0) return LSPCG_OK;
   hipStream_t st = A->ctx->stream;
   std::unique_ptr<SellCopy> c(new SellCopy());
-  int rc = sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, 1.5, true, st, &c->P);
+  int rc = sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, sell_max_pad(), true, st, &c->P);
   if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // irregular rows: the CSR kernel stays
   if (rc) return rc;
   const int vd = A->storage_dtype();

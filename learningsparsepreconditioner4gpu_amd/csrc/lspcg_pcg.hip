@@ -766,23 +766,30 @@ struct lspcg_solver {
   const SellPattern* sp[3] = {nullptr, nullptr, nullptr};
   void* sv[3] = {nullptr, nullptr, nullptr};
   int svd[3] = {0, 0, 0};
+  int32_t* xrow[3] = {nullptr, nullptr, nullptr};  // scalar row pointers of expanded BSR3 views
 };
 
 // (Re)build the SELL copy of iteration view w (0 = A, 1 = L, 2 = Lᵀ); L and Lᵀ reuse A's
 // pattern when make_view found the same index arrays.
+static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view);
+
 static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   hipStream_t st = s->ctx->stream;
   LSPCG_HIP(hipStreamSynchronize(s->stream));
   (void)hipFree(s->sv[w]);
   s->sv[w] = nullptr;
   s->spat[w].release();
+  (void)hipFree(s->xrow[w]);
+  s->xrow[w] = nullptr;
   s->sp[w] = nullptr;
-  if (!s->use_sell || view->block_size != 1 || view->n == 0 || view->nnzb == 0) return LSPCG_OK;
+  if (!s->use_sell || view->n == 0 || view->nnzb == 0) return LSPCG_OK;
+  if (view->block_size == 3) return build_sell_bsr3(s, w, view);
+  if (view->block_size != 1) return LSPCG_OK;
   const SellPattern* P = nullptr;
   if (w > 0 && s->sp[0] && view->rowptr == s->Av.rowptr && view->colind == s->Av.colind) {
     P = s->sp[0];
   } else {
-    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, 1.5, s->sell16, st,
+    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(), s->sell16, st,
                                       &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: CSR kernel
     if (rc) return rc;
@@ -791,6 +798,77 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   const int vd = view->storage_dtype();
   if (int rc = sell_fill_values(*P, view->colind, view->vals, vd, vd, st, &s->sv[w])) return rc;
   LSPCG_HIP(hipStreamSynchronize(st));
+  s->svd[w] = vd;
+  s->sp[w] = P;
+  return LSPCG_OK;
+}
+
+// BSR 3x3 -> scalar rows in the reference's own order (validate.py:51 expands the blocks to a
+// scalar CSR sorted by column: block by block, then the block's 3 columns), in-block zeros kept
+// -- the same summation sequence as the block kernel.  One thread per scalar row r = 3I + c.
+template <typename VS>
+__global__ void k_bsr3_expand(int64_t nb, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                              const VS* __restrict__ vals, int32_t* __restrict__ xrow, int32_t* __restrict__ xcol,
+                              VS* __restrict__ xval) {
+  const int64_t n = 3 * nb;
+  for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < n; r += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t I = r / 3;
+    const int c = int(r - 3 * I);
+    const int32_t b0 = rowptr[I], len = rowptr[I + 1] - b0;
+    const int32_t base = 9 * b0 + 3 * c * len;
+    if (xrow) {
+      xrow[r] = base;
+      if (r == n - 1) xrow[n] = 9 * rowptr[nb];
+    }
+    for (int32_t q = 0; q < len; ++q) {
+      const int32_t J = colind[b0 + q];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int32_t pos = base + 3 * q + k;
+        if (xcol) xcol[pos] = 3 * J + k;
+        if (xval) xval[pos] = vals[int64_t(b0 + q) * 9 + 3 * c + k];
+      }
+    }
+  }
+}
+
+static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view) {
+  hipStream_t st = s->ctx->stream;
+  const int64_t n = view->n, ne = 9 * view->nnzb;
+  if (ne >= (int64_t(1) << 31)) return LSPCG_OK;  // expanded entries must fit int32 row pointers
+  const dim3 g(elem_grid(n)), b(kThreads);
+  const int vd = view->storage_dtype();
+  const bool shared = w > 0 && s->sp[0] && view->rowptr == s->Av.rowptr && view->colind == s->Av.colind;
+  const SellPattern* P = nullptr;
+  if (shared) {
+    P = s->sp[0];
+  } else {
+    int32_t* xcol = nullptr;
+    LSPCG_HIP(hipMalloc(&s->xrow[w], sizeof(int32_t) * (n + 1)));
+    LSPCG_HIP(hipMalloc(&xcol, sizeof(int32_t) * ne));
+    hipLaunchKernelGGL(k_bsr3_expand<float>, g, b, 0, st, view->nb, view->rowptr, view->colind,
+                       static_cast<const float*>(nullptr), s->xrow[w], xcol, static_cast<float*>(nullptr));
+    const int rc = sell_build_pattern(n, ne, s->xrow[w], xcol, sell_max_pad(), s->sell16, st, &s->spat[w]);
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(xcol);
+    if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: block kernel
+    if (rc) return rc;
+    P = &s->spat[w];
+  }
+  void* xval = nullptr;
+  LSPCG_HIP(hipMalloc(&xval, (vd == LSPCG_F32 ? 4 : 8) * ne));
+  if (vd == LSPCG_F32)
+    hipLaunchKernelGGL(k_bsr3_expand<float>, g, b, 0, st, view->nb, view->rowptr, view->colind,
+                       static_cast<const float*>(view->vals), static_cast<int32_t*>(nullptr),
+                       static_cast<int32_t*>(nullptr), static_cast<float*>(xval));
+  else
+    hipLaunchKernelGGL(k_bsr3_expand<double>, g, b, 0, st, view->nb, view->rowptr, view->colind,
+                       static_cast<const double*>(view->vals), static_cast<int32_t*>(nullptr),
+                       static_cast<int32_t*>(nullptr), static_cast<double*>(xval));
+  const int rc = sell_fill_values(*P, nullptr, xval, vd, vd, st, &s->sv[w]);
+  (void)hipStreamSynchronize(st);
+  (void)hipFree(xval);
+  if (rc) return rc;
   s->svd[w] = vd;
   s->sp[w] = P;
   return LSPCG_OK;
@@ -1303,6 +1381,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   for (void* p : {s->own_A, s->own_L, s->own_LT}) (void)hipFree(p);
   for (int w = 0; w < 3; ++w) {
     (void)hipFree(s->sv[w]);
+    (void)hipFree(s->xrow[w]);
     s->spat[w].release();
   }
   (void)hipFree(s->flag);

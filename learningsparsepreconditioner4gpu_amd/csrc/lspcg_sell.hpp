@@ -172,6 +172,15 @@ inline int64_t sell_cap(bool reducing) {
   return reducing ? rcap : ncap;
 }
 
+// largest padded-slots / nnz ratio for which a SELL view is built (LSPCG_SELL_MAXPAD, read once)
+inline double sell_max_pad() {
+  static const double v = [] {
+    const char* e = std::getenv("LSPCG_SELL_MAXPAD");
+    return e ? std::atof(e) : 2.0;  // 2-D 5-point rows (5 -> 8 slots) still run faster as SELL
+  }();
+  return v;
+}
+
 inline int sell_wg() {  // workgroup size knob LSPCG_SELL_WG (256 / 512 / 1024), read once
   static const int wg = [] {
     const char* e = std::getenv("LSPCG_SELL_WG");

@@ -106,7 +106,7 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
         assert np.array_equal(out[0][2], o[2]), name
 
 
-def _expected_kind(A, max_pad=1.5):
+def _expected_kind(A, max_pad=2.0):
     """lspcg_mat_prepare_spmv's rule: SELL-64 if the padded slots stay <= max_pad * nnz, with
     16-bit column offsets if every |col - 64*slice| <= 32767."""
     n = A.shape[0]
@@ -149,3 +149,30 @@ def test_prepare_spmv_dropped_by_scale_columns(gpu_ctx):
     B.data = B.data * d[B.indices]  # lspcg_mat_scale_columns: vals[k] * d[col[k]]
     ref = B @ x
     assert np.array_equal(Ad.matvec(torch.from_numpy(x).cuda()).cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("precond", ["none", "ext_spai"])
+def test_pcg_bsr3_sell_equals_block_kernel(gpu_ctx, precond, monkeypatch):
+    """BSR 3x3 systems: the expanded scalar SELL views give the block kernel's bits."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    A, mask, _ = P.elasticity_box(9, 5, 4)
+    A = sp.csr_matrix(A)
+    n = A.shape[0]
+    L = sp.csr_matrix(sp.bsr_matrix(_cases.spai_like(A), blocksize=(3, 3)))
+    b = torch.from_numpy(A @ mask.reshape(-1).astype(np.float64)).cuda()
+    out = []
+    for env in ("1", "0"):
+        monkeypatch.setenv("LSPCG_NO_SELL", env)
+        Ad = DeviceMatrix.from_scipy(A, block_size=3)
+        s = PreconditionedConjugateGradient(Ad, device="cuda", preconditioner=precond)
+        if precond == "ext_spai":
+            s.set_spai(DeviceMatrix.from_scipy(L, block_size=3), 1e-3, block_size=3)
+        x = torch.zeros(n, dtype=torch.float64, device="cuda")
+        it, conv, _, hist = s.solve(b, x, rtol=1e-8, return_history=True)
+        out.append((it, x.cpu().numpy(), hist))
+        del s
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][2], out[1][2])
