@@ -170,6 +170,18 @@ inline void launch_transpose_fill(const lspcg_mat* A, lspcg_mat* Tm, int32_t* fi
                      static_cast<const T*>(A->vals), static_cast<T*>(Tm->vals));
 }
 
+// diagnostic gather: one 16-B load of an interleaved pair, a - alpha*b (the fused schedule's
+// r - alpha q / p beta + z gathers with the two vectors interleaved)
+struct GatherPairDiag {
+  const double* xy;
+  double alpha;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ double operator()(int64_t j) const {
+    const f64x2 v = *(const __attribute__((address_space(1))) f64x2*)(xy + 2 * j);
+    return v.x - alpha * v.y;
+  }
+};
+
 // ---- diagnostic SpMV configurations (fp64, scalar CSR) for on-device A/B tuning
 using SpmvLaunch = void (*)(const lspcg_mat*, const void*, void*, hipStream_t);
 template <int TH, int GPT, bool NT, bool LANEC = false, bool XCD = false>
@@ -599,17 +611,32 @@ int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int compact, const
   if (rc) return rc;
   void* v = nullptr;
   rc = sell_fill_values(P, A->colind, A->vals, LSPCG_F64, (compact & 1) ? LSPCG_F32 : LSPCG_F64, st, &v);
+  double* x2 = nullptr;
+  if (!rc && (compact & 4)) {  // experiment: 16-B gathers of interleaved (x, x) pairs
+    if (hipMalloc(&x2, sizeof(double) * 2 * std::max<int64_t>(A->n, 1)) != hipSuccess) rc = LSPCG_ERR_HIP;
+    else {
+      (void)hipMemcpy2DAsync(x2, 16, x, 8, 8, A->n, hipMemcpyDeviceToDevice, st);
+      (void)hipMemcpy2DAsync(x2 + 1, 16, x, 8, 8, A->n, hipMemcpyDeviceToDevice, st);
+    }
+  }
   if (!rc) {
     const GatherVec<double> gx{static_cast<const double*>(x)};
+    const GatherPairDiag gp{x2, 0.0};
     const EpiStore<double> epi{static_cast<double*>(y)};
     rc = spmv_timed_impl(ctx, A, reps, flush_bytes, avg_ms, [&]() -> int {
-      if (compact & 1) launch_spmv_sell_cfg<double, float>(P, v, gx, ProNone{}, epi, st);
-      else launch_spmv_sell_cfg<double, double>(P, v, gx, ProNone{}, epi, st);
+      if (compact & 4) {
+        if (compact & 1) launch_spmv_sell_cfg<double, float>(P, v, gp, ProNone{}, epi, st);
+        else launch_spmv_sell_cfg<double, double>(P, v, gp, ProNone{}, epi, st);
+      } else {
+        if (compact & 1) launch_spmv_sell_cfg<double, float>(P, v, gx, ProNone{}, epi, st);
+        else launch_spmv_sell_cfg<double, double>(P, v, gx, ProNone{}, epi, st);
+      }
       LSPCG_HIP(hipGetLastError());
       return LSPCG_OK;
     });
   }
   (void)hipStreamSynchronize(st);
+  (void)hipFree(x2);
   (void)hipFree(v);
   P.release();
   return rc;

@@ -41,8 +41,7 @@ VARIANTS = [("csr", {"LSPCG_NO_SELL": "1"}), ("sell32", {"LSPCG_NO_SELL": "0", "
             ("split16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_PCG_FUSED": "0", "LSPCG_SPLIT_REDUCE": "1"})]
 if os.environ.get("PROBE_VARIANTS") == "cap":
     VARIANTS = [("ticket16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "0"}),
-                ("split16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "1"}),
-                ("nogroup16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "2"})]
+                ("split16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "1"})]
 ref = None
 for name, env in VARIANTS:
     os.environ.update(env)
@@ -74,11 +73,11 @@ for label, flush in (("cold", 512 << 20), ("warm", 0)):
     r = 30 if flush else 90
     ms0 = A.spmv_timed(x, y0, r, flush_bytes=flush)
     out = [f"csr {ms0*1e3:.1f} us ({alg/ms0/1e6:.0f} GB/s)"]
-    for compact in (0, 2, 1, 3):
+    for compact in (0, 2, 1, 3, 7):
         ms = C.c_double()
         _lib.check(lib.lspcg_spmv_sell_timed(A.ctx.handle, A.handle, compact, C.c_void_p(x.data_ptr()),
                                              C.c_void_p(y1.data_ptr()), r, flush, C.byref(ms)))
-        out.append(f"sell{['', '-f32val', '-c16', '-f32val-c16'][compact]} {ms.value*1e3:.1f} us ({alg/ms.value/1e6:.0f} GB/s) "
+        out.append(f"sell{['', '-f32val', '-c16', '-f32val-c16', '', '', '', '-f32val-c16-pairgather'][compact]} {ms.value*1e3:.1f} us ({alg/ms.value/1e6:.0f} GB/s) "
                    f"bitexact={torch.equal(y0, y1)}")
     print(f"SpMV {label}: " + " | ".join(out), flush=True)
     rd = []
