@@ -151,9 +151,9 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
   finish_epi_dots<Epi>(d, epi);
 }
 
-// Reducing launches use a resident grid: 6 workgroups per CU (the kernel's __launch_bounds__
-// guarantee), i.e. 1536 on MI355X -- one wave of workgroups, each walking its row tiles, so no
-// straggler round delays the ticket (measured best of 768..3072).  Capped by the solver's 4096
+// Reducing launches use a resident grid: 6 workgroups per CU (the compact-value kernels'
+// __launch_bounds__ guarantee), i.e. 1536 on MI355X -- one wave of workgroups, each walking its
+// row tiles, so no straggler round delays the ticket (8 per CU / 2048 measured the same).  Capped by the solver's 4096
 // partial slots.  Knobs LSPCG_SELL_RCAP / LSPCG_SELL_NCAP (read once) for experiments.
 inline int64_t sell_cap(bool reducing) {
   static const int64_t rcap = [] {
@@ -202,8 +202,12 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
   grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
   SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
+  // compact-value kernels: registers for 6 workgroups per CU (the resident reducing grid)
   constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? (TH <= 1536 ? 1536 / TH : 1) : 1;
-  hipLaunchKernelGGL((k_spmv_sell<T, VT, CT, 4, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a,
+  // 2 groups of 4 entries per batch for fp32-stored values (fewer registers in flight: 89.6-90.7
+  // vs 91.2 us per PCG iteration, 25.0 vs 27.0 us cold SpMV), 4 for fp64 values
+  constexpr int QB = sizeof(VT) == 4 ? 2 : 4;
+  hipLaunchKernelGGL((k_spmv_sell<T, VT, CT, QB, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a,
                      pro, gx, epi);
 }
 
