@@ -306,7 +306,7 @@ constexpr int kFrag48 = frag_size(12);
 constexpr int kFrag16 = frag_size(4);
 constexpr int kLayerFrag = 2 * kFrag48 + kFrag16;  // [msg | edge | node]
 
-__global__ void __launch_bounds__(256) k_mp_layer(int64_t N, const float* __restrict__ frag, int node_res,
+__global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __restrict__ frag, int node_res,
                                                  int edge_res, const int32_t* __restrict__ ptr,
                                                  const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                                  const float* __restrict__ x, float* __restrict__ e,
