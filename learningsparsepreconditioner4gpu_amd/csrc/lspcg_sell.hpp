@@ -181,19 +181,11 @@ inline double sell_max_pad() {
   return v;
 }
 
-inline int sell_wg() {  // workgroup size knob LSPCG_SELL_WG (256 / 512 / 1024), read once
-  static const int wg = [] {
-    const char* e = std::getenv("LSPCG_SELL_WG");
-    const int v = e ? std::atoi(e) : 256;
-    return (v == 512 || v == 1024) ? v : 256;
-  }();
-  return wg;
-}
-
 // grid of a SELL launch (the solver sizes the split-reduction groups from it)
+constexpr int kSellWG = 256;  // 4 slices per workgroup (512 / 1024 measured slower: DESIGN.md §5)
+
 inline int64_t sell_grid(const SellPattern& P, bool reducing) {
-  const int64_t th = sell_wg();
-  return std::min<int64_t>((P.n + th - 1) / th, sell_cap(reducing));
+  return std::min<int64_t>((P.n + kSellWG - 1) / kSellWG, sell_cap(reducing));
 }
 
 template <typename T, typename VT, typename CT, int TH, class Pro, class Gx, class Epi>
@@ -211,19 +203,10 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
                      pro, gx, epi);
 }
 
-template <typename T, typename VT, typename CT, class Pro, class Gx, class Epi>
-inline void launch_spmv_sell_ct(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
-  switch (sell_wg()) {
-    case 1024: launch_spmv_sell_th<T, VT, CT, 1024>(P, vals, gx, pro, epi, st); break;
-    case 512: launch_spmv_sell_th<T, VT, CT, 512>(P, vals, gx, pro, epi, st); break;
-    default: launch_spmv_sell_th<T, VT, CT, 256>(P, vals, gx, pro, epi, st);
-  }
-}
-
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
-  if (P.col_bits == 16) launch_spmv_sell_ct<T, VT, int16_t>(P, vals, gx, pro, epi, st);
-  else launch_spmv_sell_ct<T, VT, int32_t>(P, vals, gx, pro, epi, st);
+  if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st);
+  else launch_spmv_sell_th<T, VT, int32_t, kSellWG>(P, vals, gx, pro, epi, st);
 }
 
 }  // namespace lspcg
