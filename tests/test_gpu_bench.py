@@ -1,0 +1,33 @@
+"""bench.py's JSON contract on a small system (GPU box): one line with the metric, value,
+roofline (achieved / peak / frac / traffic) and cpu_baseline objects, rank-0 only."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def test_bench_json_line():
+    env = dict(os.environ)
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--workload", "kuhn31", "--steps", "2", "--warmup",
+                          "1", "--spmv-reps", "3", "--cpu-reps", "1"], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=240, check=True)
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["higher_is_better"] is True and d["dtype"] == "f64"
+    assert d["value"] > 0 and d["config"]["iters_per_solve"] > 0
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    c = d["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] == 1 and c["value"] > 0
