@@ -58,6 +58,39 @@ def reduce_timing(elapsed: float, iters: float, device) -> tuple:
     return float(mx[0]), float(sm[0])
 
 
+def sell_slots(indptr: np.ndarray) -> int:
+    """Stored slots of the SELL-64 layout (csrc/lspcg_sell.hpp): per 64-row slice, 64 x the
+    slice's longest row rounded up to a multiple of 4."""
+    lens = np.diff(indptr)
+    ns = (lens.size + 63) // 64
+    pad = np.zeros(ns * 64, dtype=np.int64)
+    pad[: lens.size] = lens
+    return int(256 * ((pad.reshape(ns, 64).max(axis=1) + 3) // 4).sum())
+
+
+def pcg_loop_spmv(A, p, q, reps: int) -> dict:
+    """The SpMV the PCG loop runs (fp32-stored values -- exact for the reference's fp32-born
+    matrices -- and 16-bit column offsets) timed cold / warm on the same matrix, against the
+    bytes of its own format: 6 B per stored slot + x read + y written."""
+    import ctypes as C
+
+    from learningsparsepreconditioner4gpu_amd import _lib
+
+    out = {}
+    for label, flush in (("cold", FLUSH_BYTES), ("warm", 0)):
+        ms = C.c_double()
+        _lib.call("lspcg_spmv_sell_timed", A.ctx.handle, A.handle, 3, C.c_void_p(p.data_ptr()), C.c_void_p(q.data_ptr()),
+                  reps if flush else 3 * reps, flush, C.byref(ms))
+        out[label] = ms.value
+    indptr = A.to_scipy().indptr
+    fmt = 6 * sell_slots(indptr) + 16 * A.n
+    return {"kernel": "k_spmv_sell<double,float,int16> as in the PCG loop (values stored as fp32 -- lossless for the "
+                      "reference's fp32-born A and L -- 16-bit column offsets)",
+            "format_bytes": fmt, "avg_launch_ms_cold": out["cold"], "avg_launch_ms_warm": out["warm"],
+            "achieved_format_GBs_cold": fmt / (out["cold"] * 1e-3) / 1e9,
+            "frac_format_cold": fmt / (out["cold"] * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
+
 def cpu_baseline(A, L, eps, gt, max_iter: int):
     """The reference's CPU restatement (validate.py:163-201: scipy cg + explicit-Lᵀ SPAI
     operator), timed like validate.py:196-198, on a bounded number of iterations."""
@@ -176,6 +209,7 @@ def main():
               "fp64 values), bit-exact scipy order" if kind else
               "k_spmv<double,1> staged scalar CSR SpMV of A, bit-exact scipy order")
     alg = spmv_bytes(n, nnz_a)
+    pcg_spmv = pcg_loop_spmv(A, p, q, args.spmv_reps)
     gbs_cold = alg / (ms_cold * 1e-3) / 1e9
     gbs_warm = alg / (ms_warm * 1e-3) / 1e9
     it_per_solve = iters[-1]
@@ -251,6 +285,7 @@ def main():
                 "csr_staged_achieved": alg / (csr_cold * 1e-3) / 1e9,
                 "method": "HIP events on the ctx stream; cold = a 512 MiB read before every launch, launch time = (R x (flush+SpMV) - R x flush)/R",
             },
+            "pcg_loop_spmv": pcg_spmv,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
