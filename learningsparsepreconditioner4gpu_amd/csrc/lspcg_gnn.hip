@@ -46,27 +46,39 @@ __host__ __device__ constexpr int ff_size(int in, int out) { return H * in + H +
 // C2 (64 x 4) | A3 (4 x 64) | C3 (64 x 4)]
 __host__ __device__ constexpr int frag_size(int s1) { return s1 * 64 + 5 * 256; }
 
-// GELU(v) = 0.5 v erfc(-v/sqrt2).  erfc by the Chebyshev-fitted form of Numerical Recipes
-// (erfcc: fractional error < 1.2e-7 for every argument), branch-free: one rcp, one exp2 and 11
-// FMAs instead of ocml's two-branch erff -- the per-edge MLPs are VALU-bound on GELU.  Two
-// values at a time in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32) halve the polynomial's issue
-// cost.  Relative accuracy also holds in the negative tail, where GELU -> 0.
+// GELU(v) = v Phi(v) = max(v, 0) - |v| m,  m = erfc(|v|/sqrt2) / 2  (either sign of v).
+// erfc(z) = t exp(-z^2 + P(t)), t = 1/(1 + z/2): the Chebyshev-fitted erfcc of Numerical
+// Recipes (fractional error < 1.2e-7 for every argument, so the negative tail, where GELU -> 0,
+// keeps its relative accuracy), branch-free: one rcp, one exp2 and 11 FMAs instead of ocml's
+// two-branch erff -- the per-edge MLPs are VALU-bound on GELU.  With y = z sqrt(log2 e) the
+// exponent is -y^2 + log2(e) P(t) - 1 (log2 e and the 1/2 folded into the coefficients), |v|
+// enters as a free source modifier, and the sign select is a max + FMA.  Two values at a time in
+// packed fp32 (v_pk_fma_f32 / v_pk_mul_f32) halve the polynomial's issue cost.
 using f2 = float __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, float c) { return __builtin_elementwise_fma(a, b, (f2)(c)); }
+constexpr double kLog2e = 1.4426950408889634;
+constexpr float kGeluY = 0.8493218002880191f;   // sqrt(log2(e) / 2): y = |v| * kGeluY
+constexpr float kGeluT = 0.41627730557884884f;  // 0.5 / sqrt(log2(e)): t = 1 / (1 + y * kGeluT)
+// max(v, 0) as one v_max_i32 on the bit pattern (negative floats, -0 included, are negative
+// integers); fmaxf would add a canonicalising v_max
+__device__ __forceinline__ float relu(float v) {
+  return __builtin_bit_cast(float, max(__builtin_bit_cast(int, v), 0));
+}
 // K independent pairs, every step interleaved across them: a dependent packed op needs a wait
 // state on gfx950, so one chain alone would issue an s_nop between every Horner step.
 template <int K>
 __device__ __forceinline__ void gelu_n(f2 (&v)[K]) {
-  f2 z[K], t[K], p[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) z[k] = __builtin_elementwise_abs(v[k]) * (f2)(0.7071067811865476f);
+  f2 y[K], t[K], p[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const f2 u = pfma(z[k], (f2)(0.5f), 1.0f);
+    y[k] = (f2){__builtin_fabsf(v[k].x) * kGeluY, __builtin_fabsf(v[k].y) * kGeluY};
+    const f2 u = pfma(y[k], (f2)(kGeluT), 1.0f);
     t[k] = (f2){__builtin_amdgcn_rcpf(u.x), __builtin_amdgcn_rcpf(u.y)};
   }
-  constexpr float C[10] = {0.17087277f, -0.82215223f, 1.48851587f, -1.13520398f, 0.27886807f,
-                           -0.18628806f, 0.09678418f, 0.37409196f, 1.00002368f, -1.26551223f};
+  constexpr float C[10] = {float(0.17087277 * kLog2e),  float(-0.82215223 * kLog2e), float(1.48851587 * kLog2e),
+                           float(-1.13520398 * kLog2e), float(0.27886807 * kLog2e),  float(-0.18628806 * kLog2e),
+                           float(0.09678418 * kLog2e),  float(0.37409196 * kLog2e),  float(1.00002368 * kLog2e),
+                           float(-1.26551223 * kLog2e - 1.0)};
 #pragma unroll
   for (int k = 0; k < K; ++k) p[k] = pfma(t[k], (f2)(C[0]), C[1]);
 #pragma unroll
@@ -75,10 +87,10 @@ __device__ __forceinline__ void gelu_n(f2 (&v)[K]) {
     for (int k = 0; k < K; ++k) p[k] = pfma(t[k], p[k], C[c]);
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const f2 arg = __builtin_elementwise_fma(-z[k], z[k], p[k]) * (f2)(1.4426950408889634f);  // log2(e) x
-    const f2 ec = t[k] * (f2){__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};  // erfc(|v|/sqrt2)
-    const f2 phi = {v[k].x >= 0.f ? 2.0f - ec.x : ec.x, v[k].y >= 0.f ? 2.0f - ec.y : ec.y};
-    v[k] = (f2)(0.5f) * v[k] * phi;
+    const f2 arg = __builtin_elementwise_fma(-y[k], y[k], p[k]);
+    const f2 m = t[k] * (f2){__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+    v[k] = (f2){__builtin_fmaf(-__builtin_fabsf(v[k].x), m.x, relu(v[k].x)),
+                __builtin_fmaf(-__builtin_fabsf(v[k].y), m.y, relu(v[k].y))};
   }
 }
 __device__ __forceinline__ f4 gelu4(f4 a) {
@@ -159,6 +171,22 @@ __device__ __forceinline__ f4 ff_tile(const float* fr, const float (&in)[S1], in
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
+// Sum over the 4 K-quarters of an item (lanes l, l^16, l^32, l^48), every lane gets the total:
+// gfx950's row-swap permutes (VALU, no LDS round trip like ds_bpermute).  swap(v, v) returns the
+// own row's value in one register and the partner row's in the other.  (The pair is read through
+// a 64-bit bit_cast: subscripting the builtin's result folds both halves into element 0.)
+__device__ __forceinline__ float swap_sum16(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const unsigned long long r = __builtin_bit_cast(unsigned long long, __builtin_amdgcn_permlane16_swap(u, u, false, false));
+  return __builtin_bit_cast(float, unsigned(r)) + __builtin_bit_cast(float, unsigned(r >> 32));
+}
+__device__ __forceinline__ float swap_sum32(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const unsigned long long r = __builtin_bit_cast(unsigned long long, __builtin_amdgcn_permlane32_swap(u, u, false, false));
+  return __builtin_bit_cast(float, unsigned(r)) + __builtin_bit_cast(float, unsigned(r >> 32));
+}
+__device__ __forceinline__ float quad_sum(float v) { return swap_sum32(swap_sum16(v)); }
+
 // 48-feature block layout of a lane: in[s], s = 4*block + c  <->  feature 16*block + 4q + c
 __device__ __forceinline__ void pack12(f4 b0, f4 b1, f4 b2, float (&v)[12]) {
   v[0] = b0.x; v[1] = b0.y; v[2] = b0.z; v[3] = b0.w;
@@ -225,25 +253,27 @@ __global__ void k_csc_rowstart(int64_t N, int64_t E, const int64_t* __restrict__
   }
 }
 
+// Symmetric, strictly sorted pattern (k_csc_rowstart's check): the CSC slots of destination c
+// are CSR row c's own slots, and the slot of edge e = (r, c) is the position of r in row c --
+// the map is an involution (inv == perm), and slot k's endpoints are (ei[E+k], ei[k]).  Every
+// write is therefore at the thread's own index (coalesced); only the search in row c gathers.
 __global__ void k_csc_sym(int64_t E, const int64_t* __restrict__ ei, const int32_t* __restrict__ ptr,
                           int32_t* __restrict__ perm, int32_t* __restrict__ inv, int32_t* __restrict__ src,
                           int32_t* __restrict__ dst, int* flag) {
   for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += int64_t(gridDim.x) * blockDim.x) {
     const int64_t r = ei[e], c = ei[E + e];
-    int64_t lo = ptr[c], hi = ptr[c + 1];
+    const int32_t end = ptr[c + 1];
+    int32_t lo = ptr[c], hi = end;
     while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
+      const int32_t mid = (lo + hi) >> 1;
       if (ei[E + mid] < r) lo = mid + 1;
       else hi = mid;
     }
-    if (lo >= ptr[c + 1] || ei[E + lo] != r) {
-      atomicOr(flag, 2);
-      continue;
-    }
-    perm[lo] = int32_t(e);
-    inv[e] = int32_t(lo);
-    src[lo] = int32_t(r);
-    dst[lo] = int32_t(c);
+    if (lo >= end || ei[E + lo] != r) atomicOr(flag, 2);
+    perm[e] = lo;
+    inv[e] = lo;
+    src[e] = int32_t(c);
+    dst[e] = int32_t(r);
   }
 }
 
@@ -368,24 +398,25 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
           qs = src[kn];
         }
       }
-      // LayerNorm(48) statistics: 12 values per lane, 4 lanes per edge (xor 16, 32)
-      float sum = (xd.x + xd.y + xd.z + xd.w) + (xs.x + xs.y + xs.z + xs.w) + (ea.x + ea.y + ea.z + ea.w);
-      sum += __shfl_xor(sum, 16, 64);
-      sum += __shfl_xor(sum, 32, 64);
-      const float mean = sum * (1.0f / 48.0f);
-      float v[12];
-      pack12(xd, xs, ea, v);
-      float sq = 0.f;
+      // LayerNorm(48) statistics: 12 values per lane, 4 lanes per edge, packed fp32 pairs
+      f2 w[6] = {(f2){xd.x, xd.y}, (f2){xd.z, xd.w}, (f2){xs.x, xs.y},
+                 (f2){xs.z, xs.w}, (f2){ea.x, ea.y}, (f2){ea.z, ea.w}};
+      const f2 s2 = ((w[0] + w[1]) + (w[2] + w[3])) + (w[4] + w[5]);
+      const float mean = quad_sum(s2.x + s2.y) * (1.0f / 48.0f);
+      f2 q2 = (f2)(0.f);
 #pragma unroll
-      for (int j = 0; j < 12; ++j) {
-        v[j] -= mean;
-        sq = __builtin_fmaf(v[j], v[j], sq);
+      for (int j = 0; j < 6; ++j) {
+        w[j] -= (f2)(mean);
+        q2 = __builtin_elementwise_fma(w[j], w[j], q2);
       }
-      sq += __shfl_xor(sq, 16, 64);
-      sq += __shfl_xor(sq, 32, 64);
-      const float rstd = __builtin_amdgcn_rsqf(sq * (1.0f / 48.0f) + 1e-5f);
+      const float rstd = __builtin_amdgcn_rsqf(quad_sum(q2.x + q2.y) * (1.0f / 48.0f) + 1e-5f);
+      float v[12];
 #pragma unroll
-      for (int j = 0; j < 12; ++j) v[j] *= rstd;
+      for (int j = 0; j < 6; ++j) {
+        w[j] *= (f2)(rstd);
+        v[2 * j] = w[j].x;
+        v[2 * j + 1] = w[j].y;
+      }
       f4 m, u;
       ff2_48(fmsg, fedge, v, lane, m, u);
       if (edge_res) u += ea;
@@ -411,15 +442,10 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
   for (int j = 0; j < 4; ++j) {
     const int64_t i = n0 + (wave + 4 * j) * 16 + it;
     const f4 a = agg[j];
-    float sum = a.x + a.y + a.z + a.w;
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    const float mean = sum * (1.0f / 16.0f);
+    const float mean = quad_sum((a.x + a.y) + (a.z + a.w)) * (1.0f / 16.0f);
     float v[4] = {a.x - mean, a.y - mean, a.z - mean, a.w - mean};
-    float sq = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
-    sq += __shfl_xor(sq, 16, 64);
-    sq += __shfl_xor(sq, 32, 64);
-    const float rstd = __builtin_amdgcn_rsqf(sq * (1.0f / 16.0f) + 1e-5f);
+    const float sq = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+    const float rstd = __builtin_amdgcn_rsqf(quad_sum(sq) * (1.0f / 16.0f) + 1e-5f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] *= rstd;
     f4 o = ff_tile<4>(fnode, v, lane);
