@@ -255,11 +255,12 @@ __global__ void k_csc_rowstart(int64_t N, int64_t E, const int64_t* __restrict__
 
 // Symmetric, strictly sorted pattern (k_csc_rowstart's check): the CSC slots of destination c
 // are CSR row c's own slots, and the slot of edge e = (r, c) is the position of r in row c --
-// the map is an involution (inv == perm), and slot k's endpoints are (ei[E+k], ei[k]).  Every
+// the slot <-> edge map is an involution (perm, slot -> edge, is its own inverse), and slot k's
+// endpoints are (src, dst) = (ei[E+k], ei[k]).  Every
 // write is therefore at the thread's own index (coalesced); only the search in row c gathers.
 __global__ void k_csc_sym(int64_t E, const int64_t* __restrict__ ei, const int32_t* __restrict__ ptr,
-                          int32_t* __restrict__ perm, int32_t* __restrict__ inv, int32_t* __restrict__ src,
-                          int32_t* __restrict__ dst, int* flag) {
+                          int32_t* __restrict__ perm, int32_t* __restrict__ src, int32_t* __restrict__ dst,
+                          int* flag) {
   for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < E; e += int64_t(gridDim.x) * blockDim.x) {
     const int64_t r = ei[e], c = ei[E + e];
     const int32_t end = ptr[c + 1];
@@ -271,7 +272,6 @@ __global__ void k_csc_sym(int64_t E, const int64_t* __restrict__ ei, const int32
     }
     if (lo >= end || ei[E + lo] != r) atomicOr(flag, 2);
     perm[e] = lo;
-    inv[e] = lo;
     src[e] = int32_t(c);
     dst[e] = int32_t(r);
   }
@@ -280,12 +280,13 @@ __global__ void k_csc_sym(int64_t E, const int64_t* __restrict__ ei, const int32
 // ---------------------------------------------------------------------------
 // Encoders / decoder (16-item MFMA tiles, 4 waves per workgroup, grid-stride over tiles)
 // ---------------------------------------------------------------------------
-// Encoder input layout: K slot q of step s = input feature 4s + q (zero past `fin`).  Inputs
-// are read in their own (coalesced) order; EDGE: the 64-B output row of edge e goes to its CSC
-// slot outidx[e].
+// Encoder input layout: K slot q of step s = input feature 4s + q (zero past `fin`).  Items are
+// visited in output order, so the 64-B output rows are written coalesced; EDGE: CSC slot m reads
+// the (few-float) input row of its edge perm[m] -- a gather from a small, cache-resident array
+// instead of a scatter of 64-B rows into the [E,16] edge state.
 template <bool EDGE>
 __global__ void __launch_bounds__(256) k_encode(int64_t M, int fin, const float* __restrict__ fr,
-                                               const float* __restrict__ in, const int32_t* __restrict__ outidx,
+                                               const float* __restrict__ in, const int32_t* __restrict__ inidx,
                                                float* __restrict__ out) {
   const int lane = threadIdx.x & 63, it = lane & 15, q = lane >> 4;
   const int s1 = (fin + 3) / 4;
@@ -294,19 +295,21 @@ __global__ void __launch_bounds__(256) k_encode(int64_t M, int fin, const float*
     const int64_t m = t * 16 + it;
     const bool valid = m < M;
     const int64_t mm = valid ? m : M - 1;
+    const int64_t irow = EDGE ? int64_t(inidx[mm]) : mm;
     f4 h = ld4(fr + s1 * 64 + lane * 4);
     for (int s = 0; s < s1; ++s) {
       const int f = 4 * s + q;
-      const float v = f < fin ? in[mm * fin + f] : 0.f;
+      const float v = f < fin ? in[irow * fin + f] : 0.f;
       h = mfma(fr[s * 64 + lane], v, h);
     }
     const f4 o = ff_tail(fr, s1, h, lane);
-    const int64_t orow = EDGE ? int64_t(outidx[mm]) : mm;
-    if (valid) st4(out + orow * H + 4 * q, o);
+    if (valid) st4(out + mm * H + 4 * q, o);
   }
 }
 
-// out[e] = edge_dec(cat[e_attr, x[src], x[dst]])  (gnns.py:88-95; original edge order)
+// out[e] = edge_dec(cat[e_attr, x[src], x[dst]])  (gnns.py:88-95; original edge order).  Visits
+// edges e, gathering each 64-B edge-state row from its CSC slot inv[e]: measured faster than
+// visiting slots and scattering the OUT-float results (0.59 vs 0.67 ms at E = 15.2 M).
 template <int OUT>
 __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __restrict__ fr,
                                                  const int64_t* __restrict__ ei, const int32_t* __restrict__ inv,
@@ -564,8 +567,8 @@ static int64_t gnn_weight_count(const lspcg_gnn_desc& d) {
 }
 
 static void gnn_free_ws(lspcg_gnn* g) {
-  for (void* p : {(void*)g->xa, (void*)g->xb, (void*)g->ecsc, (void*)g->ptr, (void*)g->cnt, (void*)g->perm,
-                  (void*)g->inv, (void*)g->src, (void*)g->dst, g->scan_tmp})
+  for (void* p : {(void*)g->xa, (void*)g->xb, (void*)g->ecsc, (void*)g->ptr, (void*)g->cnt, (void*)g->perm, (void*)g->inv,
+                  (void*)g->src, (void*)g->dst, g->scan_tmp})
     (void)hipFree(p);
   g->xa = g->xb = g->ecsc = nullptr;
   g->ptr = g->cnt = g->perm = g->inv = g->src = g->dst = nullptr;
@@ -664,8 +667,8 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
   LSPCG_HIP(hipMemsetAsync(g->flag, 0, sizeof(int), st));
   hipLaunchKernelGGL(k_csc_rowstart, dim3(egrid(std::max(N + 1, E))), dim3(kThreads), 0, st, N, E, edge_index, g->ptr,
                      g->flag);
-  hipLaunchKernelGGL(k_csc_sym, dim3(egrid(E)), dim3(kThreads), 0, st, E, edge_index, g->ptr, g->perm, g->inv, g->src,
-                     g->dst, g->flag);
+  hipLaunchKernelGGL(k_csc_sym, dim3(egrid(E)), dim3(kThreads), 0, st, E, edge_index, g->ptr, g->perm, g->src, g->dst,
+                     g->flag);
   int hflag = 0;
   LSPCG_HIP(hipMemcpyAsync(&hflag, g->flag, sizeof(int), hipMemcpyDeviceToHost, st));
   LSPCG_HIP(hipStreamSynchronize(st));
@@ -679,11 +682,12 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
     hipLaunchKernelGGL(k_csc_sort, dim3(egrid(N)), dim3(kThreads), 0, st, N, edge_index, E, g->ptr, g->perm, g->inv,
                        g->src, g->dst);
   }
+  const int32_t* inv = hflag ? g->inv : g->perm;  // edge -> CSC slot (the involution is its own inverse)
   // encoders
   hipLaunchKernelGGL(k_encode<false>, dim3(tgrid(N)), dim3(256), 0, st, N, d.node_in, g->frag + g->o_node_enc, x,
                      static_cast<const int32_t*>(nullptr), g->xa);
   hipLaunchKernelGGL(k_encode<true>, dim3(tgrid(E)), dim3(256), 0, st, E, d.edge_in, g->frag + g->o_edge_enc,
-                     edge_attr, g->inv, g->ecsc);
+                     edge_attr, g->perm, g->ecsc);
   // message passing
   float* xc = g->xa;
   float* xn = g->xb;
@@ -696,11 +700,11 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
   // decoder
   const float* fd = g->frag + g->o_dec;
   if (d.edge_out == 1)
-    hipLaunchKernelGGL(k_edge_dec<1>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, g->inv, g->ecsc, xc, out);
+    hipLaunchKernelGGL(k_edge_dec<1>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, inv, g->ecsc, xc, out);
   else if (d.edge_out == 4)
-    hipLaunchKernelGGL(k_edge_dec<4>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, g->inv, g->ecsc, xc, out);
+    hipLaunchKernelGGL(k_edge_dec<4>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, inv, g->ecsc, xc, out);
   else
-    hipLaunchKernelGGL(k_edge_dec<9>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, g->inv, g->ecsc, xc, out);
+    hipLaunchKernelGGL(k_edge_dec<9>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, inv, g->ecsc, xc, out);
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
