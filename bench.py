@@ -156,7 +156,7 @@ def main():
     for _ in range(2):
         L, gnn_dt = ws.inference_step(dev_sample)  # warm the GNN (infer.py:270-275)
     gnn_times = []
-    for _ in range(3):
+    for _ in range(5):
         L, gnn_dt = ws.inference_step(dev_sample)
         gnn_times.append(gnn_dt)
     A = ws.system_matrix(dev_sample)

@@ -75,6 +75,9 @@ class SimpleInferenceWorkspace:
     def inference_step(self, sample: GraphSample, time_beg: Optional[float] = None, block_output: Optional[bool] = None,
                        return_scipy: bool = False) -> Tuple[Union[DeviceMatrix, sp.csr_matrix], float]:
         s = sample if sample.x.is_cuda else sample.to(self.device)
+        # the reference's clock starts with no device work pending (its to_csr_cpu is synchronous);
+        # here a previous call's assembly may still be queued
+        torch.cuda.synchronize(s.x.device)
         time_beg = time()
         boo = self.forward(s.x, s.edge_index, s.edge_attr)
         torch.cuda.synchronize(boo.device)
@@ -94,6 +97,9 @@ class ScaledInferenceWorkspace(SimpleInferenceWorkspace):
     def inference_step(self, sample: GraphSample, time_beg: Optional[float] = None, block_output: Optional[bool] = None,
                        return_scipy: bool = False):
         s = sample if sample.x.is_cuda else sample.to(self.device)
+        # the reference's clock starts with no device work pending (its to_csr_cpu is synchronous);
+        # here a previous call's assembly may still be queued
+        torch.cuda.synchronize(s.x.device)
         time_beg = time()
         boo = self.forward(s.x, s.edge_index, s.edge_attr)
         torch.cuda.synchronize(boo.device)
