@@ -209,7 +209,7 @@ def main():
               "fp64 values), bit-exact scipy order" if kind else
               "k_spmv<double,1> staged scalar CSR SpMV of A, bit-exact scipy order")
     alg = spmv_bytes(n, nnz_a)
-    pcg_spmv = pcg_loop_spmv(A, p, q, args.spmv_reps)
+    pcg_spmv = pcg_loop_spmv(A, p, q, args.spmv_reps) if A.block_size == 1 else None  # BSR: scalar SELL views only
     gbs_cold = alg / (ms_cold * 1e-3) / 1e9
     gbs_warm = alg / (ms_warm * 1e-3) / 1e9
     it_per_solve = iters[-1]

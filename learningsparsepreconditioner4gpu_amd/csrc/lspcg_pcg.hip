@@ -740,10 +740,10 @@ struct lspcg_solver {
   int gsz_l = 1, ng_l = 1, gsz_a = 1, ng_a = 1;  // group size / count of the KB and KC launches
   bool allow_fused = false;  // LSPCG_PCG_FUSED=1 selects it (measured slower: two gathers per entry)
   PcgState* S = nullptr;
-  PcgState* hS = nullptr;  // pinned host mirror
+  PcgState* hS = nullptr;  // pinned host mirrors [2] (poll slots)
   double* partials = nullptr;
   unsigned* ticket = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_poll = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_t0 = nullptr, ev_t1 = nullptr, ev_poll = nullptr, ev_poll2 = nullptr;
   std::map<int, hipGraphExec_t> graphs;
   std::map<int, hipGraph_t> graph_defs;
   // iteration views of A, L, Lᵀ: compact fp32 values when lossless, one shared index
@@ -1161,7 +1161,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
     LSPCG_HIP(hipMemsetAsync(*v, 0, vb, s->stream));
   }
   LSPCG_HIP(hipMalloc(&s->S, sizeof(PcgState)));
-  LSPCG_HIP(hipHostMalloc(&s->hS, sizeof(PcgState), hipHostMallocDefault));
+  LSPCG_HIP(hipHostMalloc(&s->hS, 2 * sizeof(PcgState), hipHostMallocDefault));
   // partial slots: largest grid of any reducing launch (SpMV grid of A / L, element grid) x 2 dots
   // (n/255 bounds the grid of a CSR (256 rows/WG) and a BSR3 (85 block rows/WG) launch,
   // so L / Lᵀ in either layout fit too)
@@ -1172,7 +1172,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   LSPCG_HIP(hipMalloc(&s->groups, sizeof(double) * 4096 * 2 * 3));
   LSPCG_HIP(hipMemsetAsync(s->groups, 0, sizeof(double) * 4096 * 2 * 3, s->stream));
   LSPCG_HIP(hipMemsetAsync(s->S, 0, sizeof(PcgState), s->stream));
-  for (hipEvent_t* e : {&s->ev_in, &s->ev_out, &s->ev_poll}) LSPCG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (hipEvent_t* e : {&s->ev_in, &s->ev_out, &s->ev_poll, &s->ev_poll2}) LSPCG_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   LSPCG_HIP(hipEventCreate(&s->ev_t0));
   LSPCG_HIP(hipEventCreate(&s->ev_t1));
   LSPCG_HIP(hipMalloc(&s->flag, sizeof(int)));
@@ -1305,40 +1305,75 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   int rc = s->dtype == LSPCG_F64 ? enqueue_init<double>(s, st) : enqueue_init<float>(s, st);
   if (rc) return rc;
 
-  // Poll loop: chunk sizes follow the observed residual decay so that at most a few
-  // early-exit launches trail the converged iteration.
-  int64_t last_it = 0;
-  double last_rr = -1.0;
+  // Poll loop, one chunk ahead: the state copied after chunk k is read while chunk k+1 runs, so
+  // the GPU does not idle through the host round trip.  Chunk sizes follow the observed residual
+  // decay minus the iterations already in flight, so that at most a few early-exit launches trail
+  // the converged iteration (every launch is predicated on the device `done` flag).
   // graphs hold <= ~4096 nodes (IC: one launch per level of each triangular solve)
   const int kpi = s->precond == LSPCG_PRECOND_IC ? s->levL.nlev + s->levU.nlev + 4 : 5;
   const int max_chunk = std::max(1, std::min(32, 4096 / kpi));
+  PcgState* const hs[2] = {s->hS, s->hS + 1};
+  const hipEvent_t evp[2] = {s->ev_poll, s->ev_poll2};
+  int64_t queued[2] = {0, 0};  // iterations launched after each outstanding poll
+  int head = 0, npend = 0;     // oldest outstanding poll slot, number outstanding (<= 2)
+  auto post = [&]() -> int {   // a state copy + event after everything enqueued so far
+    const int k = (head + npend) & 1;
+    LSPCG_HIP(hipMemcpyAsync(hs[k], s->S, sizeof(PcgState), hipMemcpyDeviceToHost, st));
+    LSPCG_HIP(hipEventRecord(evp[k], st));
+    queued[k] = 0;
+    ++npend;
+    return LSPCG_OK;
+  };
+  auto launch = [&](int c) -> int {
+    hipGraphExec_t ex = nullptr;
+    int r = get_graph(s, c, &ex);
+    if (r) return r;
+    LSPCG_HIP(hipGraphLaunch(ex, st));
+    for (int j = 0; j < npend; ++j) queued[(head + j) & 1] += c;
+    return post();
+  };
+  rc = post();
+  if (!rc) rc = launch(std::min(4, max_chunk));
+  if (rc) return rc;
+  int64_t last_it = 0;
+  double last_rr = -1.0;
   int chunk = std::min(4, max_chunk);
+  PcgState cur{};
   for (;;) {
-    LSPCG_HIP(hipMemcpyAsync(s->hS, s->S, sizeof(PcgState), hipMemcpyDeviceToHost, st));
-    LSPCG_HIP(hipEventRecord(s->ev_poll, st));
-    LSPCG_HIP(hipEventSynchronize(s->ev_poll));
-    const PcgState cur = *s->hS;
+    LSPCG_HIP(hipEventSynchronize(evp[head]));
+    cur = *hs[head];
+    const int64_t inflight = queued[head];
+    head ^= 1;
+    --npend;
     if (cur.done) break;  // ProCheck sets done (convergence, max_iter or a non-finite residual)
+    int64_t rem = -1;     // predicted iterations still needed after this state
     if (last_rr > 0 && cur.iter > last_it && cur.rr > 0 && cur.rr < last_rr) {
       const double rate = std::log(cur.rr / last_rr) / double(cur.iter - last_it);  // < 0
       const double need = std::log((cur.atol * cur.atol) / cur.rr) / rate;
-      int64_t rem = need > 0 ? int64_t(std::ceil(need)) : 1;
+      rem = need > 0 ? int64_t(std::ceil(need)) : 1;
       rem = std::max<int64_t>(1, std::min<int64_t>(rem, max_iter - cur.iter));
+    }
+    if (cur.iter > last_it || last_rr < 0) {
+      last_it = cur.iter;
+      last_rr = cur.rr;
+    }
+    if (rem >= 0) {
+      const int64_t more = rem - inflight;
+      if (more <= 0) {
+        if (npend == 0) rc = launch(1);  // predicted to converge in flight; nothing in flight
+        if (rc) return rc;
+        continue;
+      }
       int c = 1;
-      while (c * 2 <= rem && c < max_chunk) c *= 2;
+      while (c * 2 <= more && c < max_chunk) c *= 2;
       chunk = c;
-    } else if (last_rr > 0) {
+    } else {
       chunk = std::min(max_chunk, chunk * 2);
     }
-    chunk = std::min(chunk, max_chunk);
-    last_it = cur.iter;
-    last_rr = cur.rr;
-    hipGraphExec_t ex = nullptr;
-    rc = get_graph(s, chunk, &ex);
+    rc = launch(std::min(chunk, max_chunk));
     if (rc) return rc;
-    LSPCG_HIP(hipGraphLaunch(ex, st));
   }
-  const PcgState fin = *s->hS;
+  const PcgState fin = cur;  // later (early-exit) launches leave the state unchanged
   rc = s->dtype == LSPCG_F64 ? enqueue_fixup<double>(s, st) : enqueue_fixup<float>(s, st);
   if (rc) return rc;
   const void* src = (fin.bb == 0.0) ? s->b : s->x;  // scipy returns b when ‖b‖ = 0
@@ -1372,7 +1407,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipFree(s->partials);
   (void)hipFree(s->ticket);
   (void)hipFree(s->groups);
-  for (hipEvent_t e : {s->ev_in, s->ev_out, s->ev_poll, s->ev_t0, s->ev_t1}) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {s->ev_in, s->ev_out, s->ev_poll, s->ev_poll2, s->ev_t0, s->ev_t1}) (void)hipEventDestroy(e);
   if (s->LT) lspcg_mat_destroy(s->LT);
   if (s->icL) lspcg_mat_destroy(s->icL);
   if (s->icU) lspcg_mat_destroy(s->icU);
