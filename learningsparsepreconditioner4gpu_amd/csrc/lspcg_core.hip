@@ -81,29 +81,48 @@ __global__ void k_sort_gather_transpose(int64_t nb, const int32_t* __restrict__ 
 }
 
 // Symmetric-pattern transpose: Aᵀ has A's pattern, and the entry (r, j) of Aᵀ is A's entry
-// (j, r), found by binary search in row j.  One thread per row, deterministic, no atomics;
-// flag <- 1 if some (j, r) is missing (pattern not symmetric: the general path runs instead).
+// (j, r), found by binary search in row j.  Deterministic, no atomics; flag <- 1 if some (j, r)
+// is missing (pattern not symmetric: the general path runs instead).  A workgroup owns 256 rows
+// and visits their entries entry-parallel, so the column reads and the output writes are
+// coalesced; an entry's row comes from a search in the LDS copy of those rows' rowptr.
+constexpr int kTrRows = 256;
 template <typename T, int BS>
-__global__ void k_transpose_sym(int64_t nb, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
-                                const T* __restrict__ vals, T* __restrict__ tvals, int* __restrict__ flag) {
-  for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < nb; r += int64_t(gridDim.x) * blockDim.x) {
-    for (int32_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
-      const int32_t j = colind[k];
-      int32_t lo = rowptr[j], hi = rowptr[j + 1];
+__global__ void __launch_bounds__(kTrRows) k_transpose_sym(int64_t nb, const int32_t* __restrict__ rowptr,
+                                                          const int32_t* __restrict__ colind,
+                                                          const T* __restrict__ vals, T* __restrict__ tvals,
+                                                          int* __restrict__ flag) {
+  __shared__ int32_t rp[kTrRows + 1];
+  for (int64_t r0 = int64_t(blockIdx.x) * kTrRows; r0 < nb; r0 += int64_t(gridDim.x) * kTrRows) {
+    const int cnt = int(nb - r0 < kTrRows ? nb - r0 : kTrRows);
+    __syncthreads();
+    for (int t = threadIdx.x; t <= cnt; t += blockDim.x) rp[t] = rowptr[r0 + t];
+    __syncthreads();
+    for (int32_t k = rp[0] + int32_t(threadIdx.x); k < rp[cnt]; k += int32_t(blockDim.x)) {
+      int lo = 0, hi = cnt - 1;  // the row: largest t with rp[t] <= k (skips empty rows)
       while (lo < hi) {
-        const int32_t mid = (lo + hi) >> 1;
-        if (colind[mid] < r) lo = mid + 1; else hi = mid;
+        const int mid = (lo + hi + 1) >> 1;
+        if (rp[mid] <= k) lo = mid;
+        else hi = mid - 1;
       }
-      if (lo >= rowptr[j + 1] || colind[lo] != r) {
+      const int32_t r = int32_t(r0 + lo);
+      const int32_t j = colind[k];
+      int32_t a = rowptr[j], e = rowptr[j + 1];
+      const int32_t end = e;
+      while (a < e) {
+        const int32_t mid = (a + e) >> 1;
+        if (colind[mid] < r) a = mid + 1;
+        else e = mid;
+      }
+      if (a >= end || colind[a] != r) {
         atomicOr(flag, 1);
         continue;
       }
-      const T* src = vals + int64_t(lo) * BS * BS;
+      const T* src = vals + int64_t(a) * BS * BS;
       T* dst = tvals + int64_t(k) * BS * BS;
 #pragma unroll
-      for (int a = 0; a < BS; ++a)
+      for (int p = 0; p < BS; ++p)
 #pragma unroll
-        for (int b = 0; b < BS; ++b) dst[a * BS + b] = src[b * BS + a];
+        for (int q = 0; q < BS; ++q) dst[p * BS + q] = src[q * BS + p];
     }
   }
 }
@@ -351,7 +370,7 @@ int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out) {
     if (e == hipSuccess && A->nnzb)
       e = hipMemcpyAsync(Tm->colind, A->colind, sizeof(int32_t) * A->nnzb, hipMemcpyDeviceToDevice, st);
     if (e == hipSuccess && A->nb) {
-      const dim3 g(grid_for(A->nb)), b(kThreads);
+      const dim3 g(unsigned(std::min<int64_t>((A->nb + kTrRows - 1) / kTrRows, 65535))), b(kTrRows);
       if (A->dtype == LSPCG_F64) {
         if (A->block_size == 1)
           hipLaunchKernelGGL((k_transpose_sym<double, 1>), g, b, 0, st, A->nb, A->rowptr, A->colind,

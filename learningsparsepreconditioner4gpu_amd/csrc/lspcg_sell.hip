@@ -21,24 +21,33 @@ __global__ void k_sell_len(int64_t n, int64_t ns, const int32_t* __restrict__ ro
   if (lane == 0) cnt[s] = (len + 3) >> 2;
 }
 
-// one thread per row: scatter the row's columns (col32 / col16, whichever is non-null) and,
-// if src != nullptr, values into the slice layout; padding slots get value 0 and column = the
-// -1 (col32) or kSellPad16 (col16)
+// Slot-parallel fill: one workgroup per slice, threads over the slice's 256·G destination slots
+// in storage order (coalesced writes; the 4 slots of a row group read 4 consecutive entries of
+// that row).  Slot p -> row 64s + (p % 256) / 4, entry 4 (p / 256) + p % 4.  Writes column
+// indices (col32 / col16, whichever is non-null) and, if dst != nullptr, values; slots past a
+// row's end (or of rows >= n) get value 0 and the padding column (-1 / kSellPad16), so every
+// slot of the view is written.
 template <typename VS, typename VD>
-__global__ void k_sell_fill(int64_t n, const int32_t* __restrict__ gp, const int32_t* __restrict__ rowptr,
-                            const int32_t* __restrict__ colind, const VS* __restrict__ src,
-                            int32_t* __restrict__ col32, int16_t* __restrict__ col16, VD* __restrict__ dst) {
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t s = i / kSellC;
-    const int r = int(i % kSellC);
-    const int32_t b = rowptr[i], len = rowptr[i + 1] - b;
-    const int32_t slots = 4 * (gp[s + 1] - gp[s]);
-    const int64_t base = 256 * int64_t(gp[s]) + 4 * r;
-    for (int32_t k = 0; k < slots; ++k) {
-      const int64_t pos = base + 256 * int64_t(k >> 2) + (k & 3);
-      if (col32) col32[pos] = k < len ? colind[b + k] : int32_t(-1);
-      if (col16) col16[pos] = k < len ? int16_t(colind[b + k] - int32_t(s * kSellC)) : kSellPad16;
-      if (dst) dst[pos] = k < len ? VD(src[b + k]) : VD(0);
+__global__ void __launch_bounds__(256) k_sell_fill(int64_t n, int64_t ns, const int32_t* __restrict__ gp,
+                                                   const int32_t* __restrict__ rowptr,
+                                                   const int32_t* __restrict__ colind, const VS* __restrict__ src,
+                                                   int32_t* __restrict__ col32, int16_t* __restrict__ col16,
+                                                   VD* __restrict__ dst) {
+  for (int64_t s = blockIdx.x; s < ns; s += gridDim.x) {
+    const int64_t base = 256 * int64_t(gp[s]);
+    const int32_t slots = 256 * (gp[s + 1] - gp[s]);
+    for (int32_t p = threadIdx.x; p < slots; p += blockDim.x) {
+      const int64_t i = s * kSellC + ((p & 255) >> 2);
+      const int32_t k = 4 * (p >> 8) + (p & 3);
+      int32_t b = 0, len = 0;
+      if (i < n) {
+        b = rowptr[i];
+        len = rowptr[i + 1] - b;
+      }
+      const bool real = k < len;
+      if (col32) col32[base + p] = real ? colind[b + k] : int32_t(-1);
+      if (col16) col16[base + p] = real ? int16_t(colind[b + k] - int32_t(s * kSellC)) : kSellPad16;
+      if (dst) dst[base + p] = real ? VD(src[b + k]) : VD(0);
     }
   }
 }
@@ -55,6 +64,8 @@ __global__ void k_sell_fit16(int64_t n, const int32_t* __restrict__ rowptr, cons
     }
   }
 }
+
+static int slice_grid(int64_t ns) { return int(std::max<int64_t>(1, std::min<int64_t>(ns, 16384))); }
 
 static int fill_grid(int64_t n) {
   return int(std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, kElemBlocksMax)));
@@ -111,14 +122,12 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
     if (e != hipSuccess) return fail(e);
   }
   P.col_bits = fit == 0 ? 16 : 32;
-  // zero first: slots of the lanes past row n-1 in the last slice are never written by the
-  // fill and would otherwise hold garbage columns (the kernel gathers them, masked at the add)
+  // the fill writes every slot (padding included)
   const size_t cbytes = size_t(P.col_bits / 8) * size_t(std::max<int64_t>(256 * P.groups, 1));
   e = hipMalloc(&P.col, cbytes);
-  if (e == hipSuccess) e = hipMemsetAsync(P.col, 0, cbytes, st);
   if (e != hipSuccess) return fail(e);
-  if (n)
-    hipLaunchKernelGGL((k_sell_fill<float, float>), dim3(fill_grid(n)), dim3(kThreads), 0, st, n, P.gp, rowptr, colind,
+  if (P.ns)
+    hipLaunchKernelGGL((k_sell_fill<float, float>), dim3(slice_grid(P.ns)), dim3(256), 0, st, n, P.ns, P.gp, rowptr, colind,
                        static_cast<const float*>(nullptr), P.col_bits == 32 ? static_cast<int32_t*>(P.col) : nullptr,
                        P.col_bits == 16 ? static_cast<int16_t*>(P.col) : nullptr, static_cast<float*>(nullptr));
   e = hipGetLastError();
@@ -132,20 +141,19 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
   const size_t es = dst_dtype == LSPCG_F32 ? 4 : 8;
   void* v = nullptr;
   LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(256 * P.groups, 1)));
-  LSPCG_HIP(hipMemsetAsync(v, 0, es * std::max<int64_t>(256 * P.groups, 1), st));
-  const dim3 g(fill_grid(P.n)), b(kThreads);
-  if (P.n) {
+  const dim3 g(slice_grid(P.ns)), b(256);
+  if (P.ns) {
     if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F64)
-      hipLaunchKernelGGL((k_sell_fill<double, double>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
+      hipLaunchKernelGGL((k_sell_fill<double, double>), g, b, 0, st, P.n, P.ns, P.gp, P.rowptr, colind,
                          static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr), static_cast<double*>(v));
     else if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F32)
-      hipLaunchKernelGGL((k_sell_fill<double, float>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
+      hipLaunchKernelGGL((k_sell_fill<double, float>), g, b, 0, st, P.n, P.ns, P.gp, P.rowptr, colind,
                          static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr), static_cast<float*>(v));
     else if (src_dtype == LSPCG_F32 && dst_dtype == LSPCG_F32)
-      hipLaunchKernelGGL((k_sell_fill<float, float>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
+      hipLaunchKernelGGL((k_sell_fill<float, float>), g, b, 0, st, P.n, P.ns, P.gp, P.rowptr, colind,
                          static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr), static_cast<float*>(v));
     else
-      hipLaunchKernelGGL((k_sell_fill<float, double>), g, b, 0, st, P.n, P.gp, P.rowptr, colind,
+      hipLaunchKernelGGL((k_sell_fill<float, double>), g, b, 0, st, P.n, P.ns, P.gp, P.rowptr, colind,
                          static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr), static_cast<double*>(v));
   }
   hipError_t e = hipGetLastError();
