@@ -354,8 +354,13 @@ int lspcg_mat_copy_out(const lspcg_mat* A, int32_t* indptr, int32_t* indices, vo
   return LSPCG_OK;
 }
 
-int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out) {
+int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out) { return lspcg::mat_transpose(A, out, nullptr); }
+
+}  // extern "C"
+
+int lspcg::mat_transpose(const lspcg_mat* A, lspcg_mat** out, bool* same_pattern) {
   LSPCG_CHECK(A && out, LSPCG_ERR_ARG, "transpose: NULL");
+  if (same_pattern) *same_pattern = false;
   lspcg_ctx* ctx = A->ctx;
   hipStream_t st = ctx->stream;
   lspcg_mat* Tm = nullptr;
@@ -397,6 +402,7 @@ int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out) {
       return LSPCG_ERR_HIP;
     }
     if (h == 0) {
+      if (same_pattern) *same_pattern = true;
       *out = Tm;
       return LSPCG_OK;
     }
@@ -446,6 +452,8 @@ int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out) {
   *out = Tm;
   return LSPCG_OK;
 }
+
+extern "C" {
 
 int lspcg_mat_diagonal(const lspcg_mat* A, void* d) {
   LSPCG_CHECK(A && d, LSPCG_ERR_ARG, "diagonal: NULL");

@@ -349,6 +349,10 @@ namespace lspcg {
 int mat_alloc_entries(lspcg_mat* m, int64_t nnzb);
 // New handle with rowptr[nb+1] and padded entry arrays (contents uninitialised).
 int mat_alloc(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, int dtype, lspcg_mat** out);
+// lspcg_mat_transpose; *same_pattern (optional) <- the symmetric-pattern path ran, i.e. Aᵀ has
+// A's rowptr / colind and its values are a permutation of A's
+int mat_transpose(const lspcg_mat* A, lspcg_mat** out, bool* same_pattern);
+
 }  // namespace lspcg
 
 // ---------------------------------------------------------------------------

@@ -708,7 +708,7 @@ __global__ void k_to_f32(int64_t n, const double* __restrict__ v, float* __restr
 __global__ void k_i32_neq(int64_t n, const int32_t* __restrict__ a, const int32_t* __restrict__ b,
                           int* __restrict__ flag) {
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
-    if (a[i] != b[i]) atomicOr(flag, 1);
+    if (a[i] != b[i]) atomicOr(flag, 2);
 }
 
 static int elem_grid(int64_t n) {  // 2 elements per lane, >= 2 pairs per lane, <= 1024 partials
@@ -775,7 +775,7 @@ static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view);
 
 static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   hipStream_t st = s->ctx->stream;
-  LSPCG_HIP(hipStreamSynchronize(s->stream));
+  if (s->sv[w] || s->spat[w].gp || s->xrow[w]) LSPCG_HIP(hipStreamSynchronize(s->stream));  // a solve may use them
   (void)hipFree(s->sv[w]);
   s->sv[w] = nullptr;
   s->spat[w].release();
@@ -797,7 +797,6 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   }
   const int vd = view->storage_dtype();
   if (int rc = sell_fill_values(*P, view->colind, view->vals, vd, vd, st, &s->sv[w])) return rc;
-  LSPCG_HIP(hipStreamSynchronize(st));
   s->svd[w] = vd;
   s->sp[w] = P;
   return LSPCG_OK;
@@ -929,7 +928,12 @@ static int flag_run(lspcg_solver* s, hipStream_t st, int* out) {
 }
 
 // view <- M; compact fp64 values to fp32 when exact; share `base`'s index arrays when equal.
-static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const lspcg_mat* base, void** own) {
+// Both checks run before ONE host read of the flag (bit 0: some value not fp32-exact, bit 1:
+// index arrays differ).  `known` (optional) supplies that flag instead -- Lᵀ from the
+// symmetric-pattern transpose has L's pattern and a permutation of L's values.  Returns the
+// flag in *flag_out (optional).
+static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const lspcg_mat* base, void** own,
+                     const int* known = nullptr, int* flag_out = nullptr) {
   hipStream_t st = s->ctx->stream;
   if (*own) {
     LSPCG_HIP(hipStreamSynchronize(s->stream));
@@ -938,37 +942,43 @@ static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const
   }
   *view = *M;
   const int64_t ne = M->nnzb * M->block_size * M->block_size;
-  int f = 0;
-  if (s->compact && M->dtype == LSPCG_F64 && M->storage_dtype() == LSPCG_F64 && ne > 0) {
+  const bool try_compact = s->compact && M->dtype == LSPCG_F64 && M->storage_dtype() == LSPCG_F64 && ne > 0;
+  const bool try_share = base && base != M && base->nb == M->nb && base->nnzb == M->nnzb &&
+                         base->block_size == M->block_size;
+  int f = 3;
+  if (known) {
+    f = *known;
+  } else if (try_compact || try_share) {
     LSPCG_HIP(hipMemsetAsync(s->flag, 0, sizeof(int), st));
-    hipLaunchKernelGGL(k_f32_inexact, dim3(elem_grid(ne)), dim3(kThreads), 0, st, ne,
-                       static_cast<const double*>(M->vals), s->flag);
-    if (int rc = flag_run(s, st, &f)) return rc;
-    if (!f) {
-      float* v = nullptr;
-      LSPCG_HIP(hipMalloc(&v, sizeof(float) * (ne + kEntryPad)));
-      *own = v;
-      LSPCG_HIP(hipMemsetAsync(v + ne, 0, sizeof(float) * kEntryPad, st));
-      hipLaunchKernelGGL(k_to_f32, dim3(elem_grid(ne)), dim3(kThreads), 0, st, ne,
-                         static_cast<const double*>(M->vals), v);
-      view->vals = v;
-      view->val_dtype = LSPCG_F32;
+    if (try_compact)
+      hipLaunchKernelGGL(k_f32_inexact, dim3(elem_grid(ne)), dim3(kThreads), 0, st, ne,
+                         static_cast<const double*>(M->vals), s->flag);
+    if (try_share) {
+      hipLaunchKernelGGL(k_i32_neq, dim3(elem_grid(M->nb + 1)), dim3(kThreads), 0, st, M->nb + 1, M->rowptr,
+                         base->rowptr, s->flag);
+      if (M->nnzb)
+        hipLaunchKernelGGL(k_i32_neq, dim3(elem_grid(M->nnzb)), dim3(kThreads), 0, st, M->nnzb, M->colind,
+                           base->colind, s->flag);
     }
-  }
-  if (base && base != M && base->nb == M->nb && base->nnzb == M->nnzb && base->block_size == M->block_size) {
-    LSPCG_HIP(hipMemsetAsync(s->flag, 0, sizeof(int), st));
-    hipLaunchKernelGGL(k_i32_neq, dim3(elem_grid(M->nb + 1)), dim3(kThreads), 0, st, M->nb + 1, M->rowptr,
-                       base->rowptr, s->flag);
-    if (M->nnzb)
-      hipLaunchKernelGGL(k_i32_neq, dim3(elem_grid(M->nnzb)), dim3(kThreads), 0, st, M->nnzb, M->colind,
-                         base->colind, s->flag);
     if (int rc = flag_run(s, st, &f)) return rc;
-    if (!f) {
-      view->rowptr = base->rowptr;
-      view->colind = base->colind;
-    }
+    if (!try_compact) f |= 1;
+    if (!try_share) f |= 2;
   }
-  LSPCG_HIP(hipStreamSynchronize(st));
+  if (flag_out) *flag_out = f;
+  if (try_compact && !(f & 1)) {
+    float* v = nullptr;
+    LSPCG_HIP(hipMalloc(&v, sizeof(float) * (ne + kEntryPad)));
+    *own = v;
+    LSPCG_HIP(hipMemsetAsync(v + ne, 0, sizeof(float) * kEntryPad, st));
+    hipLaunchKernelGGL(k_to_f32, dim3(elem_grid(ne)), dim3(kThreads), 0, st, ne, static_cast<const double*>(M->vals), v);
+    view->vals = v;
+    view->val_dtype = LSPCG_F32;
+  }
+  if (try_share && !(f & 2)) {
+    view->rowptr = base->rowptr;
+    view->colind = base->colind;
+  }
+  LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
 
@@ -1208,14 +1218,16 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     lspcg_mat_destroy(s->LT);
     s->LT = nullptr;
   }
-  int rc = lspcg_mat_transpose(L, &s->LT);
+  bool lt_same = false;
+  int rc = mat_transpose(L, &s->LT, &lt_same);
   if (rc) return rc;
   if (s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) {
     rc = lspcg_mat_diagonal(s->A, s->d);
     if (rc) return rc;
   }
-  if ((rc = make_view(s, L, &s->Lv, &s->Av, &s->own_L))) return rc;
-  if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT))) return rc;
+  int lflag = 3;
+  if ((rc = make_view(s, L, &s->Lv, &s->Av, &s->own_L, nullptr, &lflag))) return rc;
+  if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT, lt_same ? &lflag : nullptr))) return rc;
   if ((rc = build_sell(s, 1, &s->Lv))) return rc;
   if ((rc = build_sell(s, 2, &s->LTv))) return rc;
   // the fused schedule needs SELL views; it gathers twice per entry, which costs more than the two
