@@ -159,6 +159,7 @@ def main():
     for _ in range(5):
         L, gnn_dt = ws.inference_step(dev_sample)
         gnn_times.append(gnn_dt)
+    log(f"rank {rank}: GNN forward ms {[round(t * 1e3, 3) for t in gnn_times]}")
     A = ws.system_matrix(dev_sample)
     n, nnz_a, nnz_l = A.n, A.nnz, L.nnz
     gt = dev_sample.mask.reshape(-1).to(torch.float64)

@@ -12,6 +12,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="kuhn101")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--idle-ms", type=float, default=0.0, help="host sleep before each wall-clock call")
     args = ap.parse_args()
     sys.path.insert(0, ".")
     from learningsparsepreconditioner4gpu_amd import problems as P
@@ -35,6 +36,8 @@ def main():
     walls, pre = [], []
     for _ in range(args.reps):  # host clock around one call from an idle device (inference_step's dt)
         torch.cuda.synchronize()
+        if args.idle_ms:
+            time.sleep(args.idle_ms * 1e-3)
         t0 = time.perf_counter()
         ws.forward(d.x, d.edge_index, d.edge_attr)
         t1 = time.perf_counter()
