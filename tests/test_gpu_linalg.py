@@ -102,6 +102,26 @@ def test_transpose_symmetric_pattern_fast_path(gpu_ctx, bs):
     assert abs(T2 - sp.csr_matrix(A2.T)).max() == 0
 
 
+@pytest.mark.parametrize("bs", [1, 3])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_transpose_symmetric_many_rows_and_empty_rows(gpu_ctx, bs, dtype):
+    # > 256 block rows (several workgroups of the entry-parallel kernel), isolated vertices
+    # (empty rows AND columns keep the pattern symmetric) at a workgroup boundary and inside
+    B = P.kuhn_laplacian(9).tocsr()  # 729 rows
+    keep = np.ones(B.shape[0], dtype=bool)
+    keep[[0, 255, 256, 257, 400, 728]] = False
+    D = sp.diags(keep.astype(np.float64))
+    B = sp.csr_matrix(D @ B @ D)
+    B.eliminate_zeros()
+    if bs == 3:
+        B = sp.csr_matrix(sp.kron(B, np.ones((3, 3))))
+    A = B.copy()
+    A.data = np.random.default_rng(2).normal(size=A.nnz).astype(dtype)
+    A.sort_indices()
+    T = sp.csr_matrix(_dm(A, dtype, bs).transpose().to_scipy())
+    assert abs(T - sp.csr_matrix(A.T)).max() == 0
+
+
 def _solve(A, b, method, L=None, eps=3e-3, rtol=1e-8, dtype=np.float64, max_iter=0):
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
 

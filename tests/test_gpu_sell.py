@@ -45,6 +45,9 @@ MATS = {
                                                                                   + 9000 * k) % 70000)),
                                       shape=(70000, 70000)) for k in range(4)).tocsr(),
     "zero-rows": lambda: sp.csr_matrix((sp.eye(130, format="csr").toarray() * (np.arange(130) % 3 == 0))),
+    # rows 64..191 empty: two whole slices without a single group
+    "empty-slices": lambda: sp.csr_matrix(sp.diags(np.where((np.arange(300) // 64) % 3 == 1, 0.0, 1.5 + np.arange(300)))
+                                          + sp.diags(np.where((np.arange(299) // 64) % 3 == 1, 0.0, -0.25), 1)),
 }
 
 
