@@ -83,8 +83,19 @@ class PreconditionedConjugateGradient:
         ms = C.c_double()
         _lib.call("lspcg_solver_set_spai", self.handle, Ld.handle, float(epsilon), C.byref(ms))
         self._L = Ld  # keep alive: the solver reads it
-        self._spai_key = (id(L), float(epsilon))
+        self._spai_key = self._key(L, epsilon)
         return ms.value / 1e3
+
+    @staticmethod
+    def _key(L, epsilon):
+        """Identity of an installed ext_spai factor: the object itself (held, so its id cannot be
+        reused by another object), its in-place version (DeviceMatrix) and ε."""
+        return (L, getattr(L, "version", None), float(epsilon))
+
+    def _is_installed(self, L, epsilon) -> bool:
+        k = self._spai_key
+        return (k is not None and len(k) == 3 and k[0] is L and k[1] == getattr(L, "version", None)
+                and k[2] == float(epsilon))
 
     def solve(self, b: torch.Tensor, x: torch.Tensor, rtol: float = 1e-6, max_iter: int = 0,
               return_history: bool = False):
@@ -111,7 +122,7 @@ class PreconditionedConjugateGradient:
                 raise ValueError("ext_spai=(L, epsilon) is required for this preconditioner")
             if ext_spai is not None:
                 L, eps = ext_spai
-                if self._spai_key != (id(L), float(eps)):
+                if not self._is_installed(L, eps):
                     prec = self.set_spai(L, eps, block_size=getattr(L, "block_size", 1)
                                          if isinstance(L, DeviceMatrix) else 1)
         tdt = torch.float32 if self.dtype == np.float32 else torch.float64

@@ -79,6 +79,7 @@ class DeviceMatrix:
         n, nnzb, bs, dt = C.c_int64(), C.c_int64(), C.c_int(), C.c_int()
         _lib.call("lspcg_mat_info", handle, C.byref(n), C.byref(nnzb), C.byref(bs), C.byref(dt))
         self.n, self.nnzb, self.block_size, self.dtype_code = n.value, nnzb.value, bs.value, dt.value
+        self.version = 0  # bumped by in-place value changes (solvers key their installed L on it)
 
     # ---- construction
     @classmethod
@@ -191,6 +192,7 @@ class DeviceMatrix:
         d = d.to(device=self.ctx.torch_device, dtype=self.dtype).contiguous()
         assert d.numel() == self.n
         _lib.call("lspcg_mat_scale_columns", self.handle, _ptr(d))
+        self.version += 1
         return self
 
     def matvec(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

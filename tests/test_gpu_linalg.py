@@ -193,3 +193,33 @@ def test_validate_api_raises_when_not_converged(gpu_ctx):
         get_cg_iter_time(A, np.ones(A.shape[0]), rtol=1e-12, max_iter=3, method="none")
     it, prec, solve = get_cg_iter_time(A, np.ones(A.shape[0]), rtol=1e-8, method="none")
     assert it == O.pcg(A, A @ np.ones(A.shape[0]), None, rtol=1e-8, dot="exact")[0]
+
+
+def test_reused_solver_reinstalls_a_changed_factor(gpu_ctx):
+    # the reference calls the same solver with ext_spai=(L, eps) per solve (validate.py:116-117):
+    # a reused solver must pick up a different L object and an in-place change of the same one
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    _, A, mask = _cases.spd_cases()[1]
+    b = A @ (np.ones(A.shape[0]) if mask is None else mask.ravel().astype(np.float64))
+    L1 = _cases.spai_like(A, seed=1)
+    d = np.linspace(0.5, 2.0, A.shape[0])
+    L2 = L1.copy()
+    L2.data = L1.data * d[L1.indices]  # L1 diag(d), same stored order
+    eps = 3e-3
+    want = [O.pcg(A, b, O.spai_operator(L, eps), rtol=1e-8, dot="exact")[1] for L in (L1, L2)]
+    assert np.linalg.norm(want[0] - want[1]) > 1e-10 * np.linalg.norm(want[0])  # distinguishable
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai")
+
+    def run(L, k):
+        x = np.zeros_like(b)
+        s(b.copy(), x, 1e-8, 0, ext_spai=(L, eps))
+        assert np.linalg.norm(x - want[k]) <= 1e-12 * np.linalg.norm(want[k])
+
+    run(L1, 0)
+    run(L2, 1)  # another object
+    Ld = DeviceMatrix.from_scipy(L1)
+    run(Ld, 0)
+    Ld.scale_columns_(torch.from_numpy(d))  # the same object, new values
+    run(Ld, 1)
