@@ -223,3 +223,21 @@ def test_reused_solver_reinstalls_a_changed_factor(gpu_ctx):
     run(Ld, 0)
     Ld.scale_columns_(torch.from_numpy(d))  # the same object, new values
     run(Ld, 1)
+
+
+@pytest.mark.parametrize("max_iter", [1, 4, 37, 64])
+def test_pcg_max_iter_inside_queued_chunks(gpu_ctx, max_iter):
+    # the host keeps one chunk of up to 32 iterations queued ahead of its poll: a max_iter that
+    # falls inside a queued chunk must still stop the iterate and the history at max_iter
+    _, A, mask = _cases.spd_cases()[0]
+    gt = np.ones(A.shape[0]) if mask is None else mask.ravel().astype(np.float64)
+    b = A @ gt
+    L = _cases.spai_like(A, seed=0)
+    it_full = O.pcg(A, b, O.spai_operator(L, 3e-3), rtol=1e-14, dot="exact")[0]
+    assert it_full > max_iter
+    it_o, x_o, h_o = O.pcg(A, b, O.spai_operator(L, 3e-3), rtol=1e-14, max_iter=max_iter, dot="exact")
+    it, x, h = _solve(A, b, "ext_spai", L, 3e-3, rtol=1e-14, max_iter=max_iter)
+    assert it == it_o == max_iter
+    assert len(h) == it + 1
+    np.testing.assert_allclose(h, h_o, rtol=1e-10, atol=0)
+    assert np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
