@@ -1,0 +1,51 @@
+"""Randomised parity sweep: seeded random SPD systems of assorted sizes / row-length spreads,
+random ext_spai factors (fp64 and fp32-exact values, so both the fp64 and the compact fp32-value
+views run), GPU PCG against the oracle with correctly rounded dots: equal iteration count,
+residual history 1e-10, iterate 1e-12.  Sizes cross the SELL slice (64 rows), workgroup (256)
+and group (64 workgroups) boundaries."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import linalg as O
+from tests import _cases
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_spd(n, seed):
+    rng = np.random.default_rng(seed)
+    per_row = rng.integers(1, 12, size=n)  # ragged rows
+    rows = np.repeat(np.arange(n), per_row)
+    span = max(2, int(rng.integers(2, max(3, n // 4))))
+    cols = np.clip(rows + rng.integers(-span, span + 1, size=rows.size), 0, n - 1)
+    B = sp.csr_matrix((rng.normal(size=rows.size), (rows, cols)), shape=(n, n))
+    A = (B + B.T).tocsr()
+    A.data = np.abs(A.data) * -1.0
+    A.setdiag(0.0)
+    A.eliminate_zeros()
+    d = -np.asarray(A.sum(axis=1)).ravel() + rng.uniform(0.01, 1.0, size=n)
+    A = (A + sp.diags(d)).tocsr()
+    A.sort_indices()
+    return A
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_spd_pcg_parity(gpu_ctx, seed):
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.choice([63, 65, 257, 1000, 4097, 17000, 70000]))
+    A = _random_spd(n, seed)
+    L = _cases.spai_like(A, seed=seed)
+    if seed % 2:  # fp32-exact factor values: the compact (fp32-stored) views
+        L.data = L.data.astype(np.float32).astype(np.float64)
+    b = A @ rng.uniform(-1.0, 1.0, size=n)
+    eps = float(rng.choice([1e-3, 3e-3]))
+    it_o, x_o, h_o = O.pcg(A, b, O.spai_operator(L, eps), rtol=1e-8, max_iter=400, dot="exact")
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai")
+    x = np.zeros(n)
+    it, _, _, h = s(b.copy(), x, 1e-8, 400, ext_spai=(L, eps), return_history=True)
+    assert it == it_o, (n, seed, it, it_o)
+    np.testing.assert_allclose(h, h_o, rtol=1e-10, atol=0)
+    assert np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
