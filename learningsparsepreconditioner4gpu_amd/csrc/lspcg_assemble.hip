@@ -59,57 +59,82 @@ __device__ __forceinline__ TO mask_val(const TM* mask, int64_t i) {
   return mask ? TO(mask[i]) : TO(1);
 }
 
-// One scalar row (I, a): walk its blocks in order; COUNT or FILL the kept entries.
+// Scalar CSR output, one 16-lane segment per scalar row (4 rows per wave): the segment walks the
+// row's entries 16 at a time (coalesced edge / block reads), ballots give each kept entry its
+// output slot.  Same result as scalar_row (above): an entry is kept when its masked value (plus
+// 1 - mask on the diagonal) is nonzero; a missing diagonal with 1 - mask != 0 goes right after
+// the kept entries left of it.  COUNT writes the per-row count, FILL the entries at rowptr[i].
 template <typename TO, typename TI, typename TM, int BS, bool FILL>
-__device__ __forceinline__ int32_t scalar_row(const AsmIn<TO, TI, TM>& in, int64_t I, int a, int32_t* __restrict__ cols,
-                                              TO* __restrict__ vals, int32_t pos) {
-  const int64_t i = I * BS + a;
-  const TO mi = mask_val<TO>(in.mask, i);
-  const TO ident = TO(1) - mi;
-  const bool row_masked = mi == TO(0);
-  bool diag_seen = false;
-  int32_t cnt = 0;
-  auto emit = [&](int64_t j, TO v) {
-    if (v != TO(0)) {
-      if constexpr (FILL) {
-        cols[pos + cnt] = int32_t(j);
-        vals[pos + cnt] = v;
-      }
-      ++cnt;
-    }
-  };
-  for (int32_t k = in.bptr[I]; k < in.bptr[I + 1]; ++k) {
-    const int64_t J = in.ei[in.E + k];
-    for (int c = 0; c < BS; ++c) {
-      const int64_t j = J * BS + c;
-      if (!diag_seen && j > i) {  // pattern lacks (i,i): scipy adds ident there
-        emit(i, ident);
-        diag_seen = true;
-      }
-      TO v = TO(in.blocks[(k * BS + a) * BS + c]);
+__global__ void __launch_bounds__(256) k_asm_rows(AsmIn<TO, TI, TM> in, const int32_t* __restrict__ rowptr,
+                                                  int32_t* __restrict__ cnt_out, int32_t* __restrict__ cols,
+                                                  TO* __restrict__ vals) {
+  const int lane = threadIdx.x & 63, sl = lane & 15;
+  const uint64_t segmask = 0xFFFFull << (lane & 48);
+  const uint64_t below_me = (1ull << lane) - 1;
+  const int64_t nrows = in.nb * BS;
+  const int64_t nseg = (int64_t(gridDim.x) * blockDim.x) >> 4;
+  for (int64_t i = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 4; i < nrows; i += nseg) {
+    const int64_t I = i / BS;
+    const int a = int(i - I * BS);
+    const TO mi = mask_val<TO>(in.mask, i);
+    const TO ident = TO(1) - mi;
+    const bool row_masked = mi == TO(0);
+    const int32_t b = in.bptr[I];
+    const int32_t ne = (in.bptr[I + 1] - b) * BS;
+    auto entry = [&](int32_t t, int64_t& j, TO& v) {  // t-th scalar entry of row i (t < ne)
+      const int32_t k = b + t / BS;
+      const int c = t % BS;
+      j = in.ei[in.E + k] * BS + c;
+      v = TO(in.blocks[(int64_t(k) * BS + a) * BS + c]);
       if (row_masked || mask_val<TO>(in.mask, j) == TO(0)) v = TO(0);
-      if (j == i) {
-        v = v + ident;
-        diag_seen = true;
+      if (j == i) v = v + ident;
+    };
+    int32_t kept = 0, below = 0;
+    bool has_diag = false;
+    for (int32_t t0 = 0; t0 < ne; t0 += 16) {
+      const int32_t t = t0 + sl;
+      bool keep = false, low = false, dg = false;
+      if (t < ne) {
+        int64_t j;
+        TO v;
+        entry(t, j, v);
+        keep = v != TO(0);
+        low = keep && j < i;
+        dg = j == i;
       }
-      emit(j, v);
+      kept += __popcll(__ballot(keep) & segmask);
+      below += __popcll(__ballot(low) & segmask);
+      has_diag = has_diag || (__ballot(dg) & segmask) != 0;
+    }
+    const bool ins = !has_diag && ident != TO(0);
+    if constexpr (!FILL) {
+      if (sl == 0) cnt_out[i] = kept + (ins ? 1 : 0);
+    } else {
+      const int32_t pos0 = rowptr[i];
+      if (ins && sl == 0) {
+        cols[pos0 + below] = int32_t(i);
+        vals[pos0 + below] = ident;
+      }
+      int32_t run = 0;
+      for (int32_t t0 = 0; t0 < ne; t0 += 16) {
+        const int32_t t = t0 + sl;
+        bool keep = false;
+        int64_t j = 0;
+        TO v = TO(0);
+        if (t < ne) {
+          entry(t, j, v);
+          keep = v != TO(0);
+        }
+        const uint64_t bk = __ballot(keep) & segmask;
+        if (keep) {
+          const int32_t p = pos0 + run + __popcll(bk & below_me) + ((ins && j > i) ? 1 : 0);
+          cols[p] = int32_t(j);
+          vals[p] = v;
+        }
+        run += __popcll(bk);
+      }
     }
   }
-  if (!diag_seen) emit(i, ident);
-  return cnt;
-}
-
-template <typename TO, typename TI, typename TM, int BS>
-__global__ void k_asm_count(AsmIn<TO, TI, TM> in, int32_t* __restrict__ cnt) {
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < in.nb * BS; i += int64_t(gridDim.x) * blockDim.x)
-    cnt[i] = scalar_row<TO, TI, TM, BS, false>(in, i / BS, int(i % BS), nullptr, nullptr, 0);
-}
-
-template <typename TO, typename TI, typename TM, int BS>
-__global__ void k_asm_fill(AsmIn<TO, TI, TM> in, const int32_t* __restrict__ rowptr, int32_t* __restrict__ cols,
-                           TO* __restrict__ vals) {
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < in.nb * BS; i += int64_t(gridDim.x) * blockDim.x)
-    (void)scalar_row<TO, TI, TM, BS, true>(in, i / BS, int(i % BS), cols, vals, rowptr[i]);
 }
 
 // BSR output: same block pattern; masking applied in place; requires the diagonal block
@@ -142,6 +167,11 @@ __global__ void k_asm_bsr(AsmIn<TO, TI, TM> in, int32_t* __restrict__ rowptr, in
         if (TO(1) - mask_val<TO>(in.mask, I * BS + a) != TO(0)) atomicOr(flag, 4);
     }
   }
+}
+
+static int seg_grid(int64_t rows) {  // 16 threads per row, grid-stride beyond 16384 workgroups
+  int64_t g = (rows * 16 + 255) / 256;
+  return int(g < 1 ? 1 : (g > 16384 ? 16384 : g));
 }
 
 static int grid_of(int64_t n) {
@@ -201,7 +231,8 @@ static int assemble_t(lspcg_ctx* ctx, int64_t nb, int64_t E, const int64_t* ei, 
   int32_t* cnt = nullptr;  // counts in [0,n) (+ a zero at n), scanned into rowptr[0..n]
   LSPCG_HIP(hipMalloc(&cnt, sizeof(int32_t) * (n + 1)));
   std::unique_ptr<void, void (*)(void*)> g3(cnt, [](void* p) { (void)hipFree(p); });
-  hipLaunchKernelGGL((k_asm_count<TO, TI, TM, BS>), dim3(grid_of(n)), dim3(kThreads), 0, st, in, cnt);
+  hipLaunchKernelGGL((k_asm_rows<TO, TI, TM, BS, false>), dim3(seg_grid(n)), dim3(256), 0, st, in,
+                     static_cast<const int32_t*>(nullptr), cnt, static_cast<int32_t*>(nullptr), static_cast<TO*>(nullptr));
   LSPCG_HIP(hipMemsetAsync(cnt + n, 0, sizeof(int32_t), st));
   size_t tmp_bytes = 0;
   LSPCG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, cnt, m->rowptr, int(n + 1), st));
@@ -214,8 +245,8 @@ static int assemble_t(lspcg_ctx* ctx, int64_t nb, int64_t E, const int64_t* ei, 
   (void)hipFree(tmp);
   m->nnzb = nnz;
   if (int rc = mat_alloc_entries(m.get(), nnz)) return rc;
-  hipLaunchKernelGGL((k_asm_fill<TO, TI, TM, BS>), dim3(grid_of(n)), dim3(kThreads), 0, st, in, m->rowptr, m->colind,
-                     static_cast<TO*>(m->vals));
+  hipLaunchKernelGGL((k_asm_rows<TO, TI, TM, BS, true>), dim3(seg_grid(n)), dim3(256), 0, st, in, m->rowptr,
+                     static_cast<int32_t*>(nullptr), m->colind, static_cast<TO*>(m->vals));
   LSPCG_HIP(hipGetLastError());
   LSPCG_HIP(hipStreamSynchronize(st));
   *out = m.release();

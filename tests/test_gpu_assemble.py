@@ -39,10 +39,19 @@ def _inputs(which):
         ei, vals, nb = _graph(A, 1)
         mask = (rng.random((A.shape[0], 1)) > 0.3).astype(np.float64)
         return ei, vals, 1, mask
+    if which == "missing-diag-wide":  # ~40 entries per row: the diagonal lands in a later 16-entry chunk
+        B = sp.random(300, 300, density=0.07, random_state=11, format="csr")
+        A = sp.csr_matrix(B + B.T)
+        A.setdiag(0.0)
+        A.eliminate_zeros()
+        A.sort_indices()
+        ei, vals, nb = _graph(A, 1)
+        mask = (rng.random((A.shape[0], 1)) > 0.2).astype(np.float64)
+        return ei, vals, 1, mask
     raise KeyError(which)
 
 
-@pytest.mark.parametrize("which", ["poisson", "poisson-nomask", "elast", "missing-diag"])
+@pytest.mark.parametrize("which", ["poisson", "poisson-nomask", "elast", "missing-diag", "missing-diag-wide"])
 @pytest.mark.parametrize("out_dtype", [np.float64, np.float32])
 def test_to_csr_bitwise(gpu_ctx, which, out_dtype):
     from learningsparsepreconditioner4gpu_amd.validate import to_csr_cpu
