@@ -238,18 +238,20 @@ __global__ void k_csc_sort(int64_t N, const int64_t* __restrict__ ei, int64_t E,
 // not row-major strictly sorted, bit 2: pattern not symmetric (-> generic path).
 __global__ void k_csc_rowstart(int64_t N, int64_t E, const int64_t* __restrict__ ei, int32_t* __restrict__ ptr,
                                int* flag) {
-  for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r <= N; r += int64_t(gridDim.x) * blockDim.x) {
-    int64_t lo = 0, hi = E;  // first edge with src >= r
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (ei[mid] < r) lo = mid + 1;
-      else hi = mid;
+  // ptr[r] = first edge with src >= r: edge e writes it for the rows src[e-1] < r <= src[e] (and
+  // the virtual edge E for the rows after the last source), one coalesced pass over the sources
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e <= E; e += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t r = e < E ? ei[e] : N;
+    const int64_t rp = e > 0 ? ei[e - 1] : -1;
+    if (e < E) {
+      if (r < 0 || r >= N) atomicOr(flag, 1);
+      if (e + 1 < E) {
+        const int64_t r1 = ei[e + 1];
+        if (r > r1 || (r == r1 && ei[E + e] >= ei[E + e + 1])) atomicOr(flag, 1);
+      }
     }
-    ptr[r] = int32_t(lo);
-  }
-  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e + 1 < E; e += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t r0 = ei[e], r1 = ei[e + 1];
-    if (r0 > r1 || (r0 == r1 && ei[E + e] >= ei[E + e + 1])) atomicOr(flag, 1);
+    const int64_t lo = rp + 1 > 0 ? rp + 1 : 0, hi = r < N ? r : N;
+    for (int64_t rr = lo; rr <= hi; ++rr) ptr[rr] = int32_t(e);
   }
 }
 
@@ -665,7 +667,9 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
   // CSC of the edges by destination
   LSPCG_HIP(hipMemsetAsync(g->cnt, 0, sizeof(int32_t) * (N + 1), st));
   LSPCG_HIP(hipMemsetAsync(g->flag, 0, sizeof(int), st));
-  hipLaunchKernelGGL(k_csc_rowstart, dim3(egrid(std::max(N + 1, E))), dim3(kThreads), 0, st, N, E, edge_index, g->ptr,
+  // unsorted input leaves row starts unwritten (flagged): zeroed, k_csc_sym's searches stay in range
+  LSPCG_HIP(hipMemsetAsync(g->ptr, 0, sizeof(int32_t) * (N + 1), st));
+  hipLaunchKernelGGL(k_csc_rowstart, dim3(egrid(E + 1)), dim3(kThreads), 0, st, N, E, edge_index, g->ptr,
                      g->flag);
   hipLaunchKernelGGL(k_csc_sym, dim3(egrid(E)), dim3(kThreads), 0, st, E, edge_index, g->ptr, g->perm, g->src, g->dst,
                      g->flag);
