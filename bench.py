@@ -91,6 +91,21 @@ def pcg_loop_spmv(A, p, q, reps: int) -> dict:
             "frac_format_cold": fmt / (out["cold"] * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
+def loop_dominant(kernels: dict, A, n: int) -> dict:
+    """The longest launch of the PCG iteration with its format bytes: SELL slots x 6 B (fp32
+    values, 16-bit columns -- the loop's compact views of A, L and Lᵀ, which share one pattern)
+    + the fp64 vectors it reads / writes (one pass each)."""
+    slots = sell_slots(A.to_scipy().indptr) if A.block_size == 1 else None
+    vec = {"KA t=L^T r": 2, "KB z=L t+eps r, rho": 3, "UP p, x": 5, "KC q=A p, pi": 2, "UR r": 3}
+    name = max(kernels, key=kernels.get)
+    out = {"kernel": name, "us": kernels[name] * 1e6, "all_us": {k: v * 1e6 for k, v in kernels.items()}}
+    if slots is not None:
+        fmt = (6 * slots if name.startswith("K") else 0) + 8 * n * vec[name]
+        gbs = fmt / kernels[name] / 1e9
+        out.update({"format_bytes": fmt, "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS})
+    return out
+
+
 def cpu_baseline(A, L, eps, gt, max_iter: int):
     """The reference's CPU restatement (validate.py:163-201: scipy cg + explicit-Lᵀ SPAI
     operator), timed like validate.py:196-198, on a bounded number of iterations."""
@@ -196,6 +211,15 @@ def main():
     if world > 1:
         elapsed, total_iters = reduce_timing(elapsed, total_iters, torch.device("cuda", local))
 
+    # ---- the loop's own launches, each bracketed by HIP events (one untimed 40-iteration pass on
+    # the solver stream after the timed region): the dominant kernel against its format bytes
+    try:
+        loop_kernels = solver.time_kernels(b, 40)
+    except RuntimeError as e:  # other schedules (LSPCG_NO_SELL, fused): not instrumented
+        log(f"rank {rank}: no per-launch loop timing: {e}")
+        loop_kernels = {}
+    loop_dom = loop_dominant(loop_kernels, A, n) if loop_kernels else None
+
     # ---- the SpMV of A (fp64, the reference's scalar CSR) against the HBM roofline: first the
     # staged CSR kernel, then after the analysis step (SELL-64 copy, fp64 values, 16-bit column
     # offsets) -- the product's lspcg_spmv path, which the roofline line reports
@@ -287,6 +311,7 @@ def main():
                 "method": "HIP events on the ctx stream; cold = a 512 MiB read before every launch, launch time = (R x (flush+SpMV) - R x flush)/R",
             },
             "pcg_loop_spmv": pcg_spmv,
+            "pcg_loop_kernels": loop_dom,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -140,6 +140,11 @@ int lspcg_solver_set_ic(lspcg_solver* s, double* t_prec_ms);
  * Returns LSPCG_OK when converged, LSPCG_NOT_CONVERGED when max_iter was reached. */
 int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int64_t max_iter,
                        int64_t* iters, double* res_hist, double* t_solve_ms);
+/* Measurement only (bench.py): `iters` iterations of the split ext_spai schedule from x0 = 0,
+ * each of the five launches bracketed by HIP events on the solver stream (no graph, no
+ * convergence stop); kernel_ms[0..4] = mean device time of KA (t = Lᵀr), KB (z = Lt + εr, ρ),
+ * UP (p, x), KC (q = Ap, π), UR (r); *nk = 5.  LSPCG_ERR_UNSUPPORTED for other schedules. */
+int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, double* kernel_ms, int* nk);
 int lspcg_solver_destroy(lspcg_solver* s);
 
 /* ---- CSR assembly with Dirichlet masking (to_csr_cpu on device) ----

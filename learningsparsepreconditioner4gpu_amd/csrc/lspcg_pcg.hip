@@ -739,6 +739,8 @@ struct lspcg_solver {
   double* groups = nullptr;  // [GZ: <= 4096 x 2 dots x DD | GQ: <= 4096 x DD]
   int gsz_l = 1, ng_l = 1, gsz_a = 1, ng_a = 1;  // group size / count of the KB and KC launches
   bool allow_fused = false;  // LSPCG_PCG_FUSED=1 selects it (measured slower: two gathers per entry)
+  hipEvent_t* tev = nullptr;  // lspcg_solver_time_kernels: an event recorded after every launch
+  int tev_i = 0;
   PcgState* S = nullptr;
   PcgState* hS = nullptr;  // pinned host mirrors [2] (poll slots)
   double* partials = nullptr;
@@ -982,6 +984,11 @@ static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const
   return LSPCG_OK;
 }
 
+// lspcg_solver_time_kernels only: record the next timing event behind the launch just enqueued
+static void mark(lspcg_solver* s, hipStream_t st) {
+  if (s->tev) (void)hipEventRecord(s->tev[s->tev_i++], st);
+}
+
 template <typename T, bool SC>
 static int enqueue_iteration_split(lspcg_solver* s, hipStream_t st) {
   const int64_t n = s->n;
@@ -998,16 +1005,21 @@ static int enqueue_iteration_split(lspcg_solver* s, hipStream_t st) {
   const int eg = elem_vec_grid<T>(n);
   int rc = launch_it<T>(s, 2, static_cast<const T*>(r), ProDone{S}, EpiT<T, SC>{t, d}, st);
   if (rc) return rc;
+  mark(s, st);
   rc = launch_it<T>(s, 1, static_cast<const T*>(t), ProDone{S},
                     EpiZG<T, SC>{z, r, d, T(s->eps), s->partials, s->ticket, gz, s->gsz_l}, st);
   if (rc) return rc;
+  mark(s, st);
   hipLaunchKernelGGL(k_update_p_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
                      static_cast<const T*>(z), p, x);
+  mark(s, st);
   rc = launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQG<T>{q, p, s->partials, s->ticket, gq, s->gsz_a},
                     st);
   if (rc) return rc;
+  mark(s, st);
   hipLaunchKernelGGL(k_update_r_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
                      static_cast<const double*>(gq), s->ng_a, static_cast<const T*>(q), r);
+  mark(s, st);
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
@@ -1405,6 +1417,53 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     LSPCG_HIP(hipFree(dhist));
   }
   return (fin.done == 1) ? LSPCG_OK : LSPCG_NOT_CONVERGED;
+}
+
+int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, double* kernel_ms, int* nk) {
+  LSPCG_CHECK(s && b && kernel_ms && nk && iters > 0, LSPCG_ERR_ARG, "time_kernels: bad argument");
+  *nk = 0;
+  LSPCG_CHECK(s->split, LSPCG_ERR_UNSUPPORTED, "time_kernels: only the split ext_spai schedule (set_spai on SELL views)");
+  LSPCG_HIP(hipSetDevice(s->ctx->device));
+  const int64_t n = s->n;
+  hipStream_t st = s->stream;
+  const size_t vb = esize(s->dtype) * n;
+  LSPCG_HIP(hipEventRecord(s->ev_in, s->ctx->stream));
+  LSPCG_HIP(hipStreamWaitEvent(st, s->ev_in, 0));
+  LSPCG_HIP(hipMemcpyAsync(s->b, b, vb, hipMemcpyDeviceToDevice, st));
+  LSPCG_HIP(hipMemsetAsync(s->x, 0, vb, st));
+  PcgState init{};
+  init.rtol = 0.0;  // atol 0: no convergence stop, `iters` full iterations
+  init.eps = s->eps;
+  init.max_iter = iters + 1;
+  *s->hS = init;
+  LSPCG_HIP(hipMemcpyAsync(s->S, s->hS, sizeof(PcgState), hipMemcpyHostToDevice, st));
+  int rc = s->dtype == LSPCG_F64 ? enqueue_init<double>(s, st) : enqueue_init<float>(s, st);
+  if (rc) return rc;
+  constexpr int K = 5;
+  hipEvent_t ev[K + 1];
+  for (auto& e : ev) LSPCG_HIP(hipEventCreate(&e));
+  double acc[K] = {0, 0, 0, 0, 0};
+  for (int64_t it = 0; it < iters && rc == LSPCG_OK; ++it) {
+    LSPCG_HIP(hipEventRecord(ev[0], st));
+    s->tev = ev;
+    s->tev_i = 1;
+    rc = s->dtype == LSPCG_F64 ? enqueue_iteration<double>(s, st) : enqueue_iteration<float>(s, st);
+    s->tev = nullptr;
+    if (rc) break;
+    LSPCG_HIP(hipEventSynchronize(ev[K]));
+    for (int k = 0; k < K; ++k) {
+      float ms = 0.f;
+      LSPCG_HIP(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      acc[k] += ms;
+    }
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  if (rc) return rc;
+  for (int k = 0; k < K; ++k) kernel_ms[k] = acc[k] / double(iters);
+  *nk = K;
+  LSPCG_HIP(hipEventRecord(s->ev_out, st));
+  LSPCG_HIP(hipStreamWaitEvent(s->ctx->stream, s->ev_out, 0));
+  return LSPCG_OK;
 }
 
 int lspcg_solver_destroy(lspcg_solver* s) {

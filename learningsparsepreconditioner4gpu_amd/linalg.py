@@ -114,6 +114,17 @@ class PreconditionedConjugateGradient:
             out = out + (hist[: min(it.value, mi) + 1].copy(),)
         return out
 
+    KERNELS = ("KA t=L^T r", "KB z=L t+eps r, rho", "UP p, x", "KC q=A p, pi", "UR r")
+
+    def time_kernels(self, b: torch.Tensor, iters: int = 40) -> dict:
+        """Measurement only: mean device time (s) of each launch of the ext_spai iteration
+        (HIP events around every launch, ``iters`` iterations from x0 = 0, no graphs)."""
+        assert b.is_cuda and b.numel() == self.n
+        out = (C.c_double * 8)()
+        nk = C.c_int()
+        _lib.call("lspcg_solver_time_kernels", self.handle, C.c_void_p(b.data_ptr()), int(iters), out, C.byref(nk))
+        return {self.KERNELS[k]: out[k] / 1e3 for k in range(nk.value)}
+
     def __call__(self, b, x, rtol: float = 1e-6, max_iter: int = 0, ext_spai=None,
                  return_history: bool = False) -> Tuple:
         prec = self.setup_time
