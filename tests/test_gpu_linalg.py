@@ -241,3 +241,24 @@ def test_pcg_max_iter_inside_queued_chunks(gpu_ctx, max_iter):
     assert len(h) == it + 1
     np.testing.assert_allclose(h, h_o, rtol=1e-10, atol=0)
     assert np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
+
+
+def test_time_kernels_reports_five_launches(gpu_ctx, monkeypatch):
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    _, A, _ = _cases.spd_cases()[2]
+    b = torch.from_numpy(A @ np.ones(A.shape[0])).cuda()
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai")
+    s.set_spai(_cases.spai_like(A), 3e-3)
+    k = s.time_kernels(b, 5)
+    assert list(k) == list(s.KERNELS) and all(v > 0 for v in k.values())
+    # the solver still solves correctly afterwards (the timing pass leaves no state behind)
+    x = torch.zeros_like(b)
+    it, conv, _ = s.solve(b, x, rtol=1e-8)
+    L = _cases.spai_like(A)
+    assert conv and it == O.pcg(A, A @ np.ones(A.shape[0]), O.spai_operator(L, 3e-3), rtol=1e-8, dot="exact")[0]
+    monkeypatch.setenv("LSPCG_NO_SELL", "1")  # staged CSR views: not instrumented
+    s2 = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai")
+    s2.set_spai(L, 3e-3)
+    with pytest.raises(RuntimeError):
+        s2.time_kernels(b, 5)
