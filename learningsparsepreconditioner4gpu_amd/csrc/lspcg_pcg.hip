@@ -1254,6 +1254,8 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     };
     groups(sell_grid(*s->sp[1], true), &s->gsz_l, &s->ng_l);
     groups(sell_grid(*s->sp[0], true), &s->gsz_a, &s->ng_a);
+    LSPCG_CHECK(s->gsz_l <= kMaxGroups && s->gsz_a <= kMaxGroups, LSPCG_ERR_UNSUPPORTED,
+                "set_spai: reducing grid too large for one-wave group sums");
   }
   LSPCG_HIP(hipEventRecord(s->ev_t1, cst));
   LSPCG_HIP(hipEventSynchronize(s->ev_t1));
