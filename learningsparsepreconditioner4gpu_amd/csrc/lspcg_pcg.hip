@@ -670,6 +670,207 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
   for (int64_t i = nv * W + jt; i < n; i += ts) r[i] = r[i] - alpha * q[i];
 }
 
+// ---- small systems: the whole solve in ONE workgroup --------------------------------------
+// Below a few thousand unknowns an iteration of the multi-kernel schedules is 5 dependent
+// launches of almost no work (~16 us per iteration at n = 900).  k_pcg_small runs
+// scipy's loop (iterative.py:359-418) in one 1024-thread workgroup, the phases separated by
+// workgroup barriers instead of kernel boundaries.  Thread `tid` owns rows tid + 1024 m (m < 3):
+// their x, r, z, p, q live in registers; the three gathered vectors (r for Lᵀ, t for L, p for A)
+// are mirrored in LDS, so a row sum's gathers are LDS reads and its global loads (the row's
+// column indices and values, L2-resident after the first iteration) are independent of the
+// iteration and issued 8 at a time.  Expressions are those of the split schedule: row sums in
+// CSR index order (scipy's csr_matvec), T arithmetic, compensated dots rounded to T, the same
+// top-of-loop test and history; x's last update is left to k_x_fixup (x and p are stored at the
+// end).  The loop is bounded by max_iter, so every launch ends.
+struct CsrView {
+  const int32_t* rp;
+  const int32_t* ci;
+  const void* v;
+  int f32;  // values stored as fp32 (compact view of an fp32-exact fp64 matrix, or T = float)
+};
+
+constexpr int kSmallThreads = 1024;
+constexpr int kSmallRows = 3;  // rows per thread
+constexpr int64_t kSmallLds = 61440;  // dynamic LDS: 3 gathered vectors
+
+template <typename T>
+__device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, const T* xs) {
+  T acc = T(0);
+  for (int32_t k0 = b; k0 < e; k0 += 8) {
+    int32_t c[8];
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int32_t k = min(k0 + u, e - 1);
+      c[u] = gld(M.ci + k);
+      v[u] = M.f32 ? T(gld(static_cast<const float*>(M.v) + k)) : gld(static_cast<const T*>(M.v) + k);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (k0 + u < e) acc = acc + v[u] * xs[c[u]];
+  }
+  return acc;
+}
+
+// fixed-order workgroup sum of N compensated dots, rounded to T, returned to every thread: wave
+// butterflies, one barrier, then every wave sums the 16 wave totals with a 16-lane butterfly and
+// takes lane 0's (one LDS round trip instead of a serial sum in thread 0 and a broadcast).  `lds`
+// is written again only after later barriers (each reduction site has its own buffer).
+template <typename T, int N>
+__device__ __forceinline__ void small_dots(DD (&v)[N], DD* lds, double (&out)[N]) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  wave_reduce_dd<N>(v);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) lds[wid * N + j] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    DD a = lane < kSmallThreads / 64 ? lds[lane * N + j] : dd_zero();
+#pragma unroll
+    for (int m = 1; m < kSmallThreads / 64; m <<= 1) a = dd_add(a, dd_shfl_xor(a, m));
+    out[j] = round_to<T>(dd_value(DD{__shfl(a.s, 0, 64), __shfl(a.c, 0, 64)}));
+  }
+}
+
+template <typename T, int PRE>
+__global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState* S, CsrView A, CsrView L,
+                                                             CsrView LT, const T* __restrict__ d, T* x, T* r, T* p) {
+  constexpr bool SPAI = PRE == LSPCG_PRECOND_EXT_SPAI || PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  constexpr bool SCALED = PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  constexpr int R = kSmallRows;
+  extern __shared__ __attribute__((aligned(16))) unsigned char small_lds[];
+  T* rs = reinterpret_cast<T*>(small_lds);
+  T* ts = rs + n;
+  T* ps = ts + n;
+  __shared__ DD lds_z[16 * 2];
+  __shared__ DD lds_q[16];
+  if (S->done) return;  // ‖b‖ = 0 (init)
+  const int tid = threadIdx.x;
+  const T eps = T(S->eps);
+  const double atol = S->atol;
+  const int64_t max_iter = S->max_iter;
+  double* hist = S->hist;
+  const double rr0 = S->rr;
+  double rho_prev = S->rho, rho = S->rho, pq = S->pq;
+  T alpha = T(S->alpha);
+  int64_t k = S->iter;
+  int code = 0;
+  bool own[R];
+  int32_t row[R], ab[R], ae[R], lb[R], le[R], tb[R], te[R];
+  T xr[R], rr_[R], pr[R], dr[R];
+#pragma unroll
+  for (int m = 0; m < R; ++m) {
+    row[m] = tid + kSmallThreads * m;
+    own[m] = row[m] < n;
+    const int32_t i = own[m] ? row[m] : 0;
+    ab[m] = A.rp[i];
+    ae[m] = own[m] ? A.rp[i + 1] : ab[m];
+    if constexpr (SPAI) {
+      lb[m] = L.rp[i];
+      le[m] = own[m] ? L.rp[i + 1] : lb[m];
+      tb[m] = LT.rp[i];
+      te[m] = own[m] ? LT.rp[i + 1] : tb[m];
+    }
+    xr[m] = own[m] ? x[i] : T(0);
+    rr_[m] = own[m] ? r[i] : T(0);
+    pr[m] = T(0);
+    if constexpr (SCALED || PRE == LSPCG_PRECOND_DIAGONAL) dr[m] = own[m] ? d[i] : T(1);
+    if (own[m]) rs[i] = rr_[m];
+  }
+  __syncthreads();
+  for (;; ++k) {
+    // z = M⁻¹ r ; ρ_k = r·z ; ‖r_k‖²
+    if constexpr (SPAI) {
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        if (!own[m]) continue;
+        const T s = small_row<T>(LT, tb[m], te[m], rs);
+        if constexpr (SCALED) ts[row[m]] = s / dr[m];
+        else ts[row[m]] = s;
+      }
+      __syncthreads();
+    }
+    DD dz[2] = {dd_zero(), dd_zero()};
+    T zr[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      const T ri = rr_[m];
+      T zi;
+      if constexpr (SCALED) zi = small_row<T>(L, lb[m], le[m], ts) + (eps * ri) / dr[m];
+      else if constexpr (SPAI) zi = small_row<T>(L, lb[m], le[m], ts) + eps * ri;
+      else if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) zi = ri / dr[m];
+      else zi = ri;
+      zr[m] = zi;
+      if (own[m]) {
+        dd_fma(dz[0], double(ri), double(zi));
+        dd_fma(dz[1], double(ri), double(ri));
+      }
+    }
+    double v2[2];
+    small_dots<T, 2>(dz, lds_z, v2);
+    const double rr = k > 0 ? v2[1] : rr0;
+    if (k >= max_iter) {
+      code = 2;
+    } else {
+      const double rn = double(tsqrt<T>(T(rr)));
+      if (rn < atol) code = 1;
+      else if (!(rn == rn) || rn == INFINITY) code = 3;
+    }
+    if (tid == 0 && k > 0) {
+      S->rr = rr;
+      if (hist) hist[k] = double(tsqrt<T>(T(rr)));
+    }
+    if (code) break;
+    rho_prev = rho;
+    rho = v2[0];
+    // x += α_{k-1} p_{k-1} ; p_k = p_{k-1}β + z
+    const bool first = k == 0;
+    const T beta = first ? T(0) : T(rho) / T(rho_prev);
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      if (!first) xr[m] = xr[m] + alpha * pr[m];
+      pr[m] = first ? zr[m] : (pr[m] * beta) + zr[m];
+      if (own[m]) ps[row[m]] = pr[m];
+    }
+    __syncthreads();
+    // q = A p ; π = p·q ; α = ρ/π ; r -= α q
+    DD dq[1] = {dd_zero()};
+    T qr[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      qr[m] = own[m] ? small_row<T>(A, ab[m], ae[m], ps) : T(0);
+      if (own[m]) dd_fma(dq[0], double(pr[m]), double(qr[m]));
+    }
+    double v1[1];
+    small_dots<T, 1>(dq, lds_q, v1);
+    pq = v1[0];
+    alpha = T(rho) / T(pq);
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      rr_[m] = rr_[m] - alpha * qr[m];
+      if (own[m]) rs[row[m]] = rr_[m];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int m = 0; m < R; ++m) {
+    if (!own[m]) continue;
+    x[row[m]] = xr[m];
+    p[row[m]] = pr[m];
+  }
+  if (tid == 0) {
+    S->rho_prev = rho_prev;
+    S->rho = rho;
+    S->pq = pq;
+    S->alpha = double(alpha);
+    S->iter = k;
+    S->done = code;
+  }
+}
+
 // IC: ρ = r·z after the two triangular solves
 template <typename T>
 __global__ void __launch_bounds__(kThreads) k_dot_rho(int64_t n, PcgState* S, const T* __restrict__ r,
@@ -769,6 +970,7 @@ struct lspcg_solver {
   void* sv[3] = {nullptr, nullptr, nullptr};
   int svd[3] = {0, 0, 0};
   int32_t* xrow[3] = {nullptr, nullptr, nullptr};  // scalar row pointers of expanded BSR3 views
+  int64_t small_n = 4096;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it)
 };
 
 // (Re)build the SELL copy of iteration view w (0 = A, 1 = L, 2 = Lᵀ); L and Lᵀ reuse A's
@@ -1139,6 +1341,48 @@ static int enqueue_fixup(lspcg_solver* s, hipStream_t st) {
   return LSPCG_OK;
 }
 
+static bool small_path(const lspcg_solver* s) {
+  if (s->n <= 0 || s->n > s->small_n || s->precond == LSPCG_PRECOND_IC || s->Av.block_size != 1) return false;
+  if (s->n > int64_t(kSmallThreads) * kSmallRows || 3 * s->n * (s->dtype == LSPCG_F32 ? 4 : 8) > kSmallLds) return false;
+  if (s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED)
+    return s->Lv.block_size == 1 && s->LTv.block_size == 1;
+  return true;
+}
+
+static CsrView csr_view(const lspcg_mat& M) {
+  return CsrView{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0};
+}
+
+template <typename T>
+static int launch_small(lspcg_solver* s, hipStream_t st) {
+  const bool spai = s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  const CsrView A = csr_view(s->Av);
+  const CsrView L = spai ? csr_view(s->Lv) : CsrView{};
+  const CsrView LT = spai ? csr_view(s->LTv) : CsrView{};
+  auto* x = static_cast<T*>(s->x);
+  auto* r = static_cast<T*>(s->r);
+  auto* p = static_cast<T*>(s->p);
+  const T* d = static_cast<const T*>(s->d);
+  const int32_t n = int32_t(s->n);
+  const dim3 g(1), b(kSmallThreads);
+  const size_t lds = 3 * sizeof(T) * size_t(n);
+  switch (s->precond) {
+    case LSPCG_PRECOND_NONE:
+      hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_NONE>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+      break;
+    case LSPCG_PRECOND_DIAGONAL:
+      hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_DIAGONAL>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+      break;
+    case LSPCG_PRECOND_EXT_SPAI:
+      hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+      break;
+    default:
+      hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI_SCALED>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+  }
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
 static int get_graph(lspcg_solver* s, int chunk, hipGraphExec_t* out) {
   auto it = s->graphs.find(chunk);
   if (it != s->graphs.end()) {
@@ -1202,6 +1446,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SELL32")) s->sell16 = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_PCG_FUSED")) s->allow_fused = e[0] == '1';
+  if (const char* e = std::getenv("LSPCG_SMALL_N")) s->small_n = std::max<int64_t>(0, std::atoll(e));
   if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
     s->allow_split = e[0] != '0';
     s->split_mode = std::atoi(e);
@@ -1358,14 +1603,23 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     for (int j = 0; j < npend; ++j) queued[(head + j) & 1] += c;
     return post();
   };
-  rc = post();
-  if (!rc) rc = launch(std::min(4, max_chunk));
-  if (rc) return rc;
+  PcgState cur{};
+  const bool small = small_path(s);
+  if (small) {  // one launch runs the whole loop (k_pcg_small)
+    rc = s->dtype == LSPCG_F64 ? launch_small<double>(s, st) : launch_small<float>(s, st);
+    if (!rc) rc = post();
+    if (rc) return rc;
+    LSPCG_HIP(hipEventSynchronize(evp[head]));
+    cur = *hs[head];
+  } else {
+    rc = post();
+    if (!rc) rc = launch(std::min(4, max_chunk));
+    if (rc) return rc;
+  }
   int64_t last_it = 0;
   double last_rr = -1.0;
   int chunk = std::min(4, max_chunk);
-  PcgState cur{};
-  for (;;) {
+  for (; !small;) {
     LSPCG_HIP(hipEventSynchronize(evp[head]));
     cur = *hs[head];
     const int64_t inflight = queued[head];

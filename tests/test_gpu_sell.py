@@ -89,13 +89,17 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
     b = torch.from_numpy(A @ np.ones(n)).cuda()
     out = []
     # CSR views (5 kernels); SELL int32 columns / 16-bit offsets, 5-kernel and fused 3-kernel schedules
-    # (+ split group reductions vs last-arriver reductions on the SELL 16-bit views)
-    for env, env32, fused, split in (("1", "0", "0", "1"), ("0", "1", "0", "1"), ("0", "0", "0", "1"),
-                                     ("0", "0", "0", "0"), ("0", "1", "1", "1"), ("0", "0", "1", "1")):
+    # (+ split group reductions vs last-arriver reductions on the SELL 16-bit views); last: the
+    # one-workgroup solve (k_pcg_small), which every other variant has switched off
+    for env, env32, fused, split, small in (("1", "0", "0", "1", "0"), ("0", "1", "0", "1", "0"),
+                                            ("0", "0", "0", "1", "0"), ("0", "0", "0", "0", "0"),
+                                            ("0", "1", "1", "1", "0"), ("0", "0", "1", "1", "0"),
+                                            ("0", "0", "0", "1", "1000000")):
         monkeypatch.setenv("LSPCG_NO_SELL", env)
         monkeypatch.setenv("LSPCG_SELL32", env32)
         monkeypatch.setenv("LSPCG_PCG_FUSED", fused)
         monkeypatch.setenv("LSPCG_SPLIT_REDUCE", split)
+        monkeypatch.setenv("LSPCG_SMALL_N", small)
         s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
         if precond.startswith("ext_spai"):
             s.set_spai(_cases.spai_like(A), 1e-3)
@@ -166,6 +170,7 @@ def test_pcg_bsr3_sell_equals_block_kernel(gpu_ctx, precond, monkeypatch):
     L = sp.csr_matrix(sp.bsr_matrix(_cases.spai_like(A), blocksize=(3, 3)))
     b = torch.from_numpy(A @ mask.reshape(-1).astype(np.float64)).cuda()
     out = []
+    monkeypatch.setenv("LSPCG_SMALL_N", "0")  # block views never take the one-workgroup solve
     for env in ("1", "0"):
         monkeypatch.setenv("LSPCG_NO_SELL", env)
         Ad = DeviceMatrix.from_scipy(A, block_size=3)
