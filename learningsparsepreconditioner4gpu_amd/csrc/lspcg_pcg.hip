@@ -673,8 +673,8 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
 // ---- small systems: the whole solve in ONE workgroup --------------------------------------
 // Below a few thousand unknowns an iteration of the multi-kernel schedules is 5 dependent
 // launches of almost no work (~16 us per iteration at n = 900).  k_pcg_small runs
-// scipy's loop (iterative.py:359-418) in one 1024-thread workgroup, the phases separated by
-// workgroup barriers instead of kernel boundaries.  Thread `tid` owns rows tid + 1024 m (m < 3):
+// scipy's loop (iterative.py:359-418) in one 512-thread workgroup, the phases separated by
+// workgroup barriers instead of kernel boundaries.  Thread `tid` owns rows tid + 512 m (m < R):
 // their x, r, z, p, q live in registers; the three gathered vectors (r for Lᵀ, t for L, p for A)
 // are mirrored in LDS, so a row sum's gathers are LDS reads and its global loads (the row's
 // column indices and values, L2-resident after the first iteration) are independent of the
@@ -687,15 +687,65 @@ struct CsrView {
   const int32_t* ci;
   const void* v;
   int f32;  // values stored as fp32 (compact view of an fp32-exact fp64 matrix, or T = float)
+  // the solver's SELL-64 copy of the same view (lspcg_sell.hpp) when gp != nullptr: lane-major
+  // 4-entry groups, so a wave's row loads are contiguous 16-B accesses (the CSR row-per-lane
+  // loads touch ~12 cache lines per instruction and bound the one-CU solve on L1/L2 requests)
+  const int32_t* gp;
+  const void* scol;
+  const void* sv;
+  int sf32;
+  int c16;
 };
 
-constexpr int kSmallThreads = 1024;
-constexpr int kSmallRows = 3;  // rows per thread
+constexpr int kSmallThreads = 512;  // 2 waves per SIMD: the compensated reductions are VALU work
+constexpr int kSmallRows = 5;       // largest rows per thread (template R = 1, 2 or 5)
 constexpr int64_t kSmallLds = 61440;  // dynamic LDS: 3 gathered vectors
 
+// row i; [b, e): its CSR entry range, or (SELL) its slice's group range
 template <typename T>
-__device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, const T* xs) {
+__device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, int32_t i, const T* xs) {
   T acc = T(0);
+  if (M.gp) {
+    const int32_t lane = i & 63, base = i & ~63;
+    for (int32_t q0 = b; q0 < e; q0 += 2) {
+      T v[8];
+      int32_t c[8];
+      bool ok[8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const size_t off = 256 * size_t(min(q0 + u, e - 1)) + 4 * lane;
+        if (M.sf32) {
+          const f32x4 a = *(const __attribute__((address_space(1))) f32x4*)(static_cast<const float*>(M.sv) + off);
+          v[4 * u + 0] = T(a.x); v[4 * u + 1] = T(a.y); v[4 * u + 2] = T(a.z); v[4 * u + 3] = T(a.w);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[4 * u + j] = gld(static_cast<const T*>(M.sv) + off + j);
+        }
+        int o[4];
+        if (M.c16) {
+          const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(static_cast<const int16_t*>(M.scol) + off);
+          o[0] = cc.x; o[1] = cc.y; o[2] = cc.z; o[3] = cc.w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            ok[4 * u + j] = o[j] != kSellPad16 && q0 + u < e;
+            c[4 * u + j] = ok[4 * u + j] ? base + o[j] : 0;
+          }
+        } else {
+          const i32x4 cc = *(const __attribute__((address_space(1))) i32x4*)(static_cast<const int32_t*>(M.scol) + off);
+          o[0] = cc.x; o[1] = cc.y; o[2] = cc.z; o[3] = cc.w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            ok[4 * u + j] = o[j] >= 0 && q0 + u < e;
+            c[4 * u + j] = ok[4 * u + j] ? o[j] : 0;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (ok[u]) acc = acc + v[u] * xs[c[u]];
+    }
+    return acc;
+  }
   for (int32_t k0 = b; k0 < e; k0 += 8) {
     int32_t c[8];
     T v[8];
@@ -713,7 +763,7 @@ __device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, c
 }
 
 // fixed-order workgroup sum of N compensated dots, rounded to T, returned to every thread: wave
-// butterflies, one barrier, then every wave sums the 16 wave totals with a 16-lane butterfly and
+// butterflies, one barrier, then every wave sums the 8 wave totals with an 8-lane butterfly and
 // takes lane 0's (one LDS round trip instead of a serial sum in thread 0 and a broadcast).  `lds`
 // is written again only after later barriers (each reduction site has its own buffer).
 template <typename T, int N>
@@ -735,18 +785,17 @@ __device__ __forceinline__ void small_dots(DD (&v)[N], DD* lds, double (&out)[N]
   }
 }
 
-template <typename T, int PRE>
+template <typename T, int PRE, int R>
 __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState* S, CsrView A, CsrView L,
                                                              CsrView LT, const T* __restrict__ d, T* x, T* r, T* p) {
   constexpr bool SPAI = PRE == LSPCG_PRECOND_EXT_SPAI || PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
   constexpr bool SCALED = PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
-  constexpr int R = kSmallRows;
   extern __shared__ __attribute__((aligned(16))) unsigned char small_lds[];
   T* rs = reinterpret_cast<T*>(small_lds);
   T* ts = rs + n;
   T* ps = ts + n;
-  __shared__ DD lds_z[16 * 2];
-  __shared__ DD lds_q[16];
+  __shared__ DD lds_z[kSmallThreads / 64 * 2];
+  __shared__ DD lds_q[kSmallThreads / 64];
   if (S->done) return;  // ‖b‖ = 0 (init)
   const int tid = threadIdx.x;
   const T eps = T(S->eps);
@@ -766,13 +815,16 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
     row[m] = tid + kSmallThreads * m;
     own[m] = row[m] < n;
     const int32_t i = own[m] ? row[m] : 0;
-    ab[m] = A.rp[i];
-    ae[m] = own[m] ? A.rp[i + 1] : ab[m];
+    auto range = [&](const CsrView& M, int32_t& b, int32_t& e) {  // CSR entries or SELL groups
+      const int32_t* rp = M.gp ? M.gp : M.rp;
+      const int32_t j = M.gp ? (i >> 6) : i;
+      b = rp[j];
+      e = own[m] ? rp[j + 1] : b;
+    };
+    range(A, ab[m], ae[m]);
     if constexpr (SPAI) {
-      lb[m] = L.rp[i];
-      le[m] = own[m] ? L.rp[i + 1] : lb[m];
-      tb[m] = LT.rp[i];
-      te[m] = own[m] ? LT.rp[i + 1] : tb[m];
+      range(L, lb[m], le[m]);
+      range(LT, tb[m], te[m]);
     }
     xr[m] = own[m] ? x[i] : T(0);
     rr_[m] = own[m] ? r[i] : T(0);
@@ -787,7 +839,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
 #pragma unroll
       for (int m = 0; m < R; ++m) {
         if (!own[m]) continue;
-        const T s = small_row<T>(LT, tb[m], te[m], rs);
+        const T s = small_row<T>(LT, tb[m], te[m], row[m], rs);
         if constexpr (SCALED) ts[row[m]] = s / dr[m];
         else ts[row[m]] = s;
       }
@@ -799,8 +851,8 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
     for (int m = 0; m < R; ++m) {
       const T ri = rr_[m];
       T zi;
-      if constexpr (SCALED) zi = small_row<T>(L, lb[m], le[m], ts) + (eps * ri) / dr[m];
-      else if constexpr (SPAI) zi = small_row<T>(L, lb[m], le[m], ts) + eps * ri;
+      if constexpr (SCALED) zi = small_row<T>(L, lb[m], le[m], row[m], ts) + (eps * ri) / dr[m];
+      else if constexpr (SPAI) zi = small_row<T>(L, lb[m], le[m], row[m], ts) + eps * ri;
       else if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) zi = ri / dr[m];
       else zi = ri;
       zr[m] = zi;
@@ -841,7 +893,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
     T qr[R];
 #pragma unroll
     for (int m = 0; m < R; ++m) {
-      qr[m] = own[m] ? small_row<T>(A, ab[m], ae[m], ps) : T(0);
+      qr[m] = own[m] ? small_row<T>(A, ab[m], ae[m], row[m], ps) : T(0);
       if (own[m]) dd_fma(dq[0], double(pr[m]), double(qr[m]));
     }
     double v1[1];
@@ -971,6 +1023,7 @@ struct lspcg_solver {
   int svd[3] = {0, 0, 0};
   int32_t* xrow[3] = {nullptr, nullptr, nullptr};  // scalar row pointers of expanded BSR3 views
   int64_t small_n = 4096;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it)
+  bool small_sell = true;  // k_pcg_small reads the SELL copies (LSPCG_SMALL_SELL=0: the CSR views)
 };
 
 // (Re)build the SELL copy of iteration view w (0 = A, 1 = L, 2 = Lᵀ); L and Lᵀ reuse A's
@@ -1349,16 +1402,26 @@ static bool small_path(const lspcg_solver* s) {
   return true;
 }
 
-static CsrView csr_view(const lspcg_mat& M) {
-  return CsrView{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0};
+static CsrView csr_view(const lspcg_solver* s, int w, const lspcg_mat& M) {
+  CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, nullptr, nullptr, nullptr, 0, 0};
+  if (const SellPattern* P = s->sp[w]) {
+    if (s->small_sell && s->sv[w] && !s->xrow[w]) {
+      v.gp = P->gp;
+      v.scol = P->col;
+      v.sv = s->sv[w];
+      v.sf32 = s->svd[w] == LSPCG_F32 ? 1 : 0;
+      v.c16 = P->col_bits == 16 ? 1 : 0;
+    }
+  }
+  return v;
 }
 
 template <typename T>
 static int launch_small(lspcg_solver* s, hipStream_t st) {
   const bool spai = s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
-  const CsrView A = csr_view(s->Av);
-  const CsrView L = spai ? csr_view(s->Lv) : CsrView{};
-  const CsrView LT = spai ? csr_view(s->LTv) : CsrView{};
+  const CsrView A = csr_view(s, 0, s->Av);
+  const CsrView L = spai ? csr_view(s, 1, s->Lv) : CsrView{};
+  const CsrView LT = spai ? csr_view(s, 2, s->LTv) : CsrView{};
   auto* x = static_cast<T*>(s->x);
   auto* r = static_cast<T*>(s->r);
   auto* p = static_cast<T*>(s->p);
@@ -1366,19 +1429,26 @@ static int launch_small(lspcg_solver* s, hipStream_t st) {
   const int32_t n = int32_t(s->n);
   const dim3 g(1), b(kSmallThreads);
   const size_t lds = 3 * sizeof(T) * size_t(n);
-  switch (s->precond) {
-    case LSPCG_PRECOND_NONE:
-      hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_NONE>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
-      break;
-    case LSPCG_PRECOND_DIAGONAL:
-      hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_DIAGONAL>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
-      break;
-    case LSPCG_PRECOND_EXT_SPAI:
-      hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
-      break;
-    default:
-      hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI_SCALED>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
-  }
+  auto go = [&](auto rows) {
+    constexpr int R = decltype(rows)::value;
+    switch (s->precond) {
+      case LSPCG_PRECOND_NONE:
+        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_NONE, R>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+        break;
+      case LSPCG_PRECOND_DIAGONAL:
+        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_DIAGONAL, R>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+        break;
+      case LSPCG_PRECOND_EXT_SPAI:
+        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI, R>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+        break;
+      default:
+        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI_SCALED, R>), g, b, lds, st, n, s->S, A, L, LT, d, x, r,
+                           p);
+    }
+  };
+  if (n <= kSmallThreads) go(std::integral_constant<int, 1>{});
+  else if (n <= 2 * kSmallThreads) go(std::integral_constant<int, 2>{});
+  else go(std::integral_constant<int, kSmallRows>{});
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
@@ -1447,6 +1517,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   if (const char* e = std::getenv("LSPCG_SELL32")) s->sell16 = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_PCG_FUSED")) s->allow_fused = e[0] == '1';
   if (const char* e = std::getenv("LSPCG_SMALL_N")) s->small_n = std::max<int64_t>(0, std::atoll(e));
+  if (const char* e = std::getenv("LSPCG_SMALL_SELL")) s->small_sell = e[0] != '0';
   if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
     s->allow_split = e[0] != '0';
     s->split_mode = std::atoi(e);

@@ -90,11 +90,13 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
     out = []
     # CSR views (5 kernels); SELL int32 columns / 16-bit offsets, 5-kernel and fused 3-kernel schedules
     # (+ split group reductions vs last-arriver reductions on the SELL 16-bit views); last: the
-    # one-workgroup solve (k_pcg_small), which every other variant has switched off
+    # one-workgroup solve (k_pcg_small) on the SELL copies and on the CSR views (LSPCG_NO_SELL=1),
+    # which every other variant has switched off
     for env, env32, fused, split, small in (("1", "0", "0", "1", "0"), ("0", "1", "0", "1", "0"),
                                             ("0", "0", "0", "1", "0"), ("0", "0", "0", "0", "0"),
                                             ("0", "1", "1", "1", "0"), ("0", "0", "1", "1", "0"),
-                                            ("0", "0", "0", "1", "1000000")):
+                                            ("0", "0", "0", "1", "1000000"), ("0", "1", "0", "1", "1000000"),
+                                            ("1", "0", "0", "1", "1000000")):
         monkeypatch.setenv("LSPCG_NO_SELL", env)
         monkeypatch.setenv("LSPCG_SELL32", env32)
         monkeypatch.setenv("LSPCG_PCG_FUSED", fused)
