@@ -1406,7 +1406,7 @@ static bool small_path(const lspcg_solver* s) {
 static CsrView csr_view(const lspcg_solver* s, int w, const lspcg_mat& M) {
   CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, nullptr, nullptr, nullptr, 0, 0};
   if (const SellPattern* P = s->sp[w]) {
-    if (s->small_sell && s->sv[w] && !s->xrow[w]) {
+    if (s->small_sell && s->sv[w] && !s->xrow[w] && P->groups > 0) {
       v.gp = P->gp;
       v.scol = P->col;
       v.sv = s->sv[w];
