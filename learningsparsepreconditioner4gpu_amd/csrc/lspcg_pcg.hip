@@ -1023,7 +1023,8 @@ struct lspcg_solver {
   void* sv[3] = {nullptr, nullptr, nullptr};
   int svd[3] = {0, 0, 0};
   int32_t* xrow[3] = {nullptr, nullptr, nullptr};  // scalar row pointers of expanded BSR3 views
-  int64_t small_n = 4096;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it)
+  int64_t small_n = 1024;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it): <= 2 rows
+                           // per thread; 5 rows lose to the 5-kernel schedule
   bool small_sell = true;  // k_pcg_small reads the SELL copies (LSPCG_SMALL_SELL=0: the CSR views)
 };
 

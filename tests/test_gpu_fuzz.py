@@ -36,7 +36,7 @@ SIZES = [63, 65, 257, 1000, 4097, 17000, 70000, 150000]
 @pytest.mark.parametrize("small_n", ["0", "4096"])
 @pytest.mark.parametrize("seed", range(16))
 def test_random_spd_pcg_parity(gpu_ctx, seed, small_n, monkeypatch):
-    """small_n "0": the multi-kernel schedules at every size; "4096": n <= 4096 runs k_pcg_small."""
+    """small_n "0": the multi-kernel schedules at every size; "4096": n <= 2560 runs k_pcg_small."""
     monkeypatch.setenv("LSPCG_SMALL_N", small_n)
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
 

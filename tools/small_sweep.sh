@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_pcg_small A/B on the GPU box: solve times of the heat_batch8 systems + kuhn41 with the
-# one-workgroup solve off (LSPCG_SMALL_N=0) and on where it applies (n <= 2560 fp64).
+# one-workgroup solve off (LSPCG_SMALL_N=0) and on up to n = 2560 (LSPCG_SMALL_N=4096).
 set -o pipefail
 mkdir -p gpurun_out/small
 for N in 0 4096; do
