@@ -225,10 +225,13 @@ def test_reused_solver_reinstalls_a_changed_factor(gpu_ctx):
     run(Ld, 1)
 
 
+@pytest.mark.parametrize("small_n", ["0", "4096"])
 @pytest.mark.parametrize("max_iter", [1, 4, 37, 64])
-def test_pcg_max_iter_inside_queued_chunks(gpu_ctx, max_iter):
+def test_pcg_max_iter_inside_queued_chunks(gpu_ctx, max_iter, small_n, monkeypatch):
     # the host keeps one chunk of up to 32 iterations queued ahead of its poll: a max_iter that
     # falls inside a queued chunk must still stop the iterate and the history at max_iter
+    # (small_n "4096": the same n = 2048 system in the one-workgroup solve, 5-row template)
+    monkeypatch.setenv("LSPCG_SMALL_N", small_n)
     _, A, mask = _cases.spd_cases()[0]
     gt = np.ones(A.shape[0]) if mask is None else mask.ravel().astype(np.float64)
     b = A @ gt
