@@ -2,22 +2,25 @@
 // call sites neural_cg/utils/validate.py:54-160; arithmetic of scipy 1.15 iterative.py:359-418,
 // the reference's CPU restatement validate.py:163-341).
 //
-// Schedule (DESIGN.md "PCG"): the AXPY-type updates of scipy's loop are evaluated where their
-// results are consumed, with the exact same floating-point expression, so every vector holds
-// the same bits as in scipy's order while an ext_spai iteration is THREE kernels:
-//   KA  r_k = r_{k-1} - α_{k-1} q_{k-1} (own rows, stored; recomputed in the gather),
-//       ‖r_k‖², t = Lᵀ r_k                                   [SpMV Lᵀ]
-//   KB  (test ‖r_k‖ < atol -- top of scipy's loop) z = L t + ε r_k ; ρ_k = r_k·z   [SpMV L]
-//   KC  p_k = p_{k-1}β + z (own rows stored; recomputed in the gather), x += α_{k-1} p_{k-1},
-//       q = A p_k ; π = p_k·q ; α_k = ρ_k/π                    [SpMV A]
-// Unpreconditioned / diagonal PCG: KA is elementwise (+ z = r/d, ρ) and the test moves to KC.
-// r and p ping-pong between two buffers (a gather must never see a half-updated vector); the
-// last x update is applied by one fix-up kernel after the loop.  Every kernel is predicated on
-// a device `done` flag, so the host replays graph-captured chunks of iterations and polls once
-// per chunk without changing the iteration count or the iterate.
+// Schedules, all with scipy's exact floating-point expressions, so every schedule
+// produces the same iterate and residual history bit for bit:
+//   * split ext_spai schedule (SELL views): five launches per iteration
+//       KA  t = Lᵀ r_k                                         [SpMV Lᵀ]
+//       KB  z = L t + ε r_k ; group partials of ρ_k = r_k·z, ‖r_k‖²   [SpMV L]
+//       UP  top-of-loop test on ‖r_k‖ ; x += α_{k-1} p_{k-1} ; p_k = p_{k-1}β + z
+//       KC  q = A p_k ; group partials of π_k = p_k·q              [SpMV A]
+//       UR  α_k = ρ_k/π_k ; r_{k+1} = r_k - α_k q
+//   * the same five phases with last-arriver grid reductions (CSR / BSR views, CG, Jacobi, IC);
+//   * one-workgroup solve (k_pcg_small) for n <= LSPCG_SMALL_N;
+//   * persistent multi-workgroup solve (k_pcg_persist, lspcg_persist.hpp) for the mid range.
+// Every multi-launch kernel is predicated on a device `done` flag, so the host replays
+// graph-captured chunks of iterations and polls once per chunk without changing the iteration
+// count or the iterate; the deferred x update of the last iteration is one fix-up launch.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <map>
@@ -146,170 +149,6 @@ struct EpiQ {
     if constexpr (INC) S->iter = S->iter + 1;
   }
 };
-
-// ---- fused 3-kernel ext_spai schedule (SELL views; DESIGN.md "PCG schedule") ----------------
-// The AXPY updates are evaluated where they are consumed, with scipy's exact expressions:
-//   KA  r_k = r_{k-1} - α_{k-1} q_{k-1} (gathered, own rows stored), ‖r_k‖², t = Lᵀ r_k
-//   KB  top-of-loop test on ‖r_k‖ ; z = L t + ε r_k ; ρ_k = r_k·z
-//   KC  p_k = p_{k-1}β + z (gathered, own rows stored), x += α_{k-1} p_{k-1}, q = A p_k, π, α_k
-// r_k lives in R[k & 1] and p_k in P[k & 1]: a gather never reads a buffer being written.
-// (base + parity * offset: a select between two struct members would become a dynamically
-// indexed private array, which the compiler moves to scratch / LDS)
-template <typename T>
-struct Pair {
-  T* B0;
-  int64_t delta;  // B1 - B0 in elements
-  __host__ __device__ static Pair make(T* b0, T* b1) { return Pair{b0, int64_t(b1 - b0)}; }
-  __device__ __forceinline__ T* at(int64_t k) const { return B0 + (k & 1) * delta; }
-};
-
-// gather of r_k = r_{k-1} - α_{k-1} q_{k-1} (scipy `r -= alpha*q`); r_0 itself at k = 0
-template <typename T>
-struct GatherR {
-  Pair<T> R;
-  const T* q;
-  const PcgState* S;
-  const T* rold = nullptr;
-  T alpha = T(0);
-  bool upd = false;
-  __device__ __forceinline__ void prepare() {
-    const int64_t k = S->iter;
-    upd = k > 0;
-    alpha = T(S->alpha);
-    rold = R.at(upd ? k - 1 : 0);
-  }
-  // both loads unconditional, select afterwards (no branch around the loads)
-  __device__ __forceinline__ T operator()(int64_t j) const {
-    const T a = gld(rold + j);
-    const T b = gld(q + j);
-    const T u = a - alpha * b;
-    return upd ? u : a;
-  }
-};
-
-// gather of p_k = p_{k-1}β + z_k (scipy `p *= beta; p += z`), p_0 = z_0
-template <typename T>
-struct GatherP {
-  Pair<T> P;
-  const T* z;
-  const PcgState* S;
-  const T* pold = nullptr;
-  T beta = T(0);
-  bool first = true;
-  __device__ __forceinline__ void prepare() {
-    const int64_t k = S->iter;
-    first = k == 0;
-    pold = P.at(k + 1);  // = P[(k-1) & 1]
-    beta = first ? T(0) : T(S->rho) / T(S->rho_prev);
-  }
-  __device__ __forceinline__ T operator()(int64_t j) const {
-    const T a = gld(z + j);
-    const T b = gld(pold + j);
-    const T u = (b * beta) + a;
-    return first ? a : u;
-  }
-};
-
-// KA epilogue: own-row r_k stored, t = Lᵀ r_k (scaled: (Lᵀ r_k)/d), ‖r_k‖²
-template <typename T, bool SCALED>
-struct EpiRT {
-  static constexpr int NDOT = 1;
-  GatherR<T> g;
-  T* t;
-  const T* d;
-  PcgState* S;
-  double* partials;
-  unsigned* ticket;
-  T* rnew = nullptr;
-  __device__ __forceinline__ void prepare() {
-    g.prepare();  // the epilogue's own copy of the gather (own-row r_k)
-    rnew = g.R.at(S->iter);
-  }
-  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
-    const T ri = g(i);
-    if (g.upd) gst(rnew + i, ri);
-    if constexpr (SCALED) gst(t + i, s / gld(d + i));
-    else gst(t + i, s);
-    dd_fma(dots[0], double(ri), double(ri));
-  }
-  __device__ __forceinline__ void fin(const double* v) const {
-    if (!g.upd) return;  // ‖r_0‖ comes from the init launch
-    const double rr = round_to<T>(v[0]);
-    S->rr = rr;
-    if (S->hist) S->hist[S->iter] = double(tsqrt<T>(T(rr)));
-  }
-};
-
-// KB epilogue: z = L t + ε r_k (scaled: + (ε r_k)/d) ; ρ_k = r_k·z
-template <typename T, bool SCALED>
-struct EpiZF {
-  static constexpr int NDOT = 1;
-  T* z;
-  Pair<T> R;
-  const T* d;
-  T eps;
-  PcgState* S;
-  double* partials;
-  unsigned* ticket;
-  const T* r = nullptr;
-  __device__ __forceinline__ void prepare() { r = R.at(S->iter); }
-  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
-    const T ri = gld(r + i);
-    T zi;
-    if constexpr (SCALED) zi = s + (eps * ri) / gld(d + i);
-    else zi = s + eps * ri;
-    gst(z + i, zi);
-    dd_fma(dots[0], double(ri), double(zi));
-  }
-  __device__ __forceinline__ void fin(const double* v) const {
-    S->rho_prev = S->rho;
-    S->rho = round_to<T>(v[0]);
-  }
-};
-
-// KC epilogue: own-row p_k stored, deferred x += α_{k-1} p_{k-1}, q = A p_k ; π = p_k·q ;
-// α_k = ρ_k/π ; iteration k completed
-template <typename T>
-struct EpiPQ {
-  static constexpr int NDOT = 1;
-  GatherP<T> g;
-  T* x;
-  T* q;
-  PcgState* S;
-  double* partials;
-  unsigned* ticket;
-  T* pnew = nullptr;
-  T alpha_prev = T(0);
-  __device__ __forceinline__ void prepare() {
-    g.prepare();  // the epilogue's own copy of the gather (own-row p_k)
-    pnew = g.P.at(S->iter);
-    alpha_prev = T(S->alpha);
-  }
-  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
-    const T pi = g(i);
-    gst(pnew + i, pi);
-    if (!g.first) gst(x + i, gld(x + i) + alpha_prev * gld(g.pold + i));
-    gst(q + i, s);
-    dd_fma(dots[0], double(pi), double(s));
-  }
-  __device__ __forceinline__ void fin(const double* v) const {
-    const double pq = round_to<T>(v[0]);
-    S->pq = pq;
-    S->alpha = double(T(S->rho) / T(pq));
-    S->iter = S->iter + 1;
-  }
-};
-
-// after the fused loop: the deferred x += α_{k-1} p_{k-1}, p_{k-1} = P[(iter-1) & 1]
-template <typename T>
-__global__ void __launch_bounds__(kThreads) k_x_fixup_pair(int64_t n, const PcgState* S, Pair<T> P,
-                                                           T* __restrict__ x) {
-  if (S->iter < 1 || S->bb == 0.0) return;
-  const T alpha = T(S->alpha);
-  const T* p = P.at(S->iter - 1);
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
-    x[i] = x[i] + alpha * gld(p + i);
-}
 
 // init: r_0 = b - A x0 ; ‖r_0‖², ‖b‖² (+ z_0 = r_0/d, ρ_0 = r_0·z_0 for Jacobi)
 // (scipy: r = b - matvec(x) if x.any() else b.copy(); with x0 = 0 the subtraction returns b)
@@ -985,14 +824,12 @@ struct lspcg_solver {
   double eps = 0.0;
   hipStream_t stream = nullptr;  // solver-owned (capturable) stream
   void *x = nullptr, *b = nullptr, *r = nullptr, *z = nullptr, *t = nullptr, *p = nullptr, *q = nullptr,
-       *d = nullptr, *r2 = nullptr, *p2 = nullptr;  // r2 / p2: second halves of the fused ping-pong pairs
-  bool fused = false;   // current ext_spai schedule is the fused 3-kernel one (set_spai decides)
+       *d = nullptr;
   bool split = false;   // current ext_spai schedule uses the split reductions (set_spai decides)
   bool allow_split = true;  // LSPCG_SPLIT_REDUCE=0 keeps the last-arriver reductions
   int split_mode = 1;
   double* groups = nullptr;  // [GZ: <= 4096 x 2 dots x DD | GQ: <= 4096 x DD]
   int gsz_l = 1, ng_l = 1, gsz_a = 1, ng_a = 1;  // group size / count of the KB and KC launches
-  bool allow_fused = false;  // LSPCG_PCG_FUSED=1 selects it (measured slower: two gathers per entry)
   hipEvent_t* tev = nullptr;  // lspcg_solver_time_kernels: an event recorded after every launch
   int tev_i = 0;
   PcgState* S = nullptr;
@@ -1023,6 +860,8 @@ struct lspcg_solver {
   void* sv[3] = {nullptr, nullptr, nullptr};
   int svd[3] = {0, 0, 0};
   int32_t* xrow[3] = {nullptr, nullptr, nullptr};  // scalar row pointers of expanded BSR3 views
+  double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
+  int64_t dhist_cap = 0;
   int64_t small_n = 1024;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it): <= 2 rows
                            // per thread; 5 rows lose to the 5-kernel schedule
   bool small_sell = true;  // k_pcg_small reads the SELL copies (LSPCG_SMALL_SELL=0: the CSR views)
@@ -1154,30 +993,6 @@ static int launch_it(lspcg_solver* s, int w, const T* x, Pro pro, Epi epi, hipSt
   return launch_it_gx<T>(s, w, GatherVec<T>{x}, pro, epi, st);
 }
 
-// fused 3-kernel ext_spai iteration (SELL views only)
-template <typename T, bool SC>
-static int enqueue_iteration_fused(lspcg_solver* s, hipStream_t st) {
-  PcgState* S = s->S;
-  const Pair<T> R = Pair<T>::make(static_cast<T*>(s->r), static_cast<T*>(s->r2));
-  const Pair<T> P = Pair<T>::make(static_cast<T*>(s->p), static_cast<T*>(s->p2));
-  T* t = static_cast<T*>(s->t);
-  T* z = static_cast<T*>(s->z);
-  T* q = static_cast<T*>(s->q);
-  T* x = static_cast<T*>(s->x);
-  const T* d = static_cast<const T*>(s->d);
-  const GatherR<T> gr{R, q, S};
-  int rc = launch_it_gx<T>(s, 2, gr, ProDone{S}, EpiRT<T, SC>{gr, t, d, S, s->partials, s->ticket}, st);
-  if (rc) return rc;
-  rc = launch_it<T>(s, 1, static_cast<const T*>(t), ProCheck<T>{S},
-                    EpiZF<T, SC>{z, R, d, T(s->eps), S, s->partials, s->ticket}, st);
-  if (rc) return rc;
-  const GatherP<T> gp{P, z, S};
-  rc = launch_it_gx<T>(s, 0, gp, ProDone{S}, EpiPQ<T>{gp, x, q, S, s->partials, s->ticket}, st);
-  if (rc) return rc;
-  LSPCG_HIP(hipGetLastError());
-  return LSPCG_OK;
-}
-
 static int flag_run(lspcg_solver* s, hipStream_t st, int* out) {
   int h = 0;
   LSPCG_HIP(hipMemcpyAsync(&h, s->flag, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1286,9 +1101,6 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
   if (s->split)
     return s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED ? enqueue_iteration_split<T, true>(s, st)
                                                        : enqueue_iteration_split<T, false>(s, st);
-  if (s->fused)
-    return s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED ? enqueue_iteration_fused<T, true>(s, st)
-                                                       : enqueue_iteration_fused<T, false>(s, st);
   const int64_t n = s->n;
   T* x = static_cast<T*>(s->x);
   T* r = static_cast<T*>(s->r);
@@ -1384,12 +1196,6 @@ static int enqueue_init(lspcg_solver* s, hipStream_t st) {
 
 template <typename T>
 static int enqueue_fixup(lspcg_solver* s, hipStream_t st) {
-  if (s->fused) {
-    hipLaunchKernelGGL(k_x_fixup_pair<T>, dim3(elem_grid(s->n)), dim3(kThreads), 0, st, s->n, s->S,
-                       Pair<T>::make(static_cast<T*>(s->p), static_cast<T*>(s->p2)), static_cast<T*>(s->x));
-    LSPCG_HIP(hipGetLastError());
-    return LSPCG_OK;
-  }
   hipLaunchKernelGGL(k_x_fixup<T>, dim3(elem_grid(s->n)), dim3(kThreads), 0, st, s->n, s->S,
                      static_cast<const T*>(s->p), static_cast<T*>(s->x));
   LSPCG_HIP(hipGetLastError());
@@ -1494,7 +1300,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   s->n = A->n;
   const size_t vb = esize(s->dtype) * std::max<int64_t>(s->n, 1);
   LSPCG_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-  for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d, &s->r2, &s->p2}) {
+  for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d}) {
     LSPCG_HIP(hipMalloc(v, vb));
     LSPCG_HIP(hipMemsetAsync(*v, 0, vb, s->stream));
   }
@@ -1517,7 +1323,6 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   if (const char* e = std::getenv("LSPCG_NO_COMPACT")) s->compact = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SELL32")) s->sell16 = e[0] == '0';
-  if (const char* e = std::getenv("LSPCG_PCG_FUSED")) s->allow_fused = e[0] == '1';
   if (const char* e = std::getenv("LSPCG_SMALL_N")) s->small_n = std::max<int64_t>(0, std::atoll(e));
   if (const char* e = std::getenv("LSPCG_SMALL_SELL")) s->small_sell = e[0] != '0';
   if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
@@ -1543,27 +1348,47 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   LSPCG_CHECK(L->n == s->n, LSPCG_ERR_ARG, "set_spai: L has a different size than A");
   LSPCG_CHECK(L->dtype == s->dtype, LSPCG_ERR_ARG, "set_spai: L dtype differs from A dtype");
   hipStream_t cst = s->ctx->stream;
+  // LSPCG_SETUP_PROFILE=1: host wall time of each setup phase (device drained after each) on stderr
+  static const bool prof = [] { const char* e = std::getenv("LSPCG_SETUP_PROFILE"); return e && e[0] == '1'; }();
+  std::vector<std::pair<const char*, double>> phases;
+  auto t_last = std::chrono::steady_clock::now();
+  auto phase = [&](const char* name) {
+    if (!prof) return;
+    (void)hipDeviceSynchronize();
+    const auto t = std::chrono::steady_clock::now();
+    phases.emplace_back(name, std::chrono::duration<double, std::milli>(t - t_last).count());
+    t_last = t;
+  };
+  phase("enter");
   LSPCG_HIP(hipEventRecord(s->ev_t0, cst));
   if (s->LT) {
     lspcg_mat_destroy(s->LT);
     s->LT = nullptr;
   }
+  phase("free old Lt");
   bool lt_same = false;
   int rc = mat_transpose(L, &s->LT, &lt_same);
   if (rc) return rc;
+  phase(lt_same ? "transpose (symmetric pattern)" : "transpose (general)");
   if (s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) {
     rc = lspcg_mat_diagonal(s->A, s->d);
     if (rc) return rc;
   }
   int lflag = 3;
   if ((rc = make_view(s, L, &s->Lv, &s->Av, &s->own_L, nullptr, &lflag))) return rc;
+  phase("view L");
   if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT, lt_same ? &lflag : nullptr))) return rc;
+  phase("view Lt");
   if ((rc = build_sell(s, 1, &s->Lv))) return rc;
+  phase("sell L");
   if ((rc = build_sell(s, 2, &s->LTv))) return rc;
-  // the fused schedule needs SELL views; it gathers twice per entry, which costs more than the two
-  // elementwise passes it saves (DESIGN.md "PCG schedule"), so it is opt-in
-  s->fused = s->allow_fused && s->sp[0] && s->sp[1] && s->sp[2];
-  s->split = !s->fused && s->allow_split && s->sp[0] && s->sp[1] && s->sp[2];
+  phase("sell Lt");
+  if (prof) {
+    std::fprintf(stderr, "[lspcg setup] n=%lld lflag=%d", (long long)s->n, lflag);
+    for (auto& p : phases) std::fprintf(stderr, " | %s %.3f ms", p.first, p.second);
+    std::fprintf(stderr, "\n");
+  }
+  s->split = s->allow_split && s->sp[0] && s->sp[1] && s->sp[2];
   if (s->split) {  // <= 64 groups per reducing launch (or, LSPCG_SPLIT_REDUCE=2, no groups at all)
     const bool nogroups = s->split_mode == 2;
     auto groups = [nogroups](int64_t grid, int* gsz, int* ng) {
@@ -1629,8 +1454,18 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   if (max_iter <= 0) max_iter = n;
   hipStream_t st = s->stream;
   const size_t vb = esize(s->dtype) * n;
-  double* dhist = nullptr;
-  if (res_hist) LSPCG_HIP(hipMalloc(&dhist, sizeof(double) * (max_iter + 2)));
+  double* dhist = nullptr;  // the solver's persistent history buffer, grown on demand
+  if (res_hist) {
+    if (s->dhist_cap < max_iter + 2) {
+      LSPCG_HIP(hipStreamSynchronize(st));
+      (void)hipFree(s->dhist);
+      s->dhist = nullptr;
+      s->dhist_cap = 0;
+      LSPCG_HIP(hipMalloc(&s->dhist, sizeof(double) * (max_iter + 2)));
+      s->dhist_cap = max_iter + 2;
+    }
+    dhist = s->dhist;
+  }
 
   LSPCG_HIP(hipEventRecord(s->ev_in, s->ctx->stream));
   LSPCG_HIP(hipStreamWaitEvent(st, s->ev_in, 0));
@@ -1741,9 +1576,11 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   const int64_t it = (fin.done == 3) ? max_iter : fin.iter;
   *iters = it;
   if (res_hist) {
+    // entries 0..fin.iter were written; a non-finite residual stops early while iters reports
+    // max_iter (pymathprim's count), so the rest of 0..iters is NaN-filled
     const int64_t cnt = std::min<int64_t>(fin.iter, max_iter) + 1;
     LSPCG_HIP(hipMemcpy(res_hist, dhist, sizeof(double) * cnt, hipMemcpyDeviceToHost));
-    LSPCG_HIP(hipFree(dhist));
+    for (int64_t k = cnt; k <= it; ++k) res_hist[k] = NAN;
   }
   return (fin.done == 1) ? LSPCG_OK : LSPCG_NOT_CONVERGED;
 }
@@ -1801,7 +1638,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipStreamSynchronize(s->stream);
   for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
-  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d, s->r2, s->p2}) (void)hipFree(v);
+  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d}) (void)hipFree(v);
   (void)hipFree(s->S);
   (void)hipHostFree(s->hS);
   (void)hipFree(s->partials);
@@ -1820,6 +1657,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
     s->spat[w].release();
   }
   (void)hipFree(s->flag);
+  (void)hipFree(s->dhist);
   (void)hipStreamDestroy(s->stream);
   delete s;
   return LSPCG_OK;

@@ -8,8 +8,13 @@ Drop-in for the native solver the reference calls at
 
 Arithmetic follows scipy 1.15 ``cg`` (the reference's own CPU restatement,
 validate.py:163-341): see ``include/lspcg.h`` and DESIGN.md.  ``x`` is updated in place
-with the solution (numpy arrays or device tensors).  Only the HIP path exists:
-``device="cpu"`` raises (the CPU solver is the oracle, which the product never uses).
+with the solution (numpy arrays or device tensors).  Only the HIP path exists.
+
+Device contract: the reference's own defaults are ``device="cpu"``
+(``validate.py:61,98``: pymathprim's CPU backend), and ``infer.py:323-325`` calls both
+devices.  This class replaces the ``device="cuda"`` backend only; the CPU row stays with
+pymathprim / scipy.  ``device="cpu"`` raises ``ValueError`` loudly
+instead of silently running somewhere else -- there is no CPU solver in the product.
 """
 from __future__ import annotations
 
@@ -100,8 +105,8 @@ class PreconditionedConjugateGradient:
     def solve(self, b: torch.Tensor, x: torch.Tensor, rtol: float = 1e-6, max_iter: int = 0,
               return_history: bool = False):
         """Device-tensor form: returns ``(iters, converged, solve_time_s[, res_hist])``."""
-        assert b.numel() == self.n and x.numel() == self.n
-        assert b.is_cuda and x.is_cuda and b.is_contiguous() and x.is_contiguous()
+        self._check_vector("b", b)
+        self._check_vector("x", x)
         mi = int(max_iter) if max_iter and max_iter > 0 else self.n
         it = C.c_int64()
         ms = C.c_double()
@@ -111,15 +116,33 @@ class PreconditionedConjugateGradient:
                        allow_not_converged=True)
         out = (it.value, rc == _lib.OK, ms.value / 1e3)
         if return_history:
-            out = out + (hist[: min(it.value, mi) + 1].copy(),)
+            out = out + (hist[: min(it.value, mi) + 1].copy(),)  # NaN after a non-finite stop (lspcg.h)
         return out
+
+    @property
+    def torch_dtype(self) -> torch.dtype:
+        return torch.float32 if self.dtype == np.float32 else torch.float64
+
+    def _check_vector(self, name: str, v: torch.Tensor):
+        """The C ABI copies n * sizeof(dtype) bytes from / to these pointers: reject anything
+        that is not a contiguous length-n vector of the solver's dtype on the solver's device."""
+        if not isinstance(v, torch.Tensor):
+            raise TypeError(f"{name} must be a torch tensor on {self.ctx.torch_device}")
+        if v.numel() != self.n:
+            raise ValueError(f"{name} has {v.numel()} entries, the system has {self.n}")
+        if v.dtype != self.torch_dtype:
+            raise TypeError(f"{name} is {v.dtype}, the solver computes in {self.torch_dtype}")
+        if v.device != self.ctx.torch_device:
+            raise ValueError(f"{name} is on {v.device}, the solver runs on {self.ctx.torch_device}")
+        if not v.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
 
     KERNELS = ("KA t=L^T r", "KB z=L t+eps r, rho", "UP p, x", "KC q=A p, pi", "UR r")
 
     def time_kernels(self, b: torch.Tensor, iters: int = 40) -> dict:
         """Measurement only: mean device time (s) of each launch of the ext_spai iteration
         (HIP events around every launch, ``iters`` iterations from x0 = 0, no graphs)."""
-        assert b.is_cuda and b.numel() == self.n
+        self._check_vector("b", b)
         out = (C.c_double * 8)()
         nk = C.c_int()
         _lib.call("lspcg_solver_time_kernels", self.handle, C.c_void_p(b.data_ptr()), int(iters), out, C.byref(nk))
@@ -136,7 +159,7 @@ class PreconditionedConjugateGradient:
                 if not self._is_installed(L, eps):
                     prec = self.set_spai(L, eps, block_size=getattr(L, "block_size", 1)
                                          if isinstance(L, DeviceMatrix) else 1)
-        tdt = torch.float32 if self.dtype == np.float32 else torch.float64
+        tdt = self.torch_dtype
         dev = self.ctx.torch_device
         bt = torch.as_tensor(b).to(device=dev, dtype=tdt).contiguous().reshape(-1)
         xt = torch.as_tensor(x).to(device=dev, dtype=tdt).contiguous().reshape(-1)

@@ -9,8 +9,12 @@ Same names, arguments, return values and error behaviour as the reference:
 * ``get_pcg_iter_time``          -- validate.py:89-121 (ext_spai, never raises)
 * ``get_pcg_scaled_iter_time``   -- validate.py:124-160 (ext_spai_scaled)
 
-Matrices may be scipy CSR (uploaded) or :class:`DeviceMatrix` (already in HBM);
-``device`` must be a GPU device -- there is no CPU solver in the product.
+Matrices may be scipy CSR (uploaded) or :class:`DeviceMatrix` (already in HBM).
+
+Device contract: the reference defaults ``device="cpu"`` (validate.py:61,98), i.e.
+pymathprim's CPU backend.  These functions default to ``device="cuda"`` and replace the GPU
+backend only; the reference's CPU rows keep calling pymathprim / scipy.
+``device="cpu"`` raises ``ValueError`` -- there is no CPU solver in the product.
 Right-hand sides are formed on the device exactly as ``b = A @ gt`` (bit-identical to
 scipy's csr_matvec).
 """

@@ -17,13 +17,22 @@ Fixtures (inputs and the reference's outputs, data only):
   gnn_init.npz     -- state_dict of neural_cg.nn.gnns.NodeEdgeProcessing (config/gnn.yaml)
                       constructed after torch.manual_seed(0)
   make_data.npz    -- neural_cg/data.py make_data outputs for one masked block matrix
+  pcg_traj.npz     -- the bench-sized trajectories (n = 4,096 / 19,683 / 65,536 and the
+                      synthetic C1 system, n = 10,240): the reference's scipy entry points run
+                      with scipy's ``cg`` wrapped (``rval.cg``) so that every ‖r_k‖ scipy tests
+                      (the argument of each preconditioner call) and the returned x are kept;
+                      beside them, from the oracle (labelled ``oracle_*``, not the reference):
+                      the correctly-rounded-dot trajectory and the spread of the admissible dot
+                      orderings (count band, first iteration where their histories part by
+                      more than 1e-12, largest x / true-residual difference)
   folder_free/, folder_fixed/ + folder.npz
                    -- two on-disk datasets in the datagen_helper.py folder format (written by
                       dataset.FolderWriter: .mtx + features/mask/rhs/lhs; fixed-topology 3x3
                       blocks with demo.mtx + value vectors + shared features) and the outputs of
                       the reference's FolderDataset.get(i) for every sample
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py            # every fixture
+    python tests/golden/make_golden.py traj       # pcg_traj.npz only
 """
 from __future__ import annotations
 
@@ -107,8 +116,140 @@ def reference_synthetic():
     return ns["generate_spd_sparse_matrix"]
 
 
+def spai_factor(A, seed=5):
+    """Deterministic stand-in for the GNN's L on A's pattern (fp32-representable values, like
+    the GNN output): diagonal 1/sqrt(d), off-diagonal N(0, 0.05²)/sqrt(d_row)."""
+    n = A.shape[0]
+    rng = np.random.default_rng(seed)
+    L = A.copy()
+    rows = np.repeat(np.arange(n), np.diff(A.indptr))
+    d = np.abs(A.diagonal()) + 1e-12
+    L.data = rng.normal(size=A.nnz) * 0.05 / np.sqrt(d[rows])
+    dg = rows == A.indices
+    L.data[dg] = 1.0 / np.sqrt(d[rows[dg]])
+    L.data = L.data.astype(np.float32).astype(np.float64)
+    return L
+
+
+class RecordingCG:
+    """Stands in for the ``cg`` name inside the reference's validate module: calls scipy's cg
+    with the same arguments, recording ‖r_k‖ (np.linalg.norm of the vector scipy hands to the
+    preconditioner -- the value it has just compared with atol) and the returned x.  With M=None
+    the recorder is the identity that returns its argument itself, like scipy's
+    IdentityOperator, so the arithmetic is untouched."""
+
+    def __init__(self):
+        from scipy.sparse.linalg import LinearOperator, cg
+
+        self._cg, self._LO = cg, LinearOperator
+        self.hist, self.x, self.count = [], None, 0
+
+    def __call__(self, A, b, M=None, callback=None, **kw):
+        hist = self.hist = []
+        inner = M
+        rec = self
+
+        class Rec(self._LO):
+            def __init__(self):
+                super().__init__(np.dtype(np.float64), A.shape)
+
+            def _matvec(self, v):
+                hist.append(float(np.linalg.norm(v)))
+                return v if inner is None else inner.matvec(v)
+
+        def cb(xk):
+            rec.count += 1
+            if callback is not None:
+                callback(xk)
+
+        self.count = 0
+        x, info = self._cg(A, b, M=Rec(), callback=cb, **kw)
+        self.x = np.array(x, dtype=np.float64)
+        return x, info
+
+
+def traj_fixtures(rval):
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from oracle import linalg as O
+
+    rec = RecordingCG()
+    rval.cg = rec
+    systems = {
+        "poisson64": P.poisson2d_grid(64, 64)[:2],
+        "kuhn27": (P.kuhn_laplacian(27), None),
+        "poisson256": P.poisson2d_grid(256, 256)[:2],
+        "synthetic10240": (P.synthetic_c1(), None),  # BASELINE config 1 (unpreconditioned only)
+    }
+    out = {}
+    for name, (A, mask) in systems.items():
+        A = sp.csr_matrix(A)
+        A.sort_indices()
+        n = A.shape[0]
+        gt = np.ones(n) if mask is None else mask.ravel().astype(np.float64)
+        L = spai_factor(A)
+        eps = 3e-3
+        rtol = 1e-8
+        out[f"{name}__indptr"], out[f"{name}__indices"], out[f"{name}__data"] = A.indptr, A.indices, A.data
+        out[f"{name}__gt"], out[f"{name}__eps"], out[f"{name}__rtol"] = gt, np.array(eps), np.array(rtol)
+        methods = ("none",) if name.startswith("synthetic") else ("none", "diagonal", "ext_spai", "ext_spai_scaled")
+        if len(methods) > 1:
+            out[f"{name}__L_data"] = L.data
+        b = A @ gt
+        for m in methods:
+            if m == "none":
+                cnt = rval.get_cg_iter_time_scipy(A, gt, rtol=rtol)
+                ps = None
+            elif m == "diagonal":
+                cnt = rval.get_pcg_diagonal_iter_time_scipy(A, gt, rtol=rtol)
+                ps = O.diagonal_operator(A)
+            elif m == "ext_spai":
+                cnt = rval.get_pcg_iter_time_scipy(A, gt, L, eps, rtol=rtol)
+                ps = O.spai_operator(L, eps)
+            else:
+                cnt = rval.get_pcg_scaled_iter_time_scipy(A, gt, L, eps, rtol=rtol)
+                ps = O.spai_scaled_operator(A, L, eps)
+            assert cnt == rec.count and len(rec.hist) == cnt
+            t = f"{name}__{m}"
+            out[f"{t}__count"] = np.array(cnt)
+            out[f"{t}__x"] = rec.x
+            out[f"{t}__hist"] = np.array(rec.hist)  # ‖r_k‖, k = 0 .. count-1 (reference)
+            # the oracle restatement must reproduce the reference bit for bit with numpy dots
+            it_np, x_np, h_np = O.pcg(A, b, ps, rtol=rtol, dot="numpy")
+            assert it_np == cnt and np.array_equal(x_np, rec.x) and np.array_equal(h_np[:cnt], rec.hist), (name, m)
+            # admissible dot orderings (pymathprim's own order is unknowable): their spread
+            runs = {d: O.pcg(A, b, ps, rtol=rtol, dot=d) for d in O.DOTS}
+            its = [r[0] for r in runs.values()]
+            nb = np.linalg.norm(b)
+            tres = {d: np.linalg.norm(b - A @ r[1]) / nb for d, r in runs.items()}
+            xs = {d: np.linalg.norm(r[1] - rec.x) / np.linalg.norm(rec.x) for d, r in runs.items()}
+            kstar = []
+            for d, r in runs.items():
+                h = np.asarray(r[2])
+                k = min(len(h), cnt)
+                rd = np.abs(h[:k] - rec.hist[:k]) / np.asarray(rec.hist[:k])
+                kstar.append(int(np.argmax(rd > 1e-12)) if np.any(rd > 1e-12) else k)
+            out[f"{t}__oracle_count_band"] = np.array([min(its), max(its)])
+            out[f"{t}__oracle_hist_agree_k"] = np.array(min(kstar))
+            out[f"{t}__oracle_x_spread"] = np.array(max(xs.values()))
+            out[f"{t}__oracle_true_res_spread"] = np.array(max(tres.values()) - min(tres.values()))
+            out[f"{t}__true_res"] = np.array(tres["numpy"])
+            ex = runs["exact"]
+            out[f"{t}__oracle_exact_count"] = np.array(ex[0])
+            out[f"{t}__oracle_exact_x"] = ex[1]
+            out[f"{t}__oracle_exact_hist"] = np.asarray(ex[2])
+            print(name, m, cnt, "band", (min(its), max(its)), "agree_k", min(kstar), "x spread %.1e" % max(xs.values()),
+                  flush=True)
+    np.savez_compressed(OUT / "pcg_traj.npz", **out)
+
+
 def main():
     install_shims()
+    if sys.argv[1:] == ["traj"]:
+        from neural_cg.utils import validate as rval
+
+        sys.path.insert(0, str(ROOT))
+        traj_fixtures(rval)
+        return
     from neural_cg import data as rdata
     from neural_cg.nn import gnns as rgnn
     from neural_cg.utils import validate as rval

@@ -30,9 +30,17 @@ def test_device_to_csr_matches_reference(gpu_ctx):
         assert np.array_equal(got.data, z[f"{c}__data"]), c
 
 
+@pytest.mark.parametrize("small_n", ["0", None])
 @pytest.mark.parametrize("method", ["none", "diagonal", "ext_spai", "ext_spai_scaled"])
-def test_pcg_counts_match_reference(gpu_ctx, method):
+def test_pcg_counts_match_reference(gpu_ctx, method, small_n, monkeypatch):
+    """small_n None: the default (these n <= 600 systems take the one-workgroup solve); "0": the
+    multi-kernel schedule the bench times."""
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    if small_n is not None:
+        monkeypatch.setenv("LSPCG_SMALL_N", small_n)
+    else:
+        monkeypatch.delenv("LSPCG_SMALL_N", raising=False)
 
     z = _load("pcg_counts.npz")
     for name in sorted({k.split("__")[0] for k in z.files}):

@@ -78,6 +78,14 @@ def test_sell_skips_padding_with_inf(gpu_ctx):
         assert np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])
 
 
+def _v(no_sell="0", sell32="0", split="1", small="0"):
+    return {"LSPCG_NO_SELL": no_sell, "LSPCG_SELL32": sell32, "LSPCG_SPLIT_REDUCE": split, "LSPCG_SMALL_N": small}
+
+
+VARIANTS = [_v(no_sell="1"), _v(sell32="1"), _v(), _v(split="0"),
+            _v(small="1000000"), _v(sell32="1", small="1000000"), _v(no_sell="1", small="1000000")]
+
+
 @pytest.mark.parametrize("precond", ["none", "diagonal", "ext_spai", "ext_spai_scaled"])
 @pytest.mark.parametrize("case", [0, 1, 2, 3])
 def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
@@ -88,20 +96,13 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
     n = A.shape[0]
     b = torch.from_numpy(A @ np.ones(n)).cuda()
     out = []
-    # CSR views (5 kernels); SELL int32 columns / 16-bit offsets, 5-kernel and fused 3-kernel schedules
-    # (+ split group reductions vs last-arriver reductions on the SELL 16-bit views); last: the
-    # one-workgroup solve (k_pcg_small) on the SELL copies and on the CSR views (LSPCG_NO_SELL=1),
-    # which every other variant has switched off
-    for env, env32, fused, split, small in (("1", "0", "0", "1", "0"), ("0", "1", "0", "1", "0"),
-                                            ("0", "0", "0", "1", "0"), ("0", "0", "0", "0", "0"),
-                                            ("0", "1", "1", "1", "0"), ("0", "0", "1", "1", "0"),
-                                            ("0", "0", "0", "1", "1000000"), ("0", "1", "0", "1", "1000000"),
-                                            ("1", "0", "0", "1", "1000000")):
-        monkeypatch.setenv("LSPCG_NO_SELL", env)
-        monkeypatch.setenv("LSPCG_SELL32", env32)
-        monkeypatch.setenv("LSPCG_PCG_FUSED", fused)
-        monkeypatch.setenv("LSPCG_SPLIT_REDUCE", split)
-        monkeypatch.setenv("LSPCG_SMALL_N", small)
+    # CSR views (5 kernels); SELL int32 columns / 16-bit offsets (+ split group reductions vs
+    # last-arriver reductions on the SELL 16-bit views); then the one-workgroup solve
+    # (k_pcg_small) on the SELL copies and on the CSR views (LSPCG_NO_SELL=1), which every other
+    # variant has switched off
+    for env in VARIANTS:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
         if precond.startswith("ext_spai"):
             s.set_spai(_cases.spai_like(A), 1e-3)

@@ -160,3 +160,29 @@ def test_oracle_ic_operator_matches_scipy_triangular_solves():
     T = sp.csr_matrix(sp.block_diag([np.array([[2.0 + k, -1.0], [-1.0, 3.0]]) for k in range(15)]))
     Lai = OP.ainv_spai_factor(T)
     np.testing.assert_allclose((Lai @ Lai.T).toarray() @ T.toarray(), np.eye(30), atol=1e-12)
+
+
+def traj_system(z, name):
+    """One system of pcg_traj.npz: (A, L or None, gt, eps, rtol)."""
+    ip, ix, d = z[f"{name}__indptr"], z[f"{name}__indices"], z[f"{name}__data"]
+    n = ip.size - 1
+    A = sp.csr_matrix((d, ix, ip), shape=(n, n))
+    L = sp.csr_matrix((z[f"{name}__L_data"], ix, ip), shape=(n, n)) if f"{name}__L_data" in z.files else None
+    return A, L, z[f"{name}__gt"], float(z[f"{name}__eps"]), float(z[f"{name}__rtol"])
+
+
+@pytest.mark.parametrize("name,method", [("poisson64", m) for m in ("none", "diagonal", "ext_spai", "ext_spai_scaled")]
+                         + [("kuhn27", "ext_spai"), ("synthetic10240", "none")])
+def test_pcg_trajectory_matches_reference(name, method):
+    """The oracle's numpy-dot PCG reproduces the reference's recorded trajectory (count, every
+    ‖r_k‖ scipy tested, the returned x) bit for bit -- n = 4,096 / 19,683 and BASELINE config 1
+    (n = 10,240, the reference's 3229 iterations)."""
+    z = _load("pcg_traj.npz")
+    A, L, gt, eps, rtol = traj_system(z, name)
+    t = f"{name}__{method}"
+    it, x, h = O.pcg(A, A @ gt, _psolve(method, A, L, eps), rtol=rtol, dot="numpy")
+    assert it == int(z[f"{t}__count"])
+    assert np.array_equal(np.asarray(h[:it]), z[f"{t}__hist"])
+    assert np.array_equal(x, z[f"{t}__x"])
+    if name == "synthetic10240":
+        assert it == 3229  # SURVEY.md 6: the reference's count on config 1 in this container
