@@ -16,6 +16,9 @@
  *   csr @ diags(rsqrt_diag) (scaled_workspace.py:210-211)        -> lspcg_mat_scale_columns
  *   neural_cg/nn/gnns.py:77-97 NodeEdgeProcessing.forward
  *       (+ basic_layers.py:73-109 FeedForward, :145-225 MPLayer) -> lspcg_gnn_forward
+ *   neural_cg/nn/basic_layers.py:112-142 GraphSpmv.forward        -> lspcg_graph_spmv
+ *   neural_cg/nn/basic_layers.py:228-261 AATPE.forward            -> lspcg_graph_aatpe
+ *       (edge lists prepared once by lspcg_graph_create)
  *
  * Conventions: plain pointers and sizes only.  Vector arguments of compute calls are
  * DEVICE pointers; matrix/weight uploads accept host or device pointers.  All work is
@@ -55,6 +58,7 @@ typedef struct lspcg_ctx lspcg_ctx;
 typedef struct lspcg_mat lspcg_mat;
 typedef struct lspcg_solver lspcg_solver;
 typedef struct lspcg_gnn lspcg_gnn;
+typedef struct lspcg_graph lspcg_graph;
 
 const char* lspcg_last_error(void);
 int lspcg_version(void);
@@ -180,6 +184,21 @@ int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* we
 int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const int64_t* edge_index,
                       const float* edge_attr, float* out);
 int lspcg_gnn_destroy(lspcg_gnn* g);
+
+/* ---- block SpMV over an edge list (GraphSpmv / AATPE, basic_layers.py:112-142, 228-261) ----
+ * edge_index: device int64 [2,E], any order, duplicates summed (PyG scatter-add semantics);
+ * N nodes of bs (1 or 3) components.  Values [E,bs,bs], x / y / mask / diag [N*bs], all of
+ * `dtype`, device pointers; mask and diag nullable. */
+int lspcg_graph_create(lspcg_ctx* ctx, int64_t N, int64_t E, int bs, const int64_t* edge_index, lspcg_graph** out);
+int lspcg_graph_destroy(lspcg_graph* g);
+/* GraphSpmv(use_transpose).forward: y = A x (transpose = 0: block (ei[0], ei[1]) multiplies
+ * x[ei[1]], summed at ei[0]) or y = Aᵀ x (transpose = 1), then y *= mask */
+int lspcg_graph_spmv(lspcg_graph* g, const void* vals, int dtype, int transpose, const void* x, const void* mask,
+                     void* y);
+/* AATPE(epsilon).forward: t = (mask ⊙ Aᵀx) ⊙ diag ; y = mask ⊙ (A t) + (ε x) ⊙ diag
+ * (t: caller-provided [N*bs] scratch that receives AᵀX, the reference's AT_x) */
+int lspcg_graph_aatpe(lspcg_graph* g, const void* vals, int dtype, double epsilon, const void* x, const void* mask,
+                      const void* diag, void* t, void* y);
 
 #ifdef __cplusplus
 }

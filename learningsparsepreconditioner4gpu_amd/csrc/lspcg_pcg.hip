@@ -541,18 +541,19 @@ constexpr int kSmallRows = 5;       // largest rows per thread (template R = 1, 
 constexpr int64_t kSmallLds = 61440;  // dynamic LDS: 3 gathered vectors
 constexpr int kSmallQB = 2;  // SELL groups (4 entries each) loaded per wait (4 measured slower: 13.0 vs 9.8 us per iteration)
 
-// row i; [b, e): its CSR entry range, or (SELL) its slice's group range
-template <typename T>
-__device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, int32_t i, const T* xs) {
+// row i; [b, e): its CSR entry range, or (SELL) its slice's group range; gx(c) reads the
+// gathered vector (LDS in the one-workgroup solve, sc1 global loads in the persistent one)
+template <typename T, int QB, class Gx>
+__device__ __forceinline__ T sell_row(const CsrView& M, int32_t b, int32_t e, int32_t i, Gx gx) {
   T acc = T(0);
   if (M.gp) {
     const int32_t lane = i & 63, base = i & ~63;
-    for (int32_t q0 = b; q0 < e; q0 += kSmallQB) {
-      T v[4 * kSmallQB];
-      int32_t c[4 * kSmallQB];
-      bool ok[4 * kSmallQB];
+    for (int32_t q0 = b; q0 < e; q0 += QB) {
+      T v[4 * QB];
+      int32_t c[4 * QB];
+      bool ok[4 * QB];
 #pragma unroll
-      for (int u = 0; u < kSmallQB; ++u) {
+      for (int u = 0; u < QB; ++u) {
         const size_t off = 256 * size_t(min(q0 + u, e - 1)) + 4 * lane;
         if (M.sf32) {
           const f32x4 a = *(const __attribute__((address_space(1))) f32x4*)(static_cast<const float*>(M.sv) + off);
@@ -580,9 +581,12 @@ __device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, i
           }
         }
       }
+      T xv[4 * QB];
 #pragma unroll
-      for (int u = 0; u < 4 * kSmallQB; ++u)
-        if (ok[u]) acc = acc + v[u] * xs[c[u]];
+      for (int u = 0; u < 4 * QB; ++u) xv[u] = gx(c[u]);
+#pragma unroll
+      for (int u = 0; u < 4 * QB; ++u)
+        if (ok[u]) acc = acc + v[u] * xv[u];
     }
     return acc;
   }
@@ -595,11 +599,19 @@ __device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, i
       c[u] = gld(M.ci + k);
       v[u] = M.f32 ? T(gld(static_cast<const float*>(M.v) + k)) : gld(static_cast<const T*>(M.v) + k);
     }
+    T xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xv[u] = gx(c[u]);
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (k0 + u < e) acc = acc + v[u] * xs[c[u]];
+      if (k0 + u < e) acc = acc + v[u] * xv[u];
   }
   return acc;
+}
+
+template <typename T>
+__device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, int32_t i, const T* xs) {
+  return sell_row<T, kSmallQB>(M, b, e, i, [xs](int32_t c) { return xs[c]; });
 }
 
 // fixed-order workgroup sum of N compensated dots, rounded to T, returned to every thread: wave
@@ -763,6 +775,301 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
   }
 }
 
+// ---- mid-size systems: the whole solve in ONE persistent launch over G workgroups ---------
+// Between a few thousand and a few hundred thousand unknowns an iteration of the 5-launch
+// schedule is latency, not bytes (~22 us at n = 65 k).  k_pcg_persist keeps a
+// resident grid of G <= #CU workgroups (one per CU) for the whole scipy loop; thread `tid` of
+// workgroup g owns rows (g R + m) 512 + tid, m < R, whose x, r, z, p, q live in registers.
+// Only the three gathered vectors (r for Lᵀ, t for L, p for A) and the per-workgroup dot
+// partials cross workgroups, through the hand-off of MI355X_MICROARCH.md "Valid forms", row 1:
+// every byte stored with sc1 (agent-scope relaxed) stores, every storing wave drains them
+// (s_waitcnt vmcnt(0)) before the workgroup barrier, ONE lane per workgroup signals with an
+// agent-scope atomic add on its XCD-sharded arrival counter, wave 0 polls the 8 shards with
+// sc1 loads, the other waves wait at a workgroup barrier, and every load of handed-off bytes is
+// an sc1 load -- no L1 invalidate or L2 write-back fence on the critical path.  The matrix
+// views are read with plain loads (read-only during the solve: they stay in L1 / L2).
+// Reductions: each workgroup publishes its compensated (DD) partial; after the barrier EVERY
+// workgroup sums all G partials in the same fixed order, so every workgroup takes the same
+// convergence decision at the same iteration and no extra barrier is needed.  Expressions,
+// row-sum order and the top-of-loop test are those of the split schedule (same bits).
+// Every spin is bounded: a workgroup that waits too long sets the timeout word and leaves,
+// so the grid always drains (the host reports LSPCG_ERR_HIP).
+constexpr int kPersistThreads = 512;
+constexpr int kPersistShards = 8;            // arrival counters, one per blockIdx % 8 (one 128-B line each)
+constexpr int kPersistCntStride = 32;        // uint32 per shard line
+constexpr int kPersistErr = kPersistShards * kPersistCntStride;  // timeout word after the shards
+constexpr size_t kPersistSyncBytes = sizeof(unsigned) * (kPersistErr + 32);  // memset per solve (x16 B)
+constexpr int kPersistQB = 4;                // SELL groups per batch (global sc1 gathers: more in flight)
+constexpr unsigned kPersistSpin = 1u << 22;  // polls (~1 us each) before a barrier gives up
+constexpr unsigned kPersistMaxWG = 256;      // persist_total sums <= 4 partials per lane
+constexpr int kPersistMaxRows = 4;           // rows per thread (template R = 1, 2, 4)
+
+struct PersistSync {
+  unsigned* cnt;   // [kPersistSyncBytes / 4], zeroed before every launch
+  double* pz;      // [G][2 dots][s, c]: ρ_k and ‖r_k‖² partials
+  double* pq;      // [G][s, c]: π_k partials
+};
+
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+  if constexpr (sizeof(T) == 8) {
+    const unsigned long long u = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    return __longlong_as_double(static_cast<long long>(u));
+  } else {
+    const unsigned u = __hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __uint_as_float(u);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+  if constexpr (sizeof(T) == 8)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                       static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  else
+    __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Grid barrier number `epoch` (1, 2, ...): returns false after a timeout (uniform per workgroup).
+__device__ __forceinline__ bool persist_sync(unsigned* cnt, unsigned epoch, unsigned G, int* s_ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const unsigned lane = threadIdx.x;
+    if (lane == 0)
+      __hip_atomic_fetch_add(cnt + (blockIdx.x % kPersistShards) * kPersistCntStride, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = epoch * G;
+    bool ok = false;
+    for (unsigned spin = 0; spin < kPersistSpin; ++spin) {
+      // lanes 0..7 read the shards, lane 8 the timeout word; the decision is wave-uniform
+      const unsigned w = lane <= kPersistShards
+                             ? __hip_atomic_load(cnt + (lane < kPersistShards ? lane * kPersistCntStride : kPersistErr),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0u;
+      unsigned v = lane < kPersistShards ? w : 0u;
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (__shfl(v, 0, 64) >= target) {
+        ok = true;
+        break;
+      }
+      if (__shfl(w, kPersistShards, 64) != 0u) break;  // another workgroup timed out
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) {
+      if (!ok) __hip_atomic_store(cnt + kPersistErr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_ok = ok;
+    }
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
+// this workgroup's N compensated partials -> pub[blockIdx.x][N] (sc1), before the barrier
+template <int N>
+__device__ __forceinline__ void persist_publish(DD (&v)[N], DD* lds, double* pub) {
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  wave_reduce_dd<N>(v);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) lds[wid * N + j] = v[j];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      DD a = lds[j];
+      for (int w = 1; w < kPersistThreads / 64; ++w) a = dd_add(a, lds[w * N + j]);
+      st_agent_f64(pub + (size_t(blockIdx.x) * N + j) * 2 + 0, a.s);
+      st_agent_f64(pub + (size_t(blockIdx.x) * N + j) * 2 + 1, a.c);
+    }
+  }
+}
+
+// after the barrier: the sum of all G partials in a fixed order (lane l: l, l+64, ...; then the
+// wave butterfly), rounded to T, identical in every workgroup; wave 0 computes, LDS broadcasts
+template <typename T, int N>
+__device__ __forceinline__ void persist_total(const double* pub, unsigned G, double* lds_out, double (&out)[N]) {
+  if (threadIdx.x < 64) {
+    const unsigned lane = threadIdx.x;
+    // G <= kPersistMaxWG = 4 x 64: every partial a lane sums is loaded before the first add
+    double ps[4][N], pc[4][N];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned g = min(lane + 64u * u, G - 1);
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        ps[u][j] = ld_agent_f64(pub + (size_t(g) * N + j) * 2);
+        pc[u][j] = ld_agent_f64(pub + (size_t(g) * N + j) * 2 + 1);
+      }
+    }
+    DD a[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) a[j] = dd_zero();
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = lane + 64u * u < G;
+#pragma unroll
+      for (int j = 0; j < N; ++j) a[j] = dd_add(a[j], DD{ok ? ps[u][j] : 0.0, ok ? pc[u][j] : 0.0});
+    }
+    wave_reduce_dd<N>(a);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < N; ++j) lds_out[j] = round_to<T>(dd_value(a[j]));
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < N; ++j) out[j] = lds_out[j];
+}
+
+template <typename T, int PRE, int R>
+__global__ void __launch_bounds__(kPersistThreads) k_pcg_persist(int32_t n, PcgState* S, CsrView A, CsrView L,
+                                                                 CsrView LT, const T* __restrict__ d, T* x, T* r, T* p,
+                                                                 T* t, PersistSync sy) {
+  constexpr bool SPAI = PRE == LSPCG_PRECOND_EXT_SPAI || PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  constexpr bool SCALED = PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  __shared__ DD lds_dd[kPersistThreads / 64 * 2];
+  __shared__ double lds_tot[2];
+  __shared__ int s_ok;
+  if (S->done) return;  // ‖b‖ = 0 (init): uniform
+  const unsigned G = gridDim.x;
+  const int tid = threadIdx.x;
+  const T eps = T(S->eps);
+  const double atol = S->atol;
+  const int64_t max_iter = S->max_iter;
+  double* hist = S->hist;
+  const double rr0 = S->rr;
+  double rho_prev = S->rho, rho = S->rho, pq = S->pq;
+  T alpha = T(S->alpha);
+  int64_t k = S->iter;
+  int code = 0;
+  unsigned epoch = 0;
+  const bool lead = blockIdx.x == 0 && tid == 0;
+  bool own[R];
+  int32_t row[R], ab[R], ae[R], lb[R], le[R], tb[R], te[R];
+  T xr[R], rr_[R], pr[R], dr[R];
+#pragma unroll
+  for (int m = 0; m < R; ++m) {
+    row[m] = (int32_t(blockIdx.x) * R + m) * kPersistThreads + tid;
+    own[m] = row[m] < n;
+    const int32_t i = own[m] ? row[m] : 0;
+    auto range = [&](const CsrView& M, int32_t& b, int32_t& e) {  // SELL groups of the row's slice
+      b = M.gp[i >> 6];
+      e = own[m] ? M.gp[(i >> 6) + 1] : b;
+    };
+    range(A, ab[m], ae[m]);
+    if constexpr (SPAI) {
+      range(L, lb[m], le[m]);
+      range(LT, tb[m], te[m]);
+    }
+    xr[m] = own[m] ? x[i] : T(0);
+    rr_[m] = own[m] ? r[i] : T(0);
+    pr[m] = T(0);
+    if constexpr (SCALED || PRE == LSPCG_PRECOND_DIAGONAL) dr[m] = own[m] ? d[i] : T(1);
+  }
+  auto gath = [](const T* v) { return [v](int32_t c) { return ld_sc1<T>(v + c); }; };
+  bool alive = true;
+  for (;; ++k) {
+    // t = Lᵀ r (scaled: / d) -- r_k of every workgroup is visible (previous barrier / launch)
+    if constexpr (SPAI) {
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        if (!own[m]) continue;
+        const T s = sell_row<T, kPersistQB>(LT, tb[m], te[m], row[m], gath(r));
+        st_sc1<T>(t + row[m], SCALED ? s / dr[m] : s);
+      }
+      if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
+    }
+    // z = M⁻¹ r ; partials of ρ_k = r·z and ‖r_k‖²
+    DD dz[2] = {dd_zero(), dd_zero()};
+    T zr[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      const T ri = rr_[m];
+      T zi;
+      if constexpr (SCALED) zi = own[m] ? sell_row<T, kPersistQB>(L, lb[m], le[m], row[m], gath(t)) + (eps * ri) / dr[m] : T(0);
+      else if constexpr (SPAI) zi = own[m] ? sell_row<T, kPersistQB>(L, lb[m], le[m], row[m], gath(t)) + eps * ri : T(0);
+      else if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) zi = ri / dr[m];
+      else zi = ri;
+      zr[m] = zi;
+      if (own[m]) {
+        dd_fma(dz[0], double(ri), double(zi));
+        dd_fma(dz[1], double(ri), double(ri));
+      }
+    }
+    persist_publish<2>(dz, lds_dd, sy.pz);
+    if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
+    double v2[2];
+    persist_total<T, 2>(sy.pz, G, lds_tot, v2);
+    const double rr = k > 0 ? v2[1] : rr0;
+    if (k >= max_iter) {
+      code = 2;
+    } else {
+      const double rn = double(tsqrt<T>(T(rr)));
+      if (rn < atol) code = 1;
+      else if (!(rn == rn) || rn == INFINITY) code = 3;
+    }
+    if (lead && k > 0) {
+      S->rr = rr;
+      if (hist) hist[k] = double(tsqrt<T>(T(rr)));
+    }
+    if (code) break;  // every workgroup decides on the same totals: uniform exit
+    rho_prev = rho;
+    rho = v2[0];
+    // x += α_{k-1} p_{k-1} ; p_k = p_{k-1}β + z
+    const bool first = k == 0;
+    const T beta = first ? T(0) : T(rho) / T(rho_prev);
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      if (!first) xr[m] = xr[m] + alpha * pr[m];
+      pr[m] = first ? zr[m] : (pr[m] * beta) + zr[m];
+      if (own[m]) st_sc1<T>(p + row[m], pr[m]);
+    }
+    if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
+    // q = A p ; partials of π_k = p·q
+    DD dq[1] = {dd_zero()};
+    T qr[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      qr[m] = own[m] ? sell_row<T, kPersistQB>(A, ab[m], ae[m], row[m], gath(p)) : T(0);
+      if (own[m]) dd_fma(dq[0], double(pr[m]), double(qr[m]));
+    }
+    persist_publish<1>(dq, lds_dd, sy.pq);
+    if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
+    double v1[1];
+    persist_total<T, 1>(sy.pq, G, lds_tot, v1);
+    pq = v1[0];
+    alpha = T(rho) / T(pq);
+    // r -= α q
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      rr_[m] = rr_[m] - alpha * qr[m];
+      if (own[m]) st_sc1<T>(r + row[m], rr_[m]);
+    }
+    if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
+  }
+  if (!alive) return;  // timeout word set: the host fails the solve
+#pragma unroll
+  for (int m = 0; m < R; ++m) {
+    if (!own[m]) continue;
+    x[row[m]] = xr[m];
+    p[row[m]] = pr[m];
+  }
+  if (lead) {
+    S->rho_prev = rho_prev;
+    S->rho = rho;
+    S->pq = pq;
+    S->alpha = double(alpha);
+    S->iter = k;
+    S->done = code;
+  }
+}
+
 // IC: ρ = r·z after the two triangular solves
 template <typename T>
 __global__ void __launch_bounds__(kThreads) k_dot_rho(int64_t n, PcgState* S, const T* __restrict__ r,
@@ -862,6 +1169,12 @@ struct lspcg_solver {
   int32_t* xrow[3] = {nullptr, nullptr, nullptr};  // scalar row pointers of expanded BSR3 views
   double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
   int64_t dhist_cap = 0;
+  // persistent multi-workgroup solve (k_pcg_persist): used for small_n < n <= persist_n
+  int64_t persist_n = 0;   // LSPCG_PERSIST_N (0 disables)
+  int persist_wg = 0;      // largest grid (LSPCG_PERSIST_WG; default: one workgroup per CU, <= 256)
+  unsigned* psync = nullptr;  // arrival counters + timeout word (memset before every launch)
+  double* ppart = nullptr;    // [kPersistMaxWG x (2 + 1) dots x DD] partials
+  unsigned* herr = nullptr;   // pinned copy of the timeout word
   int64_t small_n = 1024;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it): <= 2 rows
                            // per thread; 5 rows lose to the 5-kernel schedule
   bool small_sell = true;  // k_pcg_small reads the SELL copies (LSPCG_SMALL_SELL=0: the CSR views)
@@ -1261,6 +1574,81 @@ static int launch_small(lspcg_solver* s, hipStream_t st) {
   return LSPCG_OK;
 }
 
+// ---- persistent multi-workgroup solve: path choice and launch
+static bool persist_grid(const lspcg_solver* s, int64_t max_iter, int* G, int* R) {
+  if (s->persist_n <= 0 || s->n <= 0 || s->n > s->persist_n || s->precond == LSPCG_PRECOND_IC) return false;
+  const bool spai = s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  for (int w = 0; w < (spai ? 3 : 1); ++w)
+    if (!s->sp[w] || !s->sv[w] || s->sp[w]->groups <= 0) return false;  // SELL views required
+  const int64_t gmax = std::max(1, std::min<int>(s->persist_wg, int(kPersistMaxWG)));
+  for (int r = 1; r <= kPersistMaxRows; r *= 2) {
+    const int64_t g = (s->n + int64_t(kPersistThreads) * r - 1) / (int64_t(kPersistThreads) * r);
+    if (g <= gmax) {
+      // the barrier counters count epochs x G arrivals in 32 bits (<= 5 barriers per iteration)
+      if ((5 * (max_iter + 2)) * g >= (int64_t(1) << 32)) return false;
+      *G = int(g);
+      *R = r;
+      return true;
+    }
+  }
+  return false;
+}
+
+static CsrView persist_view(const lspcg_solver* s, int w) {
+  const lspcg_mat& M = w == 0 ? s->Av : (w == 1 ? s->Lv : s->LTv);
+  const SellPattern* P = s->sp[w];
+  CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, P->gp, P->col, s->sv[w],
+            s->svd[w] == LSPCG_F32 ? 1 : 0, P->col_bits == 16 ? 1 : 0};
+  return v;
+}
+
+template <typename T>
+static int launch_persist(lspcg_solver* s, int G, int R, hipStream_t st) {
+  const bool spai = s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  if (!s->psync) {
+    LSPCG_HIP(hipMalloc(&s->psync, kPersistSyncBytes));
+    LSPCG_HIP(hipMalloc(&s->ppart, sizeof(double) * kPersistMaxWG * 3 * 2));
+    LSPCG_HIP(hipHostMalloc(&s->herr, sizeof(unsigned), hipHostMallocDefault));
+  }
+  LSPCG_HIP(hipMemsetAsync(s->psync, 0, kPersistSyncBytes, st));
+  const CsrView A = persist_view(s, 0);
+  const CsrView L = spai ? persist_view(s, 1) : CsrView{};
+  const CsrView LT = spai ? persist_view(s, 2) : CsrView{};
+  const PersistSync sy{s->psync, s->ppart, s->ppart + kPersistMaxWG * 2 * 2};
+  auto* x = static_cast<T*>(s->x);
+  auto* r = static_cast<T*>(s->r);
+  auto* p = static_cast<T*>(s->p);
+  auto* t = static_cast<T*>(s->t);
+  const T* d = static_cast<const T*>(s->d);
+  const int32_t n = int32_t(s->n);
+  const dim3 g(G), b(kPersistThreads);
+  auto go = [&](auto rows) {
+    constexpr int RR = decltype(rows)::value;
+    switch (s->precond) {
+      case LSPCG_PRECOND_NONE:
+        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_NONE, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, t, sy);
+        break;
+      case LSPCG_PRECOND_DIAGONAL:
+        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_DIAGONAL, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, t,
+                           sy);
+        break;
+      case LSPCG_PRECOND_EXT_SPAI:
+        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_EXT_SPAI, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, t,
+                           sy);
+        break;
+      default:
+        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_EXT_SPAI_SCALED, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r,
+                           p, t, sy);
+    }
+  };
+  if (R == 1) go(std::integral_constant<int, 1>{});
+  else if (R == 2) go(std::integral_constant<int, 2>{});
+  else go(std::integral_constant<int, 4>{});
+  LSPCG_HIP(hipGetLastError());
+  LSPCG_HIP(hipMemcpyAsync(s->herr, s->psync + kPersistErr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  return LSPCG_OK;
+}
+
 static int get_graph(lspcg_solver* s, int chunk, hipGraphExec_t* out) {
   auto it = s->graphs.find(chunk);
   if (it != s->graphs.end()) {
@@ -1325,6 +1713,14 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   if (const char* e = std::getenv("LSPCG_SELL32")) s->sell16 = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SMALL_N")) s->small_n = std::max<int64_t>(0, std::atoll(e));
   if (const char* e = std::getenv("LSPCG_SMALL_SELL")) s->small_sell = e[0] != '0';
+  {
+    int cus = 256;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+      cus = 256;
+    s->persist_wg = cus;
+  }
+  if (const char* e = std::getenv("LSPCG_PERSIST_N")) s->persist_n = std::max<int64_t>(0, std::atoll(e));
+  if (const char* e = std::getenv("LSPCG_PERSIST_WG")) s->persist_wg = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
     s->allow_split = e[0] != '0';
     s->split_mode = std::atoi(e);
@@ -1512,13 +1908,18 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     return post();
   };
   PcgState cur{};
+  int pG = 0, pR = 0;
   const bool small = small_path(s);
-  if (small) {  // one launch runs the whole loop (k_pcg_small)
-    rc = s->dtype == LSPCG_F64 ? launch_small<double>(s, st) : launch_small<float>(s, st);
+  const bool persist = !small && persist_grid(s, max_iter, &pG, &pR);
+  if (small || persist) {  // one launch runs the whole loop (k_pcg_small / k_pcg_persist)
+    if (small) rc = s->dtype == LSPCG_F64 ? launch_small<double>(s, st) : launch_small<float>(s, st);
+    else rc = s->dtype == LSPCG_F64 ? launch_persist<double>(s, pG, pR, st) : launch_persist<float>(s, pG, pR, st);
     if (!rc) rc = post();
     if (rc) return rc;
     LSPCG_HIP(hipEventSynchronize(evp[head]));
     cur = *hs[head];
+    LSPCG_CHECK(!persist || *s->herr == 0, LSPCG_ERR_HIP,
+                "solve: a grid barrier of the persistent solve timed out (workgroups not co-resident?)");
   } else {
     rc = post();
     if (!rc) rc = launch(std::min(4, max_chunk));
@@ -1527,7 +1928,7 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   int64_t last_it = 0;
   double last_rr = -1.0;
   int chunk = std::min(4, max_chunk);
-  for (; !small;) {
+  for (; !small && !persist;) {
     LSPCG_HIP(hipEventSynchronize(evp[head]));
     cur = *hs[head];
     const int64_t inflight = queued[head];
@@ -1658,6 +2059,9 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   }
   (void)hipFree(s->flag);
   (void)hipFree(s->dhist);
+  (void)hipFree(s->psync);
+  (void)hipFree(s->ppart);
+  (void)hipHostFree(s->herr);
   (void)hipStreamDestroy(s->stream);
   delete s;
   return LSPCG_OK;

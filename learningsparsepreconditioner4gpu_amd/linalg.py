@@ -114,6 +114,7 @@ class PreconditionedConjugateGradient:
         rc = _lib.call("lspcg_solver_solve", self.handle, _ptr(b), _ptr(x), float(rtol), mi, C.byref(it),
                        hist.ctypes.data_as(_lib.p_f64) if hist is not None else None, C.byref(ms),
                        allow_not_converged=True)
+        self.last_converged = rc == _lib.OK
         out = (it.value, rc == _lib.OK, ms.value / 1e3)
         if return_history:
             out = out + (hist[: min(it.value, mi) + 1].copy(),)  # NaN after a non-finite stop (lspcg.h)

@@ -235,3 +235,110 @@ def build_gnn(node_in: int, edge_in: int, block_size: int, seed: Optional[int] =
         torch.manual_seed(seed)
     return NodeEdgeProcessing(node_in_features=node_in, node_out_features=None, edge_in_features=edge_in,
                               edge_out_features=block_size * block_size, **cfg)
+
+
+# ---------------------------------------------------------------------------
+# GraphSpmv / AATPE / LLT (basic_layers.py:112-142, 228-275) on lspcg_graph_* (HIP)
+# ---------------------------------------------------------------------------
+class _GraphCache:
+    """lspcg_graph handles keyed on the edge_index tensor (held, so its address cannot be reused
+    by another tensor while cached), its in-place version, N and the block size."""
+
+    def __init__(self, size: int = 8):
+        self.size = size
+        self.items = []  # [(key, edge_index tensor, handle)]
+
+    def get(self, edge_index: torch.Tensor, N: int, bs: int) -> C.c_void_p:
+        ctx = Context.get(edge_index.device)
+        key = (edge_index.data_ptr(), tuple(edge_index.shape), edge_index._version, N, bs, ctx.device)
+        for i, (k, t, h) in enumerate(self.items):
+            if k == key and t.data_ptr() == edge_index.data_ptr():
+                self.items.append(self.items.pop(i))
+                return h
+        ei = edge_index.to(torch.int64).contiguous()
+        h = C.c_void_p()
+        _lib.call("lspcg_graph_create", ctx.handle, int(N), int(ei.shape[1]), int(bs), _ptr(ei), C.byref(h))
+        self.items.append((key, edge_index, h))
+        while len(self.items) > self.size:
+            _, _, old = self.items.pop(0)
+            if _lib._lib is not None:
+                _lib._lib.lspcg_graph_destroy(old)
+        return h
+
+
+_GRAPHS = _GraphCache()
+
+
+def _graph_args(X: torch.Tensor, edge_index: torch.Tensor, A: torch.Tensor, *opt):
+    if not X.is_cuda:
+        raise _lib.LspcgUnavailable("GraphSpmv / AATPE run on the GPU only (HIP)")
+    if X.dtype not in (torch.float32, torch.float64):
+        raise TypeError(f"unsupported dtype {X.dtype}")
+    N = X.shape[0]
+    bs = X.shape[1] if X.ndim == 2 else 1
+    assert A.shape[0] == edge_index.shape[1] and tuple(A.shape[1:]) in ((bs, bs),) + (((1,),) if bs == 1 else ()), \
+        (tuple(A.shape), bs)
+    dev = X.device
+    x = X.contiguous()
+    vals = A.to(device=dev, dtype=X.dtype).contiguous()
+    out = []
+    for o in opt:
+        if o is None:
+            out.append(None)
+        else:
+            o = o.to(device=dev, dtype=X.dtype).contiguous()
+            assert o.numel() == N * bs, (tuple(o.shape), N, bs)
+            out.append(o)
+    return N, bs, x, vals, out, _lib.F32 if X.dtype == torch.float32 else _lib.F64
+
+
+class GraphSpmv(nn.Module):
+    """basic_layers.py:112-142: ``y_i = Σ_j A_ij x_j`` over the blocks of an edge list
+    (``use_transpose``: ``y = Aᵀ x``), then ``y * mask``.  X is [N, b], A is [E, b, b]."""
+
+    def __init__(self, use_transpose: bool = False):
+        super().__init__()
+        self.transpose = use_transpose
+
+    @torch.no_grad()
+    def forward(self, X, edge_index, A, mask=None):
+        N, bs, x, vals, (m,), code = _graph_args(X, edge_index, A, mask)
+        h = _GRAPHS.get(edge_index.to(x.device), N, bs)
+        y = torch.empty_like(x)
+        _lib.call("lspcg_graph_spmv", h, _ptr(vals), code, int(self.transpose), _ptr(x),
+                  _ptr(m) if m is not None else None, _ptr(y))
+        return y
+
+
+class AATPE(nn.Module):
+    """basic_layers.py:228-261: ``y = ε x + A Aᵀ x`` (``diag``: ``ε diag x + A diag Aᵀ x``), the
+    mask applied after each SpMV -- the ext_spai apply on the GNN's own edge-list output."""
+
+    def __init__(self, epsilon):
+        super().__init__()
+        self.epsilon = float(epsilon)
+        self.spmv = GraphSpmv()
+        self.spmv_t = GraphSpmv(use_transpose=True)
+
+    @torch.no_grad()
+    def forward(self, x, edge_index, boo_values, mask=None, diag=None):
+        N, bs, xx, vals, (m, d), code = _graph_args(x, edge_index, boo_values, mask, diag)
+        if diag is not None:
+            assert tuple(diag.shape) == tuple(x.shape), "diag must have AT_x's shape (basic_layers.py:253)"
+        h = _GRAPHS.get(edge_index.to(xx.device), N, bs)
+        t = torch.empty_like(xx)
+        y = torch.empty_like(xx)
+        _lib.call("lspcg_graph_aatpe", h, _ptr(vals), code, self.epsilon, _ptr(xx), _ptr(m) if m is not None else None,
+                  _ptr(d) if d is not None else None, _ptr(t), _ptr(y))
+        return y
+
+
+class LLT(nn.Module):
+    """basic_layers.py:264-275: ``L Lᵀ x`` with the mask after each SpMV (AATPE with ε = 0)."""
+
+    def __init__(self):
+        super().__init__()
+        self._op = AATPE(0.0)
+
+    def forward(self, x, edge_index, boo_values, mask=None):
+        return self._op(x, edge_index, boo_values, mask)

@@ -20,14 +20,15 @@ scipy's csr_matvec).
 """
 from __future__ import annotations
 
-from typing import Tuple, Union
+import math
+from typing import Optional, Tuple, Union
 
 import numpy as np
 import scipy.sparse as sp
 import torch
 
 from .linalg import PreconditionedConjugateGradient
-from .sparse import Context, DeviceMatrix, assemble, lspcg_dtype
+from .sparse import Context, DeviceMatrix, assemble, dot, lspcg_dtype
 
 
 def to_numpy(x) -> np.ndarray:
@@ -66,7 +67,7 @@ def _prepare(A, dtype, block_size=1) -> DeviceMatrix:
 
 
 def get_cg_iter_time(A, gt, rtol=1e-6, max_iter=0, dtype=np.float64, repeat=1, device="cuda",
-                     method="ainv") -> Tuple[float, float, float]:
+                     method="ainv", info: Optional[dict] = None) -> Tuple[float, float, float]:
     """validate.py:54-86: method none / diagonal / ic (IC(0), level-scheduled triangular solves) /
     ainv (AINV(0) as L Lᵀ); the prec time is the device setup of the preconditioner."""
     Ad = _prepare(A, dtype)
@@ -77,16 +78,27 @@ def get_cg_iter_time(A, gt, rtol=1e-6, max_iter=0, dtype=np.float64, repeat=1, d
     x = torch.zeros_like(b)
     for _ in range(repeat):
         solver = PreconditionedConjugateGradient(Ad, device=device, preconditioner=method, dtype=dtype)
-        this_iter, this_prec, this_solve = solver(b.clone(), x.clone(), rtol, max_iter)
+        xs = x.clone()
+        this_iter, this_prec, this_solve = solver(b.clone(), xs, rtol, max_iter)
         iter_cnt += this_iter
         time_prec += this_prec
         time_elp += this_solve
         if this_iter >= max_iter:
             raise RuntimeError("CG did not converge")
+    if info is not None:
+        info.update(x=xs, rel_res=relative_residual(Ad, xs, b), converged=bool(solver.last_converged),
+                    iters=int(this_iter))
     return iter_cnt / repeat, time_prec / repeat, time_elp / repeat
 
 
-def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device):
+def relative_residual(A: DeviceMatrix, x: torch.Tensor, b: torch.Tensor) -> float:
+    """True relative residual ‖b − A x‖ / ‖b‖ on the device (one SpMV, compensated dots)."""
+    r = b - A.matvec(x)
+    bb = dot(b, b)
+    return math.sqrt(dot(r, r) / bb) if bb > 0 else math.sqrt(dot(r, r))
+
+
+def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info=None):
     Ad = _prepare(A, dtype)
     Ld = spai if isinstance(spai, DeviceMatrix) else _prepare(spai, dtype)
     rows = Ad.n
@@ -97,20 +109,25 @@ def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, de
     x = torch.zeros_like(b)
     for _ in range(repeat):
         solver = PreconditionedConjugateGradient(Ad, device=device, preconditioner=method, dtype=dtype)
-        this_iter, this_prec, this_solve = solver(b.clone(), x.clone(), rtol, max_iter, ext_spai=(Ld, epsilon))
+        xs = x.clone()
+        this_iter, this_prec, this_solve = solver(b.clone(), xs, rtol, max_iter, ext_spai=(Ld, epsilon))
         iter_cnt += this_iter
         time_prec += this_prec
         time_elp += this_solve
+    if info is not None:  # the last solve's iterate, its true residual and the solver's verdict
+        info.update(x=xs, rel_res=relative_residual(Ad, xs, b), converged=bool(solver.last_converged),
+                    iters=int(this_iter))
     return iter_cnt / repeat, time_prec / repeat, time_elp / repeat
 
 
 def get_pcg_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat=1, dtype=np.float64,
-                      device="cuda") -> Tuple[float, float, float]:
-    """validate.py:89-121: ext_spai PCG, M⁻¹ = L Lᵀ + εI."""
-    return _pcg_generic("ext_spai", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device)
+                      device="cuda", info: Optional[dict] = None) -> Tuple[float, float, float]:
+    """validate.py:89-121: ext_spai PCG, M⁻¹ = L Lᵀ + εI.  ``info`` (optional dict, not in the
+    reference's signature) receives the last solve's x, true relative residual and convergence."""
+    return _pcg_generic("ext_spai", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info)
 
 
 def get_pcg_scaled_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat=1, dtype=np.float64,
-                             device="cuda") -> Tuple[float, float, float]:
+                             device="cuda", info: Optional[dict] = None) -> Tuple[float, float, float]:
     """validate.py:124-160: ext_spai_scaled PCG, M⁻¹ r = L((Lᵀr)/d) + εr/d, d = diag(A)."""
-    return _pcg_generic("ext_spai_scaled", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device)
+    return _pcg_generic("ext_spai_scaled", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info)

@@ -157,3 +157,34 @@ def build(node_in: int, edge_in: int, block_size: int, seed: int = 0, **over) ->
     torch.manual_seed(seed)
     return NodeEdgeProcessing(node_in_features=node_in, node_out_features=None, edge_in_features=edge_in,
                               edge_out_features=block_size * block_size, **cfg)
+
+
+# ---------------------------------------------------------------------------
+# basic_layers.py:112-142 GraphSpmv and :228-261 AATPE, PyG semantics restated in fp64
+# ---------------------------------------------------------------------------
+def graph_spmv(X, edge_index, A, mask=None, transpose=False):
+    """flow target_to_source (transpose=False): message A_e x[ei[1]] summed at ei[0];
+    source_to_target (transpose=True): message A_eᵀ x[ei[0]] summed at ei[1]; then * mask."""
+    X = torch.as_tensor(X, dtype=torch.float64)
+    A = torch.as_tensor(A, dtype=torch.float64)
+    if A.ndim == 1:
+        A = A.reshape(-1, 1, 1)
+    X2 = X.reshape(X.shape[0], -1)
+    src, dst = (edge_index[0], edge_index[1]) if transpose else (edge_index[1], edge_index[0])
+    blk = A.transpose(-1, -2) if transpose else A
+    msg = torch.bmm(blk, X2[src].unsqueeze(-1)).squeeze(-1)
+    out = torch.zeros_like(X2).index_add_(0, dst, msg)
+    if mask is not None:
+        out = out * torch.as_tensor(mask, dtype=torch.float64).reshape(out.shape)
+    return out.reshape(X.shape)
+
+
+def aatpe(x, edge_index, boo_values, epsilon, mask=None, diag=None):
+    x = torch.as_tensor(x, dtype=torch.float64)
+    at_x = graph_spmv(x, edge_index, boo_values, mask, transpose=True)
+    eps_x = epsilon * x
+    if diag is not None:
+        d = torch.as_tensor(diag, dtype=torch.float64)
+        at_x = at_x * d
+        eps_x = eps_x * d
+    return eps_x + graph_spmv(at_x, edge_index, boo_values, mask, transpose=False)

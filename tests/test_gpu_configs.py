@@ -82,7 +82,7 @@ def test_c2_poisson_gnn_spai_pcg(gpu_ctx):
     it, conv, x, h = _solve(A, L, b, ws.epsilon, 1e-8)
     assert conv and it == it_o, (it, it_o)
     assert np.linalg.norm(x - x_o) / np.linalg.norm(x_o) <= 1e-12
-    np.testing.assert_allclose(h, h_o, rtol=1e-10, atol=0)
+    np.testing.assert_allclose(h, h_o, rtol=1e-12, atol=0)
 
 
 def test_c3_heat_fp32(gpu_ctx):
@@ -118,7 +118,7 @@ def test_c4_elasticity_bsr3_full_size(gpu_ctx):
     it_o, x_o, h_o = O.pcg(A_h, b, O.spai_operator(L_h, ws.epsilon), rtol=1e-8, max_iter=25, dot="exact")
     it, _, xg, h = _solve(A, L, b, ws.epsilon, 1e-8, max_iter=25)
     assert it == it_o == 25
-    np.testing.assert_allclose(h, h_o, rtol=1e-10, atol=0)
+    np.testing.assert_allclose(h, h_o, rtol=1e-12, atol=0)
     assert np.linalg.norm(xg - x_o) / np.linalg.norm(x_o) <= 1e-12
 
 

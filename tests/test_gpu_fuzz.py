@@ -1,7 +1,7 @@
 """Randomised parity sweep: seeded random SPD systems of assorted sizes / row-length spreads,
 random ext_spai factors (fp64 and fp32-exact values, so both the fp64 and the compact fp32-value
 views run), GPU PCG against the oracle with correctly rounded dots: equal iteration count,
-residual history 1e-10, iterate 1e-12.  Sizes cross the SELL slice (64 rows), workgroup (256)
+residual history and iterate 1e-12.  Sizes cross the SELL slice (64 rows), workgroup (256)
 and group (64 workgroups) boundaries."""
 import numpy as np
 import pytest
@@ -33,11 +33,20 @@ def _random_spd(n, seed):
 SIZES = [63, 65, 257, 1000, 4097, 17000, 70000, 150000]
 
 
-@pytest.mark.parametrize("small_n", ["0", "4096"])
+MODES = {  # "multi": the multi-kernel schedules at every size; "small": n <= 2560 runs k_pcg_small;
+    # "persist": every size runs k_pcg_persist (the grid cap varies, so 1, 2 and 4 rows per thread)
+    "multi": {"LSPCG_SMALL_N": "0", "LSPCG_PERSIST_N": "0"},
+    "small": {"LSPCG_SMALL_N": "4096", "LSPCG_PERSIST_N": "0"},
+    "persist": {"LSPCG_SMALL_N": "0", "LSPCG_PERSIST_N": "100000000"},
+}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("seed", range(16))
-def test_random_spd_pcg_parity(gpu_ctx, seed, small_n, monkeypatch):
-    """small_n "0": the multi-kernel schedules at every size; "4096": n <= 2560 runs k_pcg_small."""
-    monkeypatch.setenv("LSPCG_SMALL_N", small_n)
+def test_random_spd_pcg_parity(gpu_ctx, seed, mode, monkeypatch):
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("LSPCG_PERSIST_WG", str([256, 61, 9][seed % 3]))
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
 
     rng = np.random.default_rng(100 + seed)
@@ -53,5 +62,5 @@ def test_random_spd_pcg_parity(gpu_ctx, seed, small_n, monkeypatch):
     x = np.zeros(n)
     it, _, _, h = s(b.copy(), x, 1e-8, 400, ext_spai=(L, eps), return_history=True)
     assert it == it_o, (n, seed, it, it_o)
-    np.testing.assert_allclose(h, h_o, rtol=1e-10, atol=0)
+    np.testing.assert_allclose(h, h_o, rtol=1e-12, atol=0)
     assert np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)

@@ -75,8 +75,18 @@ def test_infer_driver_end_to_end(gpu_ctx, tmp_path):
     recs = run(samples, ws, rtol=1e-8, warmup=1)
     assert [r.index for r in recs] == [0, 1, 2]
     st = Timestat()
-    for r in recs:
+    for r, s in zip(recs, samples):
         assert r.iters > 0 and r.converged
+        # the gathered record carries the true ‖b − A x‖/‖b‖ of the solution: below rtol (up to the
+        # recurrence/true residual gap) and equal to the oracle's (same trajectory) to 1e-12
+        d = s.to("cuda")
+        L, _ = ws.inference_step(d)
+        A = ws.system_matrix(d).to_scipy()
+        b = A @ s.mask.numpy().reshape(-1).astype(np.float64)
+        it_o, x_o, _ = O.pcg(A, b, O.spai_operator(L.to_scipy(), ws.epsilon), rtol=1e-8, dot="exact")
+        rel_o = np.linalg.norm(b - A @ x_o) / np.linalg.norm(b)
+        assert r.iters == it_o
+        assert r.rel_res <= 1.05e-8 and abs(r.rel_res - rel_o) <= 1e-12, (r.rel_res, rel_o)
         st.put("Neural+HIP", r.t_solve, r.t_prec, r.iters, r.n)
     df = st.timestat_to_dataframe()
     assert list(df.columns) == ["Key", "Total Time (ms)", "Solve Time (ms)", "Precond Time (ms)", "#Iteration"]

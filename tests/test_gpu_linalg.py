@@ -156,7 +156,7 @@ def test_pcg_parity_fp64(gpu_ctx, method, case):
     rel = np.linalg.norm(x - x_o) / max(np.linalg.norm(x_o), 1e-300)
     assert rel <= 1e-12, (name, method, rel)
     assert len(h) == it + 1
-    np.testing.assert_allclose(h, h_o, rtol=1e-10, atol=0)
+    np.testing.assert_allclose(h, h_o, rtol=1e-12, atol=0)
 
 
 @pytest.mark.parametrize("method", ["none", "ext_spai"])
@@ -242,7 +242,7 @@ def test_pcg_max_iter_inside_queued_chunks(gpu_ctx, max_iter, small_n, monkeypat
     it, x, h = _solve(A, b, "ext_spai", L, 3e-3, rtol=1e-14, max_iter=max_iter)
     assert it == it_o == max_iter
     assert len(h) == it + 1
-    np.testing.assert_allclose(h, h_o, rtol=1e-10, atol=0)
+    np.testing.assert_allclose(h, h_o, rtol=1e-12, atol=0)
     assert np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
 
 

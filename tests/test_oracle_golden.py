@@ -186,3 +186,25 @@ def test_pcg_trajectory_matches_reference(name, method):
     assert np.array_equal(x, z[f"{t}__x"])
     if name == "synthetic10240":
         assert it == 3229  # the reference's count on config 1 in this container
+
+
+def test_graph_spmv_oracle_is_block_spmv():
+    """oracle.gnn.graph_spmv (PyG message passing restated) = scipy's block SpMV with duplicate
+    edges summed (y = A x, and Aᵀ x for use_transpose)."""
+    rng = np.random.default_rng(0)
+    N, E, b = 50, 400, 3
+    ei = rng.integers(0, N, size=(2, E))
+    A = rng.normal(size=(E, b, b))
+    x = rng.normal(size=(N, b))
+    dense = np.zeros((N * b, N * b))
+    for e in range(E):
+        r, c = ei[:, e]
+        dense[r * b:(r + 1) * b, c * b:(c + 1) * b] += A[e]
+    y = OG.graph_spmv(x, torch.from_numpy(ei), A).numpy()
+    yt = OG.graph_spmv(x, torch.from_numpy(ei), A, transpose=True).numpy()
+    assert np.allclose(y.ravel(), dense @ x.ravel(), rtol=1e-13, atol=1e-13)
+    assert np.allclose(yt.ravel(), dense.T @ x.ravel(), rtol=1e-13, atol=1e-13)
+    m = (rng.random((N, b)) > 0.3).astype(float)
+    z = OG.aatpe(x, torch.from_numpy(ei), A, 0.5, m).numpy().ravel()
+    want = m.ravel() * (dense @ (m.ravel() * (dense.T @ x.ravel()))) + 0.5 * x.ravel()
+    assert np.allclose(z, want, rtol=1e-12, atol=1e-12)
