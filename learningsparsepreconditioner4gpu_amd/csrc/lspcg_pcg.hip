@@ -777,100 +777,175 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
 
 // ---- mid-size systems: the whole solve in ONE persistent launch over G workgroups ---------
 // Between a few thousand and a few hundred thousand unknowns an iteration of the 5-launch
-// schedule is latency, not bytes (~22 us at n = 65 k).  k_pcg_persist keeps a
-// resident grid of G <= #CU workgroups (one per CU) for the whole scipy loop; thread `tid` of
-// workgroup g owns rows (g R + m) 512 + tid, m < R, whose x, r, z, p, q live in registers.
-// Only the three gathered vectors (r for Lᵀ, t for L, p for A) and the per-workgroup dot
-// partials cross workgroups, through the hand-off of MI355X_MICROARCH.md "Valid forms", row 1:
-// every byte stored with sc1 (agent-scope relaxed) stores, every storing wave drains them
-// (s_waitcnt vmcnt(0)) before the workgroup barrier, ONE lane per workgroup signals with an
-// agent-scope atomic add on its XCD-sharded arrival counter, wave 0 polls the 8 shards with
-// sc1 loads, the other waves wait at a workgroup barrier, and every load of handed-off bytes is
-// an sc1 load -- no L1 invalidate or L2 write-back fence on the critical path.  The matrix
-// views are read with plain loads (read-only during the solve: they stay in L1 / L2).
-// Reductions: each workgroup publishes its compensated (DD) partial; after the barrier EVERY
-// workgroup sums all G partials in the same fixed order, so every workgroup takes the same
-// convergence decision at the same iteration and no extra barrier is needed.  Expressions,
-// row-sum order and the top-of-loop test are those of the split schedule (same bits).
-// Every spin is bounded: a workgroup that waits too long sets the timeout word and leaves,
-// so the grid always drains (the host reports LSPCG_ERR_HIP).
+// schedule is latency, not bytes (~17-22 us).  k_pcg_persist keeps a resident
+// grid of G <= #CU workgroups (one per CU) for the whole scipy loop; thread `tid` of workgroup g
+// owns rows (g R + m) 512 + tid, m < R, whose x, r, z, p, q live in registers.
+// There is no grid barrier.  Every value that crosses workgroups -- the gathered vectors r (for
+// Lᵀ), t (for L), p (for A) and each workgroup's compensated dot partials -- is published as
+// self-validating 8-byte granules {epoch tag, 32-bit payload}, each written by ONE sc1
+// (agent-scope relaxed) store, so the data is its own flag (MI355X_MICROARCH.md "Valid forms",
+// R2: no fence, no drain, no flag).  A consumer sc1-loads exactly the granules it needs and
+// re-reads them until every tag equals the epoch it expects; an fp64 value is two granules (high
+// and low word), each checked.  Epochs: iteration k publishes r_k (5k+1), t_k (5k+2), the ρ_k /
+// ‖r_k‖² partials (5k+3), p_k (5k+4) and the π_k partials (5k+5).
+// No slot is overwritten while a reader may still need its previous epoch: between two writes of
+// r, t or p (and of either partial set) the writer has passed an all-reduce, i.e. seen the
+// partial of EVERY workgroup, each published after that workgroup finished the reads in question.
+// All-reduces: each workgroup publishes its partial, wave 0 sweeps the G partials until all carry
+// the epoch and sums them in one fixed order -- the same total in every workgroup, so every
+// workgroup takes the same convergence decision at the same iteration.  The matrix views are read
+// with plain loads (read-only during the solve: they stay in L1 / L2).  Expressions, row-sum
+// order and the top-of-loop test are those of the split schedule (same bits).  Every wait is
+// bounded: a timed-out wait sets the timeout word, which every other wait also watches, and the
+// workgroups leave together at their next all-reduce, so the grid always drains (the host then
+// reports LSPCG_ERR_HIP).  Granules and the timeout word are zeroed before every launch.
 constexpr int kPersistThreads = 512;
-constexpr int kPersistShards = 8;            // arrival counters, one per blockIdx % 8 (one 128-B line each)
-constexpr int kPersistCntStride = 32;        // uint32 per shard line
-constexpr int kPersistErr = kPersistShards * kPersistCntStride;  // timeout word after the shards
-constexpr size_t kPersistSyncBytes = sizeof(unsigned) * (kPersistErr + 32);  // memset per solve (x16 B)
-constexpr int kPersistQB = 4;                // SELL groups per batch (global sc1 gathers: more in flight)
-constexpr unsigned kPersistSpin = 1u << 22;  // polls (~1 us each) before a barrier gives up
-constexpr unsigned kPersistMaxWG = 256;      // persist_total sums <= 4 partials per lane
+constexpr int kPersistQB = 4;                // SELL groups per batch
+constexpr unsigned kPersistSpin = 1u << 22;  // re-reads before a wait gives up
+constexpr unsigned kPersistMaxWG = 256;      // <= 4 workgroups per lane of the sweeping wave
 constexpr int kPersistMaxRows = 4;           // rows per thread (template R = 1, 2, 4)
+// sync buffer (uint32 words): [timeout | pad to 32][ρ,‖r‖² partials: G x 8 u64][π: G x 4 u64]
+inline size_t persist_gz_off() { return 32; }
+inline size_t persist_gq_off(unsigned G) { return persist_gz_off() + size_t(G) * 8 * 2; }
+inline size_t persist_sync_bytes(unsigned G) { return 4 * (persist_gq_off(G) + size_t(G) * 4 * 2); }  // x 16 B
+
+using u64 = unsigned long long;
 
 struct PersistSync {
-  unsigned* cnt;   // [kPersistSyncBytes / 4], zeroed before every launch
-  double* pz;      // [G][2 dots][s, c]: ρ_k and ‖r_k‖² partials
-  double* pq;      // [G][s, c]: π_k partials
+  unsigned* err;  // timeout word
+  u64* gz;        // [G][2 dots][s hi, s lo, c hi, c lo] granules
+  u64* gq;        // [G][1 dot][...]
+  u64* rg;        // vector granules: r, t, p ([n] fp32 / [2n] fp64 each)
+  u64* tg;
+  u64* pg;
+  u64* stamps;    // diagnostics (LSPCG_PERSIST_STAMPS=1): s_memrealtime per phase, workgroups 0 and G-1
 };
 
-template <typename T>
-__device__ __forceinline__ T ld_sc1(const T* p) {
-  if constexpr (sizeof(T) == 8) {
-    const unsigned long long u = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-    return __longlong_as_double(static_cast<long long>(u));
-  } else {
-    const unsigned u = __hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __uint_as_float(u);
-  }
-}
-template <typename T>
-__device__ __forceinline__ void st_sc1(T* p, T v) {
-  if constexpr (sizeof(T) == 8)
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
-                       static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  else
-    __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+constexpr int kStampIters = 64, kStampPhases = 8;
+// diagnostics only: thread 0 of workgroups 0 and G-1 record the 100 MHz real-time clock
+__device__ __forceinline__ void stamp(const PersistSync& sy, int64_t k, int ph) {
+  if (sy.stamps && threadIdx.x == 0 && k < kStampIters && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
+    sy.stamps[((blockIdx.x == 0 ? 0 : kStampIters) + k) * kStampPhases + ph] = __builtin_amdgcn_s_memrealtime();
 }
 
-// Grid barrier number `epoch` (1, 2, ...): returns false after a timeout (uniform per workgroup).
-__device__ __forceinline__ bool persist_sync(unsigned* cnt, unsigned epoch, unsigned G, int* s_ok) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    const unsigned lane = threadIdx.x;
-    if (lane == 0)
-      __hip_atomic_fetch_add(cnt + (blockIdx.x % kPersistShards) * kPersistCntStride, 1u, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = epoch * G;
-    bool ok = false;
+__device__ __forceinline__ u64 ld_gran(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_gran(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ bool persist_timed_out(const unsigned* err) {
+  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+__device__ __forceinline__ void persist_fail(unsigned* err) {
+  __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one vector entry as granules: fp64 = [tag | hi32][tag | lo32], fp32 = [tag | bits]
+template <typename T>
+struct Gran {
+  static constexpr int W = sizeof(T) / 4;  // granules per value
+  __device__ static __forceinline__ void put(u64* g, int32_t i, T v, unsigned tag) {
+    const u64 t = u64(tag) << 32;
+    if constexpr (W == 2) {
+      const u64 b = u64(__double_as_longlong(v));
+      st_gran(g + 2 * int64_t(i), t | (b >> 32));
+      st_gran(g + 2 * int64_t(i) + 1, t | (b & 0xffffffffull));
+    } else {
+      st_gran(g + i, t | u64(__float_as_uint(v)));
+    }
+  }
+  // raw granules of entry i (not yet validated)
+  struct Raw {
+    u64 a, b;
+  };
+  __device__ static __forceinline__ Raw get(const u64* g, int32_t i) {
+    if constexpr (W == 2) return Raw{ld_gran(g + 2 * int64_t(i)), ld_gran(g + 2 * int64_t(i) + 1)};
+    else return Raw{ld_gran(g + i), 0};
+  }
+  __device__ static __forceinline__ bool ok(const Raw& r, unsigned tag) {
+    if constexpr (W == 2) return unsigned(r.a >> 32) == tag && unsigned(r.b >> 32) == tag;
+    else return unsigned(r.a >> 32) == tag;
+  }
+  __device__ static __forceinline__ T val(const Raw& r) {
+    if constexpr (W == 2) return __longlong_as_double((long long)((r.a << 32) | (r.b & 0xffffffffull)));
+    else return __uint_as_float(unsigned(r.a));
+  }
+};
+
+// SELL row sum (sell_row's order) gathering x from granules of epoch `tag`: a batch's granules are
+// re-read until every tag matches.  Returns false after a timeout (the sum is then garbage).
+template <typename T, int QB>
+__device__ __forceinline__ bool sell_row_gran(const CsrView& M, int32_t b, int32_t e, int32_t i, const u64* xg,
+                                              unsigned tag, const unsigned* err, T& out) {
+  T acc = T(0);
+  const int32_t lane = i & 63, base = i & ~63;
+  for (int32_t q0 = b; q0 < e; q0 += QB) {
+    T v[4 * QB];
+    int32_t c[4 * QB];
+    bool okm[4 * QB];
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const size_t off = 256 * size_t(min(q0 + u, e - 1)) + 4 * lane;
+      if (M.sf32) {
+        const f32x4 a = *(const __attribute__((address_space(1))) f32x4*)(static_cast<const float*>(M.sv) + off);
+        v[4 * u + 0] = T(a.x); v[4 * u + 1] = T(a.y); v[4 * u + 2] = T(a.z); v[4 * u + 3] = T(a.w);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[4 * u + j] = gld(static_cast<const T*>(M.sv) + off + j);
+      }
+      int o[4];
+      if (M.c16) {
+        const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(static_cast<const int16_t*>(M.scol) + off);
+        o[0] = cc.x; o[1] = cc.y; o[2] = cc.z; o[3] = cc.w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          okm[4 * u + j] = o[j] != kSellPad16 && q0 + u < e;
+          c[4 * u + j] = okm[4 * u + j] ? base + o[j] : 0;
+        }
+      } else {
+        const i32x4 cc = *(const __attribute__((address_space(1))) i32x4*)(static_cast<const int32_t*>(M.scol) + off);
+        o[0] = cc.x; o[1] = cc.y; o[2] = cc.z; o[3] = cc.w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          okm[4 * u + j] = o[j] >= 0 && q0 + u < e;
+          c[4 * u + j] = okm[4 * u + j] ? o[j] : 0;
+        }
+      }
+    }
+    typename Gran<T>::Raw g[4 * QB];
+    bool ready = false;
     for (unsigned spin = 0; spin < kPersistSpin; ++spin) {
-      // lanes 0..7 read the shards, lane 8 the timeout word; the decision is wave-uniform
-      const unsigned w = lane <= kPersistShards
-                             ? __hip_atomic_load(cnt + (lane < kPersistShards ? lane * kPersistCntStride : kPersistErr),
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                             : 0u;
-      unsigned v = lane < kPersistShards ? w : 0u;
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      if (__shfl(v, 0, 64) >= target) {
-        ok = true;
+      bool all = true;
+#pragma unroll
+      for (int u = 0; u < 4 * QB; ++u) {
+        if (okm[u]) {
+          g[u] = Gran<T>::get(xg, c[u]);
+          all &= Gran<T>::ok(g[u], tag);
+        }
+      }
+      if (all) {
+        ready = true;
         break;
       }
-      if (__shfl(w, kPersistShards, 64) != 0u) break;  // another workgroup timed out
+      if ((spin & 63) == 63 && persist_timed_out(err)) break;
       __builtin_amdgcn_s_sleep(1);
     }
-    if (lane == 0) {
-      if (!ok) __hip_atomic_store(cnt + kPersistErr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *s_ok = ok;
+    if (!ready) {
+      persist_fail(const_cast<unsigned*>(err));
+      out = T(0);
+      return false;
     }
+#pragma unroll
+    for (int u = 0; u < 4 * QB; ++u)
+      if (okm[u]) acc = acc + v[u] * Gran<T>::val(g[u]);
   }
-  __syncthreads();
-  return *s_ok != 0;
+  out = acc;
+  return true;
 }
 
-// this workgroup's N compensated partials -> pub[blockIdx.x][N] (sc1), before the barrier
-template <int N>
-__device__ __forceinline__ void persist_publish(DD (&v)[N], DD* lds, double* pub) {
+// All-reduce of N compensated partials by tagged granules; `bad` (this thread's earlier waits
+// failed) is OR-ed over the workgroup.  Returns false (uniformly) when any wait failed.
+template <typename T, int N>
+__device__ __forceinline__ bool persist_allreduce(DD (&v)[N], bool bad, DD* lds, double* lds_out, u64* gran,
+                                                  unsigned* err, unsigned tag, unsigned G, int* s_ok,
+                                                  double (&out)[N]) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   wave_reduce_dd<N>(v);
@@ -878,61 +953,85 @@ __device__ __forceinline__ void persist_publish(DD (&v)[N], DD* lds, double* pub
 #pragma unroll
     for (int j = 0; j < N; ++j) lds[wid * N + j] = v[j];
   }
-  __syncthreads();
+  if (__syncthreads_or(bad)) return false;
+  const u64 t = u64(tag) << 32;
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int j = 0; j < N; ++j) {
       DD a = lds[j];
       for (int w = 1; w < kPersistThreads / 64; ++w) a = dd_add(a, lds[w * N + j]);
-      st_agent_f64(pub + (size_t(blockIdx.x) * N + j) * 2 + 0, a.s);
-      st_agent_f64(pub + (size_t(blockIdx.x) * N + j) * 2 + 1, a.c);
+      const u64 s = u64(__double_as_longlong(a.s));
+      const u64 c = u64(__double_as_longlong(a.c));
+      u64* g = gran + (size_t(blockIdx.x) * N + j) * 4;
+      st_gran(g + 0, t | (s >> 32));
+      st_gran(g + 1, t | (s & 0xffffffffull));
+      st_gran(g + 2, t | (c >> 32));
+      st_gran(g + 3, t | (c & 0xffffffffull));
     }
   }
-}
-
-// after the barrier: the sum of all G partials in a fixed order (lane l: l, l+64, ...; then the
-// wave butterfly), rounded to T, identical in every workgroup; wave 0 computes, LDS broadcasts
-template <typename T, int N>
-__device__ __forceinline__ void persist_total(const double* pub, unsigned G, double* lds_out, double (&out)[N]) {
   if (threadIdx.x < 64) {
-    const unsigned lane = threadIdx.x;
-    // G <= kPersistMaxWG = 4 x 64: every partial a lane sums is loaded before the first add
-    double ps[4][N], pc[4][N];
+    bool ok = false;
+    u64 q[4][N][4];
+    for (unsigned spin = 0; spin < kPersistSpin; ++spin) {
+      bool mine = true;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const unsigned g = min(lane + 64u * u, G - 1);
+      for (int u = 0; u < 4; ++u) {
+        const unsigned g = unsigned(lane) + 64u * u;
+        if (g < G) {
 #pragma unroll
-      for (int j = 0; j < N; ++j) {
-        ps[u][j] = ld_agent_f64(pub + (size_t(g) * N + j) * 2);
-        pc[u][j] = ld_agent_f64(pub + (size_t(g) * N + j) * 2 + 1);
+          for (int j = 0; j < N; ++j)
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+              q[u][j][h] = ld_gran(gran + (size_t(g) * N + j) * 4 + h);
+              mine &= unsigned(q[u][j][h] >> 32) == tag;
+            }
+        }
+      }
+      if (__all(mine)) {
+        ok = true;
+        break;
+      }
+      if (__shfl(int(lane == 0 && persist_timed_out(err)), 0, 64)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (ok) {
+      DD a[N];
+#pragma unroll
+      for (int j = 0; j < N; ++j) a[j] = dd_zero();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool in = unsigned(lane) + 64u * u < G;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          const u64 s = (q[u][j][0] << 32) | (q[u][j][1] & 0xffffffffull);
+          const u64 c = (q[u][j][2] << 32) | (q[u][j][3] & 0xffffffffull);
+          a[j] = dd_add(a[j], in ? DD{__longlong_as_double((long long)s), __longlong_as_double((long long)c)} : dd_zero());
+        }
+      }
+      wave_reduce_dd<N>(a);
+      if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) lds_out[j] = round_to<T>(dd_value(a[j]));
       }
     }
-    DD a[N];
-#pragma unroll
-    for (int j = 0; j < N; ++j) a[j] = dd_zero();
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const bool ok = lane + 64u * u < G;
-#pragma unroll
-      for (int j = 0; j < N; ++j) a[j] = dd_add(a[j], DD{ok ? ps[u][j] : 0.0, ok ? pc[u][j] : 0.0});
-    }
-    wave_reduce_dd<N>(a);
     if (lane == 0) {
-#pragma unroll
-      for (int j = 0; j < N; ++j) lds_out[j] = round_to<T>(dd_value(a[j]));
+      if (!ok) persist_fail(err);
+      *s_ok = ok;
     }
   }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < N; ++j) out[j] = lds_out[j];
+  return *s_ok != 0;
 }
 
 template <typename T, int PRE, int R>
 __global__ void __launch_bounds__(kPersistThreads) k_pcg_persist(int32_t n, PcgState* S, CsrView A, CsrView L,
-                                                                 CsrView LT, const T* __restrict__ d, T* x, T* r, T* p,
-                                                                 T* t, PersistSync sy) {
+                                                                 CsrView LT, const T* __restrict__ d, T* x, const T* r,
+                                                                 T* p, PersistSync sy) {
   constexpr bool SPAI = PRE == LSPCG_PRECOND_EXT_SPAI || PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
   constexpr bool SCALED = PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  constexpr int QB = R >= 4 ? 2 : kPersistQB;  // 4 rows per thread: fewer gathers in flight (registers)
   __shared__ DD lds_dd[kPersistThreads / 64 * 2];
   __shared__ double lds_tot[2];
   __shared__ int s_ok;
@@ -948,7 +1047,6 @@ __global__ void __launch_bounds__(kPersistThreads) k_pcg_persist(int32_t n, PcgS
   T alpha = T(S->alpha);
   int64_t k = S->iter;
   int code = 0;
-  unsigned epoch = 0;
   const bool lead = blockIdx.x == 0 && tid == 0;
   bool own[R];
   int32_t row[R], ab[R], ae[R], lb[R], le[R], tb[R], te[R];
@@ -971,41 +1069,53 @@ __global__ void __launch_bounds__(kPersistThreads) k_pcg_persist(int32_t n, PcgS
     rr_[m] = own[m] ? r[i] : T(0);
     pr[m] = T(0);
     if constexpr (SCALED || PRE == LSPCG_PRECOND_DIAGONAL) dr[m] = own[m] ? d[i] : T(1);
+    if constexpr (SPAI)
+      if (own[m]) Gran<T>::put(sy.rg, i, rr_[m], unsigned(5 * k + 1));  // r_k of the first iteration
   }
-  auto gath = [](const T* v) { return [v](int32_t c) { return ld_sc1<T>(v + c); }; };
   bool alive = true;
   for (;; ++k) {
-    // t = Lᵀ r (scaled: / d) -- r_k of every workgroup is visible (previous barrier / launch)
+    const unsigned ep = unsigned(5 * k);
+    bool bad = false;
+    stamp(sy, k, 0);
+    // t = Lᵀ r_k (scaled: / d), published for the L row sums of every workgroup
     if constexpr (SPAI) {
 #pragma unroll
       for (int m = 0; m < R; ++m) {
         if (!own[m]) continue;
-        const T s = sell_row<T, kPersistQB>(LT, tb[m], te[m], row[m], gath(r));
-        st_sc1<T>(t + row[m], SCALED ? s / dr[m] : s);
+        T s;
+        bad |= !sell_row_gran<T, QB>(LT, tb[m], te[m], row[m], sy.rg, ep + 1, sy.err, s);
+        Gran<T>::put(sy.tg, row[m], SCALED ? s / dr[m] : s, ep + 2);
       }
-      if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
     }
+    stamp(sy, k, 1);
     // z = M⁻¹ r ; partials of ρ_k = r·z and ‖r_k‖²
     DD dz[2] = {dd_zero(), dd_zero()};
     T zr[R];
 #pragma unroll
     for (int m = 0; m < R; ++m) {
       const T ri = rr_[m];
-      T zi;
-      if constexpr (SCALED) zi = own[m] ? sell_row<T, kPersistQB>(L, lb[m], le[m], row[m], gath(t)) + (eps * ri) / dr[m] : T(0);
-      else if constexpr (SPAI) zi = own[m] ? sell_row<T, kPersistQB>(L, lb[m], le[m], row[m], gath(t)) + eps * ri : T(0);
-      else if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) zi = ri / dr[m];
-      else zi = ri;
+      T zi = T(0);
+      if constexpr (SPAI) {
+        if (own[m]) {
+          T s;
+          bad |= !sell_row_gran<T, QB>(L, lb[m], le[m], row[m], sy.tg, ep + 2, sy.err, s);
+          if constexpr (SCALED) zi = s + (eps * ri) / dr[m];
+          else zi = s + eps * ri;
+        }
+      } else if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) {
+        zi = ri / dr[m];
+      } else {
+        zi = ri;
+      }
       zr[m] = zi;
       if (own[m]) {
         dd_fma(dz[0], double(ri), double(zi));
         dd_fma(dz[1], double(ri), double(ri));
       }
     }
-    persist_publish<2>(dz, lds_dd, sy.pz);
-    if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
+    stamp(sy, k, 2);
     double v2[2];
-    persist_total<T, 2>(sy.pz, G, lds_tot, v2);
+    if (!(alive = persist_allreduce<T, 2>(dz, bad, lds_dd, lds_tot, sy.gz, sy.err, ep + 3, G, &s_ok, v2))) break;
     const double rr = k > 0 ? v2[1] : rr0;
     if (k >= max_iter) {
       code = 2;
@@ -1019,39 +1129,43 @@ __global__ void __launch_bounds__(kPersistThreads) k_pcg_persist(int32_t n, PcgS
       if (hist) hist[k] = double(tsqrt<T>(T(rr)));
     }
     if (code) break;  // every workgroup decides on the same totals: uniform exit
+    stamp(sy, k, 3);
     rho_prev = rho;
     rho = v2[0];
-    // x += α_{k-1} p_{k-1} ; p_k = p_{k-1}β + z
+    // x += α_{k-1} p_{k-1} ; p_k = p_{k-1}β + z, published for the A row sums
     const bool first = k == 0;
     const T beta = first ? T(0) : T(rho) / T(rho_prev);
 #pragma unroll
     for (int m = 0; m < R; ++m) {
       if (!first) xr[m] = xr[m] + alpha * pr[m];
       pr[m] = first ? zr[m] : (pr[m] * beta) + zr[m];
-      if (own[m]) st_sc1<T>(p + row[m], pr[m]);
+      if (own[m]) Gran<T>::put(sy.pg, row[m], pr[m], ep + 4);
     }
-    if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
+    stamp(sy, k, 4);
     // q = A p ; partials of π_k = p·q
     DD dq[1] = {dd_zero()};
     T qr[R];
 #pragma unroll
     for (int m = 0; m < R; ++m) {
-      qr[m] = own[m] ? sell_row<T, kPersistQB>(A, ab[m], ae[m], row[m], gath(p)) : T(0);
-      if (own[m]) dd_fma(dq[0], double(pr[m]), double(qr[m]));
+      qr[m] = T(0);
+      if (own[m]) {
+        bad |= !sell_row_gran<T, QB>(A, ab[m], ae[m], row[m], sy.pg, ep + 4, sy.err, qr[m]);
+        dd_fma(dq[0], double(pr[m]), double(qr[m]));
+      }
     }
-    persist_publish<1>(dq, lds_dd, sy.pq);
-    if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
+    stamp(sy, k, 5);
     double v1[1];
-    persist_total<T, 1>(sy.pq, G, lds_tot, v1);
+    if (!(alive = persist_allreduce<T, 1>(dq, bad, lds_dd, lds_tot, sy.gq, sy.err, ep + 5, G, &s_ok, v1))) break;
+    stamp(sy, k, 6);
     pq = v1[0];
     alpha = T(rho) / T(pq);
-    // r -= α q
+    // r_{k+1} = r_k - α q, published for the next Lᵀ row sums
 #pragma unroll
     for (int m = 0; m < R; ++m) {
       rr_[m] = rr_[m] - alpha * qr[m];
-      if (own[m]) st_sc1<T>(r + row[m], rr_[m]);
+      if constexpr (SPAI)
+        if (own[m]) Gran<T>::put(sy.rg, row[m], rr_[m], ep + 6);
     }
-    if (!(alive = persist_sync(sy.cnt, ++epoch, G, &s_ok))) break;
   }
   if (!alive) return;  // timeout word set: the host fails the solve
 #pragma unroll
@@ -1172,8 +1286,9 @@ struct lspcg_solver {
   // persistent multi-workgroup solve (k_pcg_persist): used for small_n < n <= persist_n
   int64_t persist_n = 0;   // LSPCG_PERSIST_N (0 disables)
   int persist_wg = 0;      // largest grid (LSPCG_PERSIST_WG; default: one workgroup per CU, <= 256)
-  unsigned* psync = nullptr;  // arrival counters + timeout word (memset before every launch)
-  double* ppart = nullptr;    // [kPersistMaxWG x (2 + 1) dots x DD] partials
+  unsigned* psync = nullptr;  // timeout word + dot-partial granules (memset before every launch)
+  void* pgran = nullptr;      // granules of r, t, p (memset before every launch)
+  void* pstamps = nullptr;    // LSPCG_PERSIST_STAMPS diagnostics
   unsigned* herr = nullptr;   // pinned copy of the timeout word
   int64_t small_n = 1024;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it): <= 2 rows
                            // per thread; 5 rows lose to the 5-kernel schedule
@@ -1584,8 +1699,8 @@ static bool persist_grid(const lspcg_solver* s, int64_t max_iter, int* G, int* R
   for (int r = 1; r <= kPersistMaxRows; r *= 2) {
     const int64_t g = (s->n + int64_t(kPersistThreads) * r - 1) / (int64_t(kPersistThreads) * r);
     if (g <= gmax) {
-      // the barrier counters count epochs x G arrivals in 32 bits (<= 5 barriers per iteration)
-      if ((5 * (max_iter + 2)) * g >= (int64_t(1) << 32)) return false;
+      // epochs (5 per iteration) are 32-bit tags
+      if (5 * (max_iter + 2) >= (int64_t(1) << 32)) return false;
       *G = int(g);
       *R = r;
       return true;
@@ -1605,20 +1720,28 @@ static CsrView persist_view(const lspcg_solver* s, int w) {
 template <typename T>
 static int launch_persist(lspcg_solver* s, int G, int R, hipStream_t st) {
   const bool spai = s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  const size_t vg = sizeof(u64) * (sizeof(T) / 4) * size_t(s->n);  // granules of one vector
   if (!s->psync) {
-    LSPCG_HIP(hipMalloc(&s->psync, kPersistSyncBytes));
-    LSPCG_HIP(hipMalloc(&s->ppart, sizeof(double) * kPersistMaxWG * 3 * 2));
+    LSPCG_HIP(hipMalloc(&s->psync, persist_sync_bytes(kPersistMaxWG)));
     LSPCG_HIP(hipHostMalloc(&s->herr, sizeof(unsigned), hipHostMallocDefault));
   }
-  LSPCG_HIP(hipMemsetAsync(s->psync, 0, kPersistSyncBytes, st));
+  if (!s->pgran) LSPCG_HIP(hipMalloc(&s->pgran, 3 * vg));
+  LSPCG_HIP(hipMemsetAsync(s->psync, 0, persist_sync_bytes(G), st));
+  LSPCG_HIP(hipMemsetAsync(s->pgran, 0, 3 * vg, st));
   const CsrView A = persist_view(s, 0);
   const CsrView L = spai ? persist_view(s, 1) : CsrView{};
   const CsrView LT = spai ? persist_view(s, 2) : CsrView{};
-  const PersistSync sy{s->psync, s->ppart, s->ppart + kPersistMaxWG * 2 * 2};
+  u64* vgr = static_cast<u64*>(s->pgran);
+  const size_t ve = vg / sizeof(u64);
+  static const bool stamps = [] { const char* e = std::getenv("LSPCG_PERSIST_STAMPS"); return e && e[0] == '1'; }();
+  if (stamps && !s->pstamps) LSPCG_HIP(hipMalloc(&s->pstamps, sizeof(u64) * 2 * kStampIters * kStampPhases));
+  if (stamps) LSPCG_HIP(hipMemsetAsync(s->pstamps, 0, sizeof(u64) * 2 * kStampIters * kStampPhases, st));
+  const PersistSync sy{s->psync, reinterpret_cast<u64*>(s->psync + persist_gz_off()),
+                       reinterpret_cast<u64*>(s->psync + persist_gq_off(G)), vgr, vgr + ve, vgr + 2 * ve,
+                       stamps ? static_cast<u64*>(s->pstamps) : nullptr};
   auto* x = static_cast<T*>(s->x);
-  auto* r = static_cast<T*>(s->r);
+  auto* r = static_cast<const T*>(s->r);
   auto* p = static_cast<T*>(s->p);
-  auto* t = static_cast<T*>(s->t);
   const T* d = static_cast<const T*>(s->d);
   const int32_t n = int32_t(s->n);
   const dim3 g(G), b(kPersistThreads);
@@ -1626,26 +1749,45 @@ static int launch_persist(lspcg_solver* s, int G, int R, hipStream_t st) {
     constexpr int RR = decltype(rows)::value;
     switch (s->precond) {
       case LSPCG_PRECOND_NONE:
-        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_NONE, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, t, sy);
+        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_NONE, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, sy);
         break;
       case LSPCG_PRECOND_DIAGONAL:
-        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_DIAGONAL, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, t,
-                           sy);
+        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_DIAGONAL, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, sy);
         break;
       case LSPCG_PRECOND_EXT_SPAI:
-        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_EXT_SPAI, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, t,
-                           sy);
+        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_EXT_SPAI, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, sy);
         break;
       default:
         hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_EXT_SPAI_SCALED, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r,
-                           p, t, sy);
+                           p, sy);
     }
   };
   if (R == 1) go(std::integral_constant<int, 1>{});
   else if (R == 2) go(std::integral_constant<int, 2>{});
   else go(std::integral_constant<int, 4>{});
   LSPCG_HIP(hipGetLastError());
-  LSPCG_HIP(hipMemcpyAsync(s->herr, s->psync + kPersistErr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  LSPCG_HIP(hipMemcpyAsync(s->herr, s->psync, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  if (stamps) {  // diagnostics: per-phase durations (us) of iterations 1..min(iters, 64) on stderr
+    std::vector<u64> h(2 * kStampIters * kStampPhases);
+    LSPCG_HIP(hipMemcpyAsync(h.data(), s->pstamps, sizeof(u64) * h.size(), hipMemcpyDeviceToHost, st));
+    LSPCG_HIP(hipStreamSynchronize(st));
+    for (int w = 0; w < 2; ++w) {
+      double acc[kStampPhases] = {0};
+      int cnt = 0;
+      for (int k = 1; k + 1 < kStampIters; ++k) {
+        const u64* a = h.data() + (w * kStampIters + k) * kStampPhases;
+        const u64* nx = a + kStampPhases;
+        if (!a[0] || !a[6] || !nx[0]) break;
+        for (int j = 0; j < 6; ++j) acc[j] += (a[j + 1] - a[j]) * 0.01;
+        acc[6] += (nx[0] - a[6]) * 0.01;
+        ++cnt;
+      }
+      std::fprintf(stderr, "[lspcg persist] n=%lld G=%d R=%d wg %s: %d its, us/phase Lt %.2f | L %.2f | rho-red %.2f | p %.2f | A %.2f | pi-red %.2f | r %.2f\n",
+                   (long long)s->n, G, R, w ? "last" : "0", cnt, cnt ? acc[0] / cnt : 0, cnt ? acc[1] / cnt : 0,
+                   cnt ? acc[2] / cnt : 0, cnt ? acc[3] / cnt : 0, cnt ? acc[4] / cnt : 0, cnt ? acc[5] / cnt : 0,
+                   cnt ? acc[6] / cnt : 0);
+    }
+  }
   return LSPCG_OK;
 }
 
@@ -2060,7 +2202,8 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipFree(s->flag);
   (void)hipFree(s->dhist);
   (void)hipFree(s->psync);
-  (void)hipFree(s->ppart);
+  (void)hipFree(s->pgran);
+  (void)hipFree(s->pstamps);
   (void)hipHostFree(s->herr);
   (void)hipStreamDestroy(s->stream);
   delete s;

@@ -1,0 +1,125 @@
+"""Workspace drop-ins (neural_cg/workspace.py, scaled_workspace.py):
+
+* ``load_from_checkpoint`` (infer.py:237) on a synthesized Lightning-shaped checkpoint --
+  ``hyper_parameters`` as SimpleTrainingWorkspace.save_hyperparameters() stores them
+  (workspace.py:26-52: trainer / loss / convergence args beside node_features, edge_features,
+  gnn, epsilon, block_size) and ``state_dict`` with the ``gnn.*`` parameters -- loaded with
+  ``weights_only=True``; strict key matching.
+* ``ScaledInferenceWorkspace.inference_step`` (scaled_workspace.py:199-212) against the
+  reference's own expression ``csr_matrix(to_csr_cpu(...) @ diags(rsqrt_diag))`` (GPU).
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from oracle import gnn as OG
+from oracle import linalg as O
+
+
+class Opaque:  # an arbitrary pickled object (what an omegaconf DictConfig hparam would be)
+    pass
+
+
+def _ckpt(tmp_path, node_in=4, edge_in=9, bs=3, eps=2e-3, extra=None):
+    torch.manual_seed(11)
+    ref = OG.build(node_in, edge_in, bs, seed=11)
+    sd = {f"gnn.{k}": v.clone() for k, v in ref.state_dict().items()}
+    if extra:
+        sd.update(extra)
+    from learningsparsepreconditioner4gpu_amd.nn import default_gnn_config
+
+    hp = {"batch_size": 4, "batch_less": False, "block_size": bs, "test_max_iter": 100,
+          "optimizer": {"name": "adamw", "lr": 1e-3}, "scheduler": {"name": "exp", "gamma": 0.99},
+          "loss": {"name": "RelativeL2Loss_ANorm", "params": None}, "inspect_norms": False,
+          "check_converge": False, "check_methods": ["none"], "check_devices": ["cpu"],
+          "node_features": node_in, "edge_features": edge_in, "gnn": default_gnn_config(), "epsilon": eps}
+    path = tmp_path / "model.ckpt"
+    torch.save({"epoch": 3, "global_step": 120, "pytorch-lightning_version": "2.5.0", "state_dict": sd,
+                "hyper_parameters": hp}, path)
+    return path, ref
+
+
+def test_load_from_checkpoint_weights_only(tmp_path):
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    path, ref = _ckpt(tmp_path)
+    ws = SimpleInferenceWorkspace.load_from_checkpoint(str(path))
+    assert ws.block_size == 3 and ws.epsilon == 2e-3
+    got = ws.gnn.state_dict()
+    want = ref.state_dict()
+    assert set(got) == set(want)
+    for k in want:
+        assert torch.equal(got[k], want[k]), k
+    # the packed kernel blob is built from exactly these tensors
+    assert ws.gnn.pack_weights().numel() > 0
+
+
+def test_load_from_checkpoint_strict_keys(tmp_path):
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    path, _ = _ckpt(tmp_path, extra={"gnn.mp_layers.0.bogus": torch.zeros(1)})
+    with pytest.raises(RuntimeError, match="Unexpected key"):
+        SimpleInferenceWorkspace.load_from_checkpoint(str(path))
+
+
+def test_load_from_checkpoint_refuses_pickled_objects(tmp_path):
+    """weights_only=True: a checkpoint holding arbitrary pickled objects is refused (only
+    trusted=True, for files one produced oneself, unpickles them)."""
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    path, _ = _ckpt(tmp_path)
+    ck = torch.load(path, weights_only=True)
+    ck["hyper_parameters"]["optimizer"] = Opaque()
+    torch.save(ck, path)
+    with pytest.raises(Exception):
+        SimpleInferenceWorkspace.load_from_checkpoint(str(path))
+
+
+@pytest.mark.gpu
+def test_checkpoint_forward_equals_seeded_model(gpu_ctx, tmp_path):
+    """The loaded workspace's GNN forward equals the same weights constructed directly."""
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+    from learningsparsepreconditioner4gpu_amd.nn import build_gnn
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    A, mask, nodes = P.elasticity_box(5, 3, 3)
+    s = make_sample(A, mask, node_features=np.zeros((A.shape[0] // 3, 1)), block_size=3).to("cuda")
+    path, _ = _ckpt(tmp_path, node_in=s.x.shape[1], edge_in=9, bs=3)
+    ws = SimpleInferenceWorkspace.load_from_checkpoint(str(path))
+    direct = build_gnn(s.x.shape[1], 9, 3, seed=11)
+    a = ws.forward(s.x, s.edge_index, s.edge_attr)
+    _, b = direct(s.x, s.edge_index, s.edge_attr)
+    assert torch.equal(a.reshape(-1), b.reshape(-1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bs", [1, 3])
+def test_scaled_inference_step_matches_reference_expression(gpu_ctx, bs):
+    """scaled_workspace.py:207-211: csr_matrix(to_csr_cpu(ei, boo, n, mask) @ diags(rsqrt_diag)),
+    rsqrt_diag the fp32 sample field widened to fp64 -- same sorted pattern, same fp64 bits."""
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+    from learningsparsepreconditioner4gpu_amd.workspace import ScaledInferenceWorkspace
+
+    if bs == 1:
+        A, mask, _ = P.poisson2d_grid(30, 23)
+        feats = None
+    else:
+        A, mask, nodes = P.elasticity_box(6, 4, 3)
+        feats = nodes
+    s = make_sample(A, mask, node_features=feats, block_size=bs)
+    ws = ScaledInferenceWorkspace(node_features=s.x.shape[1], edge_features=s.edge_attr.shape[1], block_size=bs,
+                                  seed=3)
+    d = s.to("cuda")
+    L, _ = ws.inference_step(d, block_output=False)
+    boo = ws.forward(d.x, d.edge_index, d.edge_attr).cpu().numpy()
+    n = s.num_nodes * bs
+    ref = O.to_csr(s.edge_index.numpy(), boo, n, s.mask.numpy(), dtype=np.float64)
+    rsqrt = s.rsqrt_diag.numpy().reshape(-1).astype(np.float64)
+    ref = sp.csr_matrix(ref @ sp.diags(rsqrt))
+    ref.sort_indices()
+    got = L.to_scipy()
+    assert np.array_equal(got.indptr, ref.indptr) and np.array_equal(got.indices, ref.indices)
+    assert np.array_equal(got.data, ref.data)

@@ -1,0 +1,10 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/r2
+timeout -k 10 300 python -u -m pytest tests/test_gpu_sell.py tests/test_gpu_fuzz.py -x -v --timeout 120 --timeout-method thread -k "pcg_sell_equals or persist" > gpurun_out/r2/t3_sell.txt 2>&1
+rc=$?; echo "sell rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u -m pytest tests/test_gpu_traj.py -x -v --timeout 120 --timeout-method thread -k "persistent" > gpurun_out/r2/t3_traj.txt 2>&1
+rc=$?; echo "traj rc=$rc"; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 400 python -u tools/persist_probe.py --workloads heat_batch8,poisson256,kuhn41 > gpurun_out/r2/persist_probe3.jsonl 2> gpurun_out/r2/persist_probe3.err
+echo "probe rc=$?"
