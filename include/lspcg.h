@@ -90,10 +90,11 @@ int lspcg_mat_scale_columns(lspcg_mat* A, const void* d);
 /* ---- kernels ---- */
 /* y = A x (scipy csr_matvec bit pattern: per-row sequential sum in index order) */
 int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y);
-/* analysis step (cf. rocSPARSE csrmv_analysis): attach a SELL-64 copy of a scalar CSR matrix
- * (same values and dtype; 16-bit column offsets where they fit) that lspcg_spmv then uses -- the
+/* analysis step (cf. rocSPARSE csrmv_analysis): attach a SELL-64 copy of a scalar CSR matrix, or
+ * the BSELL-64 block copy of a BSR 3x3 (one column per block, plane-major block values), with the
+ * same values and dtype and 16-bit column offsets where they fit, that lspcg_spmv then uses -- the
  * results keep the same bits.  *kind (nullable) = 16 or 32 (column width) or 0 when the matrix
- * stays on the CSR kernel (block size 3, irregular row lengths).  lspcg_mat_scale_columns drops it. */
+ * stays on the CSR / BSR kernel (irregular row lengths).  lspcg_mat_scale_columns drops it. */
 int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind);
 /* average device ms of one SpMV launch, HIP events on the ctx stream.  flush_bytes == 0:
  * reps back-to-back launches (warm caches); > 0: before every launch a read of a flush_bytes

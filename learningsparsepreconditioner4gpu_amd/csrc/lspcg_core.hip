@@ -483,14 +483,17 @@ int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind) {
   LSPCG_HIP(hipSetDevice(A->ctx->device));
   drop_sell(A);
   if (kind) *kind = 0;
-  if (A->block_size != 1 || A->n == 0 || A->nnzb == 0) return LSPCG_OK;
+  if (A->n == 0 || A->nnzb == 0) return LSPCG_OK;
   hipStream_t st = A->ctx->stream;
   std::unique_ptr<SellCopy> c(new SellCopy());
-  int rc = sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, sell_max_pad(), true, st, &c->P);
-  if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // irregular rows: the CSR kernel stays
+  const bool blk = A->block_size == 3;  // BSR 3x3: the BSELL-64 block layout
+  int rc = blk ? bsell_build_pattern(A->nb, A->nnzb, A->rowptr, A->colind, sell_max_pad(), true, st, &c->P)
+               : sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, sell_max_pad(), true, st, &c->P);
+  if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // irregular rows: the CSR / BSR kernel stays
   if (rc) return rc;
   const int vd = A->storage_dtype();
-  rc = sell_fill_values(c->P, A->colind, A->vals, vd, vd, st, &c->vals);
+  rc = blk ? bsell_fill_values(c->P, A->vals, vd, vd, st, &c->vals)
+           : sell_fill_values(c->P, A->colind, A->vals, vd, vd, st, &c->vals);
   if (rc) {
     c->release();
     return rc;

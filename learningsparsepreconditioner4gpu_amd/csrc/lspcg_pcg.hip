@@ -1280,7 +1280,6 @@ struct lspcg_solver {
   const SellPattern* sp[3] = {nullptr, nullptr, nullptr};
   void* sv[3] = {nullptr, nullptr, nullptr};
   int svd[3] = {0, 0, 0};
-  int32_t* xrow[3] = {nullptr, nullptr, nullptr};  // scalar row pointers of expanded BSR3 views
   double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
   int64_t dhist_cap = 0;
   // persistent multi-workgroup solve (k_pcg_persist): used for small_n < n <= persist_n
@@ -1301,12 +1300,10 @@ static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view);
 
 static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   hipStream_t st = s->ctx->stream;
-  if (s->sv[w] || s->spat[w].gp || s->xrow[w]) LSPCG_HIP(hipStreamSynchronize(s->stream));  // a solve may use them
+  if (s->sv[w] || s->spat[w].gp) LSPCG_HIP(hipStreamSynchronize(s->stream));  // a solve may use them
   (void)hipFree(s->sv[w]);
   s->sv[w] = nullptr;
   s->spat[w].release();
-  (void)hipFree(s->xrow[w]);
-  s->xrow[w] = nullptr;
   s->sp[w] = nullptr;
   if (!s->use_sell || view->n == 0 || view->nnzb == 0) return LSPCG_OK;
   if (view->block_size == 3) return build_sell_bsr3(s, w, view);
@@ -1328,72 +1325,23 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   return LSPCG_OK;
 }
 
-// BSR 3x3 -> scalar rows in the reference's own order (validate.py:51 expands the blocks to a
-// scalar CSR sorted by column: block by block, then the block's 3 columns), in-block zeros kept
-// -- the same summation sequence as the block kernel.  One thread per scalar row r = 3I + c.
-template <typename VS>
-__global__ void k_bsr3_expand(int64_t nb, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
-                              const VS* __restrict__ vals, int32_t* __restrict__ xrow, int32_t* __restrict__ xcol,
-                              VS* __restrict__ xval) {
-  const int64_t n = 3 * nb;
-  for (int64_t r = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; r < n; r += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t I = r / 3;
-    const int c = int(r - 3 * I);
-    const int32_t b0 = rowptr[I], len = rowptr[I + 1] - b0;
-    const int32_t base = 9 * b0 + 3 * c * len;
-    if (xrow) {
-      xrow[r] = base;
-      if (r == n - 1) xrow[n] = 9 * rowptr[nb];
-    }
-    for (int32_t q = 0; q < len; ++q) {
-      const int32_t J = colind[b0 + q];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int32_t pos = base + 3 * q + k;
-        if (xcol) xcol[pos] = 3 * J + k;
-        if (xval) xval[pos] = vals[int64_t(b0 + q) * 9 + 3 * c + k];
-      }
-    }
-  }
-}
-
+// BSR 3x3 views: the BSELL-64 block layout (lspcg_sell.hpp), pattern shared with A's when the
+// index arrays are A's, values in the view's storage dtype (fp32 when lossless)
 static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view) {
   hipStream_t st = s->ctx->stream;
-  const int64_t n = view->n, ne = 9 * view->nnzb;
-  if (ne >= (int64_t(1) << 31)) return LSPCG_OK;  // expanded entries must fit int32 row pointers
-  const dim3 g(elem_grid(n)), b(kThreads);
-  const int vd = view->storage_dtype();
   const bool shared = w > 0 && s->sp[0] && view->rowptr == s->Av.rowptr && view->colind == s->Av.colind;
   const SellPattern* P = nullptr;
   if (shared) {
     P = s->sp[0];
   } else {
-    int32_t* xcol = nullptr;
-    LSPCG_HIP(hipMalloc(&s->xrow[w], sizeof(int32_t) * (n + 1)));
-    LSPCG_HIP(hipMalloc(&xcol, sizeof(int32_t) * ne));
-    hipLaunchKernelGGL(k_bsr3_expand<float>, g, b, 0, st, view->nb, view->rowptr, view->colind,
-                       static_cast<const float*>(nullptr), s->xrow[w], xcol, static_cast<float*>(nullptr));
-    const int rc = sell_build_pattern(n, ne, s->xrow[w], xcol, sell_max_pad(), s->sell16, st, &s->spat[w]);
-    (void)hipStreamSynchronize(st);
-    (void)hipFree(xcol);
-    if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: block kernel
+    const int rc = bsell_build_pattern(view->nb, view->nnzb, view->rowptr, view->colind, sell_max_pad(), s->sell16, st,
+                                       &s->spat[w]);
+    if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: the staged block kernel
     if (rc) return rc;
     P = &s->spat[w];
   }
-  void* xval = nullptr;
-  LSPCG_HIP(hipMalloc(&xval, (vd == LSPCG_F32 ? 4 : 8) * ne));
-  if (vd == LSPCG_F32)
-    hipLaunchKernelGGL(k_bsr3_expand<float>, g, b, 0, st, view->nb, view->rowptr, view->colind,
-                       static_cast<const float*>(view->vals), static_cast<int32_t*>(nullptr),
-                       static_cast<int32_t*>(nullptr), static_cast<float*>(xval));
-  else
-    hipLaunchKernelGGL(k_bsr3_expand<double>, g, b, 0, st, view->nb, view->rowptr, view->colind,
-                       static_cast<const double*>(view->vals), static_cast<int32_t*>(nullptr),
-                       static_cast<int32_t*>(nullptr), static_cast<double*>(xval));
-  const int rc = sell_fill_values(*P, nullptr, xval, vd, vd, st, &s->sv[w]);
-  (void)hipStreamSynchronize(st);
-  (void)hipFree(xval);
-  if (rc) return rc;
+  const int vd = view->storage_dtype();
+  if (int rc = bsell_fill_values(*P, view->vals, vd, vd, st, &s->sv[w])) return rc;
   s->svd[w] = vd;
   s->sp[w] = P;
   return LSPCG_OK;
@@ -1641,7 +1589,7 @@ static bool small_path(const lspcg_solver* s) {
 static CsrView csr_view(const lspcg_solver* s, int w, const lspcg_mat& M) {
   CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, nullptr, nullptr, nullptr, 0, 0};
   if (const SellPattern* P = s->sp[w]) {
-    if (s->small_sell && s->sv[w] && !s->xrow[w] && P->groups > 0) {
+    if (s->small_sell && s->sv[w] && P->bs == 1 && P->groups > 0) {
       v.gp = P->gp;
       v.scol = P->col;
       v.sv = s->sv[w];
@@ -1694,7 +1642,7 @@ static bool persist_grid(const lspcg_solver* s, int64_t max_iter, int* G, int* R
   if (s->persist_n <= 0 || s->n <= 0 || s->n > s->persist_n || s->precond == LSPCG_PRECOND_IC) return false;
   const bool spai = s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
   for (int w = 0; w < (spai ? 3 : 1); ++w)
-    if (!s->sp[w] || !s->sv[w] || s->sp[w]->groups <= 0) return false;  // SELL views required
+    if (!s->sp[w] || !s->sv[w] || s->sp[w]->groups <= 0 || s->sp[w]->bs != 1) return false;  // scalar SELL views
   const int64_t gmax = std::max(1, std::min<int>(s->persist_wg, int(kPersistMaxWG)));
   for (int r = 1; r <= kPersistMaxRows; r *= 2) {
     const int64_t g = (s->n + int64_t(kPersistThreads) * r - 1) / (int64_t(kPersistThreads) * r);
@@ -2196,7 +2144,6 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   for (void* p : {s->own_A, s->own_L, s->own_LT}) (void)hipFree(p);
   for (int w = 0; w < 3; ++w) {
     (void)hipFree(s->sv[w]);
-    (void)hipFree(s->xrow[w]);
     s->spat[w].release();
   }
   (void)hipFree(s->flag);

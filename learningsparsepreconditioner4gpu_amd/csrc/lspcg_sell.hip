@@ -71,10 +71,160 @@ static int fill_grid(int64_t n) {
   return int(std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, kElemBlocksMax)));
 }
 
+// ---- BSELL-64 (BSR 3x3) ----------------------------------------------------------
+// block slots per row of each slice = its longest block row
+__global__ void k_bsell_len(int64_t nb, int64_t ns, const int32_t* __restrict__ rowptr, int32_t* __restrict__ cnt) {
+  const int64_t s = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= ns) return;
+  const int64_t I = s * kSellC + lane;
+  int len = I < nb ? rowptr[I + 1] - rowptr[I] : 0;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) len = max(len, __shfl_xor(len, m, 64));
+  if (lane == 0) cnt[s] = len;
+}
+
+// one workgroup per slice, threads over its 64 x G slots in storage order: slot p -> block row
+// 64 s + p % 64, block q = p / 64; columns and/or the 9 plane-major values (padding: value 0,
+// padding column)
+template <typename VS, typename VD>
+__global__ void __launch_bounds__(256) k_bsell_fill(int64_t nb, int64_t ns, const int32_t* __restrict__ gp,
+                                                    const int32_t* __restrict__ rowptr,
+                                                    const int32_t* __restrict__ colind, const VS* __restrict__ src,
+                                                    int32_t* __restrict__ col32, int16_t* __restrict__ col16,
+                                                    VD* __restrict__ dst) {
+  for (int64_t s = blockIdx.x; s < ns; s += gridDim.x) {
+    const int64_t g0 = gp[s];
+    const int32_t slots = 64 * (gp[s + 1] - gp[s]);
+    for (int32_t p = threadIdx.x; p < slots; p += blockDim.x) {
+      const int lane = p & 63;
+      const int32_t q = p >> 6;
+      const int64_t I = s * kSellC + lane;
+      int32_t b = 0, len = 0;
+      if (I < nb) {
+        b = rowptr[I];
+        len = rowptr[I + 1] - b;
+      }
+      const bool real = q < len;
+      if (col32) col32[64 * g0 + p] = real ? colind[b + q] : int32_t(-1);
+      if (col16) col16[64 * g0 + p] = real ? int16_t(colind[b + q] - int32_t(s * kSellC)) : kSellPad16;
+      if (dst) {
+#pragma unroll
+        for (int v = 0; v < 9; ++v)
+          dst[576 * (g0 + q) + 64 * v + lane] = real ? VD(src[9 * (int64_t(b) + q) + v]) : VD(0);
+      }
+    }
+  }
+}
+
+int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
+                       bool allow16, hipStream_t st, SellPattern* out);
+
+int bsell_build_pattern(int64_t nb, int64_t nnzb, const int32_t* rowptr, const int32_t* colind, double max_pad,
+                        bool allow16, hipStream_t st, SellPattern* out) {
+  SellPattern P;
+  P.n = 3 * nb;
+  P.nb = nb;
+  P.bs = 3;
+  P.ns = (nb + kSellC - 1) / kSellC;
+  P.rowptr = rowptr;
+  int32_t* cnt = nullptr;
+  void* tmp = nullptr;
+  auto fail = [&](hipError_t e) {
+    set_error(std::string("bsell_build_pattern: ") + hipGetErrorString(e));
+    (void)hipFree(cnt);
+    (void)hipFree(tmp);
+    P.release();
+    return LSPCG_ERR_HIP;
+  };
+  hipError_t e = hipMalloc(&cnt, sizeof(int32_t) * (P.ns + 1));
+  if (e == hipSuccess) e = hipMalloc(&P.gp, sizeof(int32_t) * (P.ns + 1));
+  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (P.ns + 1), st);
+  if (e != hipSuccess) return fail(e);
+  if (P.ns) hipLaunchKernelGGL(k_bsell_len, dim3(unsigned((P.ns + 3) / 4)), dim3(256), 0, st, nb, P.ns, rowptr, cnt);
+  size_t tb = 0;
+  e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, P.gp, int(P.ns + 1), st);
+  if (e == hipSuccess) e = hipMalloc(&tmp, tb);
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, P.gp, int(P.ns + 1), st);
+  int32_t groups = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&groups, P.gp + P.ns, sizeof(int32_t), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return fail(e);
+  (void)hipFree(cnt);
+  (void)hipFree(tmp);
+  cnt = nullptr;
+  tmp = nullptr;
+  P.groups = groups;
+  if (double(64) * double(groups) > max_pad * double(std::max<int64_t>(nnzb, 1))) {
+    P.release();
+    set_error("bsell: padding exceeds the limit (irregular block-row lengths)");
+    return LSPCG_ERR_UNSUPPORTED;
+  }
+  int fit = 1;
+  if (allow16 && nb) {
+    int* flag = nullptr;
+    e = hipMalloc(&flag, sizeof(int));
+    if (e == hipSuccess) e = hipMemsetAsync(flag, 0, sizeof(int), st);
+    if (e == hipSuccess)
+      hipLaunchKernelGGL(k_sell_fit16, dim3(fill_grid(nb)), dim3(kThreads), 0, st, nb, rowptr, colind, flag);
+    if (e == hipSuccess) e = hipMemcpyAsync(&fit, flag, sizeof(int), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(flag);
+    if (e != hipSuccess) return fail(e);
+  }
+  P.col_bits = fit == 0 ? 16 : 32;
+  e = hipMalloc(&P.col, size_t(P.col_bits / 8) * size_t(std::max<int64_t>(64 * P.groups, 1)));
+  if (e != hipSuccess) return fail(e);
+  if (P.ns)
+    hipLaunchKernelGGL((k_bsell_fill<float, float>), dim3(slice_grid(P.ns)), dim3(256), 0, st, nb, P.ns, P.gp, rowptr,
+                       colind, static_cast<const float*>(nullptr),
+                       P.col_bits == 32 ? static_cast<int32_t*>(P.col) : nullptr,
+                       P.col_bits == 16 ? static_cast<int16_t*>(P.col) : nullptr, static_cast<float*>(nullptr));
+  e = hipGetLastError();
+  if (e != hipSuccess) return fail(e);
+  *out = P;
+  return LSPCG_OK;
+}
+
+int bsell_fill_values(const SellPattern& P, const void* src, int src_dtype, int dst_dtype, hipStream_t st, void** out) {
+  const size_t es = dst_dtype == LSPCG_F32 ? 4 : 8;
+  void* v = nullptr;
+  LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(576 * P.groups, 1)));
+  const dim3 g(slice_grid(P.ns)), b(256);
+  const int32_t* nocol = nullptr;
+  if (P.ns) {
+    if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F64)
+      hipLaunchKernelGGL((k_bsell_fill<double, double>), g, b, 0, st, P.nb, P.ns, P.gp, P.rowptr, nocol,
+                         static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr),
+                         static_cast<double*>(v));
+    else if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F32)
+      hipLaunchKernelGGL((k_bsell_fill<double, float>), g, b, 0, st, P.nb, P.ns, P.gp, P.rowptr, nocol,
+                         static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr),
+                         static_cast<float*>(v));
+    else if (src_dtype == LSPCG_F32 && dst_dtype == LSPCG_F32)
+      hipLaunchKernelGGL((k_bsell_fill<float, float>), g, b, 0, st, P.nb, P.ns, P.gp, P.rowptr, nocol,
+                         static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr),
+                         static_cast<float*>(v));
+    else
+      hipLaunchKernelGGL((k_bsell_fill<float, double>), g, b, 0, st, P.nb, P.ns, P.gp, P.rowptr, nocol,
+                         static_cast<const float*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr),
+                         static_cast<double*>(v));
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    (void)hipFree(v);
+    set_error(std::string("bsell_fill_values: ") + hipGetErrorString(e));
+    return LSPCG_ERR_HIP;
+  }
+  *out = v;
+  return LSPCG_OK;
+}
+
 int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
                        bool allow16, hipStream_t st, SellPattern* out) {
   SellPattern P;
   P.n = n;
+  P.nb = n;
   P.ns = (n + kSellC - 1) / kSellC;
   P.rowptr = rowptr;
   int32_t* cnt = nullptr;

@@ -31,12 +31,24 @@ constexpr int kSellC = 64;  // rows per slice = one wave64
 constexpr int16_t kSellPad16 = -32768;
 
 // Pattern shared by every matrix with the same CSR (rowptr, colind).
+//
+// Block variant (bs == 3, "BSELL-64"; BSR 3x3 matrices): a wave owns 64
+// consecutive BLOCK rows; slot q of block row I = 64 s + lane holds ONE column index (int32 block
+// column or 16-bit offset from 64 s) and the block's 9 values stored plane-major,
+//     col[64 (gp[s] + q) + lane],  vals[576 (gp[s] + q) + 64 v + lane]  (v = 3 a + c),
+// so each of the 10 loads of a slot is one coalesced 256-B (fp32) wave access and a block costs
+// 9 values + 1 column instead of 9 scalar (value, column) pairs; x is gathered once per block
+// (3 consecutive entries) for the lane's 3 scalar rows.  Row 3I + a sums its blocks in column
+// order and inside a block c = 0, 1, 2: the order of the reference's expanded scalar CSR
+// (validate.py:51), in-block zeros kept (adding an exact 0*x changes no finite sum).
 struct SellPattern {
-  int64_t n = 0;
+  int64_t n = 0;                   // scalar rows
+  int64_t nb = 0;                  // rows of the pattern: scalar rows (bs 1) or block rows (bs 3)
+  int bs = 1;
   int64_t ns = 0;                  // slices
-  int64_t groups = 0;              // gp[ns]: 4-entry groups per lane, summed over slices
+  int64_t groups = 0;              // gp[ns]: 4-entry groups (bs 1) / block slots (bs 3) per lane, summed over slices
   int32_t* gp = nullptr;           // [ns+1] exclusive prefix of per-slice groups-per-row
-  void* col = nullptr;             // [256*groups] int32 columns or int16 offsets (col_bits)
+  void* col = nullptr;             // [256*groups] (bs 1) / [64*groups] (bs 3) int32 columns or int16 offsets (col_bits)
   int col_bits = 32;
   const int32_t* rowptr = nullptr; // CSR row pointer (row lengths), not owned
   void release() {
@@ -151,6 +163,73 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
   finish_epi_dots<Epi>(d, epi);
 }
 
+// BSR 3x3 over the BSELL-64 layout (see SellPattern): one lane = one block row = 3 scalar rows,
+// QB block slots loaded per batch before the first gather.
+template <typename T, typename VT, typename CT, int QB, int TH, int MINW, class Pro, class Gx, class Epi>
+__global__ void __launch_bounds__(TH, MINW) k_spmv_bsell3(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
+  constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
+  constexpr bool C16 = sizeof(CT) == 2;
+  if (pro.exit()) return;
+  gx.prepare();
+  epi.prepare();
+  DD d[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) d[j] = dd_zero();
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t nb = a.n / 3;
+  const int64_t ntiles = (nb + TH - 1) / TH;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t s = tile * (TH / 64) + w;
+    const int64_t I = tile * TH + threadIdx.x;
+    if (s < a.ns) {  // wave-uniform
+      const int32_t g0 = a.gp[s];
+      const int nq = a.gp[s + 1] - g0;
+      const int32_t base = int32_t(s * kSellC);
+      const VT* vp = a.vals + 576 * int64_t(g0) + lane;
+      const CT* cp = a.col + 64 * int64_t(g0) + lane;
+      T acc[3] = {T(0), T(0), T(0)};
+      for (int q0 = 0; q0 < nq; q0 += QB) {
+        VT v[QB][9];
+        int c[QB];
+        bool m[QB];
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+          const int q = min(q0 + u, nq - 1);
+#pragma unroll
+          for (int j = 0; j < 9; ++j) v[u][j] = gld(vp + 576 * q + 64 * j);
+          const int o = int(gld(cp + 64 * q));
+          if constexpr (C16) {
+            m[u] = (o != kSellPad16) && (q0 + u < nq);
+            c[u] = base + (o != kSellPad16 ? o : 0);
+          } else {
+            m[u] = (o >= 0) && (q0 + u < nq);
+            c[u] = o >= 0 ? o : base;
+          }
+        }
+        T xv[QB][3];
+#pragma unroll
+        for (int u = 0; u < QB; ++u)
+#pragma unroll
+          for (int cc = 0; cc < 3; ++cc) xv[u][cc] = gx(3 * int64_t(c[u]) + cc);
+#pragma unroll
+        for (int u = 0; u < QB; ++u)
+          if (m[u]) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+              for (int cc = 0; cc < 3; ++cc) acc[r] = acc[r] + T(v[u][3 * r + cc]) * xv[u][cc];
+          }
+      }
+      if (I < nb) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) epi.row(3 * I + r, acc[r], d);
+      }
+    }
+  }
+  finish_epi_dots<Epi>(d, epi);
+}
+
 // Reducing launches use a resident grid: 6 workgroups per CU (the compact-value kernels'
 // __launch_bounds__ guarantee), i.e. 1536 on MI355X -- one wave of workgroups, each walking its
 // row tiles, so no straggler round delays the ticket (8 per CU / 2048 measured the same).  Capped by the solver's 4096
@@ -185,17 +264,23 @@ inline double sell_max_pad() {
 constexpr int kSellWG = 256;  // 4 slices per workgroup (512 / 1024 measured slower: DESIGN.md §5)
 
 inline int64_t sell_grid(const SellPattern& P, bool reducing) {
-  return std::min<int64_t>((P.n + kSellWG - 1) / kSellWG, sell_cap(reducing));
+  return std::min<int64_t>((P.nb + kSellWG - 1) / kSellWG, sell_cap(reducing));
 }
 
 template <typename T, typename VT, typename CT, int TH, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
-  int64_t grid = (P.n + TH - 1) / TH;
+  int64_t grid = (P.nb + TH - 1) / TH;  // row tiles: TH scalar rows (bs 1) or TH block rows (bs 3)
   grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
   SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
   // compact-value kernels: registers for 6 workgroups per CU (the resident reducing grid)
   constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? (TH <= 1536 ? 1536 / TH : 1) : 1;
+  if (P.bs == 3) {
+    // 2 block slots (18 values, 6 gathers) per batch
+    hipLaunchKernelGGL((k_spmv_bsell3<T, VT, CT, 2, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a,
+                       pro, gx, epi);
+    return;
+  }
   // 2 groups of 4 entries per batch for fp32-stored values (fewer registers in flight: 89.6-90.7
   // vs 91.2 us per PCG iteration, 25.0 vs 27.0 us cold SpMV), 4 for fp64 values
   constexpr int QB = sizeof(VT) == 4 ? 2 : 4;
@@ -233,4 +318,10 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
 // dst_dtype: LSPCG_F32 or LSPCG_F64 (fp64 -> fp32 only for exactly representable values).
 int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* src, int src_dtype, int dst_dtype,
                      hipStream_t st, void** out);
+// BSELL-64 pattern of a BSR 3x3 (nb block rows, nnzb blocks, sorted block columns); the same
+// padding rule on block slots (64 x groups <= max_pad x nnzb) and 16-bit block-column offsets.
+int bsell_build_pattern(int64_t nb, int64_t nnzb, const int32_t* rowptr, const int32_t* colind, double max_pad,
+                        bool allow16, hipStream_t st, SellPattern* out);
+// its plane-major block values from the BSR's [nnzb][3][3] array
+int bsell_fill_values(const SellPattern& P, const void* src, int src_dtype, int dst_dtype, hipStream_t st, void** out);
 }  // namespace lspcg

@@ -190,3 +190,41 @@ def test_pcg_bsr3_sell_equals_block_kernel(gpu_ctx, precond, monkeypatch):
     assert out[0][0] == out[1][0]
     assert np.array_equal(out[0][1], out[1][1])
     assert np.array_equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("case", ["elast", "elast-zeros", "ragged"])
+def test_prepare_spmv_bsr3_keeps_bits(gpu_ctx, dtype, case):
+    """BSR 3x3 analysis step: the BSELL-64 block copy (one column per block, plane-major values)
+    gives scipy's bsr_matvec bits (per block row: blocks in column order, c = 0, 1, 2 inside)."""
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    if case == "ragged":  # block rows of 1..40 blocks, some empty, columns up to the whole range
+        rng = np.random.default_rng(4)
+        nb = 700
+        rows, cols = [], []
+        for I in range(nb):
+            if I % 53 == 7:
+                continue
+            k = int(rng.integers(1, 40))
+            rows += [I] * k
+            cols += list(rng.choice(nb, size=k, replace=False))
+        pat = sp.csr_matrix((np.ones(len(rows)), (rows, cols)), shape=(nb, nb))
+        pat.sort_indices()
+        B = sp.bsr_matrix((rng.normal(size=(pat.nnz, 3, 3)), pat.indices, pat.indptr), shape=(3 * nb, 3 * nb))
+    else:
+        A, _, _ = P.elasticity_box(13, 6, 5)
+        B = sp.bsr_matrix(sp.csr_matrix(A), blocksize=(3, 3))
+        B.sort_indices()
+        if case == "elast-zeros":  # in-block zeros and whole zero blocks (Dirichlet masking keeps them)
+            z = np.random.default_rng(1).random(B.data.shape) < 0.2
+            B.data[z] = 0.0
+    B = sp.bsr_matrix((B.data.astype(dtype), B.indices, B.indptr), shape=B.shape)
+    x = np.random.default_rng(9).normal(size=B.shape[0]).astype(dtype)
+    ref = B @ x
+    Ad = DeviceMatrix.from_scipy(B, dtype=dtype, block_size=3)
+    y0 = Ad.matvec(torch.from_numpy(x).cuda()).cpu().numpy()  # staged block kernel
+    kind = Ad.prepare_spmv()
+    assert kind in (16, 32) if case != "ragged" else kind in (0, 16, 32)
+    y = Ad.matvec(torch.from_numpy(x).cuda()).cpu().numpy()
+    assert np.array_equal(y0, ref) and np.array_equal(y, ref), (case, kind)

@@ -44,6 +44,12 @@ def test_bench_byte_model():
     n, nnz = 1030301, 15210901
     assert bench.spmv_bytes(n, nnz) == 12 * nnz + 20 * n + 4 == 203136836
     assert bench.pcg_bytes_per_iter(n, nnz, nnz) == 3 * 203136836 + 80 * n
+    # BSR 3x3: C4's 105,300 block rows, 1,516,846 blocks -> 120.8 MB
+    assert bench.bsr3_bytes(105300, 1516846) == 76 * 1516846 + 4 * 105301 + 48 * 105300 == 120755900
+    # GNN forward: per edge 2 (1·16 + 256 + 256) + 4·2·2 (48·16 + 256 + 256) + 2 (48·16 + 256 + 16)
+    per_edge = 2 * (16 + 256 + 256) + 8 * 2 * (768 + 512) + 2 * (768 + 256 + 16)
+    per_node = 2 * (2 * 16 + 512) + 4 * 2 * (256 + 512)
+    assert bench.gnn_flops(10, 100, 2, 1, 1) == 100 * per_edge + 10 * per_node
 
 
 def test_pack_weights_layout():
