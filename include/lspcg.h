@@ -91,7 +91,7 @@ int lspcg_mat_scale_columns(lspcg_mat* A, const void* d);
 /* y = A x (scipy csr_matvec bit pattern: per-row sequential sum in index order) */
 int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y);
 /* analysis step (cf. rocSPARSE csrmv_analysis): attach a SELL-64 copy of a scalar CSR matrix, or
- * the BSELL-64 block copy of a BSR 3x3 (one column per block, plane-major block values), with the
+ * the BSELL-64 block copy of a BSR 3x3 (one column per block, block values in 16-B lane chunks), with the
  * same values and dtype and 16-bit column offsets where they fit, that lspcg_spmv then uses -- the
  * results keep the same bits.  *kind (nullable) = 16 or 32 (column width) or 0 when the matrix
  * stays on the CSR / BSR kernel (irregular row lengths).  lspcg_mat_scale_columns drops it. */

@@ -85,7 +85,7 @@ __global__ void k_bsell_len(int64_t nb, int64_t ns, const int32_t* __restrict__ 
 }
 
 // one workgroup per slice, threads over its 64 x G slots in storage order: slot p -> block row
-// 64 s + p % 64, block q = p / 64; columns and/or the 9 plane-major values (padding: value 0,
+// 64 s + p % 64, block q = p / 64; columns and/or the 9 values in 16-B lane chunks (padding: value 0,
 // padding column)
 template <typename VS, typename VD>
 __global__ void __launch_bounds__(256) k_bsell_fill(int64_t nb, int64_t ns, const int32_t* __restrict__ gp,
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) k_bsell_fill(int64_t nb, int64_t ns, cons
       if (dst) {
 #pragma unroll
         for (int v = 0; v < 9; ++v)
-          dst[576 * (g0 + q) + 64 * v + lane] = real ? VD(src[9 * (int64_t(b) + q) + v]) : VD(0);
+          dst[576 * (g0 + q) + bsell_pos<VD>(v, lane)] = real ? VD(src[9 * (int64_t(b) + q) + v]) : VD(0);
       }
     }
   }

@@ -34,11 +34,13 @@ constexpr int16_t kSellPad16 = -32768;
 //
 // Block variant (bs == 3, "BSELL-64"; BSR 3x3 matrices): a wave owns 64
 // consecutive BLOCK rows; slot q of block row I = 64 s + lane holds ONE column index (int32 block
-// column or 16-bit offset from 64 s) and the block's 9 values stored plane-major,
-//     col[64 (gp[s] + q) + lane],  vals[576 (gp[s] + q) + 64 v + lane]  (v = 3 a + c),
-// so each of the 10 loads of a slot is one coalesced 256-B (fp32) wave access and a block costs
-// 9 values + 1 column instead of 9 scalar (value, column) pairs; x is gathered once per block
-// (3 consecutive entries) for the lane's 3 scalar rows.  Row 3I + a sums its blocks in column
+// column or 16-bit offset from 64 s) and the block's 9 values (v = 3 a + c) in 16-byte lane
+// chunks: planes 0-7 in groups of W = 16 / sizeof(value) (fp64 pairs, fp32 quads), plane 8 alone,
+//     col[64 (gp[s] + q) + lane],
+//     vals[576 (gp[s] + q) + 64 W (v / W) + W lane + v % W]   (v < 8),  vals[576 (gp[s] + q) + 512 + lane]
+// so a slot is 8 / W + 1 value loads (16-B per lane, 1 KiB per wave instruction) + 1 column load
+// and a block costs 9 values + 1 column instead of 9 scalar (value, column) pairs; x is gathered
+// once per block (3 consecutive entries) for the lane's 3 scalar rows.  Row 3I + a sums its blocks in column
 // order and inside a block c = 0, 1, 2: the order of the reference's expanded scalar CSR
 // (validate.py:51), in-block zeros kept (adding an exact 0*x changes no finite sum).
 struct SellPattern {
@@ -163,6 +165,37 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
   finish_epi_dots<Epi>(d, epi);
 }
 
+// position of plane v of lane `lane` inside a BSELL-64 slot (see SellPattern)
+template <typename VT>
+__host__ __device__ constexpr int bsell_pos(int v, int lane) {
+  constexpr int W = 16 / int(sizeof(VT));
+  return v < 8 ? 64 * W * (v / W) + W * lane + v % W : 512 + lane;
+}
+
+// the 9 values of this lane's block in slot `slot` (576 values): 16-B loads
+__device__ __forceinline__ void bsell_load_block(const double* slot, double (&v)[9]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f64x2 a = *(const __attribute__((address_space(1))) f64x2*)(slot + bsell_pos<double>(2 * k, lane));
+    v[2 * k] = a.x;
+    v[2 * k + 1] = a.y;
+  }
+  v[8] = gld(slot + bsell_pos<double>(8, lane));
+}
+__device__ __forceinline__ void bsell_load_block(const float* slot, float (&v)[9]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const f32x4 a = *(const __attribute__((address_space(1))) f32x4*)(slot + bsell_pos<float>(4 * k, lane));
+    v[4 * k] = a.x;
+    v[4 * k + 1] = a.y;
+    v[4 * k + 2] = a.z;
+    v[4 * k + 3] = a.w;
+  }
+  v[8] = gld(slot + bsell_pos<float>(8, lane));
+}
+
 // BSR 3x3 over the BSELL-64 layout (see SellPattern): one lane = one block row = 3 scalar rows,
 // QB block slots loaded per batch before the first gather.
 template <typename T, typename VT, typename CT, int QB, int TH, int MINW, class Pro, class Gx, class Epi>
@@ -186,7 +219,7 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_bsell3(SellArgs<VT, CT> a, Pr
       const int32_t g0 = a.gp[s];
       const int nq = a.gp[s + 1] - g0;
       const int32_t base = int32_t(s * kSellC);
-      const VT* vp = a.vals + 576 * int64_t(g0) + lane;
+      const VT* vp = a.vals + 576 * int64_t(g0);
       const CT* cp = a.col + 64 * int64_t(g0) + lane;
       T acc[3] = {T(0), T(0), T(0)};
       for (int q0 = 0; q0 < nq; q0 += QB) {
@@ -196,8 +229,7 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_bsell3(SellArgs<VT, CT> a, Pr
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
           const int q = min(q0 + u, nq - 1);
-#pragma unroll
-          for (int j = 0; j < 9; ++j) v[u][j] = gld(vp + 576 * q + 64 * j);
+          bsell_load_block(vp + 576 * q, v[u]);
           const int o = int(gld(cp + 64 * q));
           if constexpr (C16) {
             m[u] = (o != kSellPad16) && (q0 + u < nq);
@@ -322,6 +354,6 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
 // padding rule on block slots (64 x groups <= max_pad x nnzb) and 16-bit block-column offsets.
 int bsell_build_pattern(int64_t nb, int64_t nnzb, const int32_t* rowptr, const int32_t* colind, double max_pad,
                         bool allow16, hipStream_t st, SellPattern* out);
-// its plane-major block values from the BSR's [nnzb][3][3] array
+// its block values (16-B lane chunks) from the BSR's [nnzb][3][3] array
 int bsell_fill_values(const SellPattern& P, const void* src, int src_dtype, int dst_dtype, hipStream_t st, void** out);
 }  // namespace lspcg

@@ -16,7 +16,7 @@ ROOT = Path(__file__).resolve().parents[1]
 def test_bench_json_line():
     env = dict(os.environ)
     out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--workload", "kuhn31", "--steps", "2", "--warmup",
-                          "1", "--spmv-reps", "3", "--cpu-reps", "1"], cwd=ROOT, env=env, capture_output=True,
+                          "1", "--spmv-reps", "3", "--cpu-iters", "10"], cwd=ROOT, env=env, capture_output=True,
                          text=True, timeout=240, check=True)
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, out.stdout
@@ -30,4 +30,10 @@ def test_bench_json_line():
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
     c = d["cpu_baseline"]
-    assert c["kind"] == "port" and c["cores"] == 1 and c["value"] > 0
+    assert c["kind"] == "port" and c["value"] > 0 and c["nproc"] >= 1 and c["cores"] in (1, c["nproc"])
+    assert set(c["by_threads"]) == {"nproc", "1"} and "cpu_model" in c
+    v = d["time_to_rtol_variants"]
+    assert set(v) == {"ext_spai", "none", "diagonal"} and all(set(r) == {"mask", "random"} for r in v.values())
+    c1 = d["c1_synthetic"]
+    assert c1["gpu"]["iters"] > 0 and c1["cpu"]["1"]["it_per_s"] > 0
+    assert d["gnn_tflops"] > 0 and d["pcg_loop_kernels"]["frac_format"] > 0
