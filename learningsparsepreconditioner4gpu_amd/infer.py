@@ -100,6 +100,9 @@ def synthetic_dataset(name: str) -> List[GraphSample]:
             A, mask, feats = P.heat_tet(k, k, max(4, nv // (k * k)), rho=float(rng.uniform(1e-4, 5e-4)), seed=s)
             out.append(make_sample(A, mask, node_features=feats))
         return out
+    if name == "heat_bunny":  # C3: heat on the voxelised bunny, F_in = 5 (field, xyz, mask)
+        A, mask, feats = P.heat_bunny()
+        return [make_sample(A, mask, node_features=feats)]
     if name.startswith("poisson"):
         A, mask, _ = P.poisson2d_grid(256, 256)
         return [make_sample(A, mask)]

@@ -15,6 +15,7 @@ with the same structure, as SURVEY.md section 8(d) specifies:
 * ``elasticity_box``              -- stand-in for ``datagen/elast_twist.py``:
   block_size 3 linear-elastic tet stiffness + mass/dt^2, Dirichlet x-ends.
 * ``heat_tet``                    -- stand-in for ``datagen/heat_tetmesh.py``.
+* ``heat_bunny``                  -- stand-in for ``datagen/heat.py`` on the bunny (C3).
 
 All functions return scipy CSR matrices (float64, int32 indices, sorted) and,
 where the reference has one, the Dirichlet mask ``[N, b]``.
@@ -247,6 +248,59 @@ def heat_tet(nx: int, ny: int, nz: int, rho: float = 2e-4, seed: int = 0):
     return A, mask, nodes / max(nx, ny, nz)
 
 
+MESH_DIR = __import__("pathlib").Path(__file__).resolve().parent / "meshes"
+
+
+def gaussian_random_field(points: np.ndarray, seed: int, len_scale: float = 1.0, modes: int = 256) -> np.ndarray:
+    """Seeded smooth random field at ``points`` (stand-in for ``gs.SRF(gs.Gaussian(dim=3, var=5,
+    len_scale=1))`` of ``heat.py:47-48``; gstools is absent).  Randomised spectral sum over the
+    Gaussian model's spectrum: the correlation ``exp(-π/4 (r/ℓ)²)`` has wave vectors
+    ``k ~ N(0, (π/2)/ℓ² I)``.  The variance is irrelevant: ``heat.py:83-86`` renormalises."""
+    rng = np.random.default_rng(seed)
+    k = rng.normal(scale=np.sqrt(np.pi / 2) / len_scale, size=(modes, points.shape[1]))
+    phi = rng.uniform(0, 2 * np.pi, size=modes)
+    return np.sqrt(2.0 / modes) * np.cos(points @ k.T + phi).sum(1)
+
+
+def heat_bunny(seed: int = 42, var: float = 0.99, eps: float = 1e-4, dirichlet: float = 0.05):
+    """BASELINE config 3 stand-in (``datagen/heat.py:22-96`` on ``bunny_low_res.obj``).
+
+    Mesh: Kuhn split (6 tets / cell) of every grid cell whose 8 corners lie inside the bunny
+    (``meshes/bunny_grid.npz``: winding-number voxelisation of the .obj, written by
+    ``tests/golden/make_golden.py bunny``) -- 6.3 k vertices against the reference's tetgen 6276.
+    Operator: ``L(κ_tet) + eps·M_lumped`` with ``κ_tet`` the per-tet mean (``to_tet_field``,
+    ``heat.py:15-19``) of a field renormalised as ``heat.py:83-86``.  Dirichlet: the lowest
+    ``dirichlet`` fraction of vertices by height (the reference's heat data has none; SURVEY 8(d)
+    adds them so the masked assembly is exercised).  Features: ``[field, x, y, z]`` -- the step's
+    field (``heat.py:96``) then the shared xyz (``:75-76``); make_data appends the mask: F_in = 5.
+
+    Returns ``(A_raw, mask[N,1], features[N,4])``.
+    """
+    z = np.load(MESH_DIR / "bunny_grid.npz")
+    ins = z["inside"]
+    h = float(z["h"])
+    nx, ny, nz = ins.shape
+    cell = np.ones((nx - 1, ny - 1, nz - 1), dtype=bool)
+    for a in (0, 1):
+        for b in (0, 1):
+            for c in (0, 1):
+                cell &= ins[a:nx - 1 + a, b:ny - 1 + b, c:nz - 1 + c]
+    nodes, tets = kuhn_tets(nx, ny, nz)
+    tets = tets.reshape(6, (nx - 1) * (ny - 1) * (nz - 1), 4)[:, cell.ravel()].reshape(-1, 4)
+    used, tets = np.unique(tets, return_inverse=True)
+    tets = tets.reshape(-1, 4)
+    nodes = z["lo"][None, :] + h * nodes[used]
+    field = gaussian_random_field(nodes, seed)
+    field = field - field.min()
+    field = field / (field.max() + 1e-4)
+    field = field * var + (1 - var)
+    K = p1_stiffness(nodes, tets, field[tets].mean(1))
+    A = _canon(K + sp.diags(eps * lumped_mass(nodes, tets)))
+    mask = np.ones((A.shape[0], 1))
+    mask[np.argsort(nodes[:, 1], kind="stable")[: int(dirichlet * A.shape[0])]] = 0.0
+    return A, mask, np.concatenate([field[:, None], nodes], 1)
+
+
 def elasticity_box(nx: int = 117, ny: int = 30, nz: int = 30, E: float = 3e6, nu: float = 0.4,
                    density: float = 1.0, dt: float = 0.01):
     """Elasticity-twist stand-in, block_size 3 (``datagen/elast_twist.py:17-129``).
@@ -336,6 +390,9 @@ def workload(name: str):
     if name.startswith("synthetic"):
         n = int(name[9:] or 10240)
         return synthetic_c1(n), None, None, 1, "mean"
+    if name == "bunny":
+        A, mask, feats = heat_bunny()
+        return A, mask, feats, 1, "disable"
     if name.startswith("elast"):
         A, mask, nodes = elasticity_box()
         return A, mask, np.concatenate([nodes, np.zeros_like(nodes)], 1), 3, "disable"

@@ -25,6 +25,10 @@ Fixtures (inputs and the reference's outputs, data only):
                       the correctly-rounded-dot trajectory and the spread of the admissible dot
                       orderings (count band, first iteration where their histories part by
                       more than 1e-12, largest x / true-residual difference)
+  ../../learningsparsepreconditioner4gpu_amd/meshes/bunny_grid.npz
+                   -- voxelised interior of data/objs/bunny_low_res.obj (winding numbers of a
+                      regular grid's vertices), input of the C3 heat stand-in (problems.heat_bunny);
+                      it lives with the package because bench.py / infer load it as a workload
   folder_free/, folder_fixed/ + folder.npz
                    -- two on-disk datasets in the datagen_helper.py folder format (written by
                       dataset.FolderWriter: .mtx + features/mask/rhs/lhs; fixed-topology 3x3
@@ -33,6 +37,7 @@ Fixtures (inputs and the reference's outputs, data only):
 
     python tests/golden/make_golden.py            # every fixture
     python tests/golden/make_golden.py traj       # pcg_traj.npz only
+    python tests/golden/make_golden.py bunny      # bunny_grid.npz only
 """
 from __future__ import annotations
 
@@ -49,6 +54,7 @@ from torch import nn
 REF = Path("/root/reference")
 OUT = Path(__file__).resolve().parent
 ROOT = OUT.parents[1]
+MESHES = ROOT / "learningsparsepreconditioner4gpu_amd" / "meshes"
 
 
 def install_shims():
@@ -242,8 +248,44 @@ def traj_fixtures(rval):
     np.savez_compressed(OUT / "pcg_traj.npz", **out)
 
 
+def bunny_grid():
+    """bunny_grid.npz: which vertices of a regular grid over data/objs/bunny_low_res.obj's bounding
+    box lie inside the surface (generalised winding number > 1/2) -- the voxelised interior from
+    which problems.heat_bunny builds the C3 stand-in (tetgen is absent).  The obj
+    is parsed as plain text (v / f records); nothing of the reference is imported."""
+    V, F = [], []
+    for line in (REF / "data" / "objs" / "bunny_low_res.obj").read_text().splitlines():
+        if line.startswith("v "):
+            V.append([float(t) for t in line.split()[1:4]])
+        elif line.startswith("f "):
+            F.append([int(t.split("/")[0]) - 1 for t in line.split()[1:4]])
+    V, F = np.asarray(V), np.asarray(F)
+    lo, hi = V.min(0), V.max(0)
+    h = float((hi - lo).max() / 32.0)
+    shape = (np.ceil((hi - lo) / h).astype(int) + 1)
+    P = np.stack(np.meshgrid(*[lo[k] + h * np.arange(shape[k]) for k in range(3)], indexing="ij"), -1).reshape(-1, 3)
+    a, b, c = V[F[:, 0]], V[F[:, 1]], V[F[:, 2]]
+    wn = np.zeros(len(P))
+    for i in range(0, len(P), 1024):  # Van Oosterom-Strackee solid angles / 4 pi
+        p = P[i:i + 1024, None, :]
+        A, B, C = a[None] - p, b[None] - p, c[None] - p
+        la, lb, lc = (np.linalg.norm(X, axis=2) for X in (A, B, C))
+        det = np.einsum("ijk,ijk->ij", A, np.cross(B, C))
+        den = (la * lb * lc + np.einsum("ijk,ijk->ij", A, B) * lc + np.einsum("ijk,ijk->ij", B, C) * la
+               + np.einsum("ijk,ijk->ij", C, A) * lb)
+        wn[i:i + 1024] = np.arctan2(det, den).sum(1) / (2 * np.pi)
+    inside = (wn > 0.5).reshape(tuple(shape))
+    MESHES.mkdir(exist_ok=True)
+    np.savez_compressed(MESHES / "bunny_grid.npz", lo=lo, h=np.array(h), shape=shape, inside=inside,
+                        surface_vertices=np.array(len(V)), surface_faces=np.array(len(F)))
+    print("bunny grid", tuple(shape), "inside vertices", int(inside.sum()))
+
+
 def main():
     install_shims()
+    if sys.argv[1:] == ["bunny"]:
+        bunny_grid()
+        return
     if sys.argv[1:] == ["traj"]:
         from neural_cg.utils import validate as rval
 

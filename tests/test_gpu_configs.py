@@ -4,7 +4,8 @@ C1  synthetic N=10240, unpreconditioned CG, rtol 1e-8: iteration count inside th
     admissible dot orderings (the reference's own count moves with the BLAS thread count)
 C2  Poisson-2D 256x256 (N=65,536) fp64, GNN-inferred L, ext_spai PCG rtol 1e-8: GNN output vs
     the torch restatement (fp32, 1e-5), iteration count equal to the oracle's, solution 1e-12
-C3  heat tetmesh stand-in (~6.3k vertices) fp32, GNN + PCG to 1e-6: count equal, solution 1e-5
+C3  heat on the voxelised bunny (6,310 vertices, 5 % Dirichlet, F_in = 5) fp32, GNN + PCG to 1e-6:
+    GNN input width, count equal to the oracle's, solution 1e-5
 C4  elasticity box 117x30x30 (N=315,900 dof) BSR 3x3 fp64: full-size block SpMV bit-identical to
     scalar CSR, and the first 25 PCG iterations bit-for-bit against the oracle (residual history
     1e-10, iterate 1e-12) -- the full oracle solve would take minutes on the CPU
@@ -86,9 +87,10 @@ def test_c2_poisson_gnn_spai_pcg(gpu_ctx):
 
 
 def test_c3_heat_fp32(gpu_ctx):
-    A_raw, mask, feats = P.heat_tet(19, 18, 18)
+    A_raw, mask, feats = P.heat_bunny()
     assert 5500 <= A_raw.shape[0] <= 7000
     s, ws, A64, L64 = _system(A_raw, mask, feats)
+    assert s.x.shape[1] == 5 and (mask == 0).any()
     A32 = _csr(A64).astype(np.float32)
     L32 = _csr(L64).astype(np.float32)
     b = (A32 @ mask.ravel().astype(np.float32)).astype(np.float32)

@@ -91,3 +91,30 @@ def test_timestat_csv_schema(tmp_path):
     al = st.all_time_stat()
     assert list(al.columns) == ["Key", "Solve Time (ms)", "Precond Time (ms)", "#Iteration", "Matrix Size"]
     assert len(al) == 2
+
+
+def test_heat_bunny_c3_stand_in():
+    """C3 stand-in (heat.py:22-96 on the voxelised bunny_low_res.obj): ~6.3 k vertices like the
+    reference's tetgen mesh (heat.yaml:1 says 6276), SPD, κ in [0.01, 1) as heat.py:83-86, the
+    Dirichlet rows masked, and make_data's node input [field, x, y, z, mask]: F_in = 5."""
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+
+    A, mask, feats = P.heat_bunny()
+    n = A.shape[0]
+    assert 6000 <= n <= 6600 and feats.shape == (n, 4)
+    assert abs(A - A.T).max() <= 1e-15 * abs(A).max()
+    assert (A.diagonal() > 0).all()
+    assert 0.01 - 1e-12 <= feats[:, 0].min() and feats[:, 0].max() < 1.0
+    assert 0 < (mask == 0).sum() < 0.1 * n
+    s = make_sample(A, mask, node_features=feats)
+    assert s.x.shape == (n, 5)
+    assert torch.equal(s.x[:, 4], torch.from_numpy(mask[:, 0]).float())
+    # the hot path's assembly masks the Dirichlet rows: identity there
+    from oracle import linalg as O
+
+    Am = O.to_csr(s.edge_index.numpy(), s.matrix_values.numpy(), n, s.mask.numpy())
+    d = np.flatnonzero(mask[:, 0] == 0)
+    assert np.array_equal(Am[d].toarray(), np.eye(n)[d])
+    # same seed, same system
+    A2, _, f2 = P.heat_bunny()
+    assert (A != A2).nnz == 0 and np.array_equal(feats, f2)
