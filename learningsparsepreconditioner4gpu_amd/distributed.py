@@ -85,13 +85,41 @@ def gather_records(local: List[SolveRecord], n_total: int, device: Optional[torc
     return [SolveRecord.from_list(merged[i].tolist()) for i in range(n_total) if not torch.isnan(merged[i, 0])]
 
 
+def _rank_world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
 def run_sharded(n_items: int, weights: Sequence[float], solve: Callable[[int], SolveRecord],
                 device: Optional[torch.device] = None) -> List[SolveRecord]:
     """Solve this rank's share of the batch, then gather every record (collective at the end only)."""
-    if dist.is_available() and dist.is_initialized():
-        rank, world = dist.get_rank(), dist.get_world_size()
-    else:
-        rank, world = 0, 1
+    rank, world = _rank_world()
     mine = my_items(weights, rank, world)
     local = [solve(i) for i in mine]
+    return gather_records(local, n_items, device)
+
+
+def run_sharded_concurrent(n_items: int, weights: Sequence[float], prepare: Callable[[int], object],
+                           finish: Callable[[object], SolveRecord], concurrency: int,
+                           device: Optional[torch.device] = None) -> List[SolveRecord]:
+    """run_sharded with up to ``concurrency`` solves of this rank in flight on its GPU.
+
+    The rank's systems go in windows of ``concurrency``: ``prepare`` (GNN inference + assembly:
+    one workspace, so one at a time, each timed on an otherwise idle device) runs for every
+    system of the window on this thread, then ``finish`` (the PCG solve: every solver owns a
+    non-blocking stream, and the native call releases the GIL) runs for all of them at once on a
+    thread pool.  Mid-size systems are latency-bound (a few hundred workgroups per launch, five
+    dependent launches per iteration), so concurrent solves fill the chip that one leaves idle.
+    Results are those of the sequential path; per-system solve times include the overlap."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    rank, world = _rank_world()
+    mine = my_items(weights, rank, world)
+    k = max(1, int(concurrency))
+    local: List[SolveRecord] = []
+    with ThreadPoolExecutor(k) as ex:
+        for w0 in range(0, len(mine), k):
+            batch = [prepare(i) for i in mine[w0:w0 + k]]
+            local.extend(ex.map(finish, batch))
     return gather_records(local, n_items, device)

@@ -28,7 +28,7 @@ import torch
 
 from . import problems as P
 from .data import GraphSample, make_sample
-from .distributed import SolveRecord, run_sharded
+from .distributed import SolveRecord, run_sharded, run_sharded_concurrent
 from .validate import get_cg_iter_time, get_pcg_iter_time, get_pcg_scaled_iter_time
 from .workspace import ScaledInferenceWorkspace, SimpleInferenceWorkspace
 
@@ -146,12 +146,15 @@ def rhs_for(rhs: str, mask: np.ndarray, sample: Optional[GraphSample] = None) ->
 
 
 def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: float = 1e-6, repeat: int = 1,
-        rhs: str = "mask", warmup: int = 20) -> List[SolveRecord]:
+        rhs: str = "mask", warmup: int = 20, concurrency: int = 1) -> List[SolveRecord]:
+    """The ``Neural+CUDA`` row of infer.py:278-331 (GNN -> L, A; ext_spai PCG).  ``concurrency``
+    > 1 keeps that many solves of this rank in flight at once (run_sharded_concurrent): the same
+    iterates and counts, a higher batch throughput on the reference's mid-size systems."""
     pcg = get_pcg_scaled_iter_time if isinstance(ws, ScaledInferenceWorkspace) else get_pcg_iter_time
     dev = torch.device("cuda", torch.cuda.current_device())
     warmed = set()
 
-    def solve(i: int) -> SolveRecord:
+    def prepare(i: int):
         s = samples[i].to(dev)
         if not warmed:
             for _ in range(warmup):
@@ -165,6 +168,10 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
         L, _ = ws.inference_step(s)
         A = ws.system_matrix(s)
         r = rhs_for(rhs, s.mask.cpu().numpy(), s)
+        return i, A, L, r, prec
+
+    def finish(job) -> SolveRecord:
+        i, A, L, r, prec = job
         info = {}
         it, _, sol = pcg(A, r, L, ws.epsilon, rtol=rtol, repeat=repeat, info=info)
         # the true ‖b − A x‖/‖b‖ of the solution (one device SpMV) and the solver's own verdict
@@ -172,7 +179,9 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
                            converged=info["converged"])
 
     weights = [float(s.edge_index.shape[1]) for s in samples]
-    return run_sharded(len(samples), weights, solve)
+    if concurrency > 1:
+        return run_sharded_concurrent(len(samples), weights, prepare, finish, concurrency)
+    return run_sharded(len(samples), weights, lambda i: finish(prepare(i)))
 
 
 def run_baseline(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, method: str, rtol: float = 1e-6,
@@ -219,6 +228,8 @@ def main(argv=None):
     ap.add_argument("--epsilon", type=float, default=3e-3)
     ap.add_argument("--out-dir", default="output")
     ap.add_argument("--infer-prefix", default="")
+    ap.add_argument("--concurrency", type=int, default=1,
+                    help="solves in flight at once per GPU (run_sharded_concurrent); 1 = the reference's sequential loop")
     ap.add_argument("--baselines", default="none,diagonal,ainv,ic",
                     help="comma list of PCG-{method}-cuda rows (infer.py:310-321); '' for none")
     args = ap.parse_args(argv)
@@ -245,7 +256,8 @@ def main(argv=None):
     rows = {}
     for m in [b for b in args.baselines.split(",") if b]:
         rows[f"PCG-{m}-cuda"] = run_baseline(samples, ws, m, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs)
-    rows["Neural+HIP"] = run(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, warmup=args.warmup)
+    rows["Neural+HIP"] = run(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, warmup=args.warmup,
+                             concurrency=args.concurrency)
     recs = rows["Neural+HIP"]
     if not dist.is_initialized() or dist.get_rank() == 0:
         stats = Timestat()

@@ -172,3 +172,18 @@ class PreconditionedConjugateGradient:
                 x.copy_(xt.reshape(x.shape))
         iters, _conv, solve = res[:3]
         return (iters, prec, solve) + (tuple(res[3:]) if return_history else ())
+
+
+def solve_many(jobs, rtol: float = 1e-6, max_iter: int = 0, concurrency: int = 4):
+    """Independent solves ``[(solver, b, x), ...]`` with up to ``concurrency`` of them in flight on
+    the device: every solver owns a non-blocking stream and ``lspcg_solver_solve`` releases the GIL
+    (ctypes), so host threads overlap the solves' dependent launch chains.  Each solve returns what
+    it returns alone (same iterate, count and history); ``[(iters, converged, solve_time_s), ...]``
+    in job order, the times including the overlap."""
+    jobs = list(jobs)
+    if concurrency <= 1 or len(jobs) <= 1:
+        return [s.solve(b, x, rtol, max_iter) for s, b, x in jobs]
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(min(int(concurrency), len(jobs))) as ex:
+        return list(ex.map(lambda j: j[0].solve(j[1], j[2], rtol, max_iter), jobs))

@@ -9,7 +9,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from learningsparsepreconditioner4gpu_amd.distributed import (SolveRecord, gather_records, lpt_assign, my_items,
-                                                             run_sharded)
+                                                             run_sharded, run_sharded_concurrent)
 
 
 def test_lpt_assignment_balanced_and_complete():
@@ -30,7 +30,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_items, q):
+def _worker(rank, world, port, n_items, q, concurrency=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     weights = [float(10 + (i * 7) % 5) for i in range(n_items)]
@@ -39,19 +39,33 @@ def _worker(rank, world, port, n_items, q):
         return SolveRecord(index=i, iters=100 + i, rel_res=1e-9 * (i + 1), t_prec=0.001 * i, t_solve=0.01 * (i + 1),
                            n=1000 + i, nnz=5000 + i, converged=(i % 3 != 2))
 
-    recs = run_sharded(n_items, weights, solve, device=torch.device("cpu"))
+    if concurrency:  # prepare on this thread in windows, the solves on a pool
+        import threading
+
+        main = threading.get_ident()
+        prepared = []
+
+        def prepare(i):
+            assert threading.get_ident() == main
+            prepared.append(i)
+            return i
+
+        recs = run_sharded_concurrent(n_items, weights, prepare, solve, concurrency, device=torch.device("cpu"))
+        assert prepared == my_items(weights, rank, world)
+    else:
+        recs = run_sharded(n_items, weights, solve, device=torch.device("cpu"))
     q.put((rank, [r.as_list() for r in recs], my_items(weights, rank, world)))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_sharded_gather(world):
+@pytest.mark.parametrize("world,concurrency", [(2, 0), (3, 0), (2, 3)])
+def test_gloo_sharded_gather(world, concurrency):
     n_items = 7
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_items, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_items, q, concurrency)) for r in range(world)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=120) for _ in range(world)]
@@ -70,6 +84,12 @@ def test_gloo_sharded_gather(world):
 def test_gather_without_process_group_is_local():
     recs = [SolveRecord(2, 1, 0, 0, 0, 1, 1), SolveRecord(0, 1, 0, 0, 0, 1, 1)]
     assert [r.index for r in gather_records(recs, 3)] == [0, 2]
+
+
+def test_concurrent_runner_without_process_group():
+    weights = [5.0, 1.0, 3.0, 2.0, 4.0]
+    recs = run_sharded_concurrent(5, weights, lambda i: i, lambda i: SolveRecord(i, 10 * i, 0, 0, 0, 1, 1), 2)
+    assert [(r.index, r.iters) for r in recs] == [(i, 10.0 * i) for i in range(5)]
 
 
 def _bench_worker(rank, world, port, q):

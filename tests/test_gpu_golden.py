@@ -92,6 +92,22 @@ def test_infer_driver_end_to_end(gpu_ctx, tmp_path):
     assert list(df.columns) == ["Key", "Total Time (ms)", "Solve Time (ms)", "Precond Time (ms)", "#Iteration"]
 
 
+def test_infer_concurrent_solves_match_sequential(gpu_ctx):
+    """run(..., concurrency=4): several solves in flight on one GPU give the records of the
+    sequential loop (counts, true residuals bit for bit) on the C5 heat batch."""
+    from learningsparsepreconditioner4gpu_amd.infer import run, synthetic_dataset
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    samples = synthetic_dataset("heat_batch8")
+    ws = SimpleInferenceWorkspace(node_features=samples[0].x.shape[1], edge_features=1, seed=0)
+    seq = run(samples, ws, rtol=1e-8, warmup=1)
+    con = run(samples, ws, rtol=1e-8, warmup=1, concurrency=4)
+    assert [r.index for r in con] == list(range(len(samples)))
+    for a, b in zip(seq, con):
+        assert a.converged and b.converged
+        assert (a.iters, a.rel_res, a.n, a.nnz) == (b.iters, b.rel_res, b.n, b.nnz)
+
+
 @pytest.mark.parametrize("rhs", ["mask", "neighbour"])
 def test_folder_dataset_through_hot_path(gpu_ctx, rhs):
     """On-disk dataset (reference folder format, golden folder_free) -> GNN -> L -> PCG through

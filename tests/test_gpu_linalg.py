@@ -265,3 +265,23 @@ def test_time_kernels_reports_five_launches(gpu_ctx, monkeypatch):
     s2.set_spai(L, 3e-3)
     with pytest.raises(RuntimeError):
         s2.time_kernels(b, 5)
+
+
+def test_solve_many_matches_one_by_one(gpu_ctx):
+    """linalg.solve_many: concurrent independent solves (one stream per solver, GIL released in
+    the native call) return each solve's own count and iterate, bit for bit."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient, solve_many
+
+    jobs, ref = [], []
+    for name, A, _ in _cases.spd_cases()[:4]:
+        b = torch.from_numpy(A @ np.ones(A.shape[0])).cuda()
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai")
+        s.set_spai(_cases.spai_like(A), 3e-3)
+        x = torch.zeros_like(b)
+        it, conv, _ = s.solve(b, x, rtol=1e-8)
+        ref.append((it, conv, x.clone()))
+        jobs.append((s, b, torch.zeros_like(b)))
+    out = solve_many(jobs, rtol=1e-8, concurrency=4)
+    for (it, conv, x), (it2, conv2, _), (_, _, x2) in zip(ref, out, jobs):
+        assert (it, conv) == (it2, conv2)
+        assert torch.equal(x, x2)
