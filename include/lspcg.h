@@ -201,6 +201,36 @@ int lspcg_graph_spmv(lspcg_graph* g, const void* vals, int dtype, int transpose,
 int lspcg_graph_aatpe(lspcg_graph* g, const void* vals, int dtype, double epsilon, const void* x, const void* mask,
                       const void* diag, void* t, void* y);
 
+/* ---- one system row-partitioned over ranks (NOT in the reference,
+ * whose systems each fit one process -- it replaces no reference interface).  The host driver
+ * (learningsparsepreconditioner4gpu_amd/dist_pcg.py) owns the halo all-to-alls, the all-gathers
+ * of dot partials (torch.distributed: RCCL over xGMI) and scipy cg's scalar recurrence
+ * (iterative.py:359-418, as restated at validate.py:163-201); these calls enqueue the rank-local
+ * device phases on the context's stream.  A, L, LT: the rank's rows of the global matrices as
+ * square n_ext x n_ext scalar CSR over its extended vector [n_own own rows | halo] (rows >= n_own
+ * empty; L and LT may both be NULL for plain CG).  send_idx (host or device, n_send entries):
+ * own-row indices packed for the other ranks, grouped by destination.  red: a device buffer of
+ * 64 x 2 x 2 doubles receiving per-group compensated (sum, correction) pairs of the launch's dots
+ * (zeroed by the call; the host sums every rank's groups). */
+typedef struct lspcg_part lspcg_part;
+int lspcg_part_create(lspcg_ctx* ctx, const lspcg_mat* A, const lspcg_mat* L, const lspcg_mat* LT, int64_t n_own,
+                      const int32_t* send_idx, int64_t n_send, lspcg_part** out);
+int lspcg_part_destroy(lspcg_part* p);
+/* sendbuf[k] = v[send_idx[k]] */
+int lspcg_part_pack(lspcg_part* p, const void* v, void* sendbuf);
+/* red <- groups of a·a, b·b over the own rows */
+int lspcg_part_norms(lspcg_part* p, const void* a, const void* b, double* red);
+/* t[i] = (LT r)_i, i < n_own */
+int lspcg_part_lt(lspcg_part* p, const void* r_ext, void* t_ext);
+/* z = L t + eps r ; red <- groups of r·z, r·r */
+int lspcg_part_l(lspcg_part* p, const void* t_ext, const void* r, double eps, void* z, double* red);
+/* q = A p ; red <- groups of p·q */
+int lspcg_part_a(lspcg_part* p, const void* p_ext, void* q, double* red);
+/* p = z (first != 0) or p*beta + z */
+int lspcg_part_update_p(lspcg_part* p, const void* z, void* p_ext, double beta, int first);
+/* x += alpha p ; r -= alpha q */
+int lspcg_part_update_xr(lspcg_part* p, double alpha, const void* p_ext, const void* q, void* x, void* r_ext);
+
 #ifdef __cplusplus
 }
 #endif

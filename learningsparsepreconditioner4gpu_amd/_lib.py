@@ -70,6 +70,15 @@ SIGNATURES = {
     "lspcg_graph_destroy": (C.c_int, [vp]),
     "lspcg_graph_spmv": (C.c_int, [vp, vp, C.c_int, C.c_int, vp, vp, vp]),
     "lspcg_graph_aatpe": (C.c_int, [vp, vp, C.c_int, C.c_double, vp, vp, vp, vp, vp]),
+    "lspcg_part_create": (C.c_int, [vp, vp, vp, vp, C.c_int64, vp, C.c_int64, pp]),
+    "lspcg_part_destroy": (C.c_int, [vp]),
+    "lspcg_part_pack": (C.c_int, [vp, vp, vp]),
+    "lspcg_part_norms": (C.c_int, [vp, vp, vp, vp]),
+    "lspcg_part_lt": (C.c_int, [vp, vp, vp]),
+    "lspcg_part_l": (C.c_int, [vp, vp, vp, C.c_double, vp, vp]),
+    "lspcg_part_a": (C.c_int, [vp, vp, vp, vp]),
+    "lspcg_part_update_p": (C.c_int, [vp, vp, vp, C.c_double, C.c_int]),
+    "lspcg_part_update_xr": (C.c_int, [vp, C.c_double, vp, vp, vp, vp]),
 }
 
 

@@ -58,10 +58,13 @@ __global__ void k_sell_fit16(int64_t n, const int32_t* __restrict__ rowptr, cons
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     const int32_t base = int32_t((i / kSellC) * kSellC);
     const int32_t b = rowptr[i], e = rowptr[i + 1];
-    if (e > b) {  // sorted columns: the extremes are the first and last entries
-      const int32_t lo = colind[b] - base, hi = colind[e - 1] - base;
-      if (lo < -32767 || hi > 32767) atomicOr(flag, 1);
+    // every entry (rows need not be sorted: dist_pcg's extended matrices keep the global order)
+    bool far = false;
+    for (int32_t k = b; k < e; ++k) {
+      const int32_t o = colind[k] - base;
+      far |= o < -32767 || o > 32767;
     }
+    if (far) atomicOr(flag, 1);
   }
 }
 

@@ -1,0 +1,342 @@
+"""One system row-partitioned over ranks.
+
+Not in the reference: its systems each fit one process (``infer.py:278`` loops over samples; the
+multi-GPU path of this package, ``distributed.py``, shards whole systems).  This is for a system
+too large for one GPU's 288 GB.  Every rank owns a contiguous, nnz-balanced block of rows of A, L
+and Lᵀ; one PCG iteration is scipy's ``cg`` (iterative.py:359-418, restated by the reference at
+``validate.py:163-201``) with ``M⁻¹ r = L(Lᵀ r) + εr`` (``validate.py:173-182``):
+
+    halo(r) -> t = Lᵀ r ; halo(t) -> z = L t + εr, ρ_k = r·z, ‖r_k‖²  [all-gather]
+    top-of-loop test on ‖r_k‖ ; p = z + βp ; halo(p) -> q = A p, π = p·q  [all-gather]
+    α = ρ/π ; x += αp ; r -= αq
+
+The device phases are the native ``lspcg_part_*`` calls (csrc/lspcg_part.hip: the library's SpMV
+kernels with own-row epilogues).  Exchanges go through ``torch.distributed``: the halo of a
+vector is ONE ``all_to_all_single`` whose receive buffer is the tail of the rank's extended
+vector (halo entries ordered by owner rank, so nothing is unpacked), and a dot product is an
+all-gather of every rank's 64 per-group compensated (sum, correction) pairs, summed on the host
+in rank-major order with the device's own double-double addition, then rounded -- every rank
+takes the same scalar, hence the same convergence decision.  With backend ``nccl`` (RCCL over
+xGMI) device buffers are exchanged directly; with ``gloo`` (tests: several ranks on one GPU)
+they are staged through host memory.  With one rank there is no exchange at all.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from .sparse import Context, DeviceMatrix, _ptr
+
+GROUPS = 64  # per-group DD slots of one reduction buffer (lspcg_part.hip kPartGroups)
+
+
+# ---------------------------------------------------------------------------------------------
+# host-side plan (pure numpy: tested on the CPU)
+# ---------------------------------------------------------------------------------------------
+def partition_rows(indptr: np.ndarray, world: int) -> List[int]:
+    """Contiguous row blocks balanced by nnz + rows: bounds[r]..bounds[r+1] belong to rank r."""
+    n = len(indptr) - 1
+    work = np.asarray(indptr, dtype=np.int64) + np.arange(n + 1, dtype=np.int64)
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(int(np.searchsorted(work, work[-1] * r / world)))
+    cuts.append(n)
+    for r in range(1, world + 1):  # monotone (a rank may own nothing on tiny systems)
+        cuts[r] = max(cuts[r], cuts[r - 1])
+    return cuts
+
+
+@dataclass
+class HaloPlan:
+    rank: int
+    bounds: List[int]
+    halo: np.ndarray          # global indices of the halo entries, ascending = grouped by owner
+    recv_counts: List[int]    # halo entries per owner rank
+    send_idx: np.ndarray      # own-row (local) indices sent, grouped by destination rank
+    send_counts: List[int]
+
+    @property
+    def n_own(self) -> int:
+        return self.bounds[self.rank + 1] - self.bounds[self.rank]
+
+    @property
+    def n_ext(self) -> int:
+        return self.n_own + len(self.halo)
+
+
+def _needed_columns(mats: Sequence[sp.csr_matrix], r0: int, r1: int) -> np.ndarray:
+    cols = [M.indices[M.indptr[r0]:M.indptr[r1]] for M in mats]
+    return np.unique(np.concatenate(cols)) if cols else np.zeros(0, np.int64)
+
+
+def build_plan(mats: Sequence[sp.csr_matrix], bounds: List[int], rank: int) -> HaloPlan:
+    """Halo of `rank` (columns of its rows in any of `mats` owned elsewhere) and what it sends
+    (its own rows that the other ranks' rows reference, in their halo order)."""
+    world = len(bounds) - 1
+    r0, r1 = bounds[rank], bounds[rank + 1]
+    owner = lambda g: np.searchsorted(bounds, g, side="right") - 1  # noqa: E731
+    need = _needed_columns(mats, r0, r1)
+    halo = need[(need < r0) | (need >= r1)]
+    ho = owner(halo)
+    recv_counts = [int(np.count_nonzero(ho == s)) for s in range(world)]
+    send, send_counts = [], []
+    for d in range(world):
+        if d == rank:
+            send_counts.append(0)
+            continue
+        nd = _needed_columns(mats, bounds[d], bounds[d + 1])
+        mine = nd[(nd >= r0) & (nd < r1)]
+        send.append(mine - r0)
+        send_counts.append(int(mine.size))
+    send_idx = np.concatenate(send).astype(np.int32) if send else np.zeros(0, np.int32)
+    return HaloPlan(rank, list(bounds), halo.astype(np.int64), recv_counts, send_idx, send_counts)
+
+
+def local_matrix(M: sp.csr_matrix, plan: HaloPlan) -> sp.csr_matrix:
+    """The rank's rows of M over its extended numbering [own | halo], as a square n_ext matrix
+    whose halo rows are empty.  Entries stay in GLOBAL column order inside each row (the local
+    column numbers are then not ascending where a row has halo entries left of its own block):
+    the SpMV kernels sum a row in stored order, so every row sum is scipy's csr_matvec order,
+    the single-GPU solver's bits."""
+    r0, r1 = plan.bounds[plan.rank], plan.bounds[plan.rank + 1]
+    rows = M[r0:r1].tocsr()
+    rows.sort_indices()
+    g = rows.indices.astype(np.int64)
+    own = (g >= r0) & (g < r1)
+    loc = np.where(own, g - r0, plan.n_own + np.searchsorted(plan.halo, g))
+    indptr = np.concatenate([rows.indptr, np.full(plan.n_ext - plan.n_own, rows.indptr[-1])])
+    # stored (global) order kept: upload with DeviceMatrix.from_scipy(..., keep_order=True)
+    return sp.csr_matrix((rows.data, loc.astype(np.int32), indptr), shape=(plan.n_ext, plan.n_ext))
+
+
+def dd_add(a: Tuple[float, float], b: Tuple[float, float]) -> Tuple[float, float]:
+    """lspcg_internal.hpp dd_add (TwoSum of the heads, corrections added): IEEE doubles."""
+    s = a[0] + b[0]
+    bb = s - a[0]
+    e = (a[0] - (s - bb)) + (b[0] - bb)
+    return s, (a[1] + b[1]) + e
+
+
+def sum_groups(gathered: np.ndarray, nd: int) -> List[float]:
+    """gathered: [world, 64 * nd * 2] per-group (s, c) pairs (slot (g*nd + j)*2) -> nd totals."""
+    out = []
+    for j in range(nd):
+        acc = (0.0, 0.0)
+        for row in gathered:
+            v = row.reshape(GROUPS, nd, 2)[:, j, :]
+            for s, c in v[(v[:, 0] != 0) | (v[:, 1] != 0)]:  # adding an exact (0, 0) changes nothing
+                acc = dd_add(acc, (float(s), float(c)))
+        out.append(acc[0] + acc[1])
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# exchanges
+# ---------------------------------------------------------------------------------------------
+def _backend(group) -> Optional[str]:
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    return dist.get_backend(group)
+
+
+def exchange(recv: torch.Tensor, send: torch.Tensor, recv_counts: List[int], send_counts: List[int], group=None):
+    """One all-to-all of halo entries (recv = the tail of an extended vector)."""
+    be = _backend(group)
+    if be is None or dist.get_world_size(group) == 1:
+        return
+    if be == "nccl" or not recv.is_cuda:
+        dist.all_to_all_single(recv, send, recv_counts, send_counts, group=group)
+        return
+    rc = torch.empty(recv.shape, dtype=recv.dtype)  # gloo: host staging
+    dist.all_to_all_single(rc, send.cpu(), recv_counts, send_counts, group=group)
+    recv.copy_(rc)
+
+
+def gather_rows(t: torch.Tensor, group=None) -> np.ndarray:
+    """All ranks' copies of a small fixed-size buffer -> [world, t.numel()] on the host."""
+    be = _backend(group)
+    if be is None or dist.get_world_size(group) == 1:
+        return t.reshape(1, -1).cpu().numpy()
+    w = dist.get_world_size(group)
+    if be == "nccl" or not t.is_cuda:
+        out = torch.empty(w * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.reshape(-1), group=group)
+        return out.reshape(w, -1).cpu().numpy()
+    tc = t.reshape(-1).cpu()
+    parts = [torch.empty_like(tc) for _ in range(w)]
+    dist.all_gather(parts, tc, group=group)
+    return torch.stack(parts).numpy()
+
+
+# ---------------------------------------------------------------------------------------------
+# the solver
+# ---------------------------------------------------------------------------------------------
+class DistributedPCG:
+    """ext_spai PCG (``preconditioner="ext_spai"``, M⁻¹ = L Lᵀ + εI) or plain CG (L = None) of ONE
+    system over the ranks of `group`.  A and L are the global scipy matrices (every rank reads
+    the same host data and keeps only its rows on the device).  Iteration counts and iterates
+    follow scipy's cg with compensated dot products; the dots are summed in a different order
+    than the single-GPU solver's, so iterates agree to rounding (tests: 1e-12), not bit for bit."""
+
+    def __init__(self, A, L=None, epsilon: float = 0.0, dtype=np.float64, group=None,
+                 device: Optional[torch.device] = None):
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        else:
+            self.rank, self.world = 0, 1
+        A = sp.csr_matrix(A, dtype=np.float64)
+        A.sort_indices()
+        mats = [A]
+        LT = None
+        if L is not None:
+            L = sp.csr_matrix(L, dtype=np.float64)
+            L.sort_indices()
+            LT = L.T.tocsr()
+            LT.sort_indices()
+            mats += [L, LT]
+        self.n = A.shape[0]
+        self.eps = float(epsilon)
+        self.np_dtype = np.dtype(dtype)
+        self.tdtype = torch.float64 if self.np_dtype == np.float64 else torch.float32
+        self.ctx = Context.get(device)
+        self.bounds = partition_rows(A.indptr, self.world)
+        self.plan = build_plan(mats, self.bounds, self.rank)
+        p = self.plan
+        self._mats = [DeviceMatrix.from_scipy(local_matrix(M, p), dtype=dtype, ctx=self.ctx, keep_order=True)
+                      for M in mats]
+        for M in self._mats:
+            M.prepare_spmv()
+        dA = self._mats[0]
+        dL = self._mats[1] if L is not None else None
+        dLT = self._mats[2] if L is not None else None
+        h = C.c_void_p()
+        sidx = np.ascontiguousarray(p.send_idx, dtype=np.int32)
+        _lib.call("lspcg_part_create", self.ctx.handle, dA.handle, dL.handle if dL else None,
+                  dLT.handle if dLT else None, p.n_own, sidx.ctypes.data_as(C.c_void_p), int(sidx.size),
+                  C.byref(h))
+        self.handle = h
+        dev = self.ctx.torch_device
+        ne, no = p.n_ext, p.n_own
+        self.r = torch.zeros(ne, dtype=self.tdtype, device=dev)
+        self.t = torch.zeros(ne, dtype=self.tdtype, device=dev)
+        self.p = torch.zeros(ne, dtype=self.tdtype, device=dev)
+        self.z = torch.zeros(max(no, 1), dtype=self.tdtype, device=dev)
+        self.q = torch.zeros(max(no, 1), dtype=self.tdtype, device=dev)
+        self.x = torch.zeros(max(no, 1), dtype=self.tdtype, device=dev)
+        self.send = torch.zeros(max(int(sidx.size), 1), dtype=self.tdtype, device=dev)
+        self.red = torch.zeros(GROUPS * 2 * 2, dtype=torch.float64, device=dev)
+        self.has_L = L is not None
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.lspcg_part_destroy(h)
+            self.handle = None
+
+    # ---- pieces
+    def _T(self, v: float) -> float:
+        return float(self.np_dtype.type(v))
+
+    def _sqrt(self, v: float) -> float:
+        return float(np.sqrt(self.np_dtype.type(v)))
+
+    def _halo(self, v: torch.Tensor):
+        p = self.plan
+        if self.world == 1:
+            return
+        _lib.call("lspcg_part_pack", self.handle, _ptr(v), _ptr(self.send))
+        exchange(v[p.n_own:], self.send[:p.send_idx.size], p.recv_counts, p.send_counts, self.group)
+
+    def _reduce(self, nd: int) -> List[float]:
+        return sum_groups(gather_rows(self.red[:GROUPS * nd * 2], self.group), nd)
+
+    def own_slice(self) -> slice:
+        return slice(self.bounds[self.rank], self.bounds[self.rank + 1])
+
+    # ---- solve
+    def solve(self, b_global: np.ndarray, rtol: float = 1e-6, max_iter: int = 0,
+              return_history: bool = False):
+        """scipy cg from x0 = 0 on the global rhs (every rank passes the same vector).  Returns
+        ``(iters, converged, x_own[, history])``; x_own: this rank's rows of the solution."""
+        p = self.plan
+        no = p.n_own
+        mi = int(max_iter) if max_iter and max_iter > 0 else self.n
+        b = torch.as_tensor(np.asarray(b_global)[self.own_slice()], dtype=self.tdtype).to(self.ctx.torch_device)
+        self.x.zero_()
+        self.r.zero_()
+        self.r[:no] = b
+        self.p.zero_()
+        _lib.call("lspcg_part_norms", self.handle, _ptr(self.r), _ptr(self.r), _ptr(self.red))
+        rr0, bb = (self._T(v) for v in self._reduce(2))
+        bn = self._sqrt(bb)
+        atol = max(0.0, rtol * bn)
+        hist = [self._sqrt(rr0)]
+        if bn == 0.0:  # scipy returns b
+            self.x[:no] = b
+            return (0, True, self.x[:no].clone()) + ((np.array(hist),) if return_history else ())
+        rr, rho_prev, k, code = rr0, 0.0, 0, 0
+        while True:
+            if self.has_L:
+                self._halo(self.r)
+                _lib.call("lspcg_part_lt", self.handle, _ptr(self.r), _ptr(self.t))
+                self._halo(self.t)
+                _lib.call("lspcg_part_l", self.handle, _ptr(self.t), _ptr(self.r), self.eps, _ptr(self.z),
+                          _ptr(self.red))
+                rho, rr_k = (self._T(v) for v in self._reduce(2))
+                z = self.z
+            else:  # CG: z = r, ρ = ‖r‖² (from the previous update, or the init)
+                rr_k = rr if k > 0 else rr0
+                rho = rr_k
+                z = self.r
+            if k > 0:
+                rr = rr_k
+                hist.append(self._sqrt(rr))
+            # scipy's top-of-loop test (k_update_p_g)
+            if k >= mi:
+                code = 2
+            else:
+                rn = self._sqrt(rr)
+                if rn < atol:
+                    code = 1
+                elif not math.isfinite(rn):
+                    code = 3
+            if code:
+                break
+            beta = 0.0 if k == 0 else self._T(self.np_dtype.type(rho) / self.np_dtype.type(rho_prev))
+            _lib.call("lspcg_part_update_p", self.handle, _ptr(z), _ptr(self.p), beta, int(k == 0))
+            self._halo(self.p)
+            _lib.call("lspcg_part_a", self.handle, _ptr(self.p), _ptr(self.q), _ptr(self.red))
+            (pq,) = (self._T(v) for v in self._reduce(1))
+            alpha = self._T(self.np_dtype.type(rho) / self.np_dtype.type(pq))
+            _lib.call("lspcg_part_update_xr", self.handle, alpha, _ptr(self.p), _ptr(self.q), _ptr(self.x),
+                      _ptr(self.r))
+            if not self.has_L:  # ‖r_{k+1}‖² for the next test
+                _lib.call("lspcg_part_norms", self.handle, _ptr(self.r), _ptr(self.r), _ptr(self.red))
+                rr = self._T(self._reduce(2)[0])
+            rho_prev = rho
+            k += 1
+        iters = mi if code == 3 else k
+        out = (iters, code == 1, self.x[:no].clone())
+        if return_history:
+            out = out + (np.array(hist),)
+        return out
+
+    def gather_solution(self, x_own: torch.Tensor) -> np.ndarray:
+        """The full solution on every rank (host), from each rank's own rows."""
+        w = self.world
+        if w == 1:
+            return x_own.cpu().numpy().astype(np.float64)
+        m = max(self.bounds[r + 1] - self.bounds[r] for r in range(w))
+        buf = torch.zeros(m, dtype=torch.float64, device=self.ctx.torch_device)
+        buf[:x_own.numel()] = x_own[: self.plan.n_own].to(torch.float64)
+        rows = gather_rows(buf, self.group)
+        return np.concatenate([rows[r][: self.bounds[r + 1] - self.bounds[r]] for r in range(w)])

@@ -83,13 +83,16 @@ class DeviceMatrix:
 
     # ---- construction
     @classmethod
-    def from_scipy(cls, A, dtype=np.float64, block_size: int = 1, ctx: Optional[Context] = None) -> "DeviceMatrix":
+    def from_scipy(cls, A, dtype=np.float64, block_size: int = 1, ctx: Optional[Context] = None,
+                   keep_order: bool = False) -> "DeviceMatrix":
+        """``keep_order`` (scalar CSR): upload each row's entries in their stored order (the
+        SpMV sums a row in stored order; dist_pcg's extended matrices rely on it)."""
         ctx = ctx or Context.get()
         code = lspcg_dtype(dtype)
         npdt = _NP[code]
         if block_size == 1:
             A = sp.csr_matrix(A)
-            if not A.has_sorted_indices:
+            if not keep_order and not A.has_sorted_indices:
                 A = A.sorted_indices()
             indptr = np.ascontiguousarray(A.indptr, dtype=np.int32)
             indices = np.ascontiguousarray(A.indices, dtype=np.int32)

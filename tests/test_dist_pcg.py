@@ -1,0 +1,119 @@
+"""CPU: the host side of the row-partitioned single-system PCG (dist_pcg.py, SURVEY.md §8(f)
+rank 4): partition, halo plans, extended local matrices, the compensated cross-rank sum, and the
+exchange / gather plumbing over gloo with world sizes 2 and 3 (127.0.0.1)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from learningsparsepreconditioner4gpu_amd import problems as P
+from learningsparsepreconditioner4gpu_amd.dist_pcg import (GROUPS, build_plan, dd_add, exchange, gather_rows,
+                                                          local_matrix, partition_rows, sum_groups)
+
+
+def _mats():
+    A, _, _ = P.poisson2d_grid(30, 25)
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    rng = np.random.default_rng(0)
+    L = sp.csr_matrix(A, copy=True)
+    L.data = rng.standard_normal(L.nnz)
+    return [A, L, L.T.tocsr()]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_plans_reproduce_global_spmv_in_scipy_order(world):
+    mats = _mats()
+    n = mats[0].shape[0]
+    bounds = partition_rows(mats[0].indptr, world)
+    assert bounds[0] == 0 and bounds[-1] == n and all(a <= b for a, b in zip(bounds, bounds[1:]))
+    plans = [build_plan(mats, bounds, r) for r in range(world)]
+    x = np.random.default_rng(1).standard_normal(n)
+    for M in mats:
+        y = []
+        for r, p in enumerate(plans):
+            xe = np.concatenate([x[bounds[r]:bounds[r + 1]], x[p.halo]])
+            Ml = local_matrix(M, p)
+            # stored order = global column order: the row sums are scipy's, bit for bit
+            halo = np.append(p.halo, -1)  # (sentinel: an empty halo still indexes)
+            g = np.where(Ml.indices < p.n_own, Ml.indices + bounds[r], halo[np.maximum(Ml.indices - p.n_own, 0)])
+            for i in range(p.n_own):
+                seg = slice(Ml.indptr[i], Ml.indptr[i + 1])
+                assert np.all(np.diff(g[seg]) > 0)
+            y.append((Ml @ xe)[:p.n_own])
+            assert Ml.shape == (p.n_ext, p.n_ext) and Ml[p.n_own:].nnz == 0
+        assert np.array_equal(np.concatenate(y), M @ x)
+    for r, p in enumerate(plans):  # what rank s sends to r is r's halo block owned by s, in order
+        for s, q in enumerate(plans):
+            if s == r:
+                continue
+            off = sum(q.send_counts[:r])
+            sent = q.send_idx[off:off + q.send_counts[r]] + bounds[s]
+            got = p.halo[sum(p.recv_counts[:s]):sum(p.recv_counts[:s + 1])]
+            assert np.array_equal(sent, got)
+
+
+def test_sum_groups_is_compensated_and_order_fixed():
+    rng = np.random.default_rng(2)
+    vals = rng.standard_normal((3, GROUPS)) * 10.0 ** rng.integers(-8, 8, (3, GROUPS))
+    buf = np.zeros((3, GROUPS * 2))
+    buf[:, 0::2] = vals
+    total = sum_groups(buf, 1)[0]
+    exact = float(np.sum(np.array(sorted(vals.ravel(), key=abs), dtype=np.longdouble)))
+    assert abs(total - exact) <= 2 ** -52 * abs(exact)
+    acc = (0.0, 0.0)
+    for v in vals.ravel():
+        acc = dd_add(acc, (float(v), 0.0))
+    assert total == acc[0] + acc[1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mats = _mats()
+    n = mats[0].shape[0]
+    bounds = partition_rows(mats[0].indptr, world)
+    p = build_plan(mats, bounds, rank)
+    x = np.random.default_rng(3).standard_normal(n)
+    own = torch.from_numpy(x[bounds[rank]:bounds[rank + 1]].copy())
+    ext = torch.zeros(p.n_ext, dtype=torch.float64)
+    ext[:p.n_own] = own
+    send = own[torch.from_numpy(p.send_idx.astype(np.int64))]  # the device pack, restated
+    exchange(ext[p.n_own:], send, p.recv_counts, p.send_counts)
+    ok_halo = bool(torch.equal(ext[p.n_own:], torch.from_numpy(x[p.halo])))
+    red = torch.zeros(GROUPS * 2, dtype=torch.float64)
+    red[2 * rank] = float(rank + 1)  # group `rank` of this rank's buffer
+    tot = sum_groups(gather_rows(red), 1)[0]
+    q.put((rank, ok_halo, tot))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_halo_exchange_and_gather(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    for rank, ok_halo, tot in outs:
+        assert ok_halo, rank
+        assert tot == sum(range(1, world + 1))

@@ -1,0 +1,108 @@
+"""GPU parity: ONE system row-partitioned over ranks (dist_pcg.py + csrc/lspcg_part.hip, SURVEY.md
+§8(f) rank 4) against the oracle's scipy cg with correctly rounded dots and against the
+single-GPU solver: same counts, iterates and residual histories to 1e-12.  World 1 runs in this
+process; worlds 2 and 3 run as ranks on the one GPU of the box with gloo (halo and dot buffers
+staged through the host) -- the RCCL path differs only in moving device buffers directly."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+import torch.multiprocessing as mp
+
+from oracle import linalg as O
+from tests import _cases
+from learningsparsepreconditioner4gpu_amd import problems as P
+
+pytestmark = pytest.mark.gpu
+EPS = 3e-3
+
+
+def _system(kind):
+    if kind == "kuhn":
+        A, mask = P.kuhn_dirichlet(17)
+    else:
+        A, mask, _ = P.poisson2d_grid(90, 70)
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    b = A @ np.asarray(mask, dtype=np.float64).reshape(-1)
+    return A, _cases.spai_like(A), b
+
+
+def _oracle(A, L, b, rtol):
+    ps = O.spai_operator(L, EPS) if L is not None else None
+    return O.pcg(A, b, ps, rtol=rtol, dot="exact")
+
+
+@pytest.mark.parametrize("kind,precond", [("kuhn", "ext_spai"), ("poisson", "ext_spai"), ("poisson", "none")])
+def test_world1_matches_oracle_and_single_gpu(gpu_ctx, kind, precond):
+    from learningsparsepreconditioner4gpu_amd.dist_pcg import DistributedPCG
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    A, L, b = _system(kind)
+    L = L if precond == "ext_spai" else None
+    d = DistributedPCG(A, L, EPS)
+    it, conv, x, hist = d.solve(b, rtol=1e-8, return_history=True)
+    it_o, x_o, h_o = _oracle(A, L, b, 1e-8)
+    assert conv and it == it_o
+    np.testing.assert_allclose(hist, h_o[: it + 1], rtol=1e-12, atol=0)
+    x = d.gather_solution(x)
+    assert np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
+    if L is not None:
+        s.set_spai(L, EPS)
+    bt = torch.from_numpy(b).cuda()
+    xs = torch.zeros_like(bt)
+    it_s, conv_s, _ = s.solve(bt, xs, rtol=1e-8)
+    assert it_s == it
+    np.testing.assert_allclose(x, xs.cpu().numpy(), rtol=0, atol=1e-12 * np.abs(x_o).max())
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, world, port, kind, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from learningsparsepreconditioner4gpu_amd.dist_pcg import DistributedPCG
+
+    A, L, b = _system(kind)
+    d = DistributedPCG(A, L, EPS)
+    it, conv, x, hist = d.solve(b, rtol=1e-8, return_history=True)
+    xg = d.gather_solution(x)
+    q.put((rank, it, bool(conv), xg, hist, d.plan.n_own, len(d.plan.halo)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multi_rank_matches_oracle(gpu_ctx, world):
+    kind = "kuhn"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, kind, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=100) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    A, L, b = _system(kind)
+    it_o, x_o, h_o = _oracle(A, L, b, 1e-8)
+    assert sum(o[5] for o in outs) == A.shape[0] and all(o[6] > 0 for o in outs)
+    for rank, it, conv, xg, hist, _, _ in outs:
+        assert conv and it == it_o, (rank, it, it_o)
+        np.testing.assert_allclose(hist, h_o[: it + 1], rtol=1e-12, atol=0)
+        assert np.linalg.norm(xg - x_o) <= 1e-12 * np.linalg.norm(x_o)
+    assert all(np.array_equal(outs[0][3], o[3]) for o in outs)  # every rank holds the same solution
