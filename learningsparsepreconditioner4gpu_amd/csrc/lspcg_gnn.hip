@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cmath>
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -341,11 +342,17 @@ constexpr int kFrag48 = frag_size(12);
 constexpr int kFrag16 = frag_size(4);
 constexpr int kLayerFrag = 2 * kFrag48 + kFrag16;  // [msg | edge | node]
 
+// S1E > 0 (first layer): the edge encoder is fused in -- the layer's input edge state is computed
+// from the raw edge features (fin <= 4 S1E floats of edge perm[k], fragment block `fenc` read
+// through the cache, not LDS) instead of read back from an [E,16] pass of k_encode<true>.
+template <int S1E>
 __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __restrict__ frag, int node_res,
                                                  int edge_res, const int32_t* __restrict__ ptr,
                                                  const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
                                                  const float* __restrict__ x, float* __restrict__ e,
-                                                 float* __restrict__ xout) {
+                                                 float* __restrict__ xout, const float* __restrict__ fenc, int fin,
+                                                 const float* __restrict__ eattr, const int32_t* __restrict__ perm) {
+  constexpr int SE = S1E > 0 ? S1E : 1;
   __shared__ __attribute__((aligned(16))) float wl[kLayerFrag];
   __shared__ __attribute__((aligned(16))) float msg[CE * H];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, it = lane & 15, q = lane >> 4;
@@ -367,19 +374,29 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
   const int NT = int((k1 - k0 + 15) / 16);
   const int64_t klast = k1 - 1;
   auto edge_of = [&](int T) { const int64_t k = k0 + int64_t(T) * 16 + it; return k < k1 ? k : klast; };
-  int qd = 0, qs = 0;
+  int qd = 0, qs = 0, qe = 0;
   f4 pxd{}, pxs{}, pea{};
+  float pin[SE];  // fused encoder: this lane's raw input features of the prefetched edge
+  auto load_in = [&](int row) {
+#pragma unroll
+    for (int s = 0; s < SE; ++s) {
+      const int f = 4 * s + q;
+      pin[s] = f < fin ? eattr[int64_t(row) * fin + f] : 0.f;
+    }
+  };
   if (wave < NT) {
     const int64_t kk = edge_of(wave);
     qd = dst[kk];
     qs = src[kk];
     pxd = ld4(x + int64_t(qd) * H + 4 * q);
     pxs = ld4(x + int64_t(qs) * H + 4 * q);
-    pea = ld4(e + kk * H + 4 * q);
+    if constexpr (S1E > 0) load_in(perm[kk]);
+    else pea = ld4(e + kk * H + 4 * q);
     if (wave + 4 < NT) {
       const int64_t kn = edge_of(wave + 4);
       qd = dst[kn];
       qs = src[kn];
+      if constexpr (S1E > 0) qe = perm[kn];
     }
   }
   const int nchunk = (NT + 15) / 16;
@@ -392,15 +409,26 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
       if (T >= NT) break;  // wave-uniform: MFMA needs EXEC all ones
       const int64_t k = k0 + int64_t(T) * 16 + it;
       const bool valid = k < k1;
-      const f4 xd = pxd, xs = pxs, ea = pea;  // x_i (target), x_j (source), edge attr
+      const f4 xd = pxd, xs = pxs;  // x_i (target), x_j (source)
+      f4 ea;                         // edge attr
+      if constexpr (S1E > 0) {
+        float iv[SE];
+#pragma unroll
+        for (int s = 0; s < SE; ++s) iv[s] = pin[s];
+        ea = ff_tile<SE>(fenc, iv, lane);  // k_encode<true>'s MLP on this edge
+      } else {
+        ea = pea;
+      }
       if (T + 4 < NT) {
         pxd = ld4(x + int64_t(qd) * H + 4 * q);
         pxs = ld4(x + int64_t(qs) * H + 4 * q);
-        pea = ld4(e + edge_of(T + 4) * H + 4 * q);
+        if constexpr (S1E > 0) load_in(qe);
+        else pea = ld4(e + edge_of(T + 4) * H + 4 * q);
         if (T + 8 < NT) {
           const int64_t kn = edge_of(T + 8);
           qd = dst[kn];
           qs = src[kn];
+          if constexpr (S1E > 0) qe = perm[kn];
         }
       }
       // LayerNorm(48) statistics: 12 values per lane, 4 lanes per edge, packed fp32 pairs
@@ -459,6 +487,15 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
       st4(xout + i * H + 4 * q, o);
     }
   }
+}
+
+// LSPCG_GNN_NO_FUSE=1: the separate edge-encoder pass (measurement / A-B only)
+static bool gnn_no_fuse() {
+  static const bool v = [] {
+    const char* e = std::getenv("LSPCG_GNN_NO_FUSE");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 static int egrid(int64_t n) {
@@ -687,18 +724,25 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
                        g->src, g->dst);
   }
   const int32_t* inv = hflag ? g->inv : g->perm;  // edge -> CSC slot (the involution is its own inverse)
-  // encoders
+  // encoders (the edge encoder is fused into the first layer when there is one and edge_in <= 12)
   hipLaunchKernelGGL(k_encode<false>, dim3(tgrid(N)), dim3(256), 0, st, N, d.node_in, g->frag + g->o_node_enc, x,
                      static_cast<const int32_t*>(nullptr), g->xa);
-  hipLaunchKernelGGL(k_encode<true>, dim3(tgrid(E)), dim3(256), 0, st, E, d.edge_in, g->frag + g->o_edge_enc,
-                     edge_attr, g->perm, g->ecsc);
+  const int s1e = (d.edge_in + 3) / 4;
+  const bool fuse_enc = d.num_mp_layers > 0 && s1e <= 3 && !gnn_no_fuse();
+  if (!fuse_enc)
+    hipLaunchKernelGGL(k_encode<true>, dim3(tgrid(E)), dim3(256), 0, st, E, d.edge_in, g->frag + g->o_edge_enc,
+                       edge_attr, g->perm, g->ecsc);
   // message passing
   float* xc = g->xa;
   float* xn = g->xb;
   const unsigned lg = unsigned((N + 255) / 256);
+  const float* fenc = g->frag + g->o_edge_enc;
   for (int l = 0; l < d.num_mp_layers; ++l) {
-    hipLaunchKernelGGL(k_mp_layer, dim3(lg), dim3(256), 0, st, N, g->frag + g->o_layer[l], d.node_residual,
-                       d.edge_residual, g->ptr, g->src, g->dst, xc, g->ecsc, xn);
+    const int se = (l == 0 && fuse_enc) ? s1e : 0;
+    auto kern = se == 1 ? k_mp_layer<1> : se == 2 ? k_mp_layer<2> : se == 3 ? k_mp_layer<3> : k_mp_layer<0>;
+    hipLaunchKernelGGL(kern, dim3(lg), dim3(256), 0, st, N, g->frag + g->o_layer[l], d.node_residual, d.edge_residual,
+                       g->ptr, g->src, g->dst, xc, g->ecsc, xn, fenc, d.edge_in, edge_attr,
+                       static_cast<const int32_t*>(g->perm));
     std::swap(xc, xn);
   }
   // decoder
