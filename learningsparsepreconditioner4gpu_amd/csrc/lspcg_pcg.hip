@@ -11,8 +11,7 @@
 //       KC  q = A p_k ; group partials of π_k = p_k·q              [SpMV A]
 //       UR  α_k = ρ_k/π_k ; r_{k+1} = r_k - α_k q
 //   * the same five phases with last-arriver grid reductions (CSR / BSR views, CG, Jacobi, IC);
-//   * one-workgroup solve (k_pcg_small) for n <= LSPCG_SMALL_N;
-//   * persistent multi-workgroup solve (k_pcg_persist, lspcg_persist.hpp) for the mid range.
+//   * one-workgroup solve (k_pcg_small) for n <= LSPCG_SMALL_N.
 // Every multi-launch kernel is predicated on a device `done` flag, so the host replays
 // graph-captured chunks of iterations and polls once per chunk without changing the iteration
 // count or the iterate; the deferred x update of the last iteration is one fix-up launch.
@@ -542,7 +541,7 @@ constexpr int64_t kSmallLds = 61440;  // dynamic LDS: 3 gathered vectors
 constexpr int kSmallQB = 2;  // SELL groups (4 entries each) loaded per wait (4 measured slower: 13.0 vs 9.8 us per iteration)
 
 // row i; [b, e): its CSR entry range, or (SELL) its slice's group range; gx(c) reads the
-// gathered vector (LDS in the one-workgroup solve, sc1 global loads in the persistent one)
+// gathered vector (LDS in the one-workgroup solve)
 template <typename T, int QB, class Gx>
 __device__ __forceinline__ T sell_row(const CsrView& M, int32_t b, int32_t e, int32_t i, Gx gx) {
   T acc = T(0);
@@ -775,415 +774,6 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
   }
 }
 
-// ---- mid-size systems: the whole solve in ONE persistent launch over G workgroups ---------
-// Between a few thousand and a few hundred thousand unknowns an iteration of the 5-launch
-// schedule is latency, not bytes (~17-22 us).  k_pcg_persist keeps a resident
-// grid of G <= #CU workgroups (one per CU) for the whole scipy loop; thread `tid` of workgroup g
-// owns rows (g R + m) 512 + tid, m < R, whose x, r, z, p, q live in registers.
-// There is no grid barrier.  Every value that crosses workgroups -- the gathered vectors r (for
-// Lᵀ), t (for L), p (for A) and each workgroup's compensated dot partials -- is published as
-// self-validating 8-byte granules {epoch tag, 32-bit payload}, each written by ONE sc1
-// (agent-scope relaxed) store, so the data is its own flag (MI355X_MICROARCH.md "Valid forms",
-// R2: no fence, no drain, no flag).  A consumer sc1-loads exactly the granules it needs and
-// re-reads them until every tag equals the epoch it expects; an fp64 value is two granules (high
-// and low word), each checked.  Epochs: iteration k publishes r_k (5k+1), t_k (5k+2), the ρ_k /
-// ‖r_k‖² partials (5k+3), p_k (5k+4) and the π_k partials (5k+5).
-// No slot is overwritten while a reader may still need its previous epoch: between two writes of
-// r, t or p (and of either partial set) the writer has passed an all-reduce, i.e. seen the
-// partial of EVERY workgroup, each published after that workgroup finished the reads in question.
-// All-reduces: each workgroup publishes its partial, wave 0 sweeps the G partials until all carry
-// the epoch and sums them in one fixed order -- the same total in every workgroup, so every
-// workgroup takes the same convergence decision at the same iteration.  The matrix views are read
-// with plain loads (read-only during the solve: they stay in L1 / L2).  Expressions, row-sum
-// order and the top-of-loop test are those of the split schedule (same bits).  Every wait is
-// bounded: a timed-out wait sets the timeout word, which every other wait also watches, and the
-// workgroups leave together at their next all-reduce, so the grid always drains (the host then
-// reports LSPCG_ERR_HIP).  Granules and the timeout word are zeroed before every launch.
-constexpr int kPersistThreads = 512;
-constexpr int kPersistQB = 4;                // SELL groups per batch
-constexpr unsigned kPersistSpin = 1u << 22;  // re-reads before a wait gives up
-constexpr unsigned kPersistMaxWG = 256;      // <= 4 workgroups per lane of the sweeping wave
-constexpr int kPersistMaxRows = 4;           // rows per thread (template R = 1, 2, 4)
-// sync buffer (uint32 words): [timeout | pad to 32][ρ,‖r‖² partials: G x 8 u64][π: G x 4 u64]
-inline size_t persist_gz_off() { return 32; }
-inline size_t persist_gq_off(unsigned G) { return persist_gz_off() + size_t(G) * 8 * 2; }
-inline size_t persist_sync_bytes(unsigned G) { return 4 * (persist_gq_off(G) + size_t(G) * 4 * 2); }  // x 16 B
-
-using u64 = unsigned long long;
-
-struct PersistSync {
-  unsigned* err;  // timeout word
-  u64* gz;        // [G][2 dots][s hi, s lo, c hi, c lo] granules
-  u64* gq;        // [G][1 dot][...]
-  u64* rg;        // vector granules: r, t, p ([n] fp32 / [2n] fp64 each)
-  u64* tg;
-  u64* pg;
-  u64* stamps;    // diagnostics (LSPCG_PERSIST_STAMPS=1): s_memrealtime per phase, workgroups 0 and G-1
-};
-
-constexpr int kStampIters = 64, kStampPhases = 8;
-// diagnostics only: thread 0 of workgroups 0 and G-1 record the 100 MHz real-time clock
-__device__ __forceinline__ void stamp(const PersistSync& sy, int64_t k, int ph) {
-  if (sy.stamps && threadIdx.x == 0 && k < kStampIters && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
-    sy.stamps[((blockIdx.x == 0 ? 0 : kStampIters) + k) * kStampPhases + ph] = __builtin_amdgcn_s_memrealtime();
-}
-
-__device__ __forceinline__ u64 ld_gran(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_gran(u64* p, u64 v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ bool persist_timed_out(const unsigned* err) {
-  return __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-}
-__device__ __forceinline__ void persist_fail(unsigned* err) {
-  __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// one vector entry as granules: fp64 = [tag | hi32][tag | lo32], fp32 = [tag | bits]
-template <typename T>
-struct Gran {
-  static constexpr int W = sizeof(T) / 4;  // granules per value
-  __device__ static __forceinline__ void put(u64* g, int32_t i, T v, unsigned tag) {
-    const u64 t = u64(tag) << 32;
-    if constexpr (W == 2) {
-      const u64 b = u64(__double_as_longlong(v));
-      st_gran(g + 2 * int64_t(i), t | (b >> 32));
-      st_gran(g + 2 * int64_t(i) + 1, t | (b & 0xffffffffull));
-    } else {
-      st_gran(g + i, t | u64(__float_as_uint(v)));
-    }
-  }
-  // raw granules of entry i (not yet validated)
-  struct Raw {
-    u64 a, b;
-  };
-  __device__ static __forceinline__ Raw get(const u64* g, int32_t i) {
-    if constexpr (W == 2) return Raw{ld_gran(g + 2 * int64_t(i)), ld_gran(g + 2 * int64_t(i) + 1)};
-    else return Raw{ld_gran(g + i), 0};
-  }
-  __device__ static __forceinline__ bool ok(const Raw& r, unsigned tag) {
-    if constexpr (W == 2) return unsigned(r.a >> 32) == tag && unsigned(r.b >> 32) == tag;
-    else return unsigned(r.a >> 32) == tag;
-  }
-  __device__ static __forceinline__ T val(const Raw& r) {
-    if constexpr (W == 2) return __longlong_as_double((long long)((r.a << 32) | (r.b & 0xffffffffull)));
-    else return __uint_as_float(unsigned(r.a));
-  }
-};
-
-// SELL row sum (sell_row's order) gathering x from granules of epoch `tag`: a batch's granules are
-// re-read until every tag matches.  Returns false after a timeout (the sum is then garbage).
-template <typename T, int QB>
-__device__ __forceinline__ bool sell_row_gran(const CsrView& M, int32_t b, int32_t e, int32_t i, const u64* xg,
-                                              unsigned tag, const unsigned* err, T& out) {
-  T acc = T(0);
-  const int32_t lane = i & 63, base = i & ~63;
-  for (int32_t q0 = b; q0 < e; q0 += QB) {
-    T v[4 * QB];
-    int32_t c[4 * QB];
-    bool okm[4 * QB];
-#pragma unroll
-    for (int u = 0; u < QB; ++u) {
-      const size_t off = 256 * size_t(min(q0 + u, e - 1)) + 4 * lane;
-      if (M.sf32) {
-        const f32x4 a = *(const __attribute__((address_space(1))) f32x4*)(static_cast<const float*>(M.sv) + off);
-        v[4 * u + 0] = T(a.x); v[4 * u + 1] = T(a.y); v[4 * u + 2] = T(a.z); v[4 * u + 3] = T(a.w);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[4 * u + j] = gld(static_cast<const T*>(M.sv) + off + j);
-      }
-      int o[4];
-      if (M.c16) {
-        const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(static_cast<const int16_t*>(M.scol) + off);
-        o[0] = cc.x; o[1] = cc.y; o[2] = cc.z; o[3] = cc.w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          okm[4 * u + j] = o[j] != kSellPad16 && q0 + u < e;
-          c[4 * u + j] = okm[4 * u + j] ? base + o[j] : 0;
-        }
-      } else {
-        const i32x4 cc = *(const __attribute__((address_space(1))) i32x4*)(static_cast<const int32_t*>(M.scol) + off);
-        o[0] = cc.x; o[1] = cc.y; o[2] = cc.z; o[3] = cc.w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          okm[4 * u + j] = o[j] >= 0 && q0 + u < e;
-          c[4 * u + j] = okm[4 * u + j] ? o[j] : 0;
-        }
-      }
-    }
-    typename Gran<T>::Raw g[4 * QB];
-    bool ready = false;
-    for (unsigned spin = 0; spin < kPersistSpin; ++spin) {
-      bool all = true;
-#pragma unroll
-      for (int u = 0; u < 4 * QB; ++u) {
-        if (okm[u]) {
-          g[u] = Gran<T>::get(xg, c[u]);
-          all &= Gran<T>::ok(g[u], tag);
-        }
-      }
-      if (all) {
-        ready = true;
-        break;
-      }
-      if ((spin & 63) == 63 && persist_timed_out(err)) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (!ready) {
-      persist_fail(const_cast<unsigned*>(err));
-      out = T(0);
-      return false;
-    }
-#pragma unroll
-    for (int u = 0; u < 4 * QB; ++u)
-      if (okm[u]) acc = acc + v[u] * Gran<T>::val(g[u]);
-  }
-  out = acc;
-  return true;
-}
-
-// All-reduce of N compensated partials by tagged granules; `bad` (this thread's earlier waits
-// failed) is OR-ed over the workgroup.  Returns false (uniformly) when any wait failed.
-template <typename T, int N>
-__device__ __forceinline__ bool persist_allreduce(DD (&v)[N], bool bad, DD* lds, double* lds_out, u64* gran,
-                                                  unsigned* err, unsigned tag, unsigned G, int* s_ok,
-                                                  double (&out)[N]) {
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  wave_reduce_dd<N>(v);
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) lds[wid * N + j] = v[j];
-  }
-  if (__syncthreads_or(bad)) return false;
-  const u64 t = u64(tag) << 32;
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-      DD a = lds[j];
-      for (int w = 1; w < kPersistThreads / 64; ++w) a = dd_add(a, lds[w * N + j]);
-      const u64 s = u64(__double_as_longlong(a.s));
-      const u64 c = u64(__double_as_longlong(a.c));
-      u64* g = gran + (size_t(blockIdx.x) * N + j) * 4;
-      st_gran(g + 0, t | (s >> 32));
-      st_gran(g + 1, t | (s & 0xffffffffull));
-      st_gran(g + 2, t | (c >> 32));
-      st_gran(g + 3, t | (c & 0xffffffffull));
-    }
-  }
-  if (threadIdx.x < 64) {
-    bool ok = false;
-    u64 q[4][N][4];
-    for (unsigned spin = 0; spin < kPersistSpin; ++spin) {
-      bool mine = true;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const unsigned g = unsigned(lane) + 64u * u;
-        if (g < G) {
-#pragma unroll
-          for (int j = 0; j < N; ++j)
-#pragma unroll
-            for (int h = 0; h < 4; ++h) {
-              q[u][j][h] = ld_gran(gran + (size_t(g) * N + j) * 4 + h);
-              mine &= unsigned(q[u][j][h] >> 32) == tag;
-            }
-        }
-      }
-      if (__all(mine)) {
-        ok = true;
-        break;
-      }
-      if (__shfl(int(lane == 0 && persist_timed_out(err)), 0, 64)) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (ok) {
-      DD a[N];
-#pragma unroll
-      for (int j = 0; j < N; ++j) a[j] = dd_zero();
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const bool in = unsigned(lane) + 64u * u < G;
-#pragma unroll
-        for (int j = 0; j < N; ++j) {
-          const u64 s = (q[u][j][0] << 32) | (q[u][j][1] & 0xffffffffull);
-          const u64 c = (q[u][j][2] << 32) | (q[u][j][3] & 0xffffffffull);
-          a[j] = dd_add(a[j], in ? DD{__longlong_as_double((long long)s), __longlong_as_double((long long)c)} : dd_zero());
-        }
-      }
-      wave_reduce_dd<N>(a);
-      if (lane == 0) {
-#pragma unroll
-        for (int j = 0; j < N; ++j) lds_out[j] = round_to<T>(dd_value(a[j]));
-      }
-    }
-    if (lane == 0) {
-      if (!ok) persist_fail(err);
-      *s_ok = ok;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < N; ++j) out[j] = lds_out[j];
-  return *s_ok != 0;
-}
-
-template <typename T, int PRE, int R>
-__global__ void __launch_bounds__(kPersistThreads) k_pcg_persist(int32_t n, PcgState* S, CsrView A, CsrView L,
-                                                                 CsrView LT, const T* __restrict__ d, T* x, const T* r,
-                                                                 T* p, PersistSync sy) {
-  constexpr bool SPAI = PRE == LSPCG_PRECOND_EXT_SPAI || PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
-  constexpr bool SCALED = PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
-  constexpr int QB = R >= 4 ? 2 : kPersistQB;  // 4 rows per thread: fewer gathers in flight (registers)
-  __shared__ DD lds_dd[kPersistThreads / 64 * 2];
-  __shared__ double lds_tot[2];
-  __shared__ int s_ok;
-  if (S->done) return;  // ‖b‖ = 0 (init): uniform
-  const unsigned G = gridDim.x;
-  const int tid = threadIdx.x;
-  const T eps = T(S->eps);
-  const double atol = S->atol;
-  const int64_t max_iter = S->max_iter;
-  double* hist = S->hist;
-  const double rr0 = S->rr;
-  double rho_prev = S->rho, rho = S->rho, pq = S->pq;
-  T alpha = T(S->alpha);
-  int64_t k = S->iter;
-  int code = 0;
-  const bool lead = blockIdx.x == 0 && tid == 0;
-  bool own[R];
-  int32_t row[R], ab[R], ae[R], lb[R], le[R], tb[R], te[R];
-  T xr[R], rr_[R], pr[R], dr[R];
-#pragma unroll
-  for (int m = 0; m < R; ++m) {
-    row[m] = (int32_t(blockIdx.x) * R + m) * kPersistThreads + tid;
-    own[m] = row[m] < n;
-    const int32_t i = own[m] ? row[m] : 0;
-    auto range = [&](const CsrView& M, int32_t& b, int32_t& e) {  // SELL groups of the row's slice
-      b = M.gp[i >> 6];
-      e = own[m] ? M.gp[(i >> 6) + 1] : b;
-    };
-    range(A, ab[m], ae[m]);
-    if constexpr (SPAI) {
-      range(L, lb[m], le[m]);
-      range(LT, tb[m], te[m]);
-    }
-    xr[m] = own[m] ? x[i] : T(0);
-    rr_[m] = own[m] ? r[i] : T(0);
-    pr[m] = T(0);
-    if constexpr (SCALED || PRE == LSPCG_PRECOND_DIAGONAL) dr[m] = own[m] ? d[i] : T(1);
-    if constexpr (SPAI)
-      if (own[m]) Gran<T>::put(sy.rg, i, rr_[m], unsigned(5 * k + 1));  // r_k of the first iteration
-  }
-  bool alive = true;
-  for (;; ++k) {
-    const unsigned ep = unsigned(5 * k);
-    bool bad = false;
-    stamp(sy, k, 0);
-    // t = Lᵀ r_k (scaled: / d), published for the L row sums of every workgroup
-    if constexpr (SPAI) {
-#pragma unroll
-      for (int m = 0; m < R; ++m) {
-        if (!own[m]) continue;
-        T s;
-        bad |= !sell_row_gran<T, QB>(LT, tb[m], te[m], row[m], sy.rg, ep + 1, sy.err, s);
-        Gran<T>::put(sy.tg, row[m], SCALED ? s / dr[m] : s, ep + 2);
-      }
-    }
-    stamp(sy, k, 1);
-    // z = M⁻¹ r ; partials of ρ_k = r·z and ‖r_k‖²
-    DD dz[2] = {dd_zero(), dd_zero()};
-    T zr[R];
-#pragma unroll
-    for (int m = 0; m < R; ++m) {
-      const T ri = rr_[m];
-      T zi = T(0);
-      if constexpr (SPAI) {
-        if (own[m]) {
-          T s;
-          bad |= !sell_row_gran<T, QB>(L, lb[m], le[m], row[m], sy.tg, ep + 2, sy.err, s);
-          if constexpr (SCALED) zi = s + (eps * ri) / dr[m];
-          else zi = s + eps * ri;
-        }
-      } else if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) {
-        zi = ri / dr[m];
-      } else {
-        zi = ri;
-      }
-      zr[m] = zi;
-      if (own[m]) {
-        dd_fma(dz[0], double(ri), double(zi));
-        dd_fma(dz[1], double(ri), double(ri));
-      }
-    }
-    stamp(sy, k, 2);
-    double v2[2];
-    if (!(alive = persist_allreduce<T, 2>(dz, bad, lds_dd, lds_tot, sy.gz, sy.err, ep + 3, G, &s_ok, v2))) break;
-    const double rr = k > 0 ? v2[1] : rr0;
-    if (k >= max_iter) {
-      code = 2;
-    } else {
-      const double rn = double(tsqrt<T>(T(rr)));
-      if (rn < atol) code = 1;
-      else if (!(rn == rn) || rn == INFINITY) code = 3;
-    }
-    if (lead && k > 0) {
-      S->rr = rr;
-      if (hist) hist[k] = double(tsqrt<T>(T(rr)));
-    }
-    if (code) break;  // every workgroup decides on the same totals: uniform exit
-    stamp(sy, k, 3);
-    rho_prev = rho;
-    rho = v2[0];
-    // x += α_{k-1} p_{k-1} ; p_k = p_{k-1}β + z, published for the A row sums
-    const bool first = k == 0;
-    const T beta = first ? T(0) : T(rho) / T(rho_prev);
-#pragma unroll
-    for (int m = 0; m < R; ++m) {
-      if (!first) xr[m] = xr[m] + alpha * pr[m];
-      pr[m] = first ? zr[m] : (pr[m] * beta) + zr[m];
-      if (own[m]) Gran<T>::put(sy.pg, row[m], pr[m], ep + 4);
-    }
-    stamp(sy, k, 4);
-    // q = A p ; partials of π_k = p·q
-    DD dq[1] = {dd_zero()};
-    T qr[R];
-#pragma unroll
-    for (int m = 0; m < R; ++m) {
-      qr[m] = T(0);
-      if (own[m]) {
-        bad |= !sell_row_gran<T, QB>(A, ab[m], ae[m], row[m], sy.pg, ep + 4, sy.err, qr[m]);
-        dd_fma(dq[0], double(pr[m]), double(qr[m]));
-      }
-    }
-    stamp(sy, k, 5);
-    double v1[1];
-    if (!(alive = persist_allreduce<T, 1>(dq, bad, lds_dd, lds_tot, sy.gq, sy.err, ep + 5, G, &s_ok, v1))) break;
-    stamp(sy, k, 6);
-    pq = v1[0];
-    alpha = T(rho) / T(pq);
-    // r_{k+1} = r_k - α q, published for the next Lᵀ row sums
-#pragma unroll
-    for (int m = 0; m < R; ++m) {
-      rr_[m] = rr_[m] - alpha * qr[m];
-      if constexpr (SPAI)
-        if (own[m]) Gran<T>::put(sy.rg, row[m], rr_[m], ep + 6);
-    }
-  }
-  if (!alive) return;  // timeout word set: the host fails the solve
-#pragma unroll
-  for (int m = 0; m < R; ++m) {
-    if (!own[m]) continue;
-    x[row[m]] = xr[m];
-    p[row[m]] = pr[m];
-  }
-  if (lead) {
-    S->rho_prev = rho_prev;
-    S->rho = rho;
-    S->pq = pq;
-    S->alpha = double(alpha);
-    S->iter = k;
-    S->done = code;
-  }
-}
-
 // IC: ρ = r·z after the two triangular solves
 template <typename T>
 __global__ void __launch_bounds__(kThreads) k_dot_rho(int64_t n, PcgState* S, const T* __restrict__ r,
@@ -1282,13 +872,6 @@ struct lspcg_solver {
   int svd[3] = {0, 0, 0};
   double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
   int64_t dhist_cap = 0;
-  // persistent multi-workgroup solve (k_pcg_persist): used for small_n < n <= persist_n
-  int64_t persist_n = 0;   // LSPCG_PERSIST_N (0 disables)
-  int persist_wg = 0;      // largest grid (LSPCG_PERSIST_WG; default: one workgroup per CU, <= 256)
-  unsigned* psync = nullptr;  // timeout word + dot-partial granules (memset before every launch)
-  void* pgran = nullptr;      // granules of r, t, p (memset before every launch)
-  void* pstamps = nullptr;    // LSPCG_PERSIST_STAMPS diagnostics
-  unsigned* herr = nullptr;   // pinned copy of the timeout word
   int64_t small_n = 1024;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it): <= 2 rows
                            // per thread; 5 rows lose to the 5-kernel schedule
   bool small_sell = true;  // k_pcg_small reads the SELL copies (LSPCG_SMALL_SELL=0: the CSR views)
@@ -1637,107 +1220,6 @@ static int launch_small(lspcg_solver* s, hipStream_t st) {
   return LSPCG_OK;
 }
 
-// ---- persistent multi-workgroup solve: path choice and launch
-static bool persist_grid(const lspcg_solver* s, int64_t max_iter, int* G, int* R) {
-  if (s->persist_n <= 0 || s->n <= 0 || s->n > s->persist_n || s->precond == LSPCG_PRECOND_IC) return false;
-  const bool spai = s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
-  for (int w = 0; w < (spai ? 3 : 1); ++w)
-    if (!s->sp[w] || !s->sv[w] || s->sp[w]->groups <= 0 || s->sp[w]->bs != 1) return false;  // scalar SELL views
-  const int64_t gmax = std::max(1, std::min<int>(s->persist_wg, int(kPersistMaxWG)));
-  for (int r = 1; r <= kPersistMaxRows; r *= 2) {
-    const int64_t g = (s->n + int64_t(kPersistThreads) * r - 1) / (int64_t(kPersistThreads) * r);
-    if (g <= gmax) {
-      // epochs (5 per iteration) are 32-bit tags
-      if (5 * (max_iter + 2) >= (int64_t(1) << 32)) return false;
-      *G = int(g);
-      *R = r;
-      return true;
-    }
-  }
-  return false;
-}
-
-static CsrView persist_view(const lspcg_solver* s, int w) {
-  const lspcg_mat& M = w == 0 ? s->Av : (w == 1 ? s->Lv : s->LTv);
-  const SellPattern* P = s->sp[w];
-  CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, P->gp, P->col, s->sv[w],
-            s->svd[w] == LSPCG_F32 ? 1 : 0, P->col_bits == 16 ? 1 : 0};
-  return v;
-}
-
-template <typename T>
-static int launch_persist(lspcg_solver* s, int G, int R, hipStream_t st) {
-  const bool spai = s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED;
-  const size_t vg = sizeof(u64) * (sizeof(T) / 4) * size_t(s->n);  // granules of one vector
-  if (!s->psync) {
-    LSPCG_HIP(hipMalloc(&s->psync, persist_sync_bytes(kPersistMaxWG)));
-    LSPCG_HIP(hipHostMalloc(&s->herr, sizeof(unsigned), hipHostMallocDefault));
-  }
-  if (!s->pgran) LSPCG_HIP(hipMalloc(&s->pgran, 3 * vg));
-  LSPCG_HIP(hipMemsetAsync(s->psync, 0, persist_sync_bytes(G), st));
-  LSPCG_HIP(hipMemsetAsync(s->pgran, 0, 3 * vg, st));
-  const CsrView A = persist_view(s, 0);
-  const CsrView L = spai ? persist_view(s, 1) : CsrView{};
-  const CsrView LT = spai ? persist_view(s, 2) : CsrView{};
-  u64* vgr = static_cast<u64*>(s->pgran);
-  const size_t ve = vg / sizeof(u64);
-  static const bool stamps = [] { const char* e = std::getenv("LSPCG_PERSIST_STAMPS"); return e && e[0] == '1'; }();
-  if (stamps && !s->pstamps) LSPCG_HIP(hipMalloc(&s->pstamps, sizeof(u64) * 2 * kStampIters * kStampPhases));
-  if (stamps) LSPCG_HIP(hipMemsetAsync(s->pstamps, 0, sizeof(u64) * 2 * kStampIters * kStampPhases, st));
-  const PersistSync sy{s->psync, reinterpret_cast<u64*>(s->psync + persist_gz_off()),
-                       reinterpret_cast<u64*>(s->psync + persist_gq_off(G)), vgr, vgr + ve, vgr + 2 * ve,
-                       stamps ? static_cast<u64*>(s->pstamps) : nullptr};
-  auto* x = static_cast<T*>(s->x);
-  auto* r = static_cast<const T*>(s->r);
-  auto* p = static_cast<T*>(s->p);
-  const T* d = static_cast<const T*>(s->d);
-  const int32_t n = int32_t(s->n);
-  const dim3 g(G), b(kPersistThreads);
-  auto go = [&](auto rows) {
-    constexpr int RR = decltype(rows)::value;
-    switch (s->precond) {
-      case LSPCG_PRECOND_NONE:
-        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_NONE, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, sy);
-        break;
-      case LSPCG_PRECOND_DIAGONAL:
-        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_DIAGONAL, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, sy);
-        break;
-      case LSPCG_PRECOND_EXT_SPAI:
-        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_EXT_SPAI, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r, p, sy);
-        break;
-      default:
-        hipLaunchKernelGGL((k_pcg_persist<T, LSPCG_PRECOND_EXT_SPAI_SCALED, RR>), g, b, 0, st, n, s->S, A, L, LT, d, x, r,
-                           p, sy);
-    }
-  };
-  if (R == 1) go(std::integral_constant<int, 1>{});
-  else if (R == 2) go(std::integral_constant<int, 2>{});
-  else go(std::integral_constant<int, 4>{});
-  LSPCG_HIP(hipGetLastError());
-  LSPCG_HIP(hipMemcpyAsync(s->herr, s->psync, sizeof(unsigned), hipMemcpyDeviceToHost, st));
-  if (stamps) {  // diagnostics: per-phase durations (us) of iterations 1..min(iters, 64) on stderr
-    std::vector<u64> h(2 * kStampIters * kStampPhases);
-    LSPCG_HIP(hipMemcpyAsync(h.data(), s->pstamps, sizeof(u64) * h.size(), hipMemcpyDeviceToHost, st));
-    LSPCG_HIP(hipStreamSynchronize(st));
-    for (int w = 0; w < 2; ++w) {
-      double acc[kStampPhases] = {0};
-      int cnt = 0;
-      for (int k = 1; k + 1 < kStampIters; ++k) {
-        const u64* a = h.data() + (w * kStampIters + k) * kStampPhases;
-        const u64* nx = a + kStampPhases;
-        if (!a[0] || !a[6] || !nx[0]) break;
-        for (int j = 0; j < 6; ++j) acc[j] += (a[j + 1] - a[j]) * 0.01;
-        acc[6] += (nx[0] - a[6]) * 0.01;
-        ++cnt;
-      }
-      std::fprintf(stderr, "[lspcg persist] n=%lld G=%d R=%d wg %s: %d its, us/phase Lt %.2f | L %.2f | rho-red %.2f | p %.2f | A %.2f | pi-red %.2f | r %.2f\n",
-                   (long long)s->n, G, R, w ? "last" : "0", cnt, cnt ? acc[0] / cnt : 0, cnt ? acc[1] / cnt : 0,
-                   cnt ? acc[2] / cnt : 0, cnt ? acc[3] / cnt : 0, cnt ? acc[4] / cnt : 0, cnt ? acc[5] / cnt : 0,
-                   cnt ? acc[6] / cnt : 0);
-    }
-  }
-  return LSPCG_OK;
-}
 
 static int get_graph(lspcg_solver* s, int chunk, hipGraphExec_t* out) {
   auto it = s->graphs.find(chunk);
@@ -1803,14 +1285,6 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   if (const char* e = std::getenv("LSPCG_SELL32")) s->sell16 = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SMALL_N")) s->small_n = std::max<int64_t>(0, std::atoll(e));
   if (const char* e = std::getenv("LSPCG_SMALL_SELL")) s->small_sell = e[0] != '0';
-  {
-    int cus = 256;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
-      cus = 256;
-    s->persist_wg = cus;
-  }
-  if (const char* e = std::getenv("LSPCG_PERSIST_N")) s->persist_n = std::max<int64_t>(0, std::atoll(e));
-  if (const char* e = std::getenv("LSPCG_PERSIST_WG")) s->persist_wg = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
     s->allow_split = e[0] != '0';
     s->split_mode = std::atoi(e);
@@ -1998,18 +1472,13 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     return post();
   };
   PcgState cur{};
-  int pG = 0, pR = 0;
   const bool small = small_path(s);
-  const bool persist = !small && persist_grid(s, max_iter, &pG, &pR);
-  if (small || persist) {  // one launch runs the whole loop (k_pcg_small / k_pcg_persist)
-    if (small) rc = s->dtype == LSPCG_F64 ? launch_small<double>(s, st) : launch_small<float>(s, st);
-    else rc = s->dtype == LSPCG_F64 ? launch_persist<double>(s, pG, pR, st) : launch_persist<float>(s, pG, pR, st);
+  if (small) {  // one launch runs the whole loop (k_pcg_small)
+    rc = s->dtype == LSPCG_F64 ? launch_small<double>(s, st) : launch_small<float>(s, st);
     if (!rc) rc = post();
     if (rc) return rc;
     LSPCG_HIP(hipEventSynchronize(evp[head]));
     cur = *hs[head];
-    LSPCG_CHECK(!persist || *s->herr == 0, LSPCG_ERR_HIP,
-                "solve: a grid barrier of the persistent solve timed out (workgroups not co-resident?)");
   } else {
     rc = post();
     if (!rc) rc = launch(std::min(4, max_chunk));
@@ -2018,7 +1487,7 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   int64_t last_it = 0;
   double last_rr = -1.0;
   int chunk = std::min(4, max_chunk);
-  for (; !small && !persist;) {
+  for (; !small;) {
     LSPCG_HIP(hipEventSynchronize(evp[head]));
     cur = *hs[head];
     const int64_t inflight = queued[head];
@@ -2148,10 +1617,6 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   }
   (void)hipFree(s->flag);
   (void)hipFree(s->dhist);
-  (void)hipFree(s->psync);
-  (void)hipFree(s->pgran);
-  (void)hipFree(s->pstamps);
-  (void)hipHostFree(s->herr);
   (void)hipStreamDestroy(s->stream);
   delete s;
   return LSPCG_OK;

@@ -33,11 +33,9 @@ def _random_spd(n, seed):
 SIZES = [63, 65, 257, 1000, 4097, 17000, 70000, 150000]
 
 
-MODES = {  # "multi": the multi-kernel schedules at every size; "small": n <= 2560 runs k_pcg_small;
-    # "persist": every size runs k_pcg_persist (the grid cap varies, so 1, 2 and 4 rows per thread)
-    "multi": {"LSPCG_SMALL_N": "0", "LSPCG_PERSIST_N": "0"},
-    "small": {"LSPCG_SMALL_N": "4096", "LSPCG_PERSIST_N": "0"},
-    "persist": {"LSPCG_SMALL_N": "0", "LSPCG_PERSIST_N": "100000000"},
+MODES = {  # "multi": the multi-kernel schedules at every size; "small": n <= 2560 runs k_pcg_small
+    "multi": {"LSPCG_SMALL_N": "0"},
+    "small": {"LSPCG_SMALL_N": "4096"},
 }
 
 
@@ -46,7 +44,6 @@ MODES = {  # "multi": the multi-kernel schedules at every size; "small": n <= 25
 def test_random_spd_pcg_parity(gpu_ctx, seed, mode, monkeypatch):
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
-    monkeypatch.setenv("LSPCG_PERSIST_WG", str([256, 61, 9][seed % 3]))
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
 
     rng = np.random.default_rng(100 + seed)

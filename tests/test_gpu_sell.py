@@ -78,14 +78,12 @@ def test_sell_skips_padding_with_inf(gpu_ctx):
         assert np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])
 
 
-def _v(no_sell="0", sell32="0", split="1", small="0", persist="0", wg="256"):
-    return {"LSPCG_NO_SELL": no_sell, "LSPCG_SELL32": sell32, "LSPCG_SPLIT_REDUCE": split, "LSPCG_SMALL_N": small,
-            "LSPCG_PERSIST_N": persist, "LSPCG_PERSIST_WG": wg}
+def _v(no_sell="0", sell32="0", split="1", small="0"):
+    return {"LSPCG_NO_SELL": no_sell, "LSPCG_SELL32": sell32, "LSPCG_SPLIT_REDUCE": split, "LSPCG_SMALL_N": small}
 
 
 VARIANTS = [_v(no_sell="1"), _v(sell32="1"), _v(), _v(split="0"),
-            _v(small="1000000"), _v(sell32="1", small="1000000"), _v(no_sell="1", small="1000000"),
-            _v(persist="100000000"), _v(sell32="1", persist="100000000", wg="2")]
+            _v(small="1000000"), _v(sell32="1", small="1000000"), _v(no_sell="1", small="1000000")]
 
 
 @pytest.mark.parametrize("precond", ["none", "diagonal", "ext_spai", "ext_spai_scaled"])
@@ -101,8 +99,7 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
     # CSR views (5 kernels); SELL int32 columns / 16-bit offsets (+ split group reductions vs
     # last-arriver reductions on the SELL 16-bit views); then the one-workgroup solve
     # (k_pcg_small) on the SELL copies and on the CSR views (LSPCG_NO_SELL=1), which every other
-    # variant has switched off; last the persistent solve (k_pcg_persist), one workgroup per CU
-    # and a 2-workgroup grid (several rows per thread)
+    # variant has switched off
     for env in VARIANTS:
         for k, v in env.items():
             monkeypatch.setenv(k, v)

@@ -42,7 +42,6 @@ SCHEDULES = {
     "split": {},
     "last-arriver": {"LSPCG_SPLIT_REDUCE": "0"},
     "csr-views": {"LSPCG_NO_SELL": "1"},
-    "persistent": {"LSPCG_PERSIST_N": "100000000"},
 }
 
 
