@@ -274,6 +274,62 @@ def c5_rows(rtol: float, concurrency: int = 4) -> dict:
     return out
 
 
+def config_rows() -> dict:
+    """BASELINE.md §2's other configurations beside the headline: C2 Poisson-2D 256² (rtol 1e-8),
+    C3 heat on the voxelised bunny (rtol 1e-6), C4 elasticity BSR 3×3 (rtol 1e-8) and C5 the 8
+    heat systems (rtol 1e-8, sum and max over the batch), each with the GNN-inferred L (seeded
+    random init) and ext_spai: the HIP solver (1 warm-up + median of 5 solves) and the reference's
+    scipy restatement on the same A, L, b (1 thread; 1 warm-up + median of 3; full solves, C4
+    bounded to 60 iterations per solve: its 2.5 k iterations take minutes on one core)."""
+    import scipy.sparse as sp
+    import torch
+
+    from oracle import linalg as O
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+    from learningsparsepreconditioner4gpu_amd.infer import synthetic_dataset
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    def one(sample, rtol, cpu_max_iter):
+        ws = SimpleInferenceWorkspace(node_features=sample.x.shape[1], edge_features=sample.edge_attr.shape[1],
+                                      block_size=sample.block_size, seed=0)
+        d = sample.to("cuda")
+        L, _ = ws.inference_step(d)
+        A = ws.system_matrix(d)
+        gt = d.mask.reshape(-1).to(torch.float64)
+        b = A.matvec(gt)
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", dtype=np.float64)
+        s.set_spai(L, ws.epsilon, block_size=L.block_size)
+        x = torch.zeros_like(b)
+        ts = []
+        for _ in range(6):
+            x.zero_()
+            it, conv, t = s.solve(b, x, rtol=rtol)
+            ts.append(t)
+        t_gpu = float(np.median(ts[1:]))
+        A_h, L_h = sp.csr_matrix(A.to_scipy()), sp.csr_matrix(L.to_scipy())
+        b_h = A_h @ gt.cpu().numpy()
+        M = O._Op(O.spai_operator(L_h, ws.epsilon), A_h.shape, np.float64)
+        mi = cpu_max_iter or A_h.shape[0]
+        cpu = cpu_rate(A_h, b_h, M, rtol, mi, 1, reps=3)
+        return {"n": A.n, "nnz": A.nnz, "iters": it, "converged": bool(conv), "gpu_ms": t_gpu * 1e3,
+                "gpu_it_per_s": it / t_gpu, "cpu_iters": cpu["iters_per_solve"], "cpu_s": cpu["median_s"],
+                "cpu_it_per_s": cpu["it_per_s"], "cpu_bounded": bool(cpu_max_iter)}
+
+    def wl(name):
+        A, mask, feats, bs, e2n = P.workload(name)
+        return make_sample(A, mask, node_features=feats, block_size=bs, use_edge_features_as_node_feature=e2n)
+
+    out = {"C2_poisson256": one(wl("poisson256"), 1e-8, 0), "C3_heat_bunny": one(wl("bunny"), 1e-6, 0),
+           "C4_elasticity": one(wl("elast"), 1e-8, 60)}
+    rows = [one(smp, 1e-8, 0) for smp in synthetic_dataset("heat_batch8")]
+    out["C5_heat_batch8"] = {
+        "systems": rows, "gpu_ms_sum": sum(r["gpu_ms"] for r in rows), "gpu_ms_max": max(r["gpu_ms"] for r in rows),
+        "cpu_s_sum": sum(r["cpu_s"] for r in rows), "cpu_s_max": max(r["cpu_s"] for r in rows)}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -287,6 +343,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="skip the none / diagonal / random-rhs time-to-rtol rows")
     ap.add_argument("--spmv-reps", type=int, default=30)
+    ap.add_argument("--configs", action="store_true",
+                    help="instead of the headline line: C2-C5 GPU rows beside the reference's scipy CPU path")
     args = ap.parse_args()
 
     import torch
@@ -296,6 +354,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
+    if args.configs:  # side table (BASELINE.md §2 configurations), rank 0 of a 1-GPU run only
+        print(json.dumps({"configs": config_rows(), "cpu": host_cpu(), "cpu_threads": 1}), flush=True)
+        return
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
