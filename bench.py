@@ -353,12 +353,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per local rank; more ranks than GPUs (a gloo rehearsal on one GPU) share them
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if args.configs:  # side table (BASELINE.md §2 configurations), rank 0 of a 1-GPU run only
         print(json.dumps({"configs": config_rows(), "cpu": host_cpu(), "cpu_threads": 1}), flush=True)
         return
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL over xGMI; LSPCG_DIST_BACKEND=gloo rehearses several ranks on ONE GPU (RCCL refuses that)
+        backend = os.environ.get("LSPCG_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": torch.device("cuda", local)} if backend == "nccl" else {}))
 
     from learningsparsepreconditioner4gpu_amd import problems as P
     from learningsparsepreconditioner4gpu_amd.data import make_sample

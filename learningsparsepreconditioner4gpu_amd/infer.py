@@ -238,9 +238,13 @@ def main(argv=None):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per local rank; more ranks than GPUs (a gloo rehearsal on one GPU) share them
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL over xGMI; LSPCG_DIST_BACKEND=gloo rehearses several ranks on ONE GPU (RCCL refuses that)
+        backend = os.environ.get("LSPCG_DIST_BACKEND", "nccl")
+        dist.init_process_group(backend, **({"device_id": torch.device("cuda", local)} if backend == "nccl" else {}))
     if args.folder:
         samples = folder_dataset(args.folder, args.block_size, args.fixed_topology, args.shared_features,
                                  not args.no_node_features, args.edge_to_node, args.normalize)
