@@ -209,6 +209,8 @@ class DistributedPCG:
         self.tdtype = torch.float64 if self.np_dtype == np.float64 else torch.float32
         self.ctx = Context.get(device)
         self.bounds = partition_rows(A.indptr, self.world)
+        if any(b1 <= b0 for b0, b1 in zip(self.bounds, self.bounds[1:])):
+            raise ValueError(f"{self.world} ranks for {self.n} rows: every rank must own at least one row")
         self.plan = build_plan(mats, self.bounds, self.rank)
         p = self.plan
         self._mats = [DeviceMatrix.from_scipy(local_matrix(M, p), dtype=dtype, ctx=self.ctx, keep_order=True)

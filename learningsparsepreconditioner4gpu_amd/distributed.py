@@ -118,7 +118,11 @@ def run_sharded_concurrent(n_items: int, weights: Sequence[float], prepare: Call
     mine = my_items(weights, rank, world)
     k = max(1, int(concurrency))
     local: List[SolveRecord] = []
-    with ThreadPoolExecutor(k) as ex:
+    # the device this rank selected is per-thread state: the pool's threads select it too
+    init, args = (), ()
+    if torch.cuda.is_available():
+        init, args = torch.cuda.set_device, (torch.cuda.current_device(),)
+    with ThreadPoolExecutor(k, initializer=init or None, initargs=args) as ex:
         for w0 in range(0, len(mine), k):
             batch = [prepare(i) for i in mine[w0:w0 + k]]
             local.extend(ex.map(finish, batch))

@@ -185,5 +185,6 @@ def solve_many(jobs, rtol: float = 1e-6, max_iter: int = 0, concurrency: int = 4
         return [s.solve(b, x, rtol, max_iter) for s, b, x in jobs]
     from concurrent.futures import ThreadPoolExecutor
 
-    with ThreadPoolExecutor(min(int(concurrency), len(jobs))) as ex:
+    dev = jobs[0][0].ctx.device  # the pool's threads select the solvers' device (per-thread state)
+    with ThreadPoolExecutor(min(int(concurrency), len(jobs)), initializer=torch.cuda.set_device, initargs=(dev,)) as ex:
         return list(ex.map(lambda j: j[0].solve(j[1], j[2], rtol, max_iter), jobs))

@@ -60,6 +60,21 @@ def test_world1_matches_oracle_and_single_gpu(gpu_ctx, kind, precond):
     np.testing.assert_allclose(x, xs.cpu().numpy(), rtol=0, atol=1e-12 * np.abs(x_o).max())
 
 
+def test_world1_fp32(gpu_ctx):
+    """fp32 vectors and matrices (the solver's LSPCG_F32 path): the oracle's fp32 scipy cg with
+    correctly rounded dots, counts equal, x within the fp32 tolerance 1e-5."""
+    from learningsparsepreconditioner4gpu_amd.dist_pcg import DistributedPCG
+
+    A, L, b = _system("poisson")
+    d = DistributedPCG(A, L, EPS, dtype=np.float32)
+    it, conv, x = d.solve(b, rtol=1e-5)
+    ps = O.spai_operator(L.astype(np.float32), EPS)
+    it_o, x_o, _ = O.pcg(A.astype(np.float32), b.astype(np.float32), ps, rtol=1e-5, dot="exact", dtype=np.float32)
+    assert conv and abs(it - it_o) <= 1, (it, it_o)
+    x = d.gather_solution(x)
+    assert np.linalg.norm(x - x_o) <= 1e-5 * np.linalg.norm(x_o)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
