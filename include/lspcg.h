@@ -155,6 +155,27 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
 int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, double* kernel_ms, int* nk);
 int lspcg_solver_destroy(lspcg_solver* s);
 
+/* ---- batched lockstep ext_spai PCG over independent systems (infer.py:278-331 solves its samples
+ * one after another, each a get_pcg_iter_time call, validate.py:89-121; this solves a window of
+ * them with every launch covering all systems -- DESIGN.md §6).  Each system keeps scipy cg's
+ * recurrence, its own scalars, top-of-loop test and iteration count: the result per system is
+ * what lspcg_solver_solve returns for it alone (count and history equal; iterate within the
+ * compensated dots' rounding, same bits in practice).  A[k], L[k]: nsys >= 1 matrices of one
+ * dtype and block size (L[k] the ext_spai factor of A[k]); the handles must outlive the batch
+ * only until lspcg_batch_create returns (their entries are copied into a block-diagonal system
+ * whose per-system row ranges are padded to whole 256-row workgroup tiles).
+ * LSPCG_ERR_UNSUPPORTED when a SELL view cannot be built (irregular rows): solve one by one. */
+typedef struct lspcg_batch lspcg_batch;
+int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, const lspcg_mat* const* L,
+                       double epsilon, lspcg_batch** out);
+/* b[k], x[k]: device vectors of system k (x in: x0, out: solution).  max_iter <= 0: each
+ * system's own n.  iters[k], status[k] (LSPCG_OK converged / LSPCG_NOT_CONVERGED) per system;
+ * res_hist (nullable): per-system host arrays of length max_iter_k + 2 (or NULL entries);
+ * t_solve_ms = device time of the whole batch.  Returns LSPCG_OK when every system converged. */
+int lspcg_batch_solve(lspcg_batch* bt, const void* const* b, void* const* x, double rtol, int64_t max_iter,
+                      int64_t* iters, int32_t* status, double* const* res_hist, double* t_solve_ms);
+int lspcg_batch_destroy(lspcg_batch* bt);
+
 /* ---- CSR assembly with Dirichlet masking (to_csr_cpu on device) ----
  * edge_index: device int64 [2,E] (row-major sorted, duplicate free -- checked);
  * blocks: device [E,bs,bs] of in_dtype; mask: device [nb*bs] of mask_dtype or NULL.

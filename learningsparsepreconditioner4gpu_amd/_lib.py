@@ -61,6 +61,9 @@ SIGNATURES = {
     "lspcg_solver_solve": (C.c_int, [vp, vp, vp, C.c_double, C.c_int64, p_i64, p_f64, p_f64]),
     "lspcg_solver_time_kernels": (C.c_int, [vp, vp, C.c_int64, p_f64, C.POINTER(C.c_int)]),
     "lspcg_solver_destroy": (C.c_int, [vp]),
+    "lspcg_batch_create": (C.c_int, [vp, C.c_int, pp, pp, C.c_double, pp]),
+    "lspcg_batch_solve": (C.c_int, [vp, pp, pp, C.c_double, C.c_int64, p_i64, p_i32, C.POINTER(p_f64), p_f64]),
+    "lspcg_batch_destroy": (C.c_int, [vp]),
     "lspcg_assemble": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int, vp, vp, C.c_int, vp, C.c_int, C.c_int,
                                  C.c_int, pp]),
     "lspcg_gnn_create": (C.c_int, [vp, C.POINTER(lspcg_gnn_desc), vp, C.c_int64, pp]),

@@ -1623,3 +1623,526 @@ int lspcg_solver_destroy(lspcg_solver* s) {
 }
 
 }  // extern "C"
+
+// ==== batched lockstep ext_spai PCG (lspcg_batch_*) ===========================
+// A window of independent systems is laid out block-diagonally, every system's rows padded to
+// whole SpMV row tiles (256 block rows), and ONE launch per phase covers all of them: the split
+// schedule's five launches (KA, KB, UP, KC, UR) with
+//   * one row tile per workgroup (launch_spmv_sell_cfg one_tile_per_wg), so a workgroup's dot
+//     partial is its tile's and its prologue tests the tile's own system (done systems' tiles
+//     leave at once);
+//   * per-tile dot partials (grid_partial_groups with gsz = 1: no tickets, no last arriver);
+//   * elementwise launches of one 256-row tile per workgroup that sum their system's tile
+//     partials (group_sum_dd over the system's tile range) and keep that system's scalars; the
+//     first tile of a system is the only writer of its PcgState.
+// Padding rows are empty: they stay 0 in every vector and add exact zeros to the dots.
+namespace lspcg {
+
+struct BatchMap {
+  const int32_t* etile_sys;  // [n / 256] system of each 256-row elementwise tile
+  const int32_t* tile0;      // [nsys + 1] first SpMV row tile (256 block rows) of each system
+  int bs;                    // block size: SpMV tile b covers elementwise tiles bs*b .. bs*b + bs - 1
+};
+
+struct ProTile {
+  const PcgState* S;
+  BatchMap m;
+  __device__ __forceinline__ bool exit() const { return S[m.etile_sys[int64_t(blockIdx.x) * m.bs]].done != 0; }
+};
+
+// init: r_0 = b - A x0 ; per-tile partials of ‖r_0‖², ‖b‖²
+template <typename T>
+struct EpiResidTile {
+  static constexpr int NDOT = 2;
+  static constexpr bool GROUPS = true;
+  T* r;
+  const T* b;
+  double* partials;
+  unsigned* ticket;
+  double* group_out;
+  int gsz;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T bi = gld(b + i);
+    const T ri = bi - s;
+    gst(r + i, ri);
+    dd_fma(dots[0], double(ri), double(ri));
+    dd_fma(dots[1], double(bi), double(bi));
+  }
+  __device__ __forceinline__ void fin(const double*) const {}
+};
+
+// one workgroup per system: the init state from the system's tile partials (EpiResid::fin)
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_batch_init(PcgState* S, const int32_t* __restrict__ tile0,
+                                                         const double* __restrict__ gi) {
+  const int sys = blockIdx.x;
+  const int t0 = tile0[sys], t1 = tile0[sys + 1];
+  double v[2];
+  group_sum_dd<2>(gi + size_t(t0) * 4, t1 - t0, v);
+  if (threadIdx.x) return;
+  PcgState* St = S + sys;
+  St->rr = round_to<T>(v[0]);
+  St->bb = round_to<T>(v[1]);
+  const double bn = double(tsqrt<T>(T(St->bb)));
+  St->atol = fmax(0.0, St->rtol * bn);
+  St->rho = St->rr;
+  St->alpha = 0.0;
+  St->iter = 0;
+  St->done = (bn == 0.0) ? 1 : 0;
+  if (St->hist) St->hist[0] = double(tsqrt<T>(T(St->rr)));
+}
+
+// UP of the split schedule (k_update_p_g) for the tile's system
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_batch_update_p(BatchMap m, PcgState* S, const double* __restrict__ gz,
+                                                             const T* __restrict__ z, T* __restrict__ p,
+                                                             T* __restrict__ x) {
+  const int sys = m.etile_sys[blockIdx.x];
+  PcgState* St = S + sys;
+  if (St->done) return;
+  const int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  const T zi = z[i], pi = p[i], xi = x[i];
+  const int t0 = m.tile0[sys], t1 = m.tile0[sys + 1];
+  const int64_t k = St->iter;
+  double v[2];
+  group_sum_dd<2>(gz + size_t(t0) * 4, t1 - t0, v);
+  const double rho = round_to<T>(v[0]);
+  const double rr = k > 0 ? round_to<T>(v[1]) : St->rr;
+  int code = 0;
+  if (k >= St->max_iter) {
+    code = 2;
+  } else {
+    const double rn = double(tsqrt<T>(T(rr)));
+    if (rn < St->atol) code = 1;
+    else if (!(rn == rn) || rn == INFINITY) code = 3;
+  }
+  if (int64_t(blockIdx.x) == int64_t(t0) * m.bs && threadIdx.x == 0) {
+    if (k > 0) {
+      St->rr = rr;
+      if (St->hist) St->hist[k] = double(tsqrt<T>(T(rr)));
+    }
+    if (code) St->done = code;
+  }
+  if (code) return;
+  const bool first = k == 0;
+  const T beta = first ? T(0) : T(rho) / T(St->rho);
+  const T alpha = T(St->alpha);
+  if (!first) x[i] = xi + alpha * pi;
+  p[i] = first ? zi : (pi * beta) + zi;
+}
+
+// UR of the split schedule (k_update_r_g) for the tile's system
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_batch_update_r(BatchMap m, PcgState* S, const double* __restrict__ gz,
+                                                             const double* __restrict__ gq, const T* __restrict__ q,
+                                                             T* __restrict__ r) {
+  const int sys = m.etile_sys[blockIdx.x];
+  PcgState* St = S + sys;
+  if (St->done) return;
+  const int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  const T ri = r[i], qi = q[i];
+  const int t0 = m.tile0[sys], t1 = m.tile0[sys + 1];
+  double vz[2], vq[1];
+  group_sum_dd<2>(gz + size_t(t0) * 4, t1 - t0, vz);
+  group_sum_dd<1>(gq + size_t(t0) * 2, t1 - t0, vq);
+  const double rho = round_to<T>(vz[0]);
+  const double pq = round_to<T>(vq[0]);
+  const T alpha = T(rho) / T(pq);
+  if (int64_t(blockIdx.x) == int64_t(t0) * m.bs && threadIdx.x == 0) {
+    St->rho_prev = St->rho;
+    St->rho = rho;
+    St->pq = pq;
+    St->alpha = double(alpha);
+    St->iter = St->iter + 1;
+  }
+  r[i] = ri - alpha * qi;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_batch_x_fixup(BatchMap m, const PcgState* S, const T* __restrict__ p,
+                                                            T* __restrict__ x) {
+  const PcgState* St = S + m.etile_sys[blockIdx.x];
+  if (St->iter < 1 || St->bb == 0.0) return;
+  const int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  x[i] = x[i] + T(St->alpha) * p[i];
+}
+
+// block-diagonal assembly: rows [0, cnt) of one system at its row offset (rows >= nb empty)
+__global__ void k_cat_rowptr(int64_t cnt, int64_t nb, const int32_t* __restrict__ rp, int32_t e0,
+                             int32_t* __restrict__ out) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < cnt; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = rp[i < nb ? i : nb] + e0;
+}
+__global__ void k_cat_colind(int64_t nnz, const int32_t* __restrict__ c, int32_t off, int32_t* __restrict__ out) {
+  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < nnz; k += int64_t(gridDim.x) * blockDim.x)
+    out[k] = c[k] + off;
+}
+
+}  // namespace lspcg
+
+struct lspcg_batch {
+  lspcg_ctx* ctx = nullptr;
+  int nsys = 0;
+  int bs = 1;
+  int dtype = LSPCG_F64;
+  lspcg_mat* Acat = nullptr;
+  lspcg_mat* Lcat = nullptr;
+  lspcg_solver* s = nullptr;  // solver of the block-diagonal system: views, vectors, stream
+  std::vector<int64_t> off, n;  // scalar row offset and size of every system
+  int64_t ntot = 0;             // padded scalar rows
+  int32_t* etile_sys = nullptr;
+  int32_t* tile0 = nullptr;
+  double* gi = nullptr;  // per-tile partials: init (2 dots), KB (2 dots), KC (1 dot), DD each
+  double* gz = nullptr;
+  double* gq = nullptr;
+  PcgState* S = nullptr;
+  PcgState* hS = nullptr;  // pinned: 2 poll slots x nsys
+  double* dhist = nullptr;
+  int64_t dhist_cap = 0;
+  std::map<int, hipGraphExec_t> graphs;
+  std::map<int, hipGraph_t> graph_defs;
+};
+
+namespace lspcg {
+
+static BatchMap batch_map(const lspcg_batch* bt) { return BatchMap{bt->etile_sys, bt->tile0, bt->bs}; }
+
+// SpMV of iteration view w over the block-diagonal system, one row tile per workgroup
+template <typename T, class Pro, class Epi>
+static int launch_it_tiles(lspcg_solver* s, int w, const T* x, Pro pro, Epi epi, hipStream_t st) {
+  const SellPattern* P = s->sp[w];
+  if (!P) return LSPCG_ERR_UNSUPPORTED;
+  if constexpr (sizeof(T) == 8) {
+    if (s->svd[w] == LSPCG_F32) {
+      launch_spmv_sell_cfg<T, float>(*P, s->sv[w], GatherVec<T>{x}, pro, epi, st, true);
+      return LSPCG_OK;
+    }
+  }
+  launch_spmv_sell_cfg<T, T>(*P, s->sv[w], GatherVec<T>{x}, pro, epi, st, true);
+  return LSPCG_OK;
+}
+
+template <typename T>
+static int enqueue_batch_init(lspcg_batch* bt, hipStream_t st) {
+  lspcg_solver* s = bt->s;
+  int rc = launch_it_tiles<T>(s, 0, static_cast<const T*>(s->x), ProNone{},
+                              EpiResidTile<T>{static_cast<T*>(s->r), static_cast<const T*>(s->b), nullptr, nullptr,
+                                              bt->gi, 1},
+                              st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_batch_init<T>, dim3(bt->nsys), dim3(kThreads), 0, st, bt->S,
+                     static_cast<const int32_t*>(bt->tile0), static_cast<const double*>(bt->gi));
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+template <typename T>
+static int enqueue_batch_iteration(lspcg_batch* bt, hipStream_t st) {
+  lspcg_solver* s = bt->s;
+  T* x = static_cast<T*>(s->x);
+  T* r = static_cast<T*>(s->r);
+  T* z = static_cast<T*>(s->z);
+  T* t = static_cast<T*>(s->t);
+  T* p = static_cast<T*>(s->p);
+  T* q = static_cast<T*>(s->q);
+  const BatchMap m = batch_map(bt);
+  const ProTile pro{bt->S, m};
+  const dim3 eg(unsigned(bt->ntot / kThreads));
+  int rc = launch_it_tiles<T>(s, 2, static_cast<const T*>(r), pro, EpiT<T, false>{t, nullptr}, st);
+  if (!rc)
+    rc = launch_it_tiles<T>(s, 1, static_cast<const T*>(t), pro,
+                            EpiZG<T, false>{z, r, nullptr, T(s->eps), nullptr, nullptr, bt->gz, 1}, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_batch_update_p<T>, eg, dim3(kThreads), 0, st, m, bt->S, static_cast<const double*>(bt->gz),
+                     static_cast<const T*>(z), p, x);
+  rc = launch_it_tiles<T>(s, 0, static_cast<const T*>(p), pro, EpiQG<T>{q, p, nullptr, nullptr, bt->gq, 1}, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_batch_update_r<T>, eg, dim3(kThreads), 0, st, m, bt->S, static_cast<const double*>(bt->gz),
+                     static_cast<const double*>(bt->gq), static_cast<const T*>(q), r);
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+static int get_batch_graph(lspcg_batch* bt, int chunk, hipGraphExec_t* out) {
+  auto it = bt->graphs.find(chunk);
+  if (it != bt->graphs.end()) {
+    *out = it->second;
+    return LSPCG_OK;
+  }
+  hipStream_t st = bt->s->stream;
+  hipGraph_t g = nullptr;
+  LSPCG_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  int rc = LSPCG_OK;
+  for (int i = 0; i < chunk && rc == LSPCG_OK; ++i)
+    rc = bt->dtype == LSPCG_F64 ? enqueue_batch_iteration<double>(bt, st) : enqueue_batch_iteration<float>(bt, st);
+  hipError_t e = hipStreamEndCapture(st, &g);
+  if (rc) return rc;
+  LSPCG_HIP(e);
+  hipGraphExec_t ex = nullptr;
+  LSPCG_HIP(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  bt->graphs[chunk] = ex;
+  bt->graph_defs[chunk] = g;
+  *out = ex;
+  return LSPCG_OK;
+}
+
+// block-diagonal copy of M[0..nsys) with system k's block rows starting at brow[k] (padded)
+static int cat_matrices(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* M, const std::vector<int64_t>& brow,
+                        lspcg_mat** out) {
+  const int bs = M[0]->block_size;
+  int64_t nnz = 0;
+  for (int k = 0; k < nsys; ++k) nnz += M[k]->nnzb;
+  LSPCG_CHECK(nnz < (int64_t(1) << 31), LSPCG_ERR_ARG, "batch: more than 2^31 stored blocks in the window");
+  lspcg_mat* C = nullptr;
+  if (int rc = mat_alloc(ctx, brow[nsys], nnz, bs, M[0]->dtype, &C)) return rc;
+  hipStream_t st = ctx->stream;
+  const size_t vb = (M[0]->dtype == LSPCG_F32 ? 4 : 8) * size_t(bs) * bs;
+  int64_t e0 = 0;
+  for (int k = 0; k < nsys; ++k) {
+    const int64_t cnt = brow[k + 1] - brow[k] + (k == nsys - 1 ? 1 : 0);
+    hipLaunchKernelGGL(k_cat_rowptr, dim3(unsigned(std::min<int64_t>((cnt + 255) / 256, 1024))), dim3(256), 0, st, cnt,
+                       M[k]->nb, static_cast<const int32_t*>(M[k]->rowptr), int32_t(e0), C->rowptr + brow[k]);
+    if (M[k]->nnzb) {
+      hipLaunchKernelGGL(k_cat_colind, dim3(unsigned(std::min<int64_t>((M[k]->nnzb + 255) / 256, 1024))), dim3(256), 0,
+                         st, M[k]->nnzb, static_cast<const int32_t*>(M[k]->colind), int32_t(brow[k]), C->colind + e0);
+      LSPCG_HIP(hipMemcpyAsync(static_cast<char*>(C->vals) + vb * e0, M[k]->vals, vb * M[k]->nnzb,
+                               hipMemcpyDeviceToDevice, st));
+    }
+    e0 += M[k]->nnzb;
+  }
+  LSPCG_HIP(hipGetLastError());
+  LSPCG_HIP(hipStreamSynchronize(st));
+  *out = C;
+  return LSPCG_OK;
+}
+
+}  // namespace lspcg
+
+extern "C" {
+
+int lspcg_batch_destroy(lspcg_batch* bt) {
+  if (!bt) return LSPCG_OK;
+  (void)hipSetDevice(bt->ctx->device);
+  if (bt->s) (void)hipStreamSynchronize(bt->s->stream);
+  for (auto& kv : bt->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : bt->graph_defs) (void)hipGraphDestroy(kv.second);
+  if (bt->s) lspcg_solver_destroy(bt->s);
+  if (bt->Acat) lspcg_mat_destroy(bt->Acat);
+  if (bt->Lcat) lspcg_mat_destroy(bt->Lcat);
+  for (void* v : {(void*)bt->etile_sys, (void*)bt->tile0, (void*)bt->gi, (void*)bt->gz, (void*)bt->gq,
+                  (void*)bt->S, (void*)bt->dhist})
+    (void)hipFree(v);
+  (void)hipHostFree(bt->hS);
+  delete bt;
+  return LSPCG_OK;
+}
+
+int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, const lspcg_mat* const* L,
+                       double epsilon, lspcg_batch** out) {
+  LSPCG_CHECK(ctx && A && L && out && nsys >= 1, LSPCG_ERR_ARG, "batch_create: NULL argument or nsys < 1");
+  for (int k = 0; k < nsys; ++k) {
+    LSPCG_CHECK(A[k] && L[k], LSPCG_ERR_ARG, "batch_create: NULL matrix " + std::to_string(k));
+    LSPCG_CHECK(A[k]->dtype == A[0]->dtype && L[k]->dtype == A[0]->dtype, LSPCG_ERR_ARG,
+                "batch_create: every A and L must have one dtype");
+    LSPCG_CHECK(A[k]->block_size == A[0]->block_size && L[k]->block_size == A[0]->block_size, LSPCG_ERR_ARG,
+                "batch_create: every A and L must have one block size");
+    LSPCG_CHECK(L[k]->n == A[k]->n && A[k]->n >= 1, LSPCG_ERR_ARG,
+                "batch_create: system " + std::to_string(k) + ": L and A differ in size or are empty");
+  }
+  LSPCG_HIP(hipSetDevice(ctx->device));
+  std::unique_ptr<lspcg_batch, int (*)(lspcg_batch*)> bt(new lspcg_batch(), lspcg_batch_destroy);
+  bt->ctx = ctx;
+  bt->nsys = nsys;
+  bt->bs = A[0]->block_size;
+  bt->dtype = A[0]->dtype;
+  // block-row offsets, each system padded to whole SpMV row tiles (kSellWG block rows)
+  std::vector<int64_t> brow(nsys + 1, 0);
+  for (int k = 0; k < nsys; ++k) brow[k + 1] = brow[k] + (A[k]->nb + kSellWG - 1) / kSellWG * kSellWG;
+  LSPCG_CHECK(brow[nsys] * bt->bs < (int64_t(1) << 31), LSPCG_ERR_ARG, "batch_create: window exceeds 2^31 rows");
+  for (int k = 0; k < nsys; ++k) {
+    bt->off.push_back(brow[k] * bt->bs);
+    bt->n.push_back(A[k]->n);
+  }
+  bt->ntot = brow[nsys] * bt->bs;
+  if (int rc = cat_matrices(ctx, nsys, A, brow, &bt->Acat)) return rc;
+  if (int rc = cat_matrices(ctx, nsys, L, brow, &bt->Lcat)) return rc;
+  if (int rc = lspcg_solver_create(ctx, bt->Acat, LSPCG_PRECOND_EXT_SPAI, &bt->s)) return rc;
+  if (int rc = lspcg_solver_set_spai(bt->s, bt->Lcat, epsilon, nullptr)) return rc;
+  LSPCG_CHECK(bt->s->sp[0] && bt->s->sp[1] && bt->s->sp[2], LSPCG_ERR_UNSUPPORTED,
+              "batch_create: no SELL view of the block-diagonal system (irregular rows): solve one by one");
+  // tile maps
+  const int64_t ntiles = brow[nsys] / kSellWG;
+  std::vector<int32_t> esys(size_t(bt->ntot / kThreads)), t0(nsys + 1);
+  for (int k = 0; k < nsys; ++k) {
+    t0[k] = int32_t(brow[k] / kSellWG);
+    for (int64_t e = bt->off[k] / kThreads; e < (bt->off[k] + (brow[k + 1] - brow[k]) * bt->bs) / kThreads; ++e)
+      esys[size_t(e)] = k;
+  }
+  t0[nsys] = int32_t(ntiles);
+  LSPCG_HIP(hipMalloc(&bt->etile_sys, sizeof(int32_t) * esys.size()));
+  LSPCG_HIP(hipMalloc(&bt->tile0, sizeof(int32_t) * t0.size()));
+  LSPCG_HIP(hipMemcpy(bt->etile_sys, esys.data(), sizeof(int32_t) * esys.size(), hipMemcpyHostToDevice));
+  LSPCG_HIP(hipMemcpy(bt->tile0, t0.data(), sizeof(int32_t) * t0.size(), hipMemcpyHostToDevice));
+  LSPCG_HIP(hipMalloc(&bt->gi, sizeof(double) * 4 * ntiles));
+  LSPCG_HIP(hipMalloc(&bt->gz, sizeof(double) * 4 * ntiles));
+  LSPCG_HIP(hipMalloc(&bt->gq, sizeof(double) * 2 * ntiles));
+  LSPCG_HIP(hipMalloc(&bt->S, sizeof(PcgState) * nsys));
+  LSPCG_HIP(hipHostMalloc(&bt->hS, 2 * sizeof(PcgState) * nsys, hipHostMallocDefault));
+  *out = bt.release();
+  return LSPCG_OK;
+}
+
+int lspcg_batch_solve(lspcg_batch* bt, const void* const* b, void* const* x, double rtol, int64_t max_iter,
+                      int64_t* iters, int32_t* status, double* const* res_hist, double* t_solve_ms) {
+  LSPCG_CHECK(bt && b && x && iters && status, LSPCG_ERR_ARG, "batch_solve: NULL argument");
+  const int ns = bt->nsys;
+  for (int k = 0; k < ns; ++k) LSPCG_CHECK(b[k] && x[k], LSPCG_ERR_ARG, "batch_solve: NULL vector " + std::to_string(k));
+  lspcg_solver* s = bt->s;
+  LSPCG_HIP(hipSetDevice(bt->ctx->device));
+  hipStream_t st = s->stream;
+  const size_t es = esize(bt->dtype);
+  std::vector<int64_t> mi(ns), hoff(ns + 1, 0);
+  for (int k = 0; k < ns; ++k) {
+    mi[k] = max_iter > 0 ? max_iter : bt->n[k];
+    hoff[k + 1] = hoff[k] + ((res_hist && res_hist[k]) ? mi[k] + 2 : 0);
+  }
+  if (hoff[ns] > bt->dhist_cap) {
+    LSPCG_HIP(hipStreamSynchronize(st));
+    (void)hipFree(bt->dhist);
+    bt->dhist = nullptr;
+    bt->dhist_cap = 0;
+    LSPCG_HIP(hipMalloc(&bt->dhist, sizeof(double) * hoff[ns]));
+    bt->dhist_cap = hoff[ns];
+  }
+  LSPCG_HIP(hipEventRecord(s->ev_in, bt->ctx->stream));
+  LSPCG_HIP(hipStreamWaitEvent(st, s->ev_in, 0));
+  LSPCG_HIP(hipEventRecord(s->ev_t0, st));
+  char* cb = static_cast<char*>(s->b);
+  char* cx = static_cast<char*>(s->x);
+  for (int k = 0; k < ns; ++k) {  // padding rows stay 0 (zeroed at creation, never written)
+    LSPCG_HIP(hipMemcpyAsync(cb + es * bt->off[k], b[k], es * bt->n[k], hipMemcpyDeviceToDevice, st));
+    LSPCG_HIP(hipMemcpyAsync(cx + es * bt->off[k], x[k], es * bt->n[k], hipMemcpyDeviceToDevice, st));
+  }
+  for (int k = 0; k < ns; ++k) {
+    PcgState init{};
+    init.rtol = rtol;
+    init.eps = s->eps;
+    init.hist = (res_hist && res_hist[k]) ? bt->dhist + hoff[k] : nullptr;
+    init.max_iter = mi[k];
+    bt->hS[k] = init;
+  }
+  LSPCG_HIP(hipMemcpyAsync(bt->S, bt->hS, sizeof(PcgState) * ns, hipMemcpyHostToDevice, st));
+  int rc = bt->dtype == LSPCG_F64 ? enqueue_batch_init<double>(bt, st) : enqueue_batch_init<float>(bt, st);
+  if (rc) return rc;
+
+  // the poll loop of lspcg_solver_solve over every system's state: run while any system runs;
+  // chunks sized from the slowest system's predicted remaining iterations
+  constexpr int max_chunk = 32;
+  PcgState* const hs[2] = {bt->hS, bt->hS + ns};
+  const hipEvent_t evp[2] = {s->ev_poll, s->ev_poll2};
+  int64_t queued[2] = {0, 0};
+  int head = 0, npend = 0;
+  auto post = [&]() -> int {
+    const int k = (head + npend) & 1;
+    LSPCG_HIP(hipMemcpyAsync(hs[k], bt->S, sizeof(PcgState) * ns, hipMemcpyDeviceToHost, st));
+    LSPCG_HIP(hipEventRecord(evp[k], st));
+    queued[k] = 0;
+    ++npend;
+    return LSPCG_OK;
+  };
+  auto launch = [&](int c) -> int {
+    hipGraphExec_t ex = nullptr;
+    int r = get_batch_graph(bt, c, &ex);
+    if (r) return r;
+    LSPCG_HIP(hipGraphLaunch(ex, st));
+    for (int j = 0; j < npend; ++j) queued[(head + j) & 1] += c;
+    return post();
+  };
+  rc = post();
+  if (!rc) rc = launch(4);
+  if (rc) return rc;
+  std::vector<PcgState> cur(ns);
+  std::vector<int64_t> last_it(ns, 0);
+  std::vector<double> last_rr(ns, -1.0);
+  int chunk = 4;
+  for (;;) {
+    LSPCG_HIP(hipEventSynchronize(evp[head]));
+    std::copy(hs[head], hs[head] + ns, cur.begin());
+    const int64_t inflight = queued[head];
+    head ^= 1;
+    --npend;
+    int64_t rem = 0;  // largest predicted remaining count over the running systems
+    bool unknown = false, running = false;
+    for (int k = 0; k < ns; ++k) {
+      const PcgState& c = cur[k];
+      if (c.done) continue;
+      running = true;
+      int64_t rk = -1;
+      if (last_rr[k] > 0 && c.iter > last_it[k] && c.rr > 0 && c.rr < last_rr[k]) {
+        const double rate = std::log(c.rr / last_rr[k]) / double(c.iter - last_it[k]);
+        const double need = std::log((c.atol * c.atol) / c.rr) / rate;
+        rk = need > 0 ? int64_t(std::ceil(need)) : 1;
+        rk = std::max<int64_t>(1, std::min<int64_t>(rk, mi[k] - c.iter));
+      }
+      if (c.iter > last_it[k] || last_rr[k] < 0) {
+        last_it[k] = c.iter;
+        last_rr[k] = c.rr;
+      }
+      if (rk < 0) unknown = true;
+      else rem = std::max(rem, rk);
+    }
+    if (!running) break;
+    if (unknown) rem = -1;
+    if (rem >= 0) {
+      const int64_t more = rem - inflight;
+      if (more <= 0) {
+        if (npend == 0) rc = launch(1);
+        if (rc) return rc;
+        continue;
+      }
+      int c = 1;
+      while (c * 2 <= more && c < max_chunk) c *= 2;
+      chunk = c;
+    } else {
+      chunk = std::min(max_chunk, chunk * 2);
+    }
+    rc = launch(chunk);
+    if (rc) return rc;
+  }
+  const BatchMap m = batch_map(bt);
+  if (bt->dtype == LSPCG_F64)
+    hipLaunchKernelGGL(k_batch_x_fixup<double>, dim3(unsigned(bt->ntot / kThreads)), dim3(kThreads), 0, st, m, bt->S,
+                       static_cast<const double*>(s->p), static_cast<double*>(s->x));
+  else
+    hipLaunchKernelGGL(k_batch_x_fixup<float>, dim3(unsigned(bt->ntot / kThreads)), dim3(kThreads), 0, st, m, bt->S,
+                       static_cast<const float*>(s->p), static_cast<float*>(s->x));
+  LSPCG_HIP(hipGetLastError());
+  for (int k = 0; k < ns; ++k) {
+    const char* src = (cur[k].bb == 0.0) ? cb : cx;  // scipy returns b when ‖b‖ = 0
+    LSPCG_HIP(hipMemcpyAsync(x[k], src + es * bt->off[k], es * bt->n[k], hipMemcpyDeviceToDevice, st));
+  }
+  LSPCG_HIP(hipEventRecord(s->ev_t1, st));
+  LSPCG_HIP(hipEventRecord(s->ev_out, st));
+  LSPCG_HIP(hipStreamWaitEvent(bt->ctx->stream, s->ev_out, 0));
+  LSPCG_HIP(hipEventSynchronize(s->ev_t1));
+  float ms = 0.f;
+  LSPCG_HIP(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1));
+  if (t_solve_ms) *t_solve_ms = ms;
+  bool all = true;
+  for (int k = 0; k < ns; ++k) {
+    const PcgState& f = cur[k];
+    const int64_t it = (f.done == 3) ? mi[k] : f.iter;
+    iters[k] = it;
+    status[k] = f.done == 1 ? LSPCG_OK : LSPCG_NOT_CONVERGED;
+    all = all && f.done == 1;
+    if (res_hist && res_hist[k]) {
+      const int64_t cnt = std::min<int64_t>(f.iter, mi[k]) + 1;
+      LSPCG_HIP(hipMemcpy(res_hist[k], bt->dhist + hoff[k], sizeof(double) * cnt, hipMemcpyDeviceToHost));
+      for (int64_t j = cnt; j <= it; ++j) res_hist[k][j] = NAN;
+    }
+  }
+  return all ? LSPCG_OK : LSPCG_NOT_CONVERGED;
+}
+
+}  // extern "C"

@@ -300,9 +300,12 @@ inline int64_t sell_grid(const SellPattern& P, bool reducing) {
 }
 
 template <typename T, typename VT, typename CT, int TH, class Pro, class Gx, class Epi>
-inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
+inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
+                                bool one_tile_per_wg = false) {
   int64_t grid = (P.nb + TH - 1) / TH;  // row tiles: TH scalar rows (bs 1) or TH block rows (bs 3)
-  grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
+  // one_tile_per_wg (batched solves): workgroup b owns exactly row tile b, so its dot partial is
+  // that tile's and its prologue may test the tile's own system
+  if (!one_tile_per_wg) grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
   SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
   // compact-value kernels: registers for 6 workgroups per CU (the resident reducing grid)
@@ -321,9 +324,10 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
 }
 
 template <typename T, typename VT, class Pro, class Gx, class Epi>
-inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st) {
-  if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st);
-  else launch_spmv_sell_th<T, VT, int32_t, kSellWG>(P, vals, gx, pro, epi, st);
+inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
+                                 bool one_tile_per_wg = false) {
+  if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
+  else launch_spmv_sell_th<T, VT, int32_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
 }
 
 }  // namespace lspcg

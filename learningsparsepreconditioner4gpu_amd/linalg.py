@@ -188,3 +188,85 @@ def solve_many(jobs, rtol: float = 1e-6, max_iter: int = 0, concurrency: int = 4
     dev = jobs[0][0].ctx.device  # the pool's threads select the solvers' device (per-thread state)
     with ThreadPoolExecutor(min(int(concurrency), len(jobs)), initializer=torch.cuda.set_device, initargs=(dev,)) as ex:
         return list(ex.map(lambda j: j[0].solve(j[1], j[2], rtol, max_iter), jobs))
+
+
+class BatchedConjugateGradient:
+    """ext_spai PCG of several independent systems in lockstep (``lspcg_batch_*``).
+
+    The reference solves its samples one at a time (``infer.py:278-331``: one
+    ``get_pcg_iter_time`` per sample, ``validate.py:89-121``).  Mid-size systems are
+    latency-bound on MI355X (a few hundred workgroups per launch, five dependent launches per
+    iteration), so here a window of them shares every launch: the systems are laid out
+    block-diagonally and each phase of the split schedule runs once for all of them, each system
+    with its own scalars, convergence test and iteration count.  Per system the
+    result is what ``PreconditionedConjugateGradient`` returns for it alone.
+
+    ``As[k]``, ``Ls[k]``: matrix and ext_spai factor of system k (DeviceMatrix or scipy), one
+    dtype and block size; ``epsilon``: the common ε of M⁻¹ = L Lᵀ + εI.  Raises ``LspcgError``
+    with code ``ERR_UNSUPPORTED`` when no SELL view of the batch can be built (irregular rows).
+    """
+
+    def __init__(self, As, Ls, epsilon: float, dtype=np.float64, block_size: int = 1,
+                 ctx: Optional[Context] = None):
+        As, Ls = list(As), list(Ls)
+        if not As or len(As) != len(Ls):
+            raise ValueError("need one L per A and at least one system")
+        self.ctx = ctx or (As[0].ctx if isinstance(As[0], DeviceMatrix) else Context.get())
+        self.dtype = np.dtype(dtype)
+        self.A = [_as_device_matrix(M, self.dtype, block_size, self.ctx) for M in As]
+        self.L = [_as_device_matrix(M, self.dtype, block_size, self.ctx) for M in Ls]
+        self.n = [M.n for M in self.A]
+        self.epsilon = float(epsilon)
+        k = len(self.A)
+        ha = (C.c_void_p * k)(*[M.handle.value for M in self.A])
+        hl = (C.c_void_p * k)(*[M.handle.value for M in self.L])
+        h = C.c_void_p()
+        _lib.call("lspcg_batch_create", self.ctx.handle, k, ha, hl, self.epsilon, C.byref(h))
+        self.handle = h
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.lspcg_batch_destroy(h)
+            self.handle = None
+
+    def __len__(self):
+        return len(self.n)
+
+    @property
+    def torch_dtype(self) -> torch.dtype:
+        return torch.float32 if self.dtype == np.float32 else torch.float64
+
+    def _check(self, name, vs):
+        vs = list(vs)
+        if len(vs) != len(self.n):
+            raise ValueError(f"{name}: {len(vs)} vectors for {len(self.n)} systems")
+        for k, v in enumerate(vs):
+            if not isinstance(v, torch.Tensor) or v.numel() != self.n[k] or v.dtype != self.torch_dtype \
+                    or v.device != self.ctx.torch_device or not v.is_contiguous():
+                raise ValueError(f"{name}[{k}] must be a contiguous {self.torch_dtype} tensor of {self.n[k]} entries "
+                                 f"on {self.ctx.torch_device}")
+        return vs
+
+    def solve(self, bs, xs, rtol: float = 1e-6, max_iter: int = 0, return_history: bool = False):
+        """Solve every system from its x (in place).  Returns ``(results, solve_time_s)`` with
+        ``results[k] = (iters, converged[, res_hist])``; the time is the whole batch's."""
+        bs = self._check("b", bs)
+        xs = self._check("x", xs)
+        k = len(self.n)
+        mi = [int(max_iter) if max_iter and max_iter > 0 else n for n in self.n]
+        it = (C.c_int64 * k)()
+        stt = (C.c_int32 * k)()
+        ms = C.c_double()
+        hists = [np.empty(m + 2, dtype=np.float64) for m in mi] if return_history else None
+        hp = (_lib.p_f64 * k)(*[h.ctypes.data_as(_lib.p_f64) for h in hists]) if hists else None
+        _lib.call("lspcg_batch_solve", self.handle, (C.c_void_p * k)(*[b.data_ptr() for b in bs]),
+                  (C.c_void_p * k)(*[x.data_ptr() for x in xs]), float(rtol), int(max_iter) if max_iter else 0,
+                  it, stt, hp, C.byref(ms), allow_not_converged=True)
+        res = []
+        for j in range(k):
+            r = (int(it[j]), stt[j] == _lib.OK)
+            if hists:
+                r = r + (hists[j][: min(int(it[j]), mi[j]) + 1].copy(),)
+            res.append(r)
+        return res, ms.value / 1e3

@@ -61,6 +61,34 @@ def main():
             rec = {"set": name, "threads": K, "systems": len(jobs), "iters_total": tot, "wall_ms": best * 1e3,
                    "us_per_iter_per_system": best * 1e6 / tot, "max_iters": max(its)}
             print(json.dumps(rec), flush=True)
+        # the same systems as ONE lockstep batch (linalg.BatchedConjugateGradient)
+        from learningsparsepreconditioner4gpu_amd.linalg import BatchedConjugateGradient
+
+        for rtol in (1e-6, 1e-8):
+            B = BatchedConjugateGradient([j[3] for j in jobs], [j[4] for j in jobs], ws.epsilon)
+            bs = [j[1] for j in jobs]
+            xs = [torch.zeros_like(b) for b in bs]
+            B.solve(bs, xs, rtol=rtol)  # graphs built
+            best, its = None, None
+            for _ in range(3):
+                for x in xs:
+                    x.zero_()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                res, _ = B.solve(bs, xs, rtol=rtol)
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t0
+                best = dt if best is None or dt < best else best
+                its = [r[0] for r in res]
+            ref = []
+            for j in jobs:
+                x = torch.zeros_like(j[1])
+                ref.append(j[0].solve(j[1], x, rtol=rtol)[0])
+            tot = sum(its)
+            rec = {"set": name, "mode": "batch", "rtol": rtol, "systems": len(jobs), "iters_total": tot,
+                   "wall_ms": best * 1e3, "us_per_iter_per_system": best * 1e6 / tot, "max_iters": max(its),
+                   "us_per_lockstep_iter": best * 1e6 / max(its), "iters_equal_single": its == ref}
+            print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
