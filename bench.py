@@ -234,8 +234,9 @@ def c1_rows(rtol: float) -> dict:
 
 def c5_rows(rtol: float, concurrency: int = 4) -> dict:
     """C5 (the heat-tet batch, 8 systems of 400-32 k vertices -- the reference's real
-    dataset sizes): the batch's ext_spai solves one after another (the reference's loop) and with
-    `concurrency` in flight (linalg.solve_many), best of 3 each; every system keeps its own count."""
+    dataset sizes): the batch's ext_spai solves one after another (the reference's loop), with
+    `concurrency` in flight (linalg.solve_many) and as ONE lockstep batch
+    (linalg.BatchedConjugateGradient), best of 3 each; every system keeps its own count."""
     import torch
 
     from learningsparsepreconditioner4gpu_amd.infer import synthetic_dataset
@@ -271,6 +272,26 @@ def c5_rows(rtol: float, concurrency: int = 4) -> dict:
         out[f"concurrency_{k}"] = {"wall_ms": best * 1e3, "systems_per_s": len(jobs) / best,
                                    "iters_total": int(sum(its)), "us_per_iter_per_system": best * 1e6 / sum(its)}
     out["iters"] = its
+    from learningsparsepreconditioner4gpu_amd.linalg import BatchedConjugateGradient
+
+    B = BatchedConjugateGradient([j[0].A for j in jobs], [j[0]._L for j in jobs], ws.epsilon)
+    bs = [j[1] for j in jobs]
+    xs = [torch.zeros_like(b) for b in bs]
+    B.solve(bs, xs, rtol)  # graphs built
+    best = None
+    for _ in range(3):
+        for x in xs:
+            x.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res, _ = B.solve(bs, xs, rtol)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None or dt < best else best
+    bits = [r[0] for r in res]
+    out["batched"] = {"wall_ms": best * 1e3, "systems_per_s": len(jobs) / best, "iters_total": int(sum(bits)),
+                      "us_per_iter_per_system": best * 1e6 / sum(bits), "us_per_lockstep_iter": best * 1e6 / max(bits),
+                      "iters_equal_sequential": bits == its}
     return out
 
 

@@ -1631,16 +1631,18 @@ int lspcg_solver_destroy(lspcg_solver* s) {
 //   * one row tile per workgroup (launch_spmv_sell_cfg one_tile_per_wg), so a workgroup's dot
 //     partial is its tile's and its prologue tests the tile's own system (done systems' tiles
 //     leave at once);
-//   * per-tile dot partials (grid_partial_groups with gsz = 1: no tickets, no last arriver);
-//   * elementwise launches of one 256-row tile per workgroup that sum their system's tile
-//     partials (group_sum_dd over the system's tile range) and keep that system's scalars; the
-//     first tile of a system is the only writer of its PcgState.
+//   * per-system last-arriver dot reductions (batch_sys_reduce): the last tile of a system to
+//     finish KB / KC sums the system's tile partials and updates its PcgState (scipy's scalars,
+//     the top-of-loop test, the iteration count), as the last-arriver schedule does for one system;
+//   * elementwise launches (UP, UR) of one 256-row tile per workgroup that read their system's
+//     finished scalars.
 // Padding rows are empty: they stay 0 in every vector and add exact zeros to the dots.
 namespace lspcg {
 
 struct BatchMap {
   const int32_t* etile_sys;  // [n / 256] system of each 256-row elementwise tile
   const int32_t* tile0;      // [nsys + 1] first SpMV row tile (256 block rows) of each system
+  const int32_t* tk0;        // [nsys] first ticket line of each system: [top | group 0 | group 1 | ...]
   int bs;                    // block size: SpMV tile b covers elementwise tiles bs*b .. bs*b + bs - 1
 };
 
@@ -1650,17 +1652,75 @@ struct ProTile {
   __device__ __forceinline__ bool exit() const { return S[m.etile_sys[int64_t(blockIdx.x) * m.bs]].done != 0; }
 };
 
-// init: r_0 = b - A x0 ; per-tile partials of ‖r_0‖², ‖b‖²
+// Per-system last-arriver reduction of a batched launch's N dots: each workgroup (= one row tile)
+// publishes its tile total (sc1 stores, drained, then relaxed agent-scope adds -- MI355X_MICROARCH.md
+// "Valid forms", table row 1, as grid_reduce_dd); the adds go to a two-level ticket (groups of
+// kTicketGroup tiles, then the system's top line: <= 32 serialised arrivals per line instead of a
+// system's few hundred -- the fan-in price), and the system's last arriving tile sums the system's
+// tile totals in tile order (fixed tree: the result does not depend on which tile came last);
+// thread 0 then runs fin(sys, values).  The elementwise launches read finished per-system scalars.
+template <int N, class Fin>
+__device__ __forceinline__ void batch_sys_reduce(DD (&v)[N], double* partials, unsigned* tickets, const BatchMap& m,
+                                                 Fin fin) {
+  __shared__ DD lds[16 * N];
+  __shared__ int s_last;
+  block_reduce_dd<N>(v, lds);
+  const int64_t tile = blockIdx.x;
+  const int sys = m.etile_sys[tile * m.bs];
+  const int t0 = m.tile0[sys], nt = m.tile0[sys + 1] - t0;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      st_agent_f64(&partials[(size_t(tile) * N + j) * 2 + 0], v[j].s);
+      st_agent_f64(&partials[(size_t(tile) * N + j) * 2 + 1], v[j].c);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned* top = tickets + size_t(kTicketStride) * m.tk0[sys];
+    const unsigned g = unsigned(tile - t0) / kTicketGroup;
+    const unsigned gsize = min(unsigned(kTicketGroup), unsigned(nt) - g * kTicketGroup);
+    const unsigned ng = (unsigned(nt) + kTicketGroup - 1) / kTicketGroup;
+    unsigned* gt = top + size_t(kTicketStride) * (1 + g);
+    int last = 0;
+    if (__hip_atomic_fetch_add(gt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      __hip_atomic_store(gt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+      if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  DD acc[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) acc[j] = dd_zero();
+  for (int b = threadIdx.x; b < nt; b += blockDim.x) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const size_t k = (size_t(t0 + b) * N + j) * 2;
+      acc[j] = dd_add(acc[j], DD{ld_agent_f64(&partials[k]), ld_agent_f64(&partials[k + 1])});
+    }
+  }
+  __syncthreads();
+  block_reduce_dd<N>(acc, lds);
+  if (threadIdx.x == 0) {
+    double out[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) out[j] = dd_value(acc[j]);
+    fin(sys, out);
+  }
+}
+
+// init: r_0 = b - A x0 ; ‖r_0‖², ‖b‖² -> the system's initial state (EpiResid::fin)
 template <typename T>
-struct EpiResidTile {
+struct EpiResidB {
   static constexpr int NDOT = 2;
-  static constexpr bool GROUPS = true;
+  static constexpr bool CUSTOM_FINISH = true;
   T* r;
   const T* b;
+  PcgState* S;
   double* partials;
-  unsigned* ticket;
-  double* group_out;
-  int gsz;
+  unsigned* tickets;
+  BatchMap m;
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
     const T bi = gld(b + i);
@@ -1669,94 +1729,124 @@ struct EpiResidTile {
     dd_fma(dots[0], double(ri), double(ri));
     dd_fma(dots[1], double(bi), double(bi));
   }
-  __device__ __forceinline__ void fin(const double*) const {}
+  __device__ __forceinline__ void finish(DD (&d)[2]) const {
+    PcgState* Sb = S;
+    batch_sys_reduce<2>(d, partials, tickets, m, [Sb](int sys, const double* v) {
+      PcgState* St = Sb + sys;
+      St->rr = round_to<T>(v[0]);
+      St->bb = round_to<T>(v[1]);
+      const double bn = double(tsqrt<T>(T(St->bb)));
+      St->atol = fmax(0.0, St->rtol * bn);
+      St->rho = St->rr;
+      St->alpha = 0.0;
+      St->iter = 0;
+      St->done = (bn == 0.0) ? 1 : 0;
+      if (St->hist) St->hist[0] = double(tsqrt<T>(T(St->rr)));
+    });
+  }
 };
 
-// one workgroup per system: the init state from the system's tile partials (EpiResid::fin)
+// KB: z = L t + ε r ; ρ_k = r·z, ‖r_k‖² -> the system's last arriver keeps ρ_k (EpiZ::fin) and runs
+// scipy's top-of-loop test on ‖r_k‖ (ProCheck / k_update_p_g): every tile of the system has
+// already passed this launch's prologue, so setting `done` here is seen first by UP
 template <typename T>
-__global__ void __launch_bounds__(kThreads) k_batch_init(PcgState* S, const int32_t* __restrict__ tile0,
-                                                         const double* __restrict__ gi) {
-  const int sys = blockIdx.x;
-  const int t0 = tile0[sys], t1 = tile0[sys + 1];
-  double v[2];
-  group_sum_dd<2>(gi + size_t(t0) * 4, t1 - t0, v);
-  if (threadIdx.x) return;
-  PcgState* St = S + sys;
-  St->rr = round_to<T>(v[0]);
-  St->bb = round_to<T>(v[1]);
-  const double bn = double(tsqrt<T>(T(St->bb)));
-  St->atol = fmax(0.0, St->rtol * bn);
-  St->rho = St->rr;
-  St->alpha = 0.0;
-  St->iter = 0;
-  St->done = (bn == 0.0) ? 1 : 0;
-  if (St->hist) St->hist[0] = double(tsqrt<T>(T(St->rr)));
-}
+struct EpiZB {
+  static constexpr int NDOT = 2;
+  static constexpr bool CUSTOM_FINISH = true;
+  T* z;
+  const T* r;
+  T eps;
+  PcgState* S;
+  double* partials;
+  unsigned* tickets;
+  BatchMap m;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T ri = gld(r + i);
+    const T zi = s + eps * ri;
+    gst(z + i, zi);
+    dd_fma(dots[0], double(ri), double(zi));
+    dd_fma(dots[1], double(ri), double(ri));
+  }
+  __device__ __forceinline__ void finish(DD (&d)[2]) const {
+    PcgState* Sb = S;
+    batch_sys_reduce<2>(d, partials, tickets, m, [Sb](int sys, const double* v) {
+      PcgState* St = Sb + sys;
+      St->rho_prev = St->rho;
+      St->rho = round_to<T>(v[0]);
+      const int64_t k = St->iter;
+      double rr = St->rr;  // ‖r_0‖² from the init
+      if (k > 0) {
+        rr = round_to<T>(v[1]);
+        St->rr = rr;
+        if (St->hist) St->hist[k] = double(tsqrt<T>(T(rr)));
+      }
+      int code = 0;
+      if (k >= St->max_iter) {
+        code = 2;
+      } else {
+        const double rn = double(tsqrt<T>(T(rr)));
+        if (rn < St->atol) code = 1;
+        else if (!(rn == rn) || rn == INFINITY) code = 3;
+      }
+      if (code) St->done = code;
+    });
+  }
+};
 
-// UP of the split schedule (k_update_p_g) for the tile's system
+// KC: q = A p ; π_k = p·q -> α_k = ρ_k/π_k, iteration k+1 (EpiQ<INC>::fin)
 template <typename T>
-__global__ void __launch_bounds__(kThreads) k_batch_update_p(BatchMap m, PcgState* S, const double* __restrict__ gz,
-                                                             const T* __restrict__ z, T* __restrict__ p,
-                                                             T* __restrict__ x) {
-  const int sys = m.etile_sys[blockIdx.x];
-  PcgState* St = S + sys;
-  if (St->done) return;
+struct EpiQB {
+  static constexpr int NDOT = 1;
+  static constexpr bool CUSTOM_FINISH = true;
+  T* q;
+  const T* p;
+  PcgState* S;
+  double* partials;
+  unsigned* tickets;
+  BatchMap m;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    gst(q + i, s);
+    dd_fma(dots[0], double(gld(p + i)), double(s));
+  }
+  __device__ __forceinline__ void finish(DD (&d)[1]) const {
+    PcgState* Sb = S;
+    batch_sys_reduce<1>(d, partials, tickets, m, [Sb](int sys, const double* v) {
+      PcgState* St = Sb + sys;
+      const double pq = round_to<T>(v[0]);
+      St->pq = pq;
+      St->alpha = double(T(St->rho) / T(pq));
+      St->iter = St->iter + 1;
+    });
+  }
+};
+
+// UP: x += α_{k-1} p_{k-1} (k > 0) ; p_k = p_{k-1}β + z with β = ρ_k/ρ_{k-1} (k_update_p_g's
+// expressions), one 256-row tile of one system per workgroup
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_batch_update_p(BatchMap m, const PcgState* S, const T* __restrict__ z,
+                                                             T* __restrict__ p, T* __restrict__ x) {
   const int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x;
   const T zi = z[i], pi = p[i], xi = x[i];
-  const int t0 = m.tile0[sys], t1 = m.tile0[sys + 1];
-  const int64_t k = St->iter;
-  double v[2];
-  group_sum_dd<2>(gz + size_t(t0) * 4, t1 - t0, v);
-  const double rho = round_to<T>(v[0]);
-  const double rr = k > 0 ? round_to<T>(v[1]) : St->rr;
-  int code = 0;
-  if (k >= St->max_iter) {
-    code = 2;
-  } else {
-    const double rn = double(tsqrt<T>(T(rr)));
-    if (rn < St->atol) code = 1;
-    else if (!(rn == rn) || rn == INFINITY) code = 3;
-  }
-  if (int64_t(blockIdx.x) == int64_t(t0) * m.bs && threadIdx.x == 0) {
-    if (k > 0) {
-      St->rr = rr;
-      if (St->hist) St->hist[k] = double(tsqrt<T>(T(rr)));
-    }
-    if (code) St->done = code;
-  }
-  if (code) return;
-  const bool first = k == 0;
-  const T beta = first ? T(0) : T(rho) / T(St->rho);
+  const PcgState* St = S + m.etile_sys[blockIdx.x];
+  if (St->done) return;
+  const bool first = St->iter == 0;
+  const T beta = first ? T(0) : T(St->rho) / T(St->rho_prev);
   const T alpha = T(St->alpha);
   if (!first) x[i] = xi + alpha * pi;
   p[i] = first ? zi : (pi * beta) + zi;
 }
 
-// UR of the split schedule (k_update_r_g) for the tile's system
+// UR: r_{k+1} = r_k - α_k q
 template <typename T>
-__global__ void __launch_bounds__(kThreads) k_batch_update_r(BatchMap m, PcgState* S, const double* __restrict__ gz,
-                                                             const double* __restrict__ gq, const T* __restrict__ q,
+__global__ void __launch_bounds__(kThreads) k_batch_update_r(BatchMap m, const PcgState* S, const T* __restrict__ q,
                                                              T* __restrict__ r) {
-  const int sys = m.etile_sys[blockIdx.x];
-  PcgState* St = S + sys;
-  if (St->done) return;
   const int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x;
   const T ri = r[i], qi = q[i];
-  const int t0 = m.tile0[sys], t1 = m.tile0[sys + 1];
-  double vz[2], vq[1];
-  group_sum_dd<2>(gz + size_t(t0) * 4, t1 - t0, vz);
-  group_sum_dd<1>(gq + size_t(t0) * 2, t1 - t0, vq);
-  const double rho = round_to<T>(vz[0]);
-  const double pq = round_to<T>(vq[0]);
-  const T alpha = T(rho) / T(pq);
-  if (int64_t(blockIdx.x) == int64_t(t0) * m.bs && threadIdx.x == 0) {
-    St->rho_prev = St->rho;
-    St->rho = rho;
-    St->pq = pq;
-    St->alpha = double(alpha);
-    St->iter = St->iter + 1;
-  }
-  r[i] = ri - alpha * qi;
+  const PcgState* St = S + m.etile_sys[blockIdx.x];
+  if (St->done) return;
+  r[i] = ri - T(St->alpha) * qi;
 }
 
 template <typename T>
@@ -1793,9 +1883,9 @@ struct lspcg_batch {
   int64_t ntot = 0;             // padded scalar rows
   int32_t* etile_sys = nullptr;
   int32_t* tile0 = nullptr;
-  double* gi = nullptr;  // per-tile partials: init (2 dots), KB (2 dots), KC (1 dot), DD each
-  double* gz = nullptr;
-  double* gq = nullptr;
+  int32_t* tk0 = nullptr;
+  double* partials = nullptr;  // per-tile dot partials (<= 2 dots, DD each)
+  unsigned* tickets = nullptr;  // per system: top line + one line per kTicketGroup tiles (batch_sys_reduce)
   PcgState* S = nullptr;
   PcgState* hS = nullptr;  // pinned: 2 poll slots x nsys
   double* dhist = nullptr;
@@ -1806,7 +1896,7 @@ struct lspcg_batch {
 
 namespace lspcg {
 
-static BatchMap batch_map(const lspcg_batch* bt) { return BatchMap{bt->etile_sys, bt->tile0, bt->bs}; }
+static BatchMap batch_map(const lspcg_batch* bt) { return BatchMap{bt->etile_sys, bt->tile0, bt->tk0, bt->bs}; }
 
 // SpMV of iteration view w over the block-diagonal system, one row tile per workgroup
 template <typename T, class Pro, class Epi>
@@ -1826,15 +1916,10 @@ static int launch_it_tiles(lspcg_solver* s, int w, const T* x, Pro pro, Epi epi,
 template <typename T>
 static int enqueue_batch_init(lspcg_batch* bt, hipStream_t st) {
   lspcg_solver* s = bt->s;
-  int rc = launch_it_tiles<T>(s, 0, static_cast<const T*>(s->x), ProNone{},
-                              EpiResidTile<T>{static_cast<T*>(s->r), static_cast<const T*>(s->b), nullptr, nullptr,
-                                              bt->gi, 1},
-                              st);
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_batch_init<T>, dim3(bt->nsys), dim3(kThreads), 0, st, bt->S,
-                     static_cast<const int32_t*>(bt->tile0), static_cast<const double*>(bt->gi));
-  LSPCG_HIP(hipGetLastError());
-  return LSPCG_OK;
+  return launch_it_tiles<T>(s, 0, static_cast<const T*>(s->x), ProNone{},
+                            EpiResidB<T>{static_cast<T*>(s->r), static_cast<const T*>(s->b), bt->S, bt->partials,
+                                         bt->tickets, batch_map(bt)},
+                            st);
 }
 
 template <typename T>
@@ -1852,14 +1937,15 @@ static int enqueue_batch_iteration(lspcg_batch* bt, hipStream_t st) {
   int rc = launch_it_tiles<T>(s, 2, static_cast<const T*>(r), pro, EpiT<T, false>{t, nullptr}, st);
   if (!rc)
     rc = launch_it_tiles<T>(s, 1, static_cast<const T*>(t), pro,
-                            EpiZG<T, false>{z, r, nullptr, T(s->eps), nullptr, nullptr, bt->gz, 1}, st);
+                            EpiZB<T>{z, r, T(s->eps), bt->S, bt->partials, bt->tickets, m}, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_batch_update_p<T>, eg, dim3(kThreads), 0, st, m, bt->S, static_cast<const double*>(bt->gz),
+  hipLaunchKernelGGL(k_batch_update_p<T>, eg, dim3(kThreads), 0, st, m, static_cast<const PcgState*>(bt->S),
                      static_cast<const T*>(z), p, x);
-  rc = launch_it_tiles<T>(s, 0, static_cast<const T*>(p), pro, EpiQG<T>{q, p, nullptr, nullptr, bt->gq, 1}, st);
+  rc = launch_it_tiles<T>(s, 0, static_cast<const T*>(p), pro, EpiQB<T>{q, p, bt->S, bt->partials, bt->tickets, m},
+                          st);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_batch_update_r<T>, eg, dim3(kThreads), 0, st, m, bt->S, static_cast<const double*>(bt->gz),
-                     static_cast<const double*>(bt->gq), static_cast<const T*>(q), r);
+  hipLaunchKernelGGL(k_batch_update_r<T>, eg, dim3(kThreads), 0, st, m, static_cast<const PcgState*>(bt->S),
+                     static_cast<const T*>(q), r);
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
@@ -1930,8 +2016,8 @@ int lspcg_batch_destroy(lspcg_batch* bt) {
   if (bt->s) lspcg_solver_destroy(bt->s);
   if (bt->Acat) lspcg_mat_destroy(bt->Acat);
   if (bt->Lcat) lspcg_mat_destroy(bt->Lcat);
-  for (void* v : {(void*)bt->etile_sys, (void*)bt->tile0, (void*)bt->gi, (void*)bt->gz, (void*)bt->gq,
-                  (void*)bt->S, (void*)bt->dhist})
+  for (void* v : {(void*)bt->etile_sys, (void*)bt->tile0, (void*)bt->tk0, (void*)bt->partials, (void*)bt->tickets, (void*)bt->S,
+                  (void*)bt->dhist})
     (void)hipFree(v);
   (void)hipHostFree(bt->hS);
   delete bt;
@@ -1980,13 +2066,21 @@ int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, cons
       esys[size_t(e)] = k;
   }
   t0[nsys] = int32_t(ntiles);
+  std::vector<int32_t> tk(nsys);
+  int64_t lines = 0;
+  for (int k = 0; k < nsys; ++k) {
+    tk[k] = int32_t(lines);
+    lines += 1 + (t0[k + 1] - t0[k] + kTicketGroup - 1) / kTicketGroup;
+  }
+  LSPCG_HIP(hipMalloc(&bt->tk0, sizeof(int32_t) * nsys));
+  LSPCG_HIP(hipMemcpy(bt->tk0, tk.data(), sizeof(int32_t) * nsys, hipMemcpyHostToDevice));
   LSPCG_HIP(hipMalloc(&bt->etile_sys, sizeof(int32_t) * esys.size()));
   LSPCG_HIP(hipMalloc(&bt->tile0, sizeof(int32_t) * t0.size()));
   LSPCG_HIP(hipMemcpy(bt->etile_sys, esys.data(), sizeof(int32_t) * esys.size(), hipMemcpyHostToDevice));
   LSPCG_HIP(hipMemcpy(bt->tile0, t0.data(), sizeof(int32_t) * t0.size(), hipMemcpyHostToDevice));
-  LSPCG_HIP(hipMalloc(&bt->gi, sizeof(double) * 4 * ntiles));
-  LSPCG_HIP(hipMalloc(&bt->gz, sizeof(double) * 4 * ntiles));
-  LSPCG_HIP(hipMalloc(&bt->gq, sizeof(double) * 2 * ntiles));
+  LSPCG_HIP(hipMalloc(&bt->partials, sizeof(double) * 4 * ntiles));
+  LSPCG_HIP(hipMalloc(&bt->tickets, sizeof(unsigned) * kTicketStride * lines));
+  LSPCG_HIP(hipMemset(bt->tickets, 0, sizeof(unsigned) * kTicketStride * lines));
   LSPCG_HIP(hipMalloc(&bt->S, sizeof(PcgState) * nsys));
   LSPCG_HIP(hipHostMalloc(&bt->hS, 2 * sizeof(PcgState) * nsys, hipHostMallocDefault));
   *out = bt.release();

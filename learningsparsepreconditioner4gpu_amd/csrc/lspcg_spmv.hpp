@@ -104,10 +104,18 @@ struct epi_groups : std::false_type {};
 template <class E>
 struct epi_groups<E, std::void_t<decltype(E::GROUPS)>> : std::bool_constant<E::GROUPS> {};
 
+// Epilogues with CUSTOM_FINISH = true reduce their dots themselves (epi.finish(d); batched solves)
+template <class E, class = void>
+struct epi_custom : std::false_type {};
+template <class E>
+struct epi_custom<E, std::void_t<decltype(E::CUSTOM_FINISH)>> : std::bool_constant<E::CUSTOM_FINISH> {};
+
 template <class Epi>
 __device__ __forceinline__ void finish_epi_dots(DD (&d)[Epi::NDOT > 0 ? Epi::NDOT : 1], Epi& epi) {
   if constexpr (Epi::NDOT > 0) {
-    if constexpr (epi_groups<Epi>::value)
+    if constexpr (epi_custom<Epi>::value)
+      epi.finish(d);
+    else if constexpr (epi_groups<Epi>::value)
       grid_partial_groups<Epi::NDOT>(d, epi.partials, epi.ticket, epi.gsz, epi.group_out);
     else
       grid_reduce_dd<Epi::NDOT>(d, epi.partials, epi.ticket, [&](const double* vals) { epi.fin(vals); });

@@ -28,8 +28,8 @@ import torch
 
 from . import problems as P
 from .data import GraphSample, make_sample
-from .distributed import SolveRecord, run_sharded, run_sharded_concurrent
-from .validate import get_cg_iter_time, get_pcg_iter_time, get_pcg_scaled_iter_time
+from .distributed import SolveRecord, run_sharded, run_sharded_batched, run_sharded_concurrent
+from .validate import get_cg_iter_time, get_pcg_iter_time, get_pcg_iter_time_batch, get_pcg_scaled_iter_time
 from .workspace import ScaledInferenceWorkspace, SimpleInferenceWorkspace
 
 
@@ -146,10 +146,14 @@ def rhs_for(rhs: str, mask: np.ndarray, sample: Optional[GraphSample] = None) ->
 
 
 def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: float = 1e-6, repeat: int = 1,
-        rhs: str = "mask", warmup: int = 20, concurrency: int = 1) -> List[SolveRecord]:
+        rhs: str = "mask", warmup: int = 20, concurrency: int = 1, batch: int = 1) -> List[SolveRecord]:
     """The ``Neural+CUDA`` row of infer.py:278-331 (GNN -> L, A; ext_spai PCG).  ``concurrency``
     > 1 keeps that many solves of this rank in flight at once (run_sharded_concurrent): the same
-    iterates and counts, a higher batch throughput on the reference's mid-size systems."""
+    iterates and counts, a higher batch throughput on the reference's mid-size systems.  ``batch``
+    > 1 (ext_spai, not the scaled variant) solves this rank's systems in lockstep windows of that
+    many (run_sharded_batched, validate.get_pcg_iter_time_batch): the same counts and iterates,
+    every launch covering the whole window; a record's t_solve is its share of the window's
+    device time."""
     pcg = get_pcg_scaled_iter_time if isinstance(ws, ScaledInferenceWorkspace) else get_pcg_iter_time
     dev = torch.device("cuda", torch.cuda.current_device())
     warmed = set()
@@ -178,7 +182,16 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
         return SolveRecord(index=i, iters=it, rel_res=info["rel_res"], t_prec=prec, t_solve=sol, n=A.n, nnz=A.nnz,
                            converged=info["converged"])
 
+    def finish_batch(jobs) -> List[SolveRecord]:
+        infos = [{} for _ in jobs]
+        out = get_pcg_iter_time_batch([j[1] for j in jobs], [j[3] for j in jobs], [j[2] for j in jobs], ws.epsilon,
+                                      rtol=rtol, infos=infos)
+        return [SolveRecord(index=j[0], iters=it, rel_res=info["rel_res"], t_prec=j[4], t_solve=sol, n=j[1].n,
+                            nnz=j[1].nnz, converged=info["converged"]) for j, (it, _, sol), info in zip(jobs, out, infos)]
+
     weights = [float(s.edge_index.shape[1]) for s in samples]
+    if batch > 1 and not isinstance(ws, ScaledInferenceWorkspace):
+        return run_sharded_batched(len(samples), weights, prepare, finish_batch, batch)
     if concurrency > 1:
         return run_sharded_concurrent(len(samples), weights, prepare, finish, concurrency)
     return run_sharded(len(samples), weights, lambda i: finish(prepare(i)))
@@ -230,6 +243,8 @@ def main(argv=None):
     ap.add_argument("--infer-prefix", default="")
     ap.add_argument("--concurrency", type=int, default=1,
                     help="solves in flight at once per GPU (run_sharded_concurrent); 1 = the reference's sequential loop")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="systems per lockstep batch per GPU (run_sharded_batched); 1 = one solve at a time")
     ap.add_argument("--baselines", default="none,diagonal,ainv,ic",
                     help="comma list of PCG-{method}-cuda rows (infer.py:310-321); '' for none")
     args = ap.parse_args(argv)
@@ -261,7 +276,7 @@ def main(argv=None):
     for m in [b for b in args.baselines.split(",") if b]:
         rows[f"PCG-{m}-cuda"] = run_baseline(samples, ws, m, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs)
     rows["Neural+HIP"] = run(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, warmup=args.warmup,
-                             concurrency=args.concurrency)
+                             concurrency=args.concurrency, batch=args.batch)
     recs = rows["Neural+HIP"]
     if not dist.is_initialized() or dist.get_rank() == 0:
         stats = Timestat()

@@ -8,6 +8,8 @@ Same names, arguments, return values and error behaviour as the reference:
   converge")`` when ``iter >= max_iter``, as :84-85)
 * ``get_pcg_iter_time``          -- validate.py:89-121 (ext_spai, never raises)
 * ``get_pcg_scaled_iter_time``   -- validate.py:124-160 (ext_spai_scaled)
+* ``get_pcg_iter_time_batch``    -- not in the reference: ``get_pcg_iter_time`` over a window
+  of independent systems solved as one lockstep batch
 
 Matrices may be scipy CSR (uploaded) or :class:`DeviceMatrix` (already in HBM).
 
@@ -21,13 +23,15 @@ scipy's csr_matvec).
 from __future__ import annotations
 
 import math
-from typing import Optional, Tuple, Union
+import time
+from typing import List, Optional, Tuple, Union
 
 import numpy as np
 import scipy.sparse as sp
 import torch
 
-from .linalg import PreconditionedConjugateGradient
+from . import _lib
+from .linalg import BatchedConjugateGradient, PreconditionedConjugateGradient
 from .sparse import Context, DeviceMatrix, assemble, dot, lspcg_dtype
 
 
@@ -125,6 +129,41 @@ def get_pcg_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat
     """validate.py:89-121: ext_spai PCG, M⁻¹ = L Lᵀ + εI.  ``info`` (optional dict, not in the
     reference's signature) receives the last solve's x, true relative residual and convergence."""
     return _pcg_generic("ext_spai", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info)
+
+
+def get_pcg_iter_time_batch(As, gts, spais, epsilon: float, rtol=1e-6, max_iter=0, dtype=np.float64,
+                            infos: Optional[list] = None) -> List[Tuple[float, float, float]]:
+    """get_pcg_iter_time over a window of independent systems solved as ONE lockstep batch
+    (linalg.BatchedConjugateGradient; the reference calls get_pcg_iter_time once per sample,
+    infer.py:322).  Per system ``(iters, prec_s, solve_s)``: the batch's setup (block-diagonal
+    copy, Lᵀ and views: host wall) and device solve time split evenly over its systems.  A window
+    without a SELL view (irregular rows) is solved one system at a time instead, on the GPU."""
+    Ads = [_prepare(A, dtype) for A in As]
+    Lds = [L if isinstance(L, DeviceMatrix) else _prepare(L, dtype) for L in spais]
+    bs = [_device_rhs(A, gt) for A, gt in zip(Ads, gts)]
+    k = len(Ads)
+    try:
+        t0 = time.perf_counter()
+        B = BatchedConjugateGradient(Ads, Lds, epsilon, dtype=dtype)
+        prec = time.perf_counter() - t0
+    except _lib.LspcgError as e:
+        if e.code != _lib.ERR_UNSUPPORTED:
+            raise
+        out = []
+        for j in range(k):
+            info = {} if infos is not None else None
+            out.append(get_pcg_iter_time(Ads[j], gts[j], Lds[j], epsilon, rtol, max_iter, 1, dtype, info=info))
+            if infos is not None:
+                infos[j].update(info)
+        return out
+    xs = [torch.zeros_like(b) for b in bs]
+    res, t = B.solve(bs, xs, rtol, max_iter)
+    out = []
+    for j, (it, conv) in enumerate(res):
+        if infos is not None:
+            infos[j].update(x=xs[j], rel_res=relative_residual(Ads[j], xs[j], bs[j]), converged=bool(conv), iters=it)
+        out.append((float(it), prec / k, t / k))
+    return out
 
 
 def get_pcg_scaled_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat=1, dtype=np.float64,

@@ -9,7 +9,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from learningsparsepreconditioner4gpu_amd.distributed import (SolveRecord, gather_records, lpt_assign, my_items,
-                                                             run_sharded, run_sharded_concurrent)
+                                                             run_sharded, run_sharded_batched,
+                                                             run_sharded_concurrent)
 
 
 def test_lpt_assignment_balanced_and_complete():
@@ -30,7 +31,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_items, q, concurrency=0):
+def _worker(rank, world, port, n_items, q, concurrency=0, batch=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     weights = [float(10 + (i * 7) % 5) for i in range(n_items)]
@@ -39,7 +40,17 @@ def _worker(rank, world, port, n_items, q, concurrency=0):
         return SolveRecord(index=i, iters=100 + i, rel_res=1e-9 * (i + 1), t_prec=0.001 * i, t_solve=0.01 * (i + 1),
                            n=1000 + i, nnz=5000 + i, converged=(i % 3 != 2))
 
-    if concurrency:  # prepare on this thread in windows, the solves on a pool
+    if batch:  # windows of `batch` prepared systems, each window solved by one call
+        windows = []
+
+        def finish_batch(jobs):
+            assert 1 <= len(jobs) <= batch
+            windows.append(list(jobs))
+            return [solve(i) for i in jobs]
+
+        recs = run_sharded_batched(n_items, weights, lambda i: i, finish_batch, batch, device=torch.device("cpu"))
+        assert [i for w in windows for i in w] == my_items(weights, rank, world)
+    elif concurrency:  # prepare on this thread in windows, the solves on a pool
         import threading
 
         main = threading.get_ident()
@@ -59,13 +70,13 @@ def _worker(rank, world, port, n_items, q, concurrency=0):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,concurrency", [(2, 0), (3, 0), (2, 3)])
-def test_gloo_sharded_gather(world, concurrency):
+@pytest.mark.parametrize("world,concurrency,batch", [(2, 0, 0), (3, 0, 0), (2, 3, 0), (2, 0, 2)])
+def test_gloo_sharded_gather(world, concurrency, batch):
     n_items = 7
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_items, q, concurrency)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_items, q, concurrency, batch)) for r in range(world)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=120) for _ in range(world)]

@@ -108,6 +108,24 @@ def test_infer_concurrent_solves_match_sequential(gpu_ctx):
         assert (a.iters, a.rel_res, a.n, a.nnz) == (b.iters, b.rel_res, b.n, b.nnz)
 
 
+def test_infer_batched_solves_match_sequential(gpu_ctx):
+    """run(..., batch=K): the rank's systems solved K at a time in one lockstep batch give the
+    records of the sequential loop (counts, convergence, true residuals) on the C5 heat batch."""
+    from learningsparsepreconditioner4gpu_amd.infer import run, synthetic_dataset
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    samples = synthetic_dataset("heat_batch8")
+    ws = SimpleInferenceWorkspace(node_features=samples[0].x.shape[1], edge_features=1, seed=0)
+    seq = run(samples, ws, rtol=1e-8, warmup=1)
+    for k in (3, 8):
+        bat = run(samples, ws, rtol=1e-8, warmup=1, batch=k)
+        assert [r.index for r in bat] == list(range(len(samples)))
+        for a, b in zip(seq, bat):
+            assert a.converged and b.converged
+            assert (a.iters, a.n, a.nnz) == (b.iters, b.n, b.nnz)
+            assert abs(a.rel_res - b.rel_res) <= 1e-12 and b.rel_res <= 1e-8
+
+
 @pytest.mark.parametrize("rhs", ["mask", "neighbour"])
 def test_folder_dataset_through_hot_path(gpu_ctx, rhs):
     """On-disk dataset (reference folder format, golden folder_free) -> GNN -> L -> PCG through
