@@ -402,7 +402,6 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
                                                          T* __restrict__ x) {
   using V = typename VecT<T>::type;
   constexpr int W = VecT<T>::W;
-  if (S->done) return;
   const int64_t nv = n / W;
   const int64_t ts = int64_t(gridDim.x) * blockDim.x;
   const int64_t jt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -418,10 +417,14 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
       }
     }
   };
+  // the first chunk, the group totals and the state line are all loaded before the first test:
+  // one memory latency instead of a state read followed by the loads
   load(jt);
+  const int32_t done = S->done;
   const int64_t k = S->iter;
   double v[2];
   group_sum_dd<2>(gz, ngz, v);
+  if (done) return;
   const double rho = round_to<T>(v[0]);
   const double rr = k > 0 ? round_to<T>(v[1]) : S->rr;  // ‖r_0‖² from the init launch
   int code = 0;  // scipy's top-of-loop test (ProCheck)
@@ -468,7 +471,6 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
                                                          const T* __restrict__ q, T* __restrict__ r) {
   using V = typename VecT<T>::type;
   constexpr int W = VecT<T>::W;
-  if (S->done) return;
   const int64_t nv = n / W;
   const int64_t ts = int64_t(gridDim.x) * blockDim.x;
   const int64_t jt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -483,10 +485,12 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
       }
     }
   };
-  load(jt);
+  load(jt);  // first chunk, group totals and state line together (as in UP)
+  const int32_t done = S->done;
   double vz[2], vq[1];
   group_sum_dd<2>(gz, ngz, vz);
   group_sum_dd<1>(gq, ngq, vq);
+  if (done) return;
   const double rho = round_to<T>(vz[0]);
   const double pq = round_to<T>(vq[0]);
   const T alpha = T(rho) / T(pq);

@@ -103,21 +103,32 @@ template <typename T, typename VT, typename CT, int QB, int TH, int MINW, class 
 __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
   constexpr bool C16 = sizeof(CT) == 2;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t ntiles = (a.n + TH - 1) / TH;
+  // the first tile's slice range is loaded before the prologue's state read, so the two
+  // dependent-free loads share one memory latency (the state line was written by another CU)
+  int32_t gb[2] = {0, 0};
+  if (int64_t(blockIdx.x) * (TH / 64) + w < a.ns) {
+    gb[0] = a.gp[int64_t(blockIdx.x) * (TH / 64) + w];
+    gb[1] = a.gp[int64_t(blockIdx.x) * (TH / 64) + w + 1];
+  }
   if (pro.exit()) return;
   gx.prepare();
   epi.prepare();
   DD d[ND];
 #pragma unroll
   for (int j = 0; j < ND; ++j) d[j] = dd_zero();
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int64_t ntiles = (a.n + TH - 1) / TH;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t s = tile * (TH / 64) + w;
     const int64_t i = tile * TH + threadIdx.x;
     if (s < a.ns) {  // wave-uniform
-      const int32_t g0 = a.gp[s];
-      const int nq = a.gp[s + 1] - g0;
+      if (tile != int64_t(blockIdx.x)) {
+        gb[0] = a.gp[s];
+        gb[1] = a.gp[s + 1];
+      }
+      const int32_t g0 = gb[0];
+      const int nq = gb[1] - g0;
       const int32_t base = int32_t(s * kSellC);
       const VT* vp = a.vals + 256 * int64_t(g0) + 4 * lane;
       const CT* cp = a.col + 256 * int64_t(g0) + 4 * lane;
@@ -202,22 +213,31 @@ template <typename T, typename VT, typename CT, int QB, int TH, int MINW, class 
 __global__ void __launch_bounds__(TH, MINW) k_spmv_bsell3(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
   constexpr bool C16 = sizeof(CT) == 2;
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t nb = a.n / 3;
+  const int64_t ntiles = (nb + TH - 1) / TH;
+  int32_t gb[2] = {0, 0};  // first tile's slice range, loaded beside the prologue's state read
+  if (int64_t(blockIdx.x) * (TH / 64) + w < a.ns) {
+    gb[0] = a.gp[int64_t(blockIdx.x) * (TH / 64) + w];
+    gb[1] = a.gp[int64_t(blockIdx.x) * (TH / 64) + w + 1];
+  }
   if (pro.exit()) return;
   gx.prepare();
   epi.prepare();
   DD d[ND];
 #pragma unroll
   for (int j = 0; j < ND; ++j) d[j] = dd_zero();
-  const int lane = threadIdx.x & 63;
-  const int w = threadIdx.x >> 6;
-  const int64_t nb = a.n / 3;
-  const int64_t ntiles = (nb + TH - 1) / TH;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t s = tile * (TH / 64) + w;
     const int64_t I = tile * TH + threadIdx.x;
     if (s < a.ns) {  // wave-uniform
-      const int32_t g0 = a.gp[s];
-      const int nq = a.gp[s + 1] - g0;
+      if (tile != int64_t(blockIdx.x)) {
+        gb[0] = a.gp[s];
+        gb[1] = a.gp[s + 1];
+      }
+      const int32_t g0 = gb[0];
+      const int nq = gb[1] - g0;
       const int32_t base = int32_t(s * kSellC);
       const VT* vp = a.vals + 576 * int64_t(g0);
       const CT* cp = a.col + 64 * int64_t(g0) + lane;
