@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <memory>
 #include <string>
@@ -183,9 +184,22 @@ __global__ void k_level_bounds(int64_t n, const int32_t* __restrict__ ls, int32_
 void Levels::release() {
   (void)hipFree(ptr);
   (void)hipFree(order);
-  ptr = order = nullptr;
+  (void)hipFree(pad);
+  (void)hipFree(head);
+  ptr = order = pad = nullptr;
+  head = nullptr;
+  npad = 0;
   hptr.clear();
   nlev = 0;
+}
+
+// position t of the level-sorted order -> its place in the wave-padded order
+__global__ void k_pad_order(int64_t n, const int32_t* __restrict__ lev_s, const int32_t* __restrict__ ptr,
+                            const int32_t* __restrict__ pptr, const int32_t* __restrict__ order, int32_t* __restrict__ pad) {
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < n; t += int64_t(gridDim.x) * blockDim.x) {
+    const int l = lev_s[t];
+    pad[pptr[l] + (t - ptr[l])] = order[t];
+  }
 }
 
 int build_levels(lspcg_ctx* ctx, int64_t n, const int32_t* rp, const int32_t* ci, bool lower, Levels* out) {
@@ -231,6 +245,19 @@ int build_levels(lspcg_ctx* ctx, int64_t n, const int32_t* rp, const int32_t* ci
   out->hptr.resize(maxl + 2);
   LSPCG_HIP(hipMemcpyAsync(out->hptr.data(), ptr, sizeof(int32_t) * (maxl + 2), hipMemcpyDeviceToHost, st));
   LSPCG_HIP(hipStreamSynchronize(st));
+  // wave-padded order for the sync-free solve
+  std::vector<int32_t> pptr(maxl + 2, 0);
+  for (int l = 0; l <= maxl; ++l) pptr[l + 1] = pptr[l] + (out->hptr[l + 1] - out->hptr[l] + 63) / 64 * 64;
+  int32_t* dpptr = nullptr;
+  LSPCG_HIP(hipMalloc(&dpptr, sizeof(int32_t) * (maxl + 2)));
+  LSPCG_HIP(hipMemcpy(dpptr, pptr.data(), sizeof(int32_t) * (maxl + 2), hipMemcpyHostToDevice));
+  LSPCG_HIP(hipMalloc(&out->pad, sizeof(int32_t) * pptr[maxl + 1]));
+  LSPCG_HIP(hipMemsetAsync(out->pad, 0xFF, sizeof(int32_t) * pptr[maxl + 1], st));
+  hipLaunchKernelGGL(k_pad_order, dim3(fgrid(n)), dim3(kThreads), 0, st, n, lev_s, ptr, dpptr, order, out->pad);
+  LSPCG_HIP(hipMalloc(&out->head, sizeof(unsigned)));
+  LSPCG_HIP(hipStreamSynchronize(st));
+  (void)hipFree(dpptr);
+  out->npad = pptr[maxl + 1];
   cleanup();
   out->nlev = maxl + 1;
   out->ptr = ptr;
@@ -302,8 +329,155 @@ __global__ void k_trsv_level(const int32_t* __restrict__ order, int32_t beg, int
   }
 }
 
+// Sync-free solve: ONE launch for the whole triangular solve instead of one per level.  A
+// resident grid (1 workgroup per CU: few polling waves per CU, short hand-offs) takes 256-position
+// blocks of the wave-padded level order from a dequeue counter, in order, so a block only ever
+// waits for blocks that running workgroups hold; thread t of block B owns position B*256 + t,
+// waits for its dependencies' values (all still-missing ones re-read together per poll round,
+// the row's values loaded beforehand) and runs k_trsv_level's arithmetic.  The
+// hand-off is the value itself: x is first filled with a NaN pattern no arithmetic produces, each
+// row publishes its result with one 4- / 8-byte sc1 store (a self-validating granule,
+// MI355X_MICROARCH.md R2) and waiters poll with sc1 loads.  A wave never holds rows of two
+// levels, so no lane waits for a lane of its own wave.  A row whose wait exceeds ~0.1 s (never in a
+// finished solve: the chain is one hop per level) takes NaN, so the PCG stops as non-finite.
+template <typename T>
+struct TrsvBits;
+template <>
+struct TrsvBits<double> {
+  using U = unsigned long long;
+  static constexpr U kWait = 0x7FF4C0DEDEADBEEFull;  // signalling-NaN payload: never an arithmetic result
+};
+template <>
+struct TrsvBits<float> {
+  using U = unsigned;
+  static constexpr U kWait = 0x7FA5C0DEu;
+};
+
+constexpr int kTrsvBatch = 8;
+
+// read of a dependency's value: an sc1 load (an atomic RMW poll measured the same)
+template <typename U>
+__device__ __forceinline__ U trsv_poll(const U* p) {
+  return __hip_atomic_load(const_cast<U*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T>
+__global__ void k_trsv_wait_fill(int64_t n, T* __restrict__ x, const int32_t* done) {
+  if (done && *done) return;
+  using U = typename TrsvBits<T>::U;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    reinterpret_cast<U*>(x)[i] = TrsvBits<T>::kWait;
+}
+
+template <typename T, bool LOWER>
+__global__ void __launch_bounds__(256) k_trsv_syncfree(int64_t npad, const int32_t* __restrict__ pad,
+                                                       const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                       const T* __restrict__ v, const T* __restrict__ b, T* x,
+                                                       const int32_t* done, unsigned* head) {
+  using U = typename TrsvBits<T>::U;
+  __shared__ unsigned s_blk;
+  if (done && *done) return;
+  U* xu = reinterpret_cast<U*>(x);
+  const unsigned nblk = unsigned((npad + 255) / 256);
+  for (;;) {
+    // the workgroup takes the next 256-position block (per-wave 64-position blocks measured slower:
+    // 4x the dequeues on one counter)
+    if (threadIdx.x == 0) s_blk = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned blk = s_blk;
+    __syncthreads();
+    if (blk >= nblk) return;  // every workgroup leaves through here once the blocks are taken
+    const uint64_t t0 = wall_clock64();  // the block's waits are bounded from here
+    const int64_t t = int64_t(blk) * 256 + threadIdx.x;
+    const int i = t < npad ? pad[t] : -1;
+    if (i >= 0) {
+      T s = b[i];
+      const int pd = LOWER ? rp[i + 1] - 1 : rp[i];
+      const int p0 = LOWER ? rp[i] : pd + 1;
+      const int p1 = LOWER ? pd : rp[i + 1];
+      const T diag = v[pd];
+      // the dependencies' values are loaded kTrsvBatch at a time, and every poll round re-reads ALL
+      // still-waiting ones together: one memory latency per round, not one per entry; the sum
+      // then runs in row order
+      for (int pb = p0; pb < p1; pb += kTrsvBatch) {
+        U u[kTrsvBatch];
+        T w[kTrsvBatch];  // the row's values, loaded before the wait (not after the last hand-off)
+        const U* src[kTrsvBatch];
+#pragma unroll
+        for (int k = 0; k < kTrsvBatch; ++k) {
+          const int q = pb + k < p1 ? pb + k : p0;
+          src[k] = xu + ci[q];
+          w[k] = v[q];
+        }
+#pragma unroll
+        for (int k = 0; k < kTrsvBatch; ++k) u[k] = trsv_poll(src[k]);
+        for (;;) {
+          bool wait = false;
+#pragma unroll
+          for (int k = 0; k < kTrsvBatch; ++k) wait |= (pb + k < p1) && u[k] == TrsvBits<T>::kWait;
+          if (!wait) break;
+          if (wall_clock64() - t0 > 10000000ull) {  // 0.1 s at the 100 MHz constant clock
+#pragma unroll
+            for (int k = 0; k < kTrsvBatch; ++k)
+              if (u[k] == TrsvBits<T>::kWait) u[k] = __builtin_bit_cast(U, T(NAN));
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+          for (int k = 0; k < kTrsvBatch; ++k)
+            if (u[k] == TrsvBits<T>::kWait) u[k] = trsv_poll(src[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < kTrsvBatch; ++k)
+          if (pb + k < p1) s = s - w[k] * __builtin_bit_cast(T, u[k]);
+      }
+      __hip_atomic_store(xu + i, __builtin_bit_cast(U, s / diag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+static bool trsv_levels_env() {
+  static const bool v = [] { const char* e = std::getenv("LSPCG_TRSV_LEVELS"); return e && e[0] == '1'; }();
+  return v;
+}
+
+int trsv_launches(const Levels& lv) { return trsv_levels_env() ? lv.nlev : 3; }
+
 int enqueue_trsv(const lspcg_mat* T_, const Levels& lv, bool lower, const void* b, void* x, const int32_t* done,
                  hipStream_t st) {
+  if (!trsv_levels_env() && lv.pad && lv.npad > 0) {
+    const int64_t n = T_->n;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    static const int64_t per_cu = [] {
+      const char* e = std::getenv("LSPCG_TRSV_WG_PER_CU");
+      return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1);
+    }();
+    const dim3 g(unsigned(std::min<int64_t>((lv.npad + 255) / 256, per_cu * int64_t(cus)))), blk(256);
+    LSPCG_HIP(hipMemsetAsync(lv.head, 0, sizeof(unsigned), st));
+    if (T_->dtype == LSPCG_F64) {
+      auto vx = static_cast<double*>(x);
+      hipLaunchKernelGGL(k_trsv_wait_fill<double>, dim3(fgrid(n)), dim3(kThreads), 0, st, n, vx, done);
+      if (lower)
+        hipLaunchKernelGGL((k_trsv_syncfree<double, true>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind,
+                           static_cast<const double*>(T_->vals), static_cast<const double*>(b), vx, done, lv.head);
+      else
+        hipLaunchKernelGGL((k_trsv_syncfree<double, false>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind,
+                           static_cast<const double*>(T_->vals), static_cast<const double*>(b), vx, done, lv.head);
+    } else {
+      auto vx = static_cast<float*>(x);
+      hipLaunchKernelGGL(k_trsv_wait_fill<float>, dim3(fgrid(n)), dim3(kThreads), 0, st, n, vx, done);
+      if (lower)
+        hipLaunchKernelGGL((k_trsv_syncfree<float, true>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind,
+                           static_cast<const float*>(T_->vals), static_cast<const float*>(b), vx, done, lv.head);
+      else
+        hipLaunchKernelGGL((k_trsv_syncfree<float, false>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind,
+                           static_cast<const float*>(T_->vals), static_cast<const float*>(b), vx, done, lv.head);
+    }
+    LSPCG_HIP(hipGetLastError());
+    return LSPCG_OK;
+  }
   for (int l = 0; l < lv.nlev; ++l) {
     const int beg = lv.hptr[l], cnt = lv.hptr[l + 1] - lv.hptr[l];
     if (cnt <= 0) continue;

@@ -18,15 +18,24 @@ struct Levels {
   int32_t* ptr = nullptr;
   int32_t* order = nullptr;
   std::vector<int32_t> hptr;
+  // sync-free solve (lspcg_factor.hip k_trsv_syncfree): `order` with every level padded to whole
+  // wave64s (-1 = no row), so no wave holds two rows of which one waits for the other; npad
+  // positions; head = the launch's block dequeue counter
+  int32_t* pad = nullptr;
+  int64_t npad = 0;
+  unsigned* head = nullptr;
   void release();
 };
 
 // lower: row i depends on the columns j < i of its row; upper: on the columns j > i.
 int build_levels(lspcg_ctx* ctx, int64_t n, const int32_t* rp, const int32_t* ci, bool lower, Levels* out);
-// x = T⁻¹ b by levels (lower: diagonal stored last in each row, upper: first); `done` (nullable)
-// is the solver's device done flag -- every launch returns at once when it is set.
+// x = T⁻¹ b (lower: diagonal stored last in each row, upper: first); `done` (nullable) is the
+// solver's device done flag -- every launch returns at once when it is set.  One sync-free launch
+// (rows wait for their dependencies' values) or, with LSPCG_TRSV_LEVELS=1, one launch per level.
+// Same bits either way.  launches_per_solve: graph nodes one enqueue_trsv adds.
 int enqueue_trsv(const lspcg_mat* T, const Levels& lv, bool lower, const void* b, void* x, const int32_t* done,
                  hipStream_t st);
+int trsv_launches(const Levels& lv);
 int ic0_factor(const lspcg_mat* A, lspcg_mat** L);
 int ainv0_factor(const lspcg_mat* A, lspcg_mat** L);
 

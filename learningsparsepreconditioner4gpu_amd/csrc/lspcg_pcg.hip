@@ -1453,7 +1453,7 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   // decay minus the iterations already in flight, so that at most a few early-exit launches trail
   // the converged iteration (every launch is predicated on the device `done` flag).
   // graphs hold <= ~4096 nodes (IC: one launch per level of each triangular solve)
-  const int kpi = s->precond == LSPCG_PRECOND_IC ? s->levL.nlev + s->levU.nlev + 4 : 5;
+  const int kpi = s->precond == LSPCG_PRECOND_IC ? trsv_launches(s->levL) + trsv_launches(s->levU) + 4 : 5;
   const int max_chunk = std::max(1, std::min(32, 4096 / kpi));
   PcgState* const hs[2] = {s->hS, s->hS + 1};
   const hipEvent_t evp[2] = {s->ev_poll, s->ev_poll2};

@@ -53,8 +53,17 @@ def test_ainv0_factor_bitwise(gpu_ctx, name):
     np.testing.assert_array_equal(Lg.data, Lo.data)
 
 
-def test_trsv_bitwise(gpu_ctx):
-    A, _ = _systems()["kuhn7"]
+@pytest.mark.parametrize("name", ["kuhn7", "kuhn31", "poisson100"])
+def test_trsv_bitwise(gpu_ctx, name):
+    """The sync-free one-launch solve (many blocks waiting on each other across 90-200 levels)
+    gives the oracle's bits, as the per-level launches do."""
+    if name == "kuhn31":
+        A = sp.csr_matrix(P.kuhn_laplacian(31))
+    elif name == "poisson100":
+        A1, m1, _ = P.poisson2d_grid(100, 100)
+        A = _masked(A1, m1)
+    else:
+        A, _ = _systems()[name]
     L = OP.ic0(A)
     U = sp.csr_matrix(L.T)
     U.sort_indices()
