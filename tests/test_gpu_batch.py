@@ -147,3 +147,21 @@ def test_batch_rejects_mixed_inputs(gpu_ctx):
     with pytest.raises(ValueError):
         B.solve([torch.zeros(A1.shape[0], dtype=torch.float32, device="cuda")],
                 [torch.zeros(A1.shape[0], dtype=torch.float64, device="cuda")])
+
+
+def test_batch_many_systems_memory_map(gpu_ctx):
+    """More systems than the kernel-argument map holds (16): the tile -> system map is read from
+    device memory instead; every system still equals its single solve."""
+    eps = 3e-3
+    As = []
+    for k in range(18):
+        A, _, _ = P.poisson2d_grid(9 + (k * 7) % 23, 8 + (k * 5) % 17)
+        As.append(A)
+    Ls = [_cases.spai_like(A, seed=k) for k, A in enumerate(As)]
+    bs_ = [A @ np.ones(A.shape[0]) for A in As]
+    _, res, xs = _batch(As, Ls, bs_, eps, 1e-8)
+    for A, L, b, (it, conv, h), x in zip(As, Ls, bs_, res, xs):
+        it1, conv1, x1, h1 = _single(A, L, b, eps, 1e-8)
+        assert (it, conv) == (it1, conv1)
+        np.testing.assert_allclose(h, h1, rtol=1e-12, atol=0)
+        assert _rel(x, x1) <= 1e-12
