@@ -211,6 +211,7 @@ __device__ __forceinline__ void grid_reduce_dd(DD (&v)[N], double* partials, uns
 // plain stores / loads suffice for them.  (The measured cost of the last-arriver tail of
 // grid_reduce_dd was ~4.3 us per reduction at 1536 workgroups.)
 // ---------------------------------------------------------------------------
+constexpr int kNoGroupGrid = 512;  // reducing grids up to this size skip the groups (see lspcg_solver_set_spai)
 constexpr int kMaxGroups = 64;  // also the largest group SIZE grid_partial_groups handles (one wave sums a group):
                                  // gsz = ceil(grid / 64) <= 64 for every reducing grid <= 4096 (sell_cap); 32 groups measured 90.2 vs 89.1 us
 
@@ -279,11 +280,42 @@ __device__ __forceinline__ void grid_partial_groups(DD (&v)[N], double* partials
 }
 
 // Consumer side: the N sums over the ng group totals, identical in every wave of every launch
-// (same tree); returns the DD values collapsed to double.  ng <= 64: one wave, redundantly in
-// every wave; ng > 64: the whole workgroup (fixed strided order + block tree, LDS broadcast;
-// every thread of the workgroup must call it).
+// (same tree); returns the DD values collapsed to double.  ng <= 256: one wave, redundantly in
+// every wave (lane l sums entries l, l + 64, l + 128, l + 192 in that order, then the butterfly);
+// ng > 256: the whole workgroup (fixed strided order + block tree, LDS broadcast; every thread of
+// the workgroup must call it).
 template <int N>
 __device__ __forceinline__ void group_sum_dd(const double* group_in, int ng, double (&out)[N]) {
+  if (ng > 64 && ng <= 256) {
+    const int lane = threadIdx.x & 63;
+    DD a[N];
+    double gs[4][N], gc[4][N];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int g = lane + 64 * u;
+#pragma unroll
+      for (int j = 0; j < N; ++j) {
+        const size_t k = (size_t(g < ng ? g : 0) * N + j) * 2;
+        gs[u][j] = group_in[k + 0];
+        gc[u][j] = group_in[k + 1];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      a[j] = dd_zero();
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (lane + 64 * u < ng) a[j] = dd_add(a[j], DD{gs[u][j], gc[u][j]});
+    }
+    wave_reduce_dd<N>(a);
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const double s = __shfl(a[j].s, 0, 64);
+      const double c = __shfl(a[j].c, 0, 64);
+      out[j] = dd_value(DD{s, c});
+    }
+    return;
+  }
   if (ng > 64) {
     __shared__ DD lds[16 * N];
     __shared__ double res[N];

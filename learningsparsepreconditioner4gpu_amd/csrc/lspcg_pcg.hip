@@ -842,7 +842,7 @@ struct lspcg_solver {
        *d = nullptr;
   bool split = false;   // current ext_spai schedule uses the split reductions (set_spai decides)
   bool allow_split = true;  // LSPCG_SPLIT_REDUCE=0 keeps the last-arriver reductions
-  int split_mode = 1;
+  int split_mode = -1;  // -1 auto (by grid size), 1 groups, 2 no groups (LSPCG_SPLIT_REDUCE)
   double* groups = nullptr;  // [GZ: <= 4096 x 2 dots x DD | GQ: <= 4096 x DD]
   int gsz_l = 1, ng_l = 1, gsz_a = 1, ng_a = 1;  // group size / count of the KB and KC launches
   hipEvent_t* tev = nullptr;  // lspcg_solver_time_kernels: an event recorded after every launch
@@ -1353,9 +1353,15 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     std::fprintf(stderr, "\n");
   }
   s->split = s->allow_split && s->sp[0] && s->sp[1] && s->sp[2];
-  if (s->split) {  // <= 64 groups per reducing launch (or, LSPCG_SPLIT_REDUCE=2, no groups at all)
-    const bool nogroups = s->split_mode == 2;
-    auto groups = [nogroups](int64_t grid, int* gsz, int* ng) {
+  if (s->split) {
+    // <= 64 groups per reducing launch; no groups at all (the consumers sum every workgroup's
+    // partial) for grids of <= kNoGroupGrid workgroups -- mid-size systems, where the group ticket's
+    // round trip costs more than the consumers' extra loads (Poisson 256^2: 20.6 vs 22.0 us per
+    // iteration; at 1 M rows, 1536 workgroups, the groups win: 91.4 vs 94.3).
+    // LSPCG_SPLIT_REDUCE=1 / 2 force groups / no groups.
+    const int mode = s->split_mode;
+    auto groups = [mode](int64_t grid, int* gsz, int* ng) {
+      const bool nogroups = mode == 2 || (mode < 0 && grid <= kNoGroupGrid);
       *gsz = nogroups ? 1 : int((grid + kMaxGroups - 1) / kMaxGroups);
       *ng = int((grid + *gsz - 1) / *gsz);
     };
