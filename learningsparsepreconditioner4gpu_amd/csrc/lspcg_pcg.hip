@@ -1859,6 +1859,120 @@ __global__ void __launch_bounds__(kThreads) k_batch_update_r(BatchMap m, const P
   r[i] = ri - T(St->alpha) * qi;
 }
 
+// ---- consumer-sum mode (windows whose systems have <= 128 tiles each): KB / KC only store
+// per-tile partials (grid_partial_groups, gsz = 1: no tickets) and every UP / UR workgroup sums its
+// system's tile partials itself (group_sum_dd, one wave for <= 256) ------------------------------
+// init: r_0 = b - A x0 ; per-tile partials of ‖r_0‖², ‖b‖²
+template <typename T>
+struct EpiResidTile {
+  static constexpr int NDOT = 2;
+  static constexpr bool GROUPS = true;
+  T* r;
+  const T* b;
+  double* partials;
+  unsigned* ticket;
+  double* group_out;
+  int gsz;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
+    const T bi = gld(b + i);
+    const T ri = bi - s;
+    gst(r + i, ri);
+    dd_fma(dots[0], double(ri), double(ri));
+    dd_fma(dots[1], double(bi), double(bi));
+  }
+  __device__ __forceinline__ void fin(const double*) const {}
+};
+
+// one workgroup per system: the init state from the system's tile partials (EpiResid::fin)
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_batch_init(PcgState* S, const int32_t* __restrict__ tile0,
+                                                         const double* __restrict__ gi) {
+  const int sys = blockIdx.x;
+  const int t0 = tile0[sys], t1 = tile0[sys + 1];
+  double v[2];
+  group_sum_dd<2>(gi + size_t(t0) * 4, t1 - t0, v);
+  if (threadIdx.x) return;
+  PcgState* St = S + sys;
+  St->rr = round_to<T>(v[0]);
+  St->bb = round_to<T>(v[1]);
+  const double bn = double(tsqrt<T>(T(St->bb)));
+  St->atol = fmax(0.0, St->rtol * bn);
+  St->rho = St->rr;
+  St->alpha = 0.0;
+  St->iter = 0;
+  St->done = (bn == 0.0) ? 1 : 0;
+  if (St->hist) St->hist[0] = double(tsqrt<T>(T(St->rr)));
+}
+
+// consumer-sum mode: UP of the split schedule (k_update_p_g) for the tile's system, summing the
+// system's tile partials itself
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_batch_update_p_sums(BatchMap m, PcgState* S, const double* __restrict__ gz,
+                                                             const T* __restrict__ z, T* __restrict__ p,
+                                                             T* __restrict__ x) {
+  const int sys = m.etile_sys[blockIdx.x];
+  PcgState* St = S + sys;
+  if (St->done) return;
+  const int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  const T zi = z[i], pi = p[i], xi = x[i];
+  const int t0 = m.tile0[sys], t1 = m.tile0[sys + 1];
+  const int64_t k = St->iter;
+  double v[2];
+  group_sum_dd<2>(gz + size_t(t0) * 4, t1 - t0, v);
+  const double rho = round_to<T>(v[0]);
+  const double rr = k > 0 ? round_to<T>(v[1]) : St->rr;
+  int code = 0;
+  if (k >= St->max_iter) {
+    code = 2;
+  } else {
+    const double rn = double(tsqrt<T>(T(rr)));
+    if (rn < St->atol) code = 1;
+    else if (!(rn == rn) || rn == INFINITY) code = 3;
+  }
+  if (int64_t(blockIdx.x) == int64_t(t0) * m.bs && threadIdx.x == 0) {
+    if (k > 0) {
+      St->rr = rr;
+      if (St->hist) St->hist[k] = double(tsqrt<T>(T(rr)));
+    }
+    if (code) St->done = code;
+  }
+  if (code) return;
+  const bool first = k == 0;
+  const T beta = first ? T(0) : T(rho) / T(St->rho);
+  const T alpha = T(St->alpha);
+  if (!first) x[i] = xi + alpha * pi;
+  p[i] = first ? zi : (pi * beta) + zi;
+}
+
+// consumer-sum mode: UR of the split schedule (k_update_r_g) for the tile's system
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_batch_update_r_sums(BatchMap m, PcgState* S, const double* __restrict__ gz,
+                                                             const double* __restrict__ gq, const T* __restrict__ q,
+                                                             T* __restrict__ r) {
+  const int sys = m.etile_sys[blockIdx.x];
+  PcgState* St = S + sys;
+  if (St->done) return;
+  const int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x;
+  const T ri = r[i], qi = q[i];
+  const int t0 = m.tile0[sys], t1 = m.tile0[sys + 1];
+  double vz[2], vq[1];
+  group_sum_dd<2>(gz + size_t(t0) * 4, t1 - t0, vz);
+  group_sum_dd<1>(gq + size_t(t0) * 2, t1 - t0, vq);
+  const double rho = round_to<T>(vz[0]);
+  const double pq = round_to<T>(vq[0]);
+  const T alpha = T(rho) / T(pq);
+  if (int64_t(blockIdx.x) == int64_t(t0) * m.bs && threadIdx.x == 0) {
+    St->rho_prev = St->rho;
+    St->rho = rho;
+    St->pq = pq;
+    St->alpha = double(alpha);
+    St->iter = St->iter + 1;
+  }
+  r[i] = ri - alpha * qi;
+}
+
+
 template <typename T>
 __global__ void __launch_bounds__(kThreads) k_batch_x_fixup(BatchMap m, const PcgState* S, const T* __restrict__ p,
                                                             T* __restrict__ x) {
@@ -1896,6 +2010,9 @@ struct lspcg_batch {
   int32_t* tk0 = nullptr;
   double* partials = nullptr;  // per-tile dot partials (<= 2 dots, DD each)
   unsigned* tickets = nullptr;  // per system: top line + one line per kTicketGroup tiles (batch_sys_reduce)
+  bool sums = false;            // consumer-sum reductions (every system <= 128 tiles; LSPCG_BATCH_REDUCE)
+  double* gsum = nullptr;       // consumer-sum partials: init (2 dots) | KB (2 dots) | KC (1 dot), per tile
+  int64_t ntiles = 0;
   PcgState* S = nullptr;
   PcgState* hS = nullptr;  // pinned: 2 poll slots x nsys
   double* dhist = nullptr;
@@ -1926,6 +2043,17 @@ static int launch_it_tiles(lspcg_solver* s, int w, const T* x, Pro pro, Epi epi,
 template <typename T>
 static int enqueue_batch_init(lspcg_batch* bt, hipStream_t st) {
   lspcg_solver* s = bt->s;
+  if (bt->sums) {
+    int rc = launch_it_tiles<T>(s, 0, static_cast<const T*>(s->x), ProNone{},
+                                EpiResidTile<T>{static_cast<T*>(s->r), static_cast<const T*>(s->b), nullptr, nullptr,
+                                                bt->gsum, 1},
+                                st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_batch_init<T>, dim3(bt->nsys), dim3(kThreads), 0, st, bt->S,
+                       static_cast<const int32_t*>(bt->tile0), static_cast<const double*>(bt->gsum));
+    LSPCG_HIP(hipGetLastError());
+    return LSPCG_OK;
+  }
   return launch_it_tiles<T>(s, 0, static_cast<const T*>(s->x), ProNone{},
                             EpiResidB<T>{static_cast<T*>(s->r), static_cast<const T*>(s->b), bt->S, bt->partials,
                                          bt->tickets, batch_map(bt)},
@@ -1945,9 +2073,24 @@ static int enqueue_batch_iteration(lspcg_batch* bt, hipStream_t st) {
   const ProTile pro{bt->S, m};
   const dim3 eg(unsigned(bt->ntot / kThreads));
   int rc = launch_it_tiles<T>(s, 2, static_cast<const T*>(r), pro, EpiT<T, false>{t, nullptr}, st);
-  if (!rc)
+  if (rc) return rc;
+  if (bt->sums) {
+    double* gz = bt->gsum + 4 * bt->ntiles;
+    double* gq = bt->gsum + 8 * bt->ntiles;
     rc = launch_it_tiles<T>(s, 1, static_cast<const T*>(t), pro,
-                            EpiZB<T>{z, r, T(s->eps), bt->S, bt->partials, bt->tickets, m}, st);
+                            EpiZG<T, false>{z, r, nullptr, T(s->eps), nullptr, nullptr, gz, 1}, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_batch_update_p_sums<T>, eg, dim3(kThreads), 0, st, m, bt->S, static_cast<const double*>(gz),
+                       static_cast<const T*>(z), p, x);
+    rc = launch_it_tiles<T>(s, 0, static_cast<const T*>(p), pro, EpiQG<T>{q, p, nullptr, nullptr, gq, 1}, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_batch_update_r_sums<T>, eg, dim3(kThreads), 0, st, m, bt->S, static_cast<const double*>(gz),
+                       static_cast<const double*>(gq), static_cast<const T*>(q), r);
+    LSPCG_HIP(hipGetLastError());
+    return LSPCG_OK;
+  }
+  rc = launch_it_tiles<T>(s, 1, static_cast<const T*>(t), pro,
+                          EpiZB<T>{z, r, T(s->eps), bt->S, bt->partials, bt->tickets, m}, st);
   if (rc) return rc;
   hipLaunchKernelGGL(k_batch_update_p<T>, eg, dim3(kThreads), 0, st, m, static_cast<const PcgState*>(bt->S),
                      static_cast<const T*>(z), p, x);
@@ -2026,7 +2169,7 @@ int lspcg_batch_destroy(lspcg_batch* bt) {
   if (bt->s) lspcg_solver_destroy(bt->s);
   if (bt->Acat) lspcg_mat_destroy(bt->Acat);
   if (bt->Lcat) lspcg_mat_destroy(bt->Lcat);
-  for (void* v : {(void*)bt->etile_sys, (void*)bt->tile0, (void*)bt->tk0, (void*)bt->partials, (void*)bt->tickets, (void*)bt->S,
+  for (void* v : {(void*)bt->etile_sys, (void*)bt->tile0, (void*)bt->tk0, (void*)bt->gsum, (void*)bt->partials, (void*)bt->tickets, (void*)bt->S,
                   (void*)bt->dhist})
     (void)hipFree(v);
   (void)hipHostFree(bt->hS);
@@ -2089,6 +2232,15 @@ int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, cons
   LSPCG_HIP(hipMemcpy(bt->etile_sys, esys.data(), sizeof(int32_t) * esys.size(), hipMemcpyHostToDevice));
   LSPCG_HIP(hipMemcpy(bt->tile0, t0.data(), sizeof(int32_t) * t0.size(), hipMemcpyHostToDevice));
   LSPCG_HIP(hipMalloc(&bt->partials, sizeof(double) * 4 * ntiles));
+  // reductions: consumer sums when every system has <= 128 tiles (C5 heat, <= 117 tiles: 25.6 vs
+  // 26.8 us per lockstep iteration), else per-system last arrivers (8 x Poisson 256^2, 256 tiles:
+  // 47.1 vs 49.9); LSPCG_BATCH_REDUCE=0 / 1 forces either
+  int max_nt = 0;
+  for (int k = 0; k < nsys; ++k) max_nt = std::max(max_nt, t0[k + 1] - t0[k]);
+  bt->sums = max_nt <= 128;
+  if (const char* e = std::getenv("LSPCG_BATCH_REDUCE")) bt->sums = e[0] == '1';
+  bt->ntiles = ntiles;
+  LSPCG_HIP(hipMalloc(&bt->gsum, sizeof(double) * 10 * ntiles));
   LSPCG_HIP(hipMalloc(&bt->tickets, sizeof(unsigned) * kTicketStride * lines));
   LSPCG_HIP(hipMemset(bt->tickets, 0, sizeof(unsigned) * kTicketStride * lines));
   LSPCG_HIP(hipMalloc(&bt->S, sizeof(PcgState) * nsys));

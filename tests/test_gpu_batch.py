@@ -57,7 +57,11 @@ def _rel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
 
 
-def test_batch_matches_single_and_oracle(gpu_ctx):
+@pytest.mark.parametrize("reduce", ["auto", "0", "1"])
+def test_batch_matches_single_and_oracle(gpu_ctx, monkeypatch, reduce):
+    """reduce: the window's reductions (auto / 0 = per-system last arrivers / 1 = consumer sums)."""
+    if reduce != "auto":
+        monkeypatch.setenv("LSPCG_BATCH_REDUCE", reduce)
     eps = 3e-3
     As = _systems()
     Ls = [_cases.spai_like(A, seed=k) for k, A in enumerate(As)]
@@ -89,7 +93,9 @@ def test_batch_fp32(gpu_ctx):
         assert _rel(x.astype(np.float64), x1.astype(np.float64)) <= 1e-5
 
 
-def test_batch_bsr3(gpu_ctx):
+@pytest.mark.parametrize("reduce", ["0", "1"])
+def test_batch_bsr3(gpu_ctx, monkeypatch, reduce):
+    monkeypatch.setenv("LSPCG_BATCH_REDUCE", reduce)
     eps = 1e-3
     As = []
     for dims in ((9, 5, 5), (12, 6, 5), (5, 4, 4)):

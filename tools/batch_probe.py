@@ -64,7 +64,13 @@ def main():
         # the same systems as ONE lockstep batch (linalg.BatchedConjugateGradient)
         from learningsparsepreconditioner4gpu_amd.linalg import BatchedConjugateGradient
 
-        for rtol in (1e-6, 1e-8):
+        import os
+
+        for rtol, red in ((1e-6, "auto"), (1e-8, "auto"), (1e-8, "0"), (1e-8, "1")):
+            if red == "auto":
+                os.environ.pop("LSPCG_BATCH_REDUCE", None)
+            else:
+                os.environ["LSPCG_BATCH_REDUCE"] = red
             B = BatchedConjugateGradient([j[3] for j in jobs], [j[4] for j in jobs], ws.epsilon)
             bs = [j[1] for j in jobs]
             xs = [torch.zeros_like(b) for b in bs]
@@ -85,7 +91,7 @@ def main():
                 x = torch.zeros_like(j[1])
                 ref.append(j[0].solve(j[1], x, rtol=rtol)[0])
             tot = sum(its)
-            rec = {"set": name, "mode": "batch", "rtol": rtol, "systems": len(jobs), "iters_total": tot,
+            rec = {"set": name, "mode": "batch", "reduce": red, "rtol": rtol, "systems": len(jobs), "iters_total": tot,
                    "wall_ms": best * 1e3, "us_per_iter_per_system": best * 1e6 / tot, "max_iters": max(its),
                    "us_per_lockstep_iter": best * 1e6 / max(its), "iters_equal_single": its == ref}
             print(json.dumps(rec), flush=True)
