@@ -143,9 +143,9 @@ int lspcg_solver_set_ic(lspcg_solver* s, double* t_prec_ms);
  * of completed iterations, max_iter <= 0 means n.  res_hist (host, nullable, length
  * max_iter+2) receives ||r_k|| for k = 0..iters.  t_solve_ms = device time of the solve.
  * Returns LSPCG_OK when converged, LSPCG_NOT_CONVERGED when max_iter was reached.
- * Scalar systems with n <= LSPCG_SMALL_N (env read at solver creation; default 1024, 0 = off,
- * at most 2560; IC excluded) run the whole loop in one single-workgroup launch -- same bits as
- * the multi-kernel schedule. */
+ * Scalar systems with n <= LSPCG_SMALL_N (env read at solver creation; default 3072, 0 = off;
+ * at most 3 rows per thread of 1024 and 3 vectors in 60 KiB of LDS: 2560 in fp64; IC excluded)
+ * run the whole loop in one single-workgroup launch -- same bits as the multi-kernel schedule. */
 int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int64_t max_iter,
                        int64_t* iters, double* res_hist, double* t_solve_ms);
 /* Measurement only (bench.py): `iters` iterations of the split ext_spai schedule from x0 = 0,

@@ -540,7 +540,8 @@ struct CsrView {
 };
 
 constexpr int kSmallThreads = 512;  // 2 waves per SIMD: the compensated reductions are VALU work
-constexpr int kSmallRows = 5;       // largest rows per thread (template R = 1, 2 or 5)
+constexpr int kSmallThreadsBig = 1024;  // n > 1024: 4 waves per SIMD keep rows per thread <= 3
+constexpr int kSmallRows = 5;       // largest rows per thread (template R = 1, 2 or 5 at 512 threads)
 constexpr int64_t kSmallLds = 61440;  // dynamic LDS: 3 gathered vectors
 constexpr int kSmallQB = 2;  // SELL groups (4 entries each) loaded per wait (4 measured slower: 13.0 vs 9.8 us per iteration)
 
@@ -621,7 +622,7 @@ __device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, i
 // butterflies, one barrier, then every wave sums the 8 wave totals with an 8-lane butterfly and
 // takes lane 0's (one LDS round trip instead of a serial sum in thread 0 and a broadcast).  `lds`
 // is written again only after later barriers (each reduction site has its own buffer).
-template <typename T, int N>
+template <typename T, int N, int TH>
 __device__ __forceinline__ void small_dots(DD (&v)[N], DD* lds, double (&out)[N]) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -633,24 +634,24 @@ __device__ __forceinline__ void small_dots(DD (&v)[N], DD* lds, double (&out)[N]
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    DD a = lane < kSmallThreads / 64 ? lds[lane * N + j] : dd_zero();
+    DD a = lane < TH / 64 ? lds[lane * N + j] : dd_zero();
 #pragma unroll
-    for (int m = 1; m < kSmallThreads / 64; m <<= 1) a = dd_add(a, dd_shfl_xor(a, m));
+    for (int m = 1; m < TH / 64; m <<= 1) a = dd_add(a, dd_shfl_xor(a, m));
     out[j] = round_to<T>(dd_value(DD{__shfl(a.s, 0, 64), __shfl(a.c, 0, 64)}));
   }
 }
 
-template <typename T, int PRE, int R>
-__global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState* S, CsrView A, CsrView L,
-                                                             CsrView LT, const T* __restrict__ d, T* x, T* r, T* p) {
+template <typename T, int PRE, int R, int TH>
+__global__ void __launch_bounds__(TH) k_pcg_small(int32_t n, PcgState* S, CsrView A, CsrView L, CsrView LT,
+                                                  const T* __restrict__ d, T* x, T* r, T* p) {
   constexpr bool SPAI = PRE == LSPCG_PRECOND_EXT_SPAI || PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
   constexpr bool SCALED = PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
   extern __shared__ __attribute__((aligned(16))) unsigned char small_lds[];
   T* rs = reinterpret_cast<T*>(small_lds);
   T* ts = rs + n;
   T* ps = ts + n;
-  __shared__ DD lds_z[kSmallThreads / 64 * 2];
-  __shared__ DD lds_q[kSmallThreads / 64];
+  __shared__ DD lds_z[TH / 64 * 2];
+  __shared__ DD lds_q[TH / 64];
   if (S->done) return;  // ‖b‖ = 0 (init)
   const int tid = threadIdx.x;
   const T eps = T(S->eps);
@@ -667,7 +668,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
   T xr[R], rr_[R], pr[R], dr[R];
 #pragma unroll
   for (int m = 0; m < R; ++m) {
-    row[m] = tid + kSmallThreads * m;
+    row[m] = tid + TH * m;
     own[m] = row[m] < n;
     const int32_t i = own[m] ? row[m] : 0;
     auto range = [&](const CsrView& M, int32_t& b, int32_t& e) {  // CSR entries or SELL groups
@@ -717,7 +718,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
       }
     }
     double v2[2];
-    small_dots<T, 2>(dz, lds_z, v2);
+    small_dots<T, 2, TH>(dz, lds_z, v2);
     const double rr = k > 0 ? v2[1] : rr0;
     if (k >= max_iter) {
       code = 2;
@@ -752,7 +753,7 @@ __global__ void __launch_bounds__(kSmallThreads) k_pcg_small(int32_t n, PcgState
       if (own[m]) dd_fma(dq[0], double(pr[m]), double(qr[m]));
     }
     double v1[1];
-    small_dots<T, 1>(dq, lds_q, v1);
+    small_dots<T, 1, TH>(dq, lds_q, v1);
     pq = v1[0];
     alpha = T(rho) / T(pq);
 #pragma unroll
@@ -876,8 +877,8 @@ struct lspcg_solver {
   int svd[3] = {0, 0, 0};
   double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
   int64_t dhist_cap = 0;
-  int64_t small_n = 1024;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it): <= 2 rows
-                           // per thread; 5 rows lose to the 5-kernel schedule
+  int64_t small_n = 3072;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it; also bounded by
+                           // 3 rows per thread at 1024 threads and the LDS of 3 vectors: 2560 in fp64)
   bool small_sell = true;  // k_pcg_small reads the SELL copies (LSPCG_SMALL_SELL=0: the CSR views)
 };
 
@@ -1165,9 +1166,15 @@ static int enqueue_fixup(lspcg_solver* s, hipStream_t st) {
   return LSPCG_OK;
 }
 
+// LSPCG_SMALL_BIG=0: n in (1024, 2560] on the previous 512-thread, 5-row one-workgroup kernel
+static bool small_big() {
+  static const bool v = [] { const char* e = std::getenv("LSPCG_SMALL_BIG"); return !(e && e[0] == '0'); }();
+  return v;
+}
+
 static bool small_path(const lspcg_solver* s) {
   if (s->n <= 0 || s->n > s->small_n || s->precond == LSPCG_PRECOND_IC || s->Av.block_size != 1) return false;
-  if (s->n > int64_t(kSmallThreads) * kSmallRows || 3 * s->n * (s->dtype == LSPCG_F32 ? 4 : 8) > kSmallLds) return false;
+  if (s->n > (small_big() ? int64_t(kSmallThreadsBig) * 3 : int64_t(kSmallThreads) * kSmallRows) || 3 * s->n * (s->dtype == LSPCG_F32 ? 4 : 8) > kSmallLds) return false;
   if (s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED)
     return s->Lv.block_size == 1 && s->LTv.block_size == 1;
   return true;
@@ -1198,28 +1205,42 @@ static int launch_small(lspcg_solver* s, hipStream_t st) {
   auto* p = static_cast<T*>(s->p);
   const T* d = static_cast<const T*>(s->d);
   const int32_t n = int32_t(s->n);
-  const dim3 g(1), b(kSmallThreads);
+  const dim3 g(1);
   const size_t lds = 3 * sizeof(T) * size_t(n);
-  auto go = [&](auto rows) {
+  auto go = [&](auto rows, auto threads) {
     constexpr int R = decltype(rows)::value;
+    constexpr int TH = decltype(threads)::value;
+    const dim3 b(TH);
     switch (s->precond) {
       case LSPCG_PRECOND_NONE:
-        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_NONE, R>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_NONE, R, TH>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
         break;
       case LSPCG_PRECOND_DIAGONAL:
-        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_DIAGONAL, R>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_DIAGONAL, R, TH>), g, b, lds, st, n, s->S, A, L, LT, d, x, r,
+                           p);
         break;
       case LSPCG_PRECOND_EXT_SPAI:
-        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI, R>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI, R, TH>), g, b, lds, st, n, s->S, A, L, LT, d, x, r,
+                           p);
         break;
       default:
-        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI_SCALED, R>), g, b, lds, st, n, s->S, A, L, LT, d, x, r,
-                           p);
+        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI_SCALED, R, TH>), g, b, lds, st, n, s->S, A, L, LT, d,
+                           x, r, p);
     }
   };
-  if (n <= kSmallThreads) go(std::integral_constant<int, 1>{});
-  else if (n <= 2 * kSmallThreads) go(std::integral_constant<int, 2>{});
-  else go(std::integral_constant<int, kSmallRows>{});
+  using I = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using T512 = std::integral_constant<int, kSmallThreads>;
+  using T1024 = std::integral_constant<int, kSmallThreadsBig>;
+  // n <= 1024: 512 threads, <= 2 rows each (the measured best there); above: 1024 threads, 2-3 rows
+  // (LSPCG_SMALL_BIG=0: the previous 512-thread, 5-row variant)
+  const bool big = small_big();
+  if (n <= kSmallThreads) go(I{}, T512{});
+  else if (n <= 2 * kSmallThreads) go(I2{}, T512{});
+  else if (!big) go(std::integral_constant<int, kSmallRows>{}, T512{});
+  else if (n <= 2 * kSmallThreadsBig) go(I2{}, T1024{});
+  else go(I3{}, T1024{});
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }

@@ -116,6 +116,30 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
         assert np.array_equal(out[0][2], o[2]), name
 
 
+@pytest.mark.parametrize("grid", [11, 13])
+def test_small_solve_1024_threads(gpu_ctx, grid, monkeypatch):
+    """n = 1331 (2 rows per thread) and 2197 (3 rows): the 1024-thread one-workgroup solve gives the
+    5-kernel schedule's count, history and iterate bit for bit."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    A = sp.csr_matrix(P.kuhn_laplacian(grid, 1e-2))
+    n = A.shape[0]
+    b = torch.from_numpy(A @ np.ones(n)).cuda()
+    out = []
+    for small in ("0", "4096"):
+        monkeypatch.setenv("LSPCG_SMALL_N", small)
+        for pre in ("none", "ext_spai"):
+            s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=pre)
+            if pre == "ext_spai":
+                s.set_spai(_cases.spai_like(A), 1e-3)
+            x = torch.zeros(n, dtype=torch.float64, device="cuda")
+            it, conv, _, hist = s.solve(b, x, rtol=1e-10, return_history=True)
+            out.append((it, x.cpu().numpy(), hist))
+    for a, c in ((0, 2), (1, 3)):
+        assert out[a][0] == out[c][0]
+        assert np.array_equal(out[a][1], out[c][1]) and np.array_equal(out[a][2], out[c][2])
+
+
 def _expected_kind(A, max_pad=2.0):
     """lspcg_mat_prepare_spmv's rule: SELL-64 if the padded slots stay <= max_pad * nnz, with
     16-bit column offsets if every |col - 64*slice| <= 32767."""
