@@ -51,7 +51,7 @@ extern "C" {
 #define LSPCG_PRECOND_DIAGONAL 1
 #define LSPCG_PRECOND_EXT_SPAI 2
 #define LSPCG_PRECOND_EXT_SPAI_SCALED 3
-/* IC(0) of A, applied by two level-scheduled triangular solves (pymathprim "ic") */
+/* IC(0) of A, applied by two sync-free triangular solves (pymathprim "ic") */
 #define LSPCG_PRECOND_IC 4
 
 typedef struct lspcg_ctx lspcg_ctx;
@@ -124,8 +124,9 @@ int lspcg_ic0(const lspcg_mat* A, lspcg_mat** L, double* t_ms);
 /* AINV(0): *L = Z D^{-1/2} (Z unit upper, pattern triu(A)) so that L L^T = Z D^{-1} Z^T ~ A^{-1};
  * use it as an ext_spai factor with epsilon = 0 */
 int lspcg_ainv0(const lspcg_mat* A, lspcg_mat** L, double* t_ms);
-/* x = T^{-1} b, T triangular (lower != 0: diagonal stored last in each row; else first),
- * level-scheduled; b, x device vectors of T's dtype */
+/* x = T^{-1} b, T triangular (lower != 0: diagonal stored last in each row; else first): one
+ * sync-free launch over the level-ordered rows (LSPCG_TRSV_LEVELS=1: one launch per level, same
+ * bits); b, x device vectors of T's dtype */
 int lspcg_trsv(const lspcg_mat* T, int lower, const void* b, void* x);
 /* compensated, deterministic dot product of two device vectors; result to host */
 int lspcg_dot(lspcg_ctx* ctx, int64_t n, int dtype, const void* x, const void* y, double* out);
