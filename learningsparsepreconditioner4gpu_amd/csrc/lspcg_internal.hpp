@@ -280,32 +280,34 @@ __device__ __forceinline__ void grid_partial_groups(DD (&v)[N], double* partials
 }
 
 // Consumer side: the N sums over the ng group totals, identical in every wave of every launch
-// (same tree); returns the DD values collapsed to double.  ng <= 256: one wave, redundantly in
-// every wave (lane l sums entries l, l + 64, l + 128, l + 192 in that order, then the butterfly);
-// ng > 256: the whole workgroup (fixed strided order + block tree, LDS broadcast; every thread of
+// (same tree); returns the DD values collapsed to double.  ng <= 512: one wave, redundantly in
+// every wave (lane l sums entries l, l + 64, l + 128, ... in that order, then the butterfly);
+// ng > 512: the whole workgroup (fixed strided order + block tree, LDS broadcast; every thread of
 // the workgroup must call it).
 template <int N>
 __device__ __forceinline__ void group_sum_dd(const double* group_in, int ng, double (&out)[N]) {
-  if (ng > 64 && ng <= 256) {
+  if (ng > 64 && ng <= 512) {
     const int lane = threadIdx.x & 63;
     DD a[N];
-    double gs[4][N], gc[4][N];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int g = lane + 64 * u;
+    for (int j = 0; j < N; ++j) a[j] = dd_zero();
+    for (int u0 = 0; u0 < 8 && 64 * u0 < ng; u0 += 4) {  // wave-uniform: 1 or 2 rounds of 4 loads
+      double gs[4][N], gc[4][N];
 #pragma unroll
-      for (int j = 0; j < N; ++j) {
-        const size_t k = (size_t(g < ng ? g : 0) * N + j) * 2;
-        gs[u][j] = group_in[k + 0];
-        gc[u][j] = group_in[k + 1];
+      for (int u = 0; u < 4; ++u) {
+        const int g = lane + 64 * (u0 + u);
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+          const size_t k = (size_t(g < ng ? g : 0) * N + j) * 2;
+          gs[u][j] = group_in[k + 0];
+          gc[u][j] = group_in[k + 1];
+        }
       }
-    }
 #pragma unroll
-    for (int j = 0; j < N; ++j) {
-      a[j] = dd_zero();
+      for (int j = 0; j < N; ++j)
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (lane + 64 * u < ng) a[j] = dd_add(a[j], DD{gs[u][j], gc[u][j]});
+        for (int u = 0; u < 4; ++u)
+          if (lane + 64 * (u0 + u) < ng) a[j] = dd_add(a[j], DD{gs[u][j], gc[u][j]});
     }
     wave_reduce_dd<N>(a);
 #pragma unroll
