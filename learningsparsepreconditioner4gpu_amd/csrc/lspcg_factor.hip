@@ -222,14 +222,18 @@ int build_levels(lspcg_ctx* ctx, int64_t n, const int32_t* rp, const int32_t* ci
   LSPCG_HIP(hipMalloc(&order, sizeof(int32_t) * n));
   LSPCG_HIP(hipMalloc(&changed, sizeof(int)));
   LSPCG_HIP(hipMemsetAsync(lev, 0, sizeof(int32_t) * n, st));
-  // relaxation sweeps until a sweep changes nothing (<= longest dependency chain + 1 sweeps)
+  // relaxation sweeps until a round of sweeps changes nothing (<= longest dependency chain + 1
+  // sweeps); kSweepRound sweeps per host check of the flag (extra sweeps change nothing)
+  constexpr int kSweepRound = 8;
   int h = 1;
-  for (int64_t sweep = 0; h && sweep <= n; ++sweep) {
+  for (int64_t sweep = 0; h && sweep <= n; sweep += kSweepRound) {
     LSPCG_HIP(hipMemsetAsync(changed, 0, sizeof(int), st));
-    if (lower)
-      hipLaunchKernelGGL(k_level_sweep<true>, dim3(fgrid(n)), dim3(kThreads), 0, st, n, rp, ci, lev, changed);
-    else
-      hipLaunchKernelGGL(k_level_sweep<false>, dim3(fgrid(n)), dim3(kThreads), 0, st, n, rp, ci, lev, changed);
+    for (int r = 0; r < kSweepRound; ++r) {
+      if (lower)
+        hipLaunchKernelGGL(k_level_sweep<true>, dim3(fgrid(n)), dim3(kThreads), 0, st, n, rp, ci, lev, changed);
+      else
+        hipLaunchKernelGGL(k_level_sweep<false>, dim3(fgrid(n)), dim3(kThreads), 0, st, n, rp, ci, lev, changed);
+    }
     LSPCG_HIP(hipMemcpyAsync(&h, changed, sizeof(int), hipMemcpyDeviceToHost, st));
     LSPCG_HIP(hipStreamSynchronize(st));
   }
