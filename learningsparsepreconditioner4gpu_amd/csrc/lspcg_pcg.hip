@@ -355,6 +355,7 @@ template <typename T, bool SCALED>
 struct EpiZG {
   static constexpr int NDOT = 2;
   static constexpr bool GROUPS = true;
+  static constexpr bool PREFETCH = !SCALED;  // r[i] loaded before the row's gathers (SELL kernel)
   T* z;
   const T* r;
   const T* d;
@@ -364,6 +365,13 @@ struct EpiZG {
   double* group_out;
   int gsz;
   __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ T prefetch(int64_t i) const { return gld(r + i); }
+  __device__ __forceinline__ void row_pf(int64_t i, T s, DD* dots, T ri) const {
+    const T zi = s + eps * ri;
+    gst(z + i, zi);
+    dd_fma(dots[0], double(ri), double(zi));
+    dd_fma(dots[1], double(ri), double(ri));
+  }
   __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
     const T ri = gld(r + i);
     T zi;
@@ -380,6 +388,7 @@ template <typename T>
 struct EpiQG {
   static constexpr int NDOT = 1;
   static constexpr bool GROUPS = true;
+  static constexpr bool PREFETCH = true;  // p[i] loaded before the row's gathers (SELL kernel)
   T* q;
   const T* p;
   double* partials;
@@ -387,6 +396,11 @@ struct EpiQG {
   double* group_out;
   int gsz;
   __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ T prefetch(int64_t i) const { return gld(p + i); }
+  __device__ __forceinline__ void row_pf(int64_t i, T s, DD* dots, T pi) const {
+    gst(q + i, s);
+    dd_fma(dots[0], double(pi), double(s));
+  }
   __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
     gst(q + i, s);
     dd_fma(dots[0], double(gld(p + i)), double(s));

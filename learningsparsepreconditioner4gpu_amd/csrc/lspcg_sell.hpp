@@ -92,6 +92,14 @@ struct Vec4Ld<double> {
 
 using i16x4 = short __attribute__((ext_vector_type(4)));
 
+// Epilogues with a PREFETCH member (a device pointer) read one own-row value in row(); the SELL
+// kernel loads it before the row's slot loop so it does not add a memory latency after the
+// gathers, and passes it to row_pf() (latency-bound mid-size systems).
+template <class E, class = void>
+struct epi_prefetch : std::false_type {};
+template <class E>
+struct epi_prefetch<E, std::void_t<decltype(E::PREFETCH)>> : std::bool_constant<E::PREFETCH> {};
+
 // 256-thread workgroups = 4 slices = one 256-row tile (the same row tiles as k_spmv, so the
 // prologue / epilogue functors and the dot-product reduction are shared).  QB groups of 4
 // entries are loaded per lane before the first gather (branch-free: the group index is
@@ -133,6 +141,10 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
       const VT* vp = a.vals + 256 * int64_t(g0) + 4 * lane;
       const CT* cp = a.col + 256 * int64_t(g0) + 4 * lane;
       T acc = T(0);
+      T pf = T(0);
+      if constexpr (epi_prefetch<Epi>::value) {
+        if (i < a.n) pf = epi.prefetch(i);
+      }
       for (int q0 = 0; q0 < nq; q0 += QB) {
         VT v[QB][4];
         int c[QB][4];
@@ -170,7 +182,11 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
           for (int j = 0; j < 4; ++j)
             if (m[u][j]) acc = acc + T(v[u][j]) * xv[u][j];
       }
-      if (i < a.n) epi.row(i, acc, d);
+      if constexpr (epi_prefetch<Epi>::value) {
+        if (i < a.n) epi.row_pf(i, acc, d, pf);
+      } else {
+        if (i < a.n) epi.row(i, acc, d);
+      }
     }
   }
   finish_epi_dots<Epi>(d, epi);
