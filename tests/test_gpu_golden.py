@@ -150,13 +150,17 @@ def test_folder_dataset_through_hot_path(gpu_ctx, rhs):
         assert rec.iters == it_o, (rec.index, rec.iters, it_o)  # (tiny systems may need n iterations)
 
 
-def test_infer_main_writes_baseline_rows(gpu_ctx, tmp_path):
-    """infer CLI on an on-disk dataset: Neural+HIP and PCG-{none,diagonal,ainv,ic}-cuda rows."""
+@pytest.mark.parametrize("batch", ["1", "4"])
+def test_infer_main_writes_baseline_rows(gpu_ctx, tmp_path, batch):
+    """infer CLI on an on-disk dataset: Neural+HIP and PCG-{none,diagonal,ainv,ic}-cuda rows (the
+    Neural rows solved one by one or, --batch 4, as one lockstep batch)."""
     import pandas as pd
 
     from learningsparsepreconditioner4gpu_amd.infer import main
 
-    main(["--folder", str(GOLDEN / "folder_free"), "--rtol", "1e-8", "--warmup", "1", "--out-dir", str(tmp_path)])
+    recs = main(["--folder", str(GOLDEN / "folder_free"), "--rtol", "1e-8", "--warmup", "1", "--out-dir", str(tmp_path),
+                 "--batch", batch])
+    assert len(recs) == 4 and all(r.iters == r.iters for r in recs)
     df = pd.read_csv(tmp_path / "infer_folder_free_8.csv")
     keys = set(df["Key"])  # (a row whose every solve hit max_iter = n is left out, like the reference)
     assert {"Neural+HIP", "PCG-ainv-cuda", "PCG-ic-cuda"} <= keys
