@@ -627,9 +627,10 @@ __device__ __forceinline__ T sell_row(const CsrView& M, int32_t b, int32_t e, in
   return acc;
 }
 
+// row i (global index) of M with the gathered vector mirrored in LDS from global row `off` on
 template <typename T>
-__device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, int32_t i, const T* xs) {
-  return sell_row<T, kSmallQB>(M, b, e, i, [xs](int32_t c) { return xs[c]; });
+__device__ __forceinline__ T small_row(const CsrView& M, int32_t b, int32_t e, int32_t i, const T* xs, int32_t off) {
+  return sell_row<T, kSmallQB>(M, b, e, i, [xs, off](int32_t c) { return xs[c - off]; });
 }
 
 // fixed-order workgroup sum of N compensated dots, rounded to T, returned to every thread: wave
@@ -655,11 +656,21 @@ __device__ __forceinline__ void small_dots(DD (&v)[N], DD* lds, double (&out)[N]
   }
 }
 
+// boff / bn (batched solves, lspcg_batch_solve): workgroup k solves system k of a block-diagonal
+// window -- rows [boff[k], boff[k] + bn[k]) of the views and vectors, state S[k]; nullptr: the one
+// system of n rows.
 template <typename T, int PRE, int R, int TH>
 __global__ void __launch_bounds__(TH) k_pcg_small(int32_t n, PcgState* S, CsrView A, CsrView L, CsrView LT,
-                                                  const T* __restrict__ d, T* x, T* r, T* p) {
+                                                  const T* __restrict__ d, T* x, T* r, T* p,
+                                                  const int32_t* __restrict__ boff, const int32_t* __restrict__ bn) {
   constexpr bool SPAI = PRE == LSPCG_PRECOND_EXT_SPAI || PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
   constexpr bool SCALED = PRE == LSPCG_PRECOND_EXT_SPAI_SCALED;
+  int32_t off = 0;
+  if (boff) {
+    off = boff[blockIdx.x];
+    n = bn[blockIdx.x];
+    S += blockIdx.x;
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char small_lds[];
   T* rs = reinterpret_cast<T*>(small_lds);
   T* ts = rs + n;
@@ -684,7 +695,7 @@ __global__ void __launch_bounds__(TH) k_pcg_small(int32_t n, PcgState* S, CsrVie
   for (int m = 0; m < R; ++m) {
     row[m] = tid + TH * m;
     own[m] = row[m] < n;
-    const int32_t i = own[m] ? row[m] : 0;
+    const int32_t i = off + (own[m] ? row[m] : 0);  // global row
     auto range = [&](const CsrView& M, int32_t& b, int32_t& e) {  // CSR entries or SELL groups
       const int32_t* rp = M.gp ? M.gp : M.rp;
       const int32_t j = M.gp ? (i >> 6) : i;
@@ -700,7 +711,7 @@ __global__ void __launch_bounds__(TH) k_pcg_small(int32_t n, PcgState* S, CsrVie
     rr_[m] = own[m] ? r[i] : T(0);
     pr[m] = T(0);
     if constexpr (SCALED || PRE == LSPCG_PRECOND_DIAGONAL) dr[m] = own[m] ? d[i] : T(1);
-    if (own[m]) rs[i] = rr_[m];
+    if (own[m]) rs[row[m]] = rr_[m];
   }
   __syncthreads();
   for (;; ++k) {
@@ -709,7 +720,7 @@ __global__ void __launch_bounds__(TH) k_pcg_small(int32_t n, PcgState* S, CsrVie
 #pragma unroll
       for (int m = 0; m < R; ++m) {
         if (!own[m]) continue;
-        const T s = small_row<T>(LT, tb[m], te[m], row[m], rs);
+        const T s = small_row<T>(LT, tb[m], te[m], off + row[m], rs, off);
         if constexpr (SCALED) ts[row[m]] = s / dr[m];
         else ts[row[m]] = s;
       }
@@ -721,8 +732,8 @@ __global__ void __launch_bounds__(TH) k_pcg_small(int32_t n, PcgState* S, CsrVie
     for (int m = 0; m < R; ++m) {
       const T ri = rr_[m];
       T zi;
-      if constexpr (SCALED) zi = small_row<T>(L, lb[m], le[m], row[m], ts) + (eps * ri) / dr[m];
-      else if constexpr (SPAI) zi = small_row<T>(L, lb[m], le[m], row[m], ts) + eps * ri;
+      if constexpr (SCALED) zi = small_row<T>(L, lb[m], le[m], off + row[m], ts, off) + (eps * ri) / dr[m];
+      else if constexpr (SPAI) zi = small_row<T>(L, lb[m], le[m], off + row[m], ts, off) + eps * ri;
       else if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) zi = ri / dr[m];
       else zi = ri;
       zr[m] = zi;
@@ -763,7 +774,7 @@ __global__ void __launch_bounds__(TH) k_pcg_small(int32_t n, PcgState* S, CsrVie
     T qr[R];
 #pragma unroll
     for (int m = 0; m < R; ++m) {
-      qr[m] = own[m] ? small_row<T>(A, ab[m], ae[m], row[m], ps) : T(0);
+      qr[m] = own[m] ? small_row<T>(A, ab[m], ae[m], off + row[m], ps, off) : T(0);
       if (own[m]) dd_fma(dq[0], double(pr[m]), double(qr[m]));
     }
     double v1[1];
@@ -780,8 +791,8 @@ __global__ void __launch_bounds__(TH) k_pcg_small(int32_t n, PcgState* S, CsrVie
 #pragma unroll
   for (int m = 0; m < R; ++m) {
     if (!own[m]) continue;
-    x[row[m]] = xr[m];
-    p[row[m]] = pr[m];
+    x[off + row[m]] = xr[m];
+    p[off + row[m]] = pr[m];
   }
   if (tid == 0) {
     S->rho_prev = rho_prev;
@@ -1227,19 +1238,20 @@ static int launch_small(lspcg_solver* s, hipStream_t st) {
     const dim3 b(TH);
     switch (s->precond) {
       case LSPCG_PRECOND_NONE:
-        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_NONE, R, TH>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p);
+        hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_NONE, R, TH>), g, b, lds, st, n, s->S, A, L, LT, d, x, r, p,
+                           nullptr, nullptr);
         break;
       case LSPCG_PRECOND_DIAGONAL:
         hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_DIAGONAL, R, TH>), g, b, lds, st, n, s->S, A, L, LT, d, x, r,
-                           p);
+                           p, nullptr, nullptr);
         break;
       case LSPCG_PRECOND_EXT_SPAI:
         hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI, R, TH>), g, b, lds, st, n, s->S, A, L, LT, d, x, r,
-                           p);
+                           p, nullptr, nullptr);
         break;
       default:
         hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI_SCALED, R, TH>), g, b, lds, st, n, s->S, A, L, LT, d,
-                           x, r, p);
+                           x, r, p, nullptr, nullptr);
     }
   };
   using I = std::integral_constant<int, 1>;
@@ -2046,6 +2058,10 @@ struct lspcg_batch {
   double* partials = nullptr;  // per-tile dot partials (<= 2 dots, DD each)
   unsigned* tickets = nullptr;  // per system: top line + one line per kTicketGroup tiles (batch_sys_reduce)
   bool sums = false;            // consumer-sum reductions (every system <= 128 tiles; LSPCG_BATCH_REDUCE)
+  bool small = false;           // every system fits the one-workgroup solve: one launch, one workgroup per system
+  int64_t max_n = 0;
+  int32_t* boff = nullptr;      // [nsys] scalar row offset / size of each system (small mode)
+  int32_t* bn = nullptr;
   double* gsum = nullptr;       // consumer-sum partials: init (2 dots) | KB (2 dots) | KC (1 dot), per tile
   int64_t ntiles = 0;
   PcgState* S = nullptr;
@@ -2138,6 +2154,36 @@ static int enqueue_batch_iteration(lspcg_batch* bt, hipStream_t st) {
   return LSPCG_OK;
 }
 
+// every system of the window in its own workgroup (k_pcg_small in batch mode): the whole loop in
+// one launch; rows per thread / threads from the window's largest system (launch_small's rule)
+template <typename T>
+static int launch_batch_small(lspcg_batch* bt, hipStream_t st) {
+  lspcg_solver* s = bt->s;
+  const CsrView A = csr_view(s, 0, s->Av), L = csr_view(s, 1, s->Lv), LT = csr_view(s, 2, s->LTv);
+  auto* x = static_cast<T*>(s->x);
+  auto* r = static_cast<T*>(s->r);
+  auto* p = static_cast<T*>(s->p);
+  const T* d = static_cast<const T*>(s->d);
+  const int64_t n = bt->max_n;
+  const dim3 g(unsigned(bt->nsys));
+  const size_t lds = 3 * sizeof(T) * size_t(n);
+  auto go = [&](auto rows, auto threads) {
+    constexpr int R = decltype(rows)::value;
+    constexpr int TH = decltype(threads)::value;
+    hipLaunchKernelGGL((k_pcg_small<T, LSPCG_PRECOND_EXT_SPAI, R, TH>), g, dim3(TH), lds, st, int32_t(n), bt->S, A, L,
+                       LT, d, x, r, p, static_cast<const int32_t*>(bt->boff), static_cast<const int32_t*>(bt->bn));
+  };
+  using T512 = std::integral_constant<int, kSmallThreads>;
+  using T1024 = std::integral_constant<int, kSmallThreadsBig>;
+  if (n <= kSmallThreads) go(std::integral_constant<int, 1>{}, T512{});
+  else if (n <= 2 * kSmallThreads) go(std::integral_constant<int, 2>{}, T512{});
+  else if (!small_big()) go(std::integral_constant<int, kSmallRows>{}, T512{});
+  else if (n <= 2 * kSmallThreadsBig) go(std::integral_constant<int, 2>{}, T1024{});
+  else go(std::integral_constant<int, 3>{}, T1024{});
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
 static int get_batch_graph(lspcg_batch* bt, int chunk, hipGraphExec_t* out) {
   auto it = bt->graphs.find(chunk);
   if (it != bt->graphs.end()) {
@@ -2204,7 +2250,7 @@ int lspcg_batch_destroy(lspcg_batch* bt) {
   if (bt->s) lspcg_solver_destroy(bt->s);
   if (bt->Acat) lspcg_mat_destroy(bt->Acat);
   if (bt->Lcat) lspcg_mat_destroy(bt->Lcat);
-  for (void* v : {(void*)bt->etile_sys, (void*)bt->tile0, (void*)bt->tk0, (void*)bt->gsum, (void*)bt->partials, (void*)bt->tickets, (void*)bt->S,
+  for (void* v : {(void*)bt->boff, (void*)bt->bn, (void*)bt->etile_sys, (void*)bt->tile0, (void*)bt->tk0, (void*)bt->gsum, (void*)bt->partials, (void*)bt->tickets, (void*)bt->S,
                   (void*)bt->dhist})
     (void)hipFree(v);
   (void)hipHostFree(bt->hS);
@@ -2276,6 +2322,26 @@ int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, cons
   if (const char* e = std::getenv("LSPCG_BATCH_REDUCE")) bt->sums = e[0] == '1';
   bt->ntiles = ntiles;
   LSPCG_HIP(hipMalloc(&bt->gsum, sizeof(double) * 10 * ntiles));
+  // one workgroup per system when every system fits the one-workgroup solve (scalar views; its
+  // row and LDS bounds, small_path); LSPCG_BATCH_SMALL=0 keeps the lockstep phases
+  for (int k = 0; k < nsys; ++k) bt->max_n = std::max<int64_t>(bt->max_n, bt->n[k]);
+  {
+    const char* e = std::getenv("LSPCG_BATCH_SMALL");
+    const int64_t row_cap = small_big() ? int64_t(kSmallThreadsBig) * 3 : int64_t(kSmallThreads) * kSmallRows;
+    bt->small = !(e && e[0] == '0') && bt->bs == 1 && bt->max_n <= std::min<int64_t>(row_cap, bt->s->small_n) &&
+                3 * bt->max_n * int64_t(esize(bt->dtype)) <= kSmallLds;
+  }
+  if (bt->small) {
+    std::vector<int32_t> ho(nsys), hn(nsys);
+    for (int k = 0; k < nsys; ++k) {
+      ho[k] = int32_t(bt->off[k]);
+      hn[k] = int32_t(bt->n[k]);
+    }
+    LSPCG_HIP(hipMalloc(&bt->boff, sizeof(int32_t) * nsys));
+    LSPCG_HIP(hipMalloc(&bt->bn, sizeof(int32_t) * nsys));
+    LSPCG_HIP(hipMemcpy(bt->boff, ho.data(), sizeof(int32_t) * nsys, hipMemcpyHostToDevice));
+    LSPCG_HIP(hipMemcpy(bt->bn, hn.data(), sizeof(int32_t) * nsys, hipMemcpyHostToDevice));
+  }
   LSPCG_HIP(hipMalloc(&bt->tickets, sizeof(unsigned) * kTicketStride * lines));
   LSPCG_HIP(hipMemset(bt->tickets, 0, sizeof(unsigned) * kTicketStride * lines));
   LSPCG_HIP(hipMalloc(&bt->S, sizeof(PcgState) * nsys));
@@ -2328,7 +2394,7 @@ int lspcg_batch_solve(lspcg_batch* bt, const void* const* b, void* const* x, dou
   if (rc) return rc;
 
   // the poll loop of lspcg_solver_solve over every system's state: run while any system runs;
-  // chunks sized from the slowest system's predicted remaining iterations
+  // chunks sized from the slowest system's predicted remaining iterations (small mode: one launch)
   constexpr int max_chunk = 32;
   PcgState* const hs[2] = {bt->hS, bt->hS + ns};
   const hipEvent_t evp[2] = {s->ev_poll, s->ev_poll2};
@@ -2350,14 +2416,23 @@ int lspcg_batch_solve(lspcg_batch* bt, const void* const* b, void* const* x, dou
     for (int j = 0; j < npend; ++j) queued[(head + j) & 1] += c;
     return post();
   };
-  rc = post();
-  if (!rc) rc = launch(4);
-  if (rc) return rc;
   std::vector<PcgState> cur(ns);
+  if (bt->small) {
+    rc = bt->dtype == LSPCG_F64 ? launch_batch_small<double>(bt, st) : launch_batch_small<float>(bt, st);
+    if (!rc) rc = post();
+    if (rc) return rc;
+    LSPCG_HIP(hipEventSynchronize(evp[head]));
+    std::copy(hs[head], hs[head] + ns, cur.begin());
+  }
+  if (!bt->small) {
+    rc = post();
+    if (!rc) rc = launch(4);
+    if (rc) return rc;
+  }
   std::vector<int64_t> last_it(ns, 0);
   std::vector<double> last_rr(ns, -1.0);
   int chunk = 4;
-  for (;;) {
+  for (; !bt->small;) {
     LSPCG_HIP(hipEventSynchronize(evp[head]));
     std::copy(hs[head], hs[head] + ns, cur.begin());
     const int64_t inflight = queued[head];

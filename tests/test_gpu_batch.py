@@ -171,3 +171,26 @@ def test_batch_many_systems_memory_map(gpu_ctx):
         assert (it, conv) == (it1, conv1)
         np.testing.assert_allclose(h, h1, rtol=1e-12, atol=0)
         assert _rel(x, x1) <= 1e-12
+
+
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_batch_small_systems_one_workgroup_each(gpu_ctx, monkeypatch, small):
+    """Windows of systems that fit the one-workgroup solve run it with one workgroup per system in
+    ONE launch (small = 1, the default) or the lockstep phases (LSPCG_BATCH_SMALL=0): either way each
+    system matches its single solve (count, history, iterate), a zero rhs returns b and max_iter
+    stops per system."""
+    monkeypatch.setenv("LSPCG_BATCH_SMALL", small)
+    eps = 3e-3
+    As = [P.poisson2d_grid(nx, ny)[0] for nx, ny in ((24, 20), (40, 33), (7, 9), (45, 50))]
+    As += [P.kuhn_laplacian(9), P.kuhn_laplacian(13), P.heat_tet(7, 6, 5)[0]]
+    Ls = [_cases.spai_like(A, seed=k) for k, A in enumerate(As)]
+    bs_ = [A @ np.ones(A.shape[0]) for A in As]
+    bs_[2] = np.zeros(As[2].shape[0])
+    for max_iter in (0, 12):
+        _, res, xs = _batch(As, Ls, bs_, eps, 1e-9, max_iter=max_iter)
+        assert res[2][0] == 0 and res[2][1] and not xs[2].any()
+        for A, L, b, (it, conv, h), x in zip(As, Ls, bs_, res, xs):
+            it1, conv1, x1, h1 = _single(A, L, b, eps, 1e-9, max_iter=max_iter)
+            assert (it, conv) == (it1, conv1), (A.shape, it, it1)
+            np.testing.assert_allclose(h, h1, rtol=1e-12, atol=0)
+            assert _rel(x, x1) <= 1e-12 or not np.linalg.norm(x1)
