@@ -165,6 +165,8 @@ int lspcg_solver_destroy(lspcg_solver* s);
  * dtype and block size (L[k] the ext_spai factor of A[k]); the handles must outlive the batch
  * only until lspcg_batch_create returns (their entries are copied into a block-diagonal system
  * whose per-system row ranges are padded to whole 256-row workgroup tiles).
+ * Windows whose systems all fit the one-workgroup solve (n <= 2560 in fp64) run it with one
+ * workgroup per system in one launch; others run the five phases in lockstep.
  * LSPCG_ERR_UNSUPPORTED when a SELL view cannot be built (irregular rows): solve one by one. */
 typedef struct lspcg_batch lspcg_batch;
 int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, const lspcg_mat* const* L,
