@@ -131,14 +131,19 @@ def run_sharded_concurrent(n_items: int, weights: Sequence[float], prepare: Call
 
 def run_sharded_batched(n_items: int, weights: Sequence[float], prepare: Callable[[int], object],
                         finish_batch: Callable[[list], List[SolveRecord]], batch: int,
-                        device: Optional[torch.device] = None) -> List[SolveRecord]:
-    """run_sharded with this rank's systems solved ``batch`` at a time as ONE lockstep batch
-    (``finish_batch`` over a window of prepared systems: linalg.BatchedConjugateGradient, every
-    launch covering the whole window).  The records are gathered once at the end, as run_sharded."""
+                        device: Optional[torch.device] = None,
+                        prepare_batch: Optional[Callable[[list], list]] = None) -> List[SolveRecord]:
+    """run_sharded with this rank's systems solved ``batch`` at a time as ONE batch (``finish_batch``
+    over a window of prepared systems: linalg.BatchedConjugateGradient, every launch covering the
+    whole window).  ``prepare_batch`` (optional) prepares a whole window at once (one GNN forward
+    over the window's graphs) instead of ``prepare`` per system.  The records are gathered once at
+    the end, as run_sharded."""
     rank, world = _rank_world()
     mine = my_items(weights, rank, world)
     k = max(1, int(batch))
     local: List[SolveRecord] = []
     for w0 in range(0, len(mine), k):
-        local.extend(finish_batch([prepare(i) for i in mine[w0:w0 + k]]))
+        window = mine[w0:w0 + k]
+        jobs = prepare_batch(window) if prepare_batch is not None else [prepare(i) for i in window]
+        local.extend(finish_batch(jobs))
     return gather_records(local, n_items, device)

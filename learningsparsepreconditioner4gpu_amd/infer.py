@@ -151,9 +151,10 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
     > 1 keeps that many solves of this rank in flight at once (run_sharded_concurrent): the same
     iterates and counts, a higher batch throughput on the reference's mid-size systems.  ``batch``
     > 1 (ext_spai, not the scaled variant) solves this rank's systems in lockstep windows of that
-    many (run_sharded_batched, validate.get_pcg_iter_time_batch): the same counts and iterates,
-    every launch covering the whole window; a record's t_solve is its share of the window's
-    device time."""
+    many (run_sharded_batched, validate.get_pcg_iter_time_batch) after ONE GNN forward over the
+    window's graphs (workspace.inference_step_batch): the same L, counts and iterates, every launch
+    covering the whole window; a record's t_prec / t_solve are its shares of the window's forward
+    / device solve time."""
     pcg = get_pcg_scaled_iter_time if isinstance(ws, ScaledInferenceWorkspace) else get_pcg_iter_time
     dev = torch.device("cuda", torch.cuda.current_device())
     warmed = set()
@@ -189,9 +190,26 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
         return [SolveRecord(index=j[0], iters=it, rel_res=info["rel_res"], t_prec=j[4], t_solve=sol, n=j[1].n,
                             nnz=j[1].nnz, converged=info["converged"]) for j, (it, _, sol), info in zip(jobs, out, infos)]
 
+    def prepare_batch(items):
+        # one GNN forward over the window's graphs (inference_step_batch: the same L bits); each
+        # record's t_prec is its share of the window's forward
+        ss = [samples[i].to(dev) for i in items]
+        if not warmed:
+            for _ in range(warmup):
+                ws.inference_step_batch(ss)
+            warmed.add(True)
+        prec = 0.0
+        for _ in range(repeat):
+            _, dt = ws.inference_step_batch(ss)
+            prec += dt
+        prec /= repeat * len(items)
+        Ls, _ = ws.inference_step_batch(ss)
+        return [(i, ws.system_matrix(s), L, rhs_for(rhs, s.mask.cpu().numpy(), s), prec)
+                for i, s, L in zip(items, ss, Ls)]
+
     weights = [float(s.edge_index.shape[1]) for s in samples]
     if batch > 1 and not isinstance(ws, ScaledInferenceWorkspace):
-        return run_sharded_batched(len(samples), weights, prepare, finish_batch, batch)
+        return run_sharded_batched(len(samples), weights, prepare, finish_batch, batch, prepare_batch=prepare_batch)
     if concurrency > 1:
         return run_sharded_concurrent(len(samples), weights, prepare, finish, concurrency)
     return run_sharded(len(samples), weights, lambda i: finish(prepare(i)))

@@ -85,6 +85,32 @@ class SimpleInferenceWorkspace:
         L = self._assemble(s, boo, block_output)
         return (L.to_scipy().tocsr() if return_scipy else L), dt
 
+    def inference_step_batch(self, samples, block_output: Optional[bool] = None):
+        """inference_step over a window of graphs as ONE GNN forward on their disjoint union (not in
+        the reference, which runs one forward per sample, infer.py:280): node ids offset per graph,
+        so the union keeps row-major sorted edges and every node aggregates exactly its own graph's
+        messages in the same order -- each L equals the single forward's bit for bit.  Returns
+        ``([L_k], dt)`` with dt the wall time of the one forward (the reference's clock)."""
+        ss = [s if s.x.is_cuda else s.to(self.device) for s in samples]
+        offs, off = [], 0
+        for s in ss:
+            offs.append(off)
+            off += s.num_nodes
+        x = torch.cat([s.x for s in ss])
+        ei = torch.cat([s.edge_index + o for s, o in zip(ss, offs)], dim=1)
+        ea = torch.cat([s.edge_attr for s in ss])
+        torch.cuda.synchronize(x.device)
+        time_beg = time()
+        boo = self.forward(x, ei, ea)
+        torch.cuda.synchronize(boo.device)
+        dt = time() - time_beg
+        Ls, e0 = [], 0
+        for s in ss:
+            E = s.edge_index.shape[1]
+            Ls.append(self._assemble(s, boo[e0:e0 + E], block_output))
+            e0 += E
+        return Ls, dt
+
     def system_matrix(self, sample: GraphSample, block_output: Optional[bool] = None) -> DeviceMatrix:
         """``to_csr_cpu(edge_index, matrix_values, n, mask)`` (infer.py:282) on the device."""
         s = sample if sample.x.is_cuda else sample.to(self.device)
