@@ -54,6 +54,10 @@ extern "C" {
 /* IC(0) of A, applied by two sync-free triangular solves (pymathprim "ic") */
 #define LSPCG_PRECOND_IC 4
 
+/* dot-product summation order of the PCG loop (lspcg_solver_set_dot_order) */
+#define LSPCG_DOT_COMPENSATED 0 /* default: compensated (Dot2) dots in a fixed tree, ~correctly rounded */
+#define LSPCG_DOT_OPENBLAS 1    /* parity mode: numpy's ddot as recorded (OpenBLAS 0.3.29 SkylakeX) */
+
 typedef struct lspcg_ctx lspcg_ctx;
 typedef struct lspcg_mat lspcg_mat;
 typedef struct lspcg_solver lspcg_solver;
@@ -62,6 +66,9 @@ typedef struct lspcg_graph lspcg_graph;
 
 const char* lspcg_last_error(void);
 int lspcg_version(void);
+/* provenance: hash of the sources, headers, compiler flags and arch this library was built from
+ * (learningsparsepreconditioner4gpu_amd/_build.py tree_hash) */
+const char* lspcg_build_id(void);
 
 /* ---- context: one per GPU per host thread; stream NULL = the default (null) stream ---- */
 int lspcg_ctx_create(int device, void* stream, lspcg_ctx** out);
@@ -154,6 +161,15 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
  * convergence stop); kernel_ms[0..4] = mean device time of KA (t = Lᵀr), KB (z = Lt + εr, ρ),
  * UP (p, x), KC (q = Ap, π), UR (r); *nk = 5.  LSPCG_ERR_UNSUPPORTED for other schedules. */
 int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, double* kernel_ms, int* nk);
+/* Summation order of every dot / norm of the loop (scipy cg's np.dot / np.linalg.norm,
+ * iterative.py:398-418).  LSPCG_DOT_COMPENSATED (default): split / one-workgroup schedules,
+ * ~correctly rounded.  LSPCG_DOT_OPENBLAS: parity mode, fp64 only -- each dot is recomputed in
+ * the order of numpy's cblas_ddot in the container that recorded the reference's trajectories
+ * (OpenBLAS 0.3.29 SkylakeX kernel, split over `threads` (1..16) OpenBLAS threads when n > 10000;
+ * restated in oracle/openblas_ddot.c) by one extra single-workgroup launch after each reducing
+ * launch, on the last-arriver multi-kernel schedule: the solve then reproduces the reference's
+ * recorded count, ||r_k|| history and x bit for bit.  Measurement: DESIGN.md §3. */
+int lspcg_solver_set_dot_order(lspcg_solver* s, int order, int threads);
 int lspcg_solver_destroy(lspcg_solver* s);
 
 /* ---- batched lockstep ext_spai PCG over independent systems (infer.py:278-331 solves its samples

@@ -1,11 +1,18 @@
 """Build liblspcg_hip.so in-tree with hipcc for gfx950 (no JIT cache, no torch extension).
 
 ``python -m learningsparsepreconditioner4gpu_amd._build`` or ``__graft_entry__.build()``.
-Each translation unit compiles to its own object under build/ (in parallel, only when stale),
-then hipcc links the shared library.
+Each translation unit compiles to its own object under build/ (in parallel), then hipcc links
+the shared library.
+
+Provenance: ``tree_hash()`` hashes every source and header, the C ABI header, the compiler flags
+and the target arch; the hash is compiled into the library (``lspcg_build_id()``, plus a
+``LSPCG_BUILD_ID=<hash>`` marker string), and the library is rebuilt whenever the marker in the
+binary differs from the tree's hash (not on file times).  ``__graft_entry__.smoke()`` asserts the
+loaded library's id equals the tree's.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -27,6 +34,7 @@ ARCH = os.environ.get("LSPCG_ARCH", "gfx950")
 # scipy's csr_matvec and numpy's ufuncs (bit-identical SpMV / AXPY, DESIGN.md "Parity").
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off",
           "-Wall", "-Wno-unused-result", "-munsafe-fp-atomics"]
+MARKER = b"LSPCG_BUILD_ID="
 
 
 def hipcc() -> str:
@@ -36,37 +44,66 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (ROCm is required to build liblspcg_hip.so)")
 
 
-def _mtime(p: Path) -> float:
-    return p.stat().st_mtime if p.exists() else 0.0
+def _inputs():
+    return [CSRC / s for s in SOURCES] + [CSRC / h for h in HEADERS] + [ROOT / "include" / "lspcg.h"]
 
 
-def _hdr_time() -> float:
-    return max(_mtime(p) for p in [CSRC / h for h in HEADERS] + [ROOT / "include" / "lspcg.h"])
+def tree_hash() -> str:
+    """16 hex digits of SHA-256 over (name, bytes) of every input, the flags and the arch."""
+    h = hashlib.sha256()
+    for p in _inputs():
+        h.update(p.name.encode() + b"\0" + p.read_bytes() + b"\0")
+    h.update(" ".join(CFLAGS).encode() + b"\0" + ARCH.encode())
+    return h.hexdigest()[:16]
+
+
+def binary_id(path: Path = LIB) -> str:
+    """The build id recorded in a built library (its marker string), or '' if absent."""
+    if not path.exists():
+        return ""
+    data = path.read_bytes()
+    i = data.find(MARKER)
+    return data[i + len(MARKER): i + len(MARKER) + 16].decode(errors="replace") if i >= 0 else ""
+
+
+def _stale() -> bool:
+    return binary_id() != tree_hash()
 
 
 def _obj(src: str) -> Path:
     return OBJ / (Path(src).stem + ".o")
 
 
-def _stale() -> bool:
-    if not LIB.exists():
-        return True
-    t = LIB.stat().st_mtime
-    return _hdr_time() > t or any(_mtime(CSRC / s) > t for s in SOURCES)
+def _cmd(src: str, bid: str):
+    extra = [f'-DLSPCG_BUILD_ID="{bid}"'] if src == "lspcg_core.hip" else []  # the id lives in one TU
+    return [hipcc(), *CFLAGS, *extra, f"-I{ROOT / 'include'}", "-c", str(CSRC / src), "-o", str(_obj(src))]
+
+
+def _obj_hash(src: str, bid: str) -> str:
+    """An object is reused only if it was compiled from the same source, headers and command."""
+    h = hashlib.sha256(" ".join(_cmd(src, bid)).encode())
+    for p in [CSRC / src] + [CSRC / x for x in HEADERS] + [ROOT / "include" / "lspcg.h"]:
+        h.update(p.read_bytes())
+    return h.hexdigest()
 
 
 def build(force: bool = False, verbose: bool = True) -> Path:
     if not force and not _stale():
         return LIB
+    bid = tree_hash()
     OBJ.mkdir(parents=True, exist_ok=True)
-    hdr = _hdr_time()
-    todo = [s for s in SOURCES if force or _mtime(_obj(s)) < max(hdr, _mtime(CSRC / s))]
+    stamp = lambda src: _obj(src).with_suffix(".hash")
+    todo = [s for s in SOURCES if force or not _obj(s).exists() or not stamp(s).exists()
+            or stamp(s).read_text() != _obj_hash(s, bid)]
 
     def compile_one(src: str) -> None:
-        cmd = [hipcc(), *CFLAGS, f"-I{ROOT / 'include'}", "-c", str(CSRC / src), "-o", str(_obj(src))]
+        if stamp(src).exists():
+            stamp(src).unlink()
+        cmd = _cmd(src, bid)
         if verbose:
             print("[lspcg build]", " ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
+        stamp(src).write_text(_obj_hash(src, bid))
 
     jobs = max(1, min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
     with ThreadPoolExecutor(jobs) as ex:
@@ -77,6 +114,7 @@ def build(force: bool = False, verbose: bool = True) -> Path:
         print("[lspcg build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    assert binary_id() == bid, "build id marker missing from the linked library"
     return LIB
 
 

@@ -17,6 +17,7 @@ OK, NOT_CONVERGED = 0, 1
 ERR_ARG, ERR_HIP, ERR_UNSUPPORTED, ERR_FORMAT, ERR_BREAKDOWN = -1, -2, -3, -4, -5
 F32, F64 = 0, 1
 PRECOND = {"none": 0, "diagonal": 1, "ext_spai": 2, "ext_spai_scaled": 3, "ic": 4}
+DOT_ORDER = {"compensated": 0, "openblas": 1}
 
 p_i32 = C.POINTER(C.c_int32)
 p_i64 = C.POINTER(C.c_int64)
@@ -34,6 +35,7 @@ class lspcg_gnn_desc(C.Structure):
 SIGNATURES = {
     "lspcg_last_error": (C.c_char_p, []),
     "lspcg_version": (C.c_int, []),
+    "lspcg_build_id": (C.c_char_p, []),
     "lspcg_ctx_create": (C.c_int, [C.c_int, vp, pp]),
     "lspcg_ctx_destroy": (C.c_int, [vp]),
     "lspcg_ctx_synchronize": (C.c_int, [vp]),
@@ -60,6 +62,7 @@ SIGNATURES = {
     "lspcg_solver_set_ic": (C.c_int, [vp, p_f64]),
     "lspcg_solver_solve": (C.c_int, [vp, vp, vp, C.c_double, C.c_int64, p_i64, p_f64, p_f64]),
     "lspcg_solver_time_kernels": (C.c_int, [vp, vp, C.c_int64, p_f64, C.POINTER(C.c_int)]),
+    "lspcg_solver_set_dot_order": (C.c_int, [vp, C.c_int, C.c_int]),
     "lspcg_solver_destroy": (C.c_int, [vp]),
     "lspcg_batch_create": (C.c_int, [vp, C.c_int, pp, pp, C.c_double, pp]),
     "lspcg_batch_solve": (C.c_int, [vp, pp, pp, C.c_double, C.c_int64, p_i64, p_i32, C.POINTER(p_f64), p_f64]),
@@ -117,6 +120,12 @@ def load() -> C.CDLL:
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def build_id() -> str:
+    """Hash of the sources, headers, flags and arch the loaded library was built from
+    (``_build.tree_hash()`` at build time)."""
+    return load().lspcg_build_id().decode()
 
 
 def last_error() -> str:

@@ -232,6 +232,14 @@ extern "C" {
 const char* lspcg_last_error(void) { return g_last_error.c_str(); }
 int lspcg_version(void) { return 10000; }
 
+// hash of the sources, headers, flags and arch (_build.tree_hash(), passed by the build); the
+// marker string lets the build check a binary's provenance without loading it
+#ifndef LSPCG_BUILD_ID
+#define LSPCG_BUILD_ID "unknown"
+#endif
+__attribute__((used)) static const char kBuildMarker[] = "LSPCG_BUILD_ID=" LSPCG_BUILD_ID;
+const char* lspcg_build_id(void) { return kBuildMarker + 15; }
+
 int lspcg_ctx_create(int device, void* stream, lspcg_ctx** out) {
   LSPCG_CHECK(out != nullptr, LSPCG_ERR_ARG, "ctx_create: out is NULL");
   int ndev = 0;

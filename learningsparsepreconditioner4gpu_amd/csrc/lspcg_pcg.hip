@@ -818,6 +818,128 @@ __global__ void __launch_bounds__(kThreads) k_dot_rho(int64_t n, PcgState* S, co
   });
 }
 
+// ---- OpenBLAS-order dots (lspcg_solver_set_dot_order(s, LSPCG_DOT_OPENBLAS, threads)) --------
+// Parity mode: the dots and norms of the loop are recomputed in the summation order of the
+// reference's own recorded runs -- numpy's cblas_ddot = OpenBLAS 0.3.29, SkylakeX kernel, split
+// over `threads` OpenBLAS threads for n > 10000 (oracle/openblas_ddot.c restates the algorithm and
+// cites it): per chunk, 32 FMA accumulators (element i into i % 32) over the 32-aligned prefix,
+// folded 8 -> 4 lanes, one 16-element step on 4 x 4 lanes, a fixed lane tree, then a sequential
+// FMA tail; chunks summed in order.  One workgroup; each wave owns one (dot, chunk) item at a
+// time, lanes 0..31 its accumulators.  The launch follows the reducing launch whose scalars it
+// replaces (same predicate on `done`), so the loop's order of state updates is unchanged.
+constexpr int kObMaxThreads = 16;
+constexpr int kObBlock = 1024;
+
+// chunk c of OpenBLAS's blas_level1_thread split of [0, n) (width = ceil(rest / threads left))
+__device__ __forceinline__ void ob_chunk(int64_t n, int nch, int c, int64_t* start, int64_t* width) {
+  int64_t m = n, s = 0, w = 0;
+  for (int t = 0; t <= c; ++t) {
+    w = (m + (nch - t) - 1) / (nch - t);
+    m -= w;
+    if (m < 0) w += m;
+    if (t < c) s += w;
+  }
+  *start = s;
+  *width = w > 0 ? w : 0;
+}
+
+// dot_compute(w, x, y) of one chunk; the result is returned to every lane of the wave
+__device__ double ob_chunk_dot(const double* __restrict__ x, const double* __restrict__ y, int64_t w) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n1 = w & -int64_t(16);
+  const int64_t n32 = n1 & ~int64_t(31);
+  double acc = 0.0;
+  if (lane < 32) {
+    int64_t i = lane;
+    for (; i + 7 * 32 < n32; i += 8 * 32) {  // loads of 8 steps issued before the FMA chain
+      double xv[8], yv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        xv[u] = x[i + 32 * u];
+        yv[u] = y[i + 32 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = __builtin_fma(xv[u], yv[u], acc);
+    }
+    for (; i < n32; i += 32) acc = __builtin_fma(x[i], y[i], acc);
+  }
+  // fold the 512-bit accumulators: lane 8v + j (j < 4) <- acc[8v + j] + acc[8v + 4 + j]
+  double a = acc + __shfl_down(acc, 4, 64);
+  if (n1 > n32 && lane < 32 && (lane & 7) < 4) {
+    const int64_t e = n32 + 4 * (lane >> 3) + (lane & 3);
+    a = __builtin_fma(x[e], y[e], a);
+  }
+  const int j = lane & 3;
+  const double s = ((__shfl(a, j, 64) + __shfl(a, 8 + j, 64)) + __shfl(a, 16 + j, 64)) + __shfl(a, 24 + j, 64);
+  double dot = (__shfl(s, 0, 64) + __shfl(s, 2, 64)) + (__shfl(s, 1, 64) + __shfl(s, 3, 64));
+  for (int64_t i = n1; i < w; ++i) dot = __builtin_fma(y[i], x[i], dot);
+  return dot;
+}
+
+enum ObWhich { kObInit = 0, kObZ = 1, kObQ = 2, kObR = 3, kObRho = 4, kObRR = 5 };
+
+// up to 3 dots (xs[j] · ys[j]); thread 0 then writes the scalars of phase WHICH:
+//   kObInit  rr = r·r, bb = b·b, atol, rho = (DIAG ? r·z : rr), done (‖b‖ = 0), hist[0]
+//   kObZ     rho = r·z ; rr = r·r and hist[k] for k > 0           (after KB's EpiZ)
+//   kObQ     pq = p·q ; alpha = rho / pq                           (after KC's EpiQ)
+//   kObR     rr = r·r ; rho = (DIAG ? r·z : rr) ; hist[k]           (after CG / Jacobi k_update_r)
+//   kObRho   rho = r·z                                             (after IC's k_dot_rho)
+//   kObRR    rr = r·r ; hist[k]                                    (after IC's k_update_r)
+template <int WHICH, bool DIAG>
+__global__ void __launch_bounds__(kObBlock) k_dot_openblas(int64_t n, int nch, int nd, PcgState* S, const double* x0,
+                                                           const double* y0, const double* x1, const double* y1,
+                                                           const double* x2, const double* y2) {
+  __shared__ double part[3][kObMaxThreads];
+  if (WHICH != kObInit && S->done) return;
+  const double* xs[3] = {x0, x1, x2};
+  const double* ys[3] = {y0, y1, y2};
+  const int ch = (n > 10000 && nch > 1) ? nch : 1;
+  const int nw = blockDim.x >> 6;
+  for (int item = threadIdx.x >> 6; item < nd * ch; item += nw) {
+    const int j = item / ch, c = item % ch;
+    int64_t s = 0, w = n;
+    if (ch > 1) ob_chunk(n, ch, c, &s, &w);
+    const double v = ob_chunk_dot(xs[j] + s, ys[j] + s, w);
+    if ((threadIdx.x & 63) == 0) part[j][c] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double v[3] = {0.0, 0.0, 0.0};
+  for (int j = 0; j < nd; ++j) {
+    double d = 0.0;
+    for (int c = 0; c < ch; ++c) d = d + part[j][c];
+    v[j] = ch > 1 ? d : part[j][0];
+  }
+  const int64_t k = S->iter;
+  if constexpr (WHICH == kObInit) {
+    S->rr = v[0];
+    S->bb = v[1];
+    const double bn = sqrt(v[1]);
+    S->atol = fmax(0.0, S->rtol * bn);
+    S->rho = DIAG ? v[2] : v[0];
+    S->done = (bn == 0.0) ? 1 : 0;
+    if (S->hist) S->hist[0] = sqrt(v[0]);
+  } else if constexpr (WHICH == kObZ) {
+    S->rho = v[0];
+    if (k > 0) {
+      S->rr = v[1];
+      if (S->hist) S->hist[k] = sqrt(v[1]);
+    }
+  } else if constexpr (WHICH == kObQ) {
+    S->pq = v[0];
+    S->alpha = S->rho / v[0];
+  } else if constexpr (WHICH == kObR) {
+    S->rr = v[0];
+    S->rho = DIAG ? v[1] : v[0];
+    if (S->hist) S->hist[k] = sqrt(v[0]);
+  } else if constexpr (WHICH == kObRho) {
+    S->rho = v[0];
+  } else {
+    S->rr = v[0];
+    if (S->hist) S->hist[k] = sqrt(v[0]);
+  }
+}
+
 // after the loop: the deferred x += α_{k-1} p_{k-1} of the last completed iteration
 template <typename T>
 __global__ void __launch_bounds__(kThreads) k_x_fixup(int64_t n, const PcgState* S, const T* __restrict__ p,
@@ -905,7 +1027,23 @@ struct lspcg_solver {
   int64_t small_n = 3072;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it; also bounded by
                            // 3 rows per thread at 1024 threads and the LDS of 3 vectors: 2560 in fp64)
   bool small_sell = true;  // k_pcg_small reads the SELL copies (LSPCG_SMALL_SELL=0: the CSR views)
+  bool split_ok = false;   // set_spai found SELL views for the split schedule
+  int dot_order = LSPCG_DOT_COMPENSATED;  // lspcg_solver_set_dot_order
+  int dot_threads = 1;
 };
+
+// parity mode: every reducing launch is followed by k_dot_openblas, which rewrites its scalars
+template <int WHICH, bool DIAG = false>
+static void enqueue_ob(lspcg_solver* s, hipStream_t st, int nd, const void* x0, const void* y0,
+                       const void* x1 = nullptr, const void* y1 = nullptr, const void* x2 = nullptr,
+                       const void* y2 = nullptr) {
+  if (s->dot_order != LSPCG_DOT_OPENBLAS) return;
+  const int ch = (s->n > 10000 && s->dot_threads > 1) ? s->dot_threads : 1;
+  const int waves = std::min(kObBlock / 64, std::max(1, nd * ch));
+  hipLaunchKernelGGL((k_dot_openblas<WHICH, DIAG>), dim3(1), dim3(64 * waves), 0, st, s->n, s->dot_threads, nd, s->S,
+                     static_cast<const double*>(x0), static_cast<const double*>(y0), static_cast<const double*>(x1),
+                     static_cast<const double*>(y1), static_cast<const double*>(x2), static_cast<const double*>(y2));
+}
 
 // (Re)build the SELL copy of iteration view w (0 = A, 1 = L, 2 = Lᵀ); L and Lᵀ reuse A's
 // pattern when make_view found the same index arrays.
@@ -1113,6 +1251,7 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
               : launch_it<T>(s, 1, static_cast<const T*>(t), ProDone{S},
                                    EpiZ<T, false>{z, r, d, T(s->eps), S, s->partials, s->ticket}, st);
       if (rc) return rc;
+      enqueue_ob<kObZ>(s, st, 2, r, z, r, r);
       // top-of-loop test on ‖r_k‖ (reduced by KB) before the first update of iteration k
       hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S,
                          static_cast<const T*>(z), p, x);
@@ -1130,6 +1269,7 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
       if ((rc = enqueue_trsv(s->icU, s->levU, false, t, z, done, st))) return rc;
       hipLaunchKernelGGL(k_dot_rho<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const T*>(r),
                          static_cast<const T*>(z), s->partials, s->ticket);
+      enqueue_ob<kObRho>(s, st, 1, r, z);
       hipLaunchKernelGGL((k_update_p<T, ProCheck<T>>), dim3(eg), dim3(kThreads), 0, st, n, ProCheck<T>{S}, S,
                          static_cast<const T*>(z), p, x);
       break;
@@ -1143,6 +1283,7 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
                            st)
             : launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQ<T>{q, p, S, s->partials, s->ticket}, st);
   if (rc) return rc;
+  enqueue_ob<kObQ>(s, st, 1, p, q);
   switch (s->precond) {
     case LSPCG_PRECOND_EXT_SPAI:
     case LSPCG_PRECOND_EXT_SPAI_SCALED:
@@ -1151,14 +1292,17 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
     case LSPCG_PRECOND_NONE:
       hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_NONE>), dim3(eg), dim3(kThreads), 0, st, n, S, q, r, d, z,
                          s->partials, s->ticket);
+      enqueue_ob<kObR>(s, st, 1, r, r);
       break;
     case LSPCG_PRECOND_DIAGONAL:
       hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_DIAGONAL>), dim3(eg), dim3(kThreads), 0, st, n, S, q, r, d, z,
                          s->partials, s->ticket);
+      enqueue_ob<kObR, true>(s, st, 2, r, r, r, z);
       break;
-    default:
+    default:  // IC
       hipLaunchKernelGGL((k_update_r<T, LSPCG_PRECOND_EXT_SPAI>), dim3(eg), dim3(kThreads), 0, st, n, S, q, r, d, z,
                          s->partials, s->ticket);
+      enqueue_ob<kObRR>(s, st, 1, r, r);
   }
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
@@ -1179,6 +1323,8 @@ static int enqueue_init(lspcg_solver* s, hipStream_t st) {
                                           EpiResid<T, LSPCG_PRECOND_NONE>{r, b, d, z, s->S, s->partials, s->ticket},
                                           st);
   if (rc) return rc;
+  if (s->precond == LSPCG_PRECOND_DIAGONAL) enqueue_ob<kObInit, true>(s, st, 3, r, r, b, b, r, z);
+  else enqueue_ob<kObInit>(s, st, 2, r, r, b, b);
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
@@ -1198,6 +1344,7 @@ static bool small_big() {
 }
 
 static bool small_path(const lspcg_solver* s) {
+  if (s->dot_order != LSPCG_DOT_COMPENSATED) return false;  // parity mode: the multi-kernel schedule
   if (s->n <= 0 || s->n > s->small_n || s->precond == LSPCG_PRECOND_IC || s->Av.block_size != 1) return false;
   if (s->n > (small_big() ? int64_t(kSmallThreadsBig) * 3 : int64_t(kSmallThreads) * kSmallRows) || 3 * s->n * (s->dtype == LSPCG_F32 ? 4 : 8) > kSmallLds) return false;
   if (s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED)
@@ -1399,8 +1546,9 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     for (auto& p : phases) std::fprintf(stderr, " | %s %.3f ms", p.first, p.second);
     std::fprintf(stderr, "\n");
   }
-  s->split = s->allow_split && s->sp[0] && s->sp[1] && s->sp[2];
-  if (s->split) {
+  s->split_ok = s->allow_split && s->sp[0] && s->sp[1] && s->sp[2];
+  s->split = s->split_ok && s->dot_order == LSPCG_DOT_COMPENSATED;
+  if (s->split_ok) {
     // <= 64 groups per reducing launch; no groups at all (the consumers sum every workgroup's
     // partial) for grids of <= kNoGroupGrid workgroups -- mid-size systems, where the group ticket's
     // round trip costs more than the consumers' extra loads (Poisson 256^2: 20.6 vs 22.0 us per
@@ -1600,6 +1748,25 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     for (int64_t k = cnt; k <= it; ++k) res_hist[k] = NAN;
   }
   return (fin.done == 1) ? LSPCG_OK : LSPCG_NOT_CONVERGED;
+}
+
+int lspcg_solver_set_dot_order(lspcg_solver* s, int order, int threads) {
+  LSPCG_CHECK(s, LSPCG_ERR_ARG, "set_dot_order: NULL");
+  LSPCG_CHECK(order == LSPCG_DOT_COMPENSATED || order == LSPCG_DOT_OPENBLAS, LSPCG_ERR_ARG,
+              "set_dot_order: unknown order " + std::to_string(order));
+  LSPCG_CHECK(order == LSPCG_DOT_COMPENSATED || (threads >= 1 && threads <= kObMaxThreads), LSPCG_ERR_ARG,
+              "set_dot_order: threads must be in [1, 16]");
+  LSPCG_CHECK(order == LSPCG_DOT_COMPENSATED || s->dtype == LSPCG_F64, LSPCG_ERR_UNSUPPORTED,
+              "set_dot_order: the OpenBLAS order is the fp64 ddot's (the reference solves in fp64)");
+  LSPCG_HIP(hipStreamSynchronize(s->stream));
+  s->dot_order = order;
+  s->dot_threads = order == LSPCG_DOT_OPENBLAS ? threads : 1;
+  s->split = s->split_ok && order == LSPCG_DOT_COMPENSATED;
+  for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
+  s->graphs.clear();
+  s->graph_defs.clear();
+  return LSPCG_OK;
 }
 
 int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, double* kernel_ms, int* nk) {

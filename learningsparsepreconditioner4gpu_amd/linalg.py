@@ -43,7 +43,8 @@ def _as_device_matrix(M, dtype, block_size: int, ctx: Context) -> DeviceMatrix:
 
 class PreconditionedConjugateGradient:
     def __init__(self, matrix, device: str = "cuda", preconditioner: str = "none", dtype=np.float64,
-                 block_size: int = 1, ctx: Optional[Context] = None):
+                 block_size: int = 1, ctx: Optional[Context] = None, dot_order: str = "compensated",
+                 dot_threads: int = 1):
         if str(device).split(":")[0] not in GPU_DEVICES:
             raise ValueError(
                 f"device={device!r}: this framework runs PCG on MI355X only (device='cuda'); the CPU "
@@ -66,6 +67,7 @@ class PreconditionedConjugateGradient:
         self.handle = h
         self._L = None
         self._spai_key = None
+        self.dot_order = ("compensated", 1)
         self.setup_time = 0.0  # device setup of the ic / ainv preconditioner (seconds)
         if preconditioner == "ic":
             ms = C.c_double()
@@ -75,6 +77,20 @@ class PreconditionedConjugateGradient:
             L, t = self.A.ainv0()
             self.setup_time = t + self.set_spai(L, 0.0)
             self._spai_key = ("ainv",)
+        if dot_order != "compensated":
+            self.set_dot_order(dot_order, dot_threads)
+
+    def set_dot_order(self, order: str = "compensated", threads: int = 1):
+        """Summation order of the loop's dots and norms (include/lspcg.h lspcg_solver_set_dot_order).
+        ``"compensated"`` (default): compensated dots in a fixed tree (~correctly rounded) on the
+        fastest schedule.  ``"openblas"``: parity mode (fp64) -- numpy's ddot as in the container
+        that recorded the reference's trajectories (OpenBLAS 0.3.29 SkylakeX, ``threads`` OpenBLAS
+        threads), reproducing scipy cg's recorded count, history and x bit for bit, at the cost of
+        one extra single-workgroup launch per dot."""
+        if order not in _lib.DOT_ORDER:
+            raise ValueError(f"unknown dot order {order!r}; expected one of {tuple(_lib.DOT_ORDER)}")
+        _lib.call("lspcg_solver_set_dot_order", self.handle, _lib.DOT_ORDER[order], int(threads))
+        self.dot_order = (order, int(threads) if order == "openblas" else 1)
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -120,21 +120,33 @@ def pairwise_dot(a: np.ndarray, b: np.ndarray) -> float:
     return float(np.sum(np.asarray(a) * np.asarray(b)))
 
 
-def reversed_dot(a: np.ndarray, b: np.ndarray) -> float:
-    return float(np.dot(np.asarray(a)[::-1].copy(), np.asarray(b)[::-1].copy()))
+def openblas_dot(a: np.ndarray, b: np.ndarray, threads: int = 1) -> float:
+    """The reference's own dot: numpy's cblas_ddot = OpenBLAS 0.3.29 (SkylakeX kernel) with
+    ``threads`` OpenBLAS threads, restated in C (oracle/openblas_ddot.c, which cites the
+    algorithm).  Equals np.dot bit for bit in the container the fixtures were made in."""
+    from ._cbuild import lib
+
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    assert a.shape == b.shape and a.ndim == 1
+    return float(lib().lspcg_oracle_openblas_ddot(a.size, a.ctypes.data, b.ctypes.data, int(threads)))
 
 
-DOTS = {"numpy": np.dot, "exact": exact_dot, "pairwise": pairwise_dot, "reversed": reversed_dot}
+# Dot orderings of the scipy-ordered PCG: "numpy" (whatever BLAS this process has -- the
+# reference itself when run where the fixtures were made), "blas<T>" (that BLAS restated at T
+# OpenBLAS threads: the recorded reference runs, machine independent), "exact" (correctly
+# rounded: the HIP path's default compensated dots), "pairwise" (numpy's pairwise sum).
+DOTS = {"numpy": np.dot, "exact": exact_dot, "pairwise": pairwise_dot,
+        "blas1": lambda a, b: openblas_dot(a, b, 1), "blas8": lambda a, b: openblas_dot(a, b, 8)}
 
 
-def count_spread(A, b, psolve, rtol, max_iter=0, dtype=np.float64):
-    """Iteration counts of the scipy-ordered PCG under every admissible dot ordering in DOTS.
-
-    On ill-conditioned systems CG's count depends on rounding (e.g. the synthetic κ≈1e10
-    matrices): the reference itself changes count with the BLAS thread count.  Returns
-    (min, max) over the orderings -- the band a faithful implementation must land in."""
-    its = [pcg(A, b, psolve, rtol=rtol, max_iter=max_iter, dot=d, dtype=dtype)[0] for d in DOTS]
-    return min(its), max(its)
+def dot_fn(dot: str):
+    if dot in DOTS:
+        return DOTS[dot]
+    if dot.startswith("blas"):
+        t = int(dot[4:])
+        return lambda a, b: openblas_dot(a, b, t)
+    raise KeyError(dot)
 
 
 # ---------------------------------------------------------------------------
@@ -151,7 +163,7 @@ def pcg(A: csr_matrix, b: np.ndarray, psolve: Optional[Callable] = None, rtol: f
     dot/norm with the correctly rounded one (the HIP path's reductions).
     """
     dt = np.dtype(dtype).type
-    d0 = DOTS[dot]
+    d0 = dot_fn(dot)
     # scipy's scalars have the vectors' dtype (np.dot of float32 arrays is a float32): ρ, π, α, β
     # and ‖r‖ are rounded to it before they are used (a no-op for fp64)
     d = (lambda u, v: dt(d0(u, v))) if dot != "numpy" else d0

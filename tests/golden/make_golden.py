@@ -3,9 +3,11 @@
 Runs only in the development container, where /root/reference exists (never on the GPU
 box; the committed .npz files are what travels).  The reference targets Python 3.12 with
 loguru / torch_geometric / lightning, so a few import shims are installed first
-(SURVEY.md 8(c)): ``typing.override`` and stub modules for loguru and torch_geometric
-(placeholders only; the functions exercised here do not call into them, except that the
-GNN fixture constructs modules whose PyG base classes are parameter-holder stand-ins).
+(SURVEY.md 8(c)): ``typing.override`` and stub modules for loguru and torch_geometric.  The
+torch_geometric stub carries PyG 2.6.1's ``MessagePassing`` dispatch (collect x_i / x_j by
+``flow``, sum-aggregate at i with dim_size = N, then ``update``; ``edge_updater``) and
+``utils.scatter`` (sum / mean) restated -- the only PyG code the reference's modules call --
+so the GNN / GraphSpmv / AATPE fixtures run the reference's own forward code.
 
 Fixtures (inputs and the reference's outputs, data only):
   to_csr.npz       -- neural_cg/utils/validate.py:22-51 to_csr_cpu on 4 masked/unmasked
@@ -20,11 +22,14 @@ Fixtures (inputs and the reference's outputs, data only):
   pcg_traj.npz     -- the bench-sized trajectories (n = 4,096 / 19,683 / 65,536 and the
                       synthetic C1 system, n = 10,240): the reference's scipy entry points run
                       with scipy's ``cg`` wrapped (``rval.cg``) so that every ‖r_k‖ scipy tests
-                      (the argument of each preconditioner call) and the returned x are kept;
-                      beside them, from the oracle (labelled ``oracle_*``, not the reference):
-                      the correctly-rounded-dot trajectory and the spread of the admissible dot
-                      orderings (count band, first iteration where their histories part by
-                      more than 1e-12, largest x / true-residual difference)
+                      (the argument of each preconditioner call) and the returned x are kept,
+                      at 1 / 2 / 4 / 8 OpenBLAS threads (counts of all; history and x of the 1-
+                      and 8-thread runs; the BLAS build in ``blas_info``); beside them, labelled
+                      ``oracle_exact_*`` (not the reference), the oracle's correctly-rounded-dot
+                      trajectory
+  gnn_forward.npz  -- the reference's NodeEdgeProcessing.forward (seeded) on make_data inputs of
+                      the BASELINE configs' layouts (F_in 1 / 2 / 5 / 9), with its state_dict
+  graph_spmv.npz   -- the reference's GraphSpmv / AATPE / LLT on random edge lists (fp32, fp64)
   ../../learningsparsepreconditioner4gpu_amd/meshes/bunny_grid.npz
                    -- voxelised interior of data/objs/bunny_low_res.obj (winding numbers of a
                       regular grid's vertices), input of the C3 heat stand-in (problems.heat_bunny);
@@ -37,10 +42,12 @@ Fixtures (inputs and the reference's outputs, data only):
 
     python tests/golden/make_golden.py            # every fixture
     python tests/golden/make_golden.py traj       # pcg_traj.npz only
+    python tests/golden/make_golden.py gnn        # gnn_forward.npz + graph_spmv.npz only
     python tests/golden/make_golden.py bunny      # bunny_grid.npz only
 """
 from __future__ import annotations
 
+import inspect
 import sys
 import types
 import typing
@@ -89,9 +96,59 @@ def install_shims():
         def __getitem__(self, i):
             return self.get(i)
 
-    class MessagePassing(nn.Module):  # construction-only stand-in (no propagate)
-        def __init__(self, aggr="add", flow="source_to_target", **kw):
+    class MessagePassing(nn.Module):
+        """PyG 2.6.1's MessagePassing dispatch (torch_geometric/nn/conv/message_passing.py:
+        _collect / propagate / edge_updater; SumAggregation -> utils.scatter(reduce="sum")),
+        restated for a plain [2, E] edge_index -- the only part of PyG the reference's modules
+        call.  Everything the reference computes (message / edge_update / update bodies, the
+        MLPs, the residuals) runs from the reference's own source."""
+
+        def __init__(self, aggr="add", flow="source_to_target", node_dim=-2, **kw):
             super().__init__()
+            assert aggr in ("add", "sum"), aggr  # the reference uses aggr='add' only (config/gnn.yaml)
+            assert flow in ("source_to_target", "target_to_source"), flow
+            self.aggr, self.flow, self.node_dim = aggr, flow, node_dim
+
+        def _collect(self, fn, edge_index, kwargs):
+            # _collect: i, j = (1, 0) for source_to_target else (0, 1); '<name>_i' / '<name>_j'
+            # args are kwargs[name] lifted by index_select(node_dim, edge_index[dim]); the
+            # sizes are recorded per side; index = edge_index[i], dim_size = size[i] or size[j]
+            assert edge_index.dtype == torch.long and edge_index.dim() == 2 and edge_index.size(0) == 2
+            i, j = (1, 0) if self.flow == "source_to_target" else (0, 1)
+            size = [None, None]
+            out = {}
+            for arg in inspect.signature(fn).parameters:
+                if arg[-2:] in ("_i", "_j"):
+                    dim = j if arg[-2:] == "_j" else i
+                    data = kwargs[arg[:-2]]
+                    n = data.size(self.node_dim)
+                    assert size[dim] in (None, n), "node counts differ"
+                    size[dim] = n
+                    out[arg] = data.index_select(self.node_dim, edge_index[dim])
+                elif arg in kwargs:
+                    out[arg] = kwargs[arg]
+            return out, edge_index[i], size[i] if size[i] is not None else size[j]
+
+        def propagate(self, edge_index, size=None, **kwargs):
+            assert size is None
+            msg_kw, index, dim_size = self._collect(self.message, edge_index, kwargs)
+            msg = self.message(**msg_kw)
+            # SumAggregation: scatter(msg, index, dim=node_dim, dim_size, reduce="sum") =
+            # msg.new_zeros(size).scatter_add_(dim, broadcast(index), msg)
+            dim = msg.dim() + self.node_dim if self.node_dim < 0 else self.node_dim
+            shape = list(msg.shape)
+            shape[dim] = dim_size
+            idx = index.view([-1 if d == dim else 1 for d in range(msg.dim())]).expand_as(msg)
+            aggr = msg.new_zeros(shape).scatter_add_(dim, idx, msg)
+            upd = {k: kwargs[k] for k in list(inspect.signature(self.update).parameters)[1:] if k in kwargs}
+            return self.update(aggr, **upd)
+
+        def update(self, inputs):  # PyG's default update
+            return inputs
+
+        def edge_updater(self, edge_index, size=None, **kwargs):
+            kw, _, _ = self._collect(self.edge_update, edge_index, kwargs)
+            return self.edge_update(**kw)
 
     class MessageNorm(nn.Module):  # parameter holder with PyG's state (scale = 1)
         def __init__(self, learn_scale=False):
@@ -102,9 +159,26 @@ def install_shims():
         def reset_parameters(self):
             self.scale.data.fill_(1.0)
 
+    def scatter(src, index, dim=0, dim_size=None, reduce="sum"):
+        """torch_geometric.utils.scatter (PyG 2.6.1) for reduce sum / mean: broadcast index,
+        new_zeros(...).scatter_add_; mean divides by the per-node count clamped to >= 1."""
+        dim = src.dim() + dim if dim < 0 else dim
+        if dim_size is None:
+            dim_size = int(index.max()) + 1 if index.numel() > 0 else 0
+        shape = list(src.shape)
+        shape[dim] = dim_size
+        idx = index.view([-1 if d == dim else 1 for d in range(src.dim())]).expand_as(src)
+        out = src.new_zeros(shape).scatter_add_(dim, idx, src)
+        if reduce in ("sum", "add"):
+            return out
+        assert reduce == "mean", reduce
+        count = src.new_zeros(dim_size).scatter_add_(0, index, src.new_ones(src.size(dim))).clamp(min=1)
+        return out / count.view([-1 if d == dim else 1 for d in range(out.dim())])
+
     tgd.Data, tgd.Dataset = Data, Dataset
-    for name in ("scatter", "coalesce", "remove_self_loops", "to_torch_coo_tensor", "to_edge_index"):
+    for name in ("coalesce", "remove_self_loops", "to_torch_coo_tensor", "to_edge_index"):
         setattr(tgu, name, None)
+    tgu.scatter = scatter
     tgn.MessagePassing, tgn.MessageNorm = MessagePassing, MessageNorm
     sys.modules.update({"torch_geometric": tg, "torch_geometric.data": tgd, "torch_geometric.utils": tgu,
                         "torch_geometric.nn": tgn})
@@ -174,7 +248,30 @@ class RecordingCG:
         return x, info
 
 
+TRAJ_THREADS = (1, 2, 4, 8)  # OpenBLAS thread counts the reference is run at (8 = nproc here)
+
+
+def blas_info() -> str:
+    """numpy / scipy / BLAS build of the process that ran the reference (stored in the fixture)."""
+    import json
+
+    import scipy
+    import threadpoolctl
+
+    return json.dumps({"numpy": np.__version__, "scipy": scipy.__version__,
+                       "threadpool_info": threadpoolctl.threadpool_info()})
+
+
 def traj_fixtures(rval):
+    """pcg_traj.npz.  Every system / method is run through the reference's scipy entry point at
+    each OpenBLAS thread count in TRAJ_THREADS (threadpoolctl): numpy's ddot splits vectors of
+    n > 10,000 over the threads, so the reference's own rounding -- and on ill-conditioned
+    systems its count -- moves with the thread count.  Stored: every run's count; the 1- and
+    8-thread runs' ‖r_k‖ history and x; the reference's own spread (x and true residual between
+    thread counts); and, labelled ``oracle_exact_*``, the oracle's correctly-rounded-dot
+    trajectory (the HIP default's contract)."""
+    import threadpoolctl
+
     from learningsparsepreconditioner4gpu_amd import problems as P
     from oracle import linalg as O
 
@@ -186,7 +283,7 @@ def traj_fixtures(rval):
         "poisson256": P.poisson2d_grid(256, 256)[:2],
         "synthetic10240": (P.synthetic_c1(), None),  # BASELINE config 1 (unpreconditioned only)
     }
-    out = {}
+    out = {"blas_info": np.array(blas_info()), "ref_threads": np.array(TRAJ_THREADS)}
     for name, (A, mask) in systems.items():
         A = sp.csr_matrix(A)
         A.sort_indices()
@@ -201,51 +298,141 @@ def traj_fixtures(rval):
         if len(methods) > 1:
             out[f"{name}__L_data"] = L.data
         b = A @ gt
+        nb = np.linalg.norm(b)
         for m in methods:
-            if m == "none":
-                cnt = rval.get_cg_iter_time_scipy(A, gt, rtol=rtol)
-                ps = None
-            elif m == "diagonal":
-                cnt = rval.get_pcg_diagonal_iter_time_scipy(A, gt, rtol=rtol)
-                ps = O.diagonal_operator(A)
-            elif m == "ext_spai":
-                cnt = rval.get_pcg_iter_time_scipy(A, gt, L, eps, rtol=rtol)
-                ps = O.spai_operator(L, eps)
-            else:
-                cnt = rval.get_pcg_scaled_iter_time_scipy(A, gt, L, eps, rtol=rtol)
-                ps = O.spai_scaled_operator(A, L, eps)
-            assert cnt == rec.count and len(rec.hist) == cnt
             t = f"{name}__{m}"
-            out[f"{t}__count"] = np.array(cnt)
-            out[f"{t}__x"] = rec.x
-            out[f"{t}__hist"] = np.array(rec.hist)  # ‖r_k‖, k = 0 .. count-1 (reference)
-            # the oracle restatement must reproduce the reference bit for bit with numpy dots
-            it_np, x_np, h_np = O.pcg(A, b, ps, rtol=rtol, dot="numpy")
-            assert it_np == cnt and np.array_equal(x_np, rec.x) and np.array_equal(h_np[:cnt], rec.hist), (name, m)
-            # admissible dot orderings (pymathprim's own order is unknowable): their spread
-            runs = {d: O.pcg(A, b, ps, rtol=rtol, dot=d) for d in O.DOTS}
-            its = [r[0] for r in runs.values()]
-            nb = np.linalg.norm(b)
-            tres = {d: np.linalg.norm(b - A @ r[1]) / nb for d, r in runs.items()}
-            xs = {d: np.linalg.norm(r[1] - rec.x) / np.linalg.norm(rec.x) for d, r in runs.items()}
-            kstar = []
-            for d, r in runs.items():
-                h = np.asarray(r[2])
-                k = min(len(h), cnt)
-                rd = np.abs(h[:k] - rec.hist[:k]) / np.asarray(rec.hist[:k])
-                kstar.append(int(np.argmax(rd > 1e-12)) if np.any(rd > 1e-12) else k)
-            out[f"{t}__oracle_count_band"] = np.array([min(its), max(its)])
-            out[f"{t}__oracle_hist_agree_k"] = np.array(min(kstar))
-            out[f"{t}__oracle_x_spread"] = np.array(max(xs.values()))
-            out[f"{t}__oracle_true_res_spread"] = np.array(max(tres.values()) - min(tres.values()))
-            out[f"{t}__true_res"] = np.array(tres["numpy"])
-            ex = runs["exact"]
+            runs = {}
+            for th in TRAJ_THREADS:
+                with threadpoolctl.threadpool_limits(th):
+                    if m == "none":
+                        cnt = rval.get_cg_iter_time_scipy(A, gt, rtol=rtol)
+                    elif m == "diagonal":
+                        cnt = rval.get_pcg_diagonal_iter_time_scipy(A, gt, rtol=rtol)
+                    elif m == "ext_spai":
+                        cnt = rval.get_pcg_iter_time_scipy(A, gt, L, eps, rtol=rtol)
+                    else:
+                        cnt = rval.get_pcg_scaled_iter_time_scipy(A, gt, L, eps, rtol=rtol)
+                assert cnt == rec.count and len(rec.hist) == cnt
+                runs[th] = (cnt, rec.x.copy(), np.array(rec.hist))
+                if th in (1, 8):
+                    out[f"{t}__t{th}__count"] = np.array(cnt)
+                    out[f"{t}__t{th}__x"] = rec.x.copy()
+                    out[f"{t}__t{th}__hist"] = np.array(rec.hist)  # ‖r_k‖, k = 0 .. count-1
+                    out[f"{t}__t{th}__true_res"] = np.array(np.linalg.norm(b - A @ rec.x) / nb)
+            counts = [runs[th][0] for th in TRAJ_THREADS]
+            out[f"{t}__ref_counts"] = np.array(counts)
+            x1 = runs[1][1]
+            out[f"{t}__ref_x_spread"] = np.array(max(np.linalg.norm(r[1] - x1) / np.linalg.norm(x1) for r in runs.values()))
+            tr = [np.linalg.norm(b - A @ r[1]) / nb for r in runs.values()]
+            out[f"{t}__ref_true_res_spread"] = np.array(max(tr) - min(tr))
+            ps = {"none": None, "diagonal": O.diagonal_operator(A), "ext_spai": O.spai_operator(L, eps),
+                  "ext_spai_scaled": O.spai_scaled_operator(A, L, eps)}[m]
+            # the oracle's OpenBLAS restatement reproduces every recorded run bit for bit
+            for th in (1, 8):
+                it_b, x_b, h_b = O.pcg(A, b, ps, rtol=rtol, dot=f"blas{th}")
+                assert it_b == runs[th][0] and np.array_equal(x_b, runs[th][1]), (name, m, th)
+                assert np.array_equal(np.asarray(h_b[:it_b]), runs[th][2]), (name, m, th)
+            ex = O.pcg(A, b, ps, rtol=rtol, dot="exact")
             out[f"{t}__oracle_exact_count"] = np.array(ex[0])
             out[f"{t}__oracle_exact_x"] = ex[1]
             out[f"{t}__oracle_exact_hist"] = np.asarray(ex[2])
-            print(name, m, cnt, "band", (min(its), max(its)), "agree_k", min(kstar), "x spread %.1e" % max(xs.values()),
-                  flush=True)
+            print(name, m, "reference counts", dict(zip(TRAJ_THREADS, counts)), "exact-dot", ex[0],
+                  "ref x spread %.1e" % float(out[f"{t}__ref_x_spread"]), flush=True)
     np.savez_compressed(OUT / "pcg_traj.npz", **out)
+
+
+def _gnn_cfg():
+    ff = lambda norm: {"pre_norm": norm, "hidden_channels": 16, "num_layers": 2}
+    return dict(node_encoder=ff("none"), edge_encoder=ff("none"), node_decoder=ff("none"), edge_decoder=ff("none"),
+                num_mp_layers=4, node_residual=True, edge_residual=True, node_features=16, edge_features=16,
+                node_mlp=ff("layer"), edge_mlp=ff("layer"), msg_mlp=ff("layer"), msg_norm=True, aggr="add")
+
+
+def gnn_forward_fixtures(rdata, rgnn):
+    """gnn_forward.npz: the REFERENCE's NodeEdgeProcessing.forward (gnns.py:77-97, MPLayer
+    basic_layers.py:193-225 over the PyG dispatch above) on inputs built by the reference's own
+    make_data (data.py:218-336), seeded construction (torch.manual_seed(seed), config/gnn.yaml).
+    Cases: the BASELINE configs' input layouts -- Poisson (F_in 1), synthetic with the mean edge
+    feature (F_in 2), the heat bunny (field + xyz + mask, F_in 5), elasticity b = 3 (xyz + deform
+    + mask, F_in 9, 9 edge features)."""
+    from learningsparsepreconditioner4gpu_amd import problems as P
+
+    gen = reference_synthetic()
+    cases = {}
+    A, m, _ = P.poisson2d_grid(23, 19)
+    cases["poisson"] = (A, m, None, 1, "disable", 3)
+    A = gen(1500, 4e-3, 1e-5, np.random.RandomState(1))
+    cases["synthetic"] = (A, None, None, 1, "mean", 4)
+    A, m, f = P.heat_bunny()
+    cases["bunny"] = (A, m, f, 1, "disable", 5)
+    A, m, nodes = P.elasticity_box(7, 4, 4)
+    cases["elast"] = (A, m, np.concatenate([nodes, nodes * 0.5], 1), 3, "disable", 6)
+    out = {}
+    for name, (A, m, feats, bs, e2n, seed) in cases.items():
+        A = sp.csr_matrix(A)
+        A.sort_indices()
+        g = P.to_block_graph(A, bs)
+        if m is None:
+            m = np.ones((g.num_nodes, bs))
+        raw = rdata.RawData(block_values=g.block_values, diagonals=A.diagonal().reshape(-1, bs),
+                            edge_index=g.edge_index, node_features=feats, lhs=None, rhs=None,
+                            mask=np.asarray(m, dtype=np.float64).reshape(g.num_nodes, bs), num_nodes=g.num_nodes,
+                            block_size=bs)
+        d = rdata.make_data(raw, use_matrix_as_edge_feature=True, use_mask_as_node_feature=True,
+                            use_node_features_as_edge_feature=False, use_edge_features_as_node_feature=e2n,
+                            use_random_rhs=True, normalize_matrix="mean", is_inference=True)
+        torch.manual_seed(seed)
+        net = rgnn.NodeEdgeProcessing(node_in_features=d.x.shape[1], node_out_features=None,
+                                      edge_in_features=d.edge_attr.shape[1], edge_out_features=bs * bs, **_gnn_cfg())
+        net.eval()
+        with torch.no_grad():
+            node_out, edge_out = net(d.x, d.edge_index, d.edge_attr)
+        out[f"{name}__x"] = d.x.numpy()
+        out[f"{name}__edge_index"] = d.edge_index.numpy()
+        out[f"{name}__edge_attr"] = d.edge_attr.numpy()
+        out[f"{name}__mask"] = d.mask.numpy()
+        out[f"{name}__block_size"] = np.array(bs)
+        out[f"{name}__seed"] = np.array(seed)
+        out[f"{name}__edge_out"] = edge_out.numpy()
+        out[f"{name}__node_out"] = node_out.numpy()
+        for k, v in net.state_dict().items():
+            out[f"{name}__sd__{k}"] = v.numpy()
+        print("gnn", name, "N", d.x.shape, "E", d.edge_attr.shape, "out |max|", float(edge_out.abs().max()), flush=True)
+    np.savez_compressed(OUT / "gnn_forward.npz", **out)
+
+
+def graph_spmv_fixtures(rbl):
+    """graph_spmv.npz: the REFERENCE's GraphSpmv(use_transpose) (basic_layers.py:112-142), AATPE(ε)
+    (:228-261, with mask and with mask + diag) and LLT (:264-275) over the PyG dispatch above, on
+    random edge lists (unsorted, with duplicated (row, col) pairs), b = 1 and b = 3, fp32 and fp64."""
+    out = {}
+    for bs in (1, 3):
+        g = torch.Generator().manual_seed(40 + bs)
+        N, E = 700, 5000
+        ei = torch.randint(0, N, (2, E), generator=g)
+        ei[:, : E // 10] = ei[:, E // 2: E // 2 + E // 10]
+        A = torch.randn(E, bs, bs, generator=g, dtype=torch.float64)
+        X = torch.randn(N, bs, generator=g, dtype=torch.float64)
+        mask = (torch.rand(N, bs, generator=g) > 0.2).to(torch.float64)
+        diag = torch.rand(N, bs, generator=g, dtype=torch.float64) + 0.5
+        t = f"b{bs}"
+        out[f"{t}__edge_index"], out[f"{t}__A"], out[f"{t}__X"] = ei.numpy(), A.numpy(), X.numpy()
+        out[f"{t}__mask"], out[f"{t}__diag"] = mask.numpy(), diag.numpy()
+        for dt, dn in ((torch.float64, "f64"), (torch.float32, "f32")):
+            Ad, Xd, md, dd = A.to(dt), X.to(dt), mask.to(dt), diag.to(dt)
+            with torch.no_grad():
+                for tr in (False, True):
+                    op = rbl.GraphSpmv(use_transpose=tr)
+                    out[f"{t}__{dn}__spmv_t{int(tr)}"] = op(Xd, ei, Ad).numpy()
+                    out[f"{t}__{dn}__spmv_t{int(tr)}_mask"] = op(Xd, ei, Ad, md).numpy()
+                op = rbl.AATPE(3e-3)
+                out[f"{t}__{dn}__aatpe_mask"] = op(Xd, ei, Ad, md).numpy()
+                out[f"{t}__{dn}__aatpe_mask_diag"] = op(Xd, ei, Ad, md, dd).numpy()
+                out[f"{t}__{dn}__aatpe"] = op(Xd, ei, Ad).numpy()
+                out[f"{t}__{dn}__llt_mask"] = rbl.LLT()(Xd, ei, Ad, md).numpy()
+    out["epsilon"] = np.array(3e-3)
+    np.savez_compressed(OUT / "graph_spmv.npz", **out)
+    print("graph_spmv fixtures", len(out))
 
 
 def bunny_grid():
@@ -291,6 +478,15 @@ def main():
 
         sys.path.insert(0, str(ROOT))
         traj_fixtures(rval)
+        return
+    if sys.argv[1:] == ["gnn"]:
+        from neural_cg import data as rdata
+        from neural_cg.nn import basic_layers as rbl
+        from neural_cg.nn import gnns as rgnn
+
+        sys.path.insert(0, str(ROOT))
+        gnn_forward_fixtures(rdata, rgnn)
+        graph_spmv_fixtures(rbl)
         return
     from neural_cg import data as rdata
     from neural_cg.nn import gnns as rgnn
@@ -441,6 +637,11 @@ def main():
                 if hasattr(dd, key):
                     fx[f"{name}__{i}__{key}"] = getattr(dd, key).numpy()
     np.savez_compressed(OUT / "folder.npz", **fx)
+
+    from neural_cg.nn import basic_layers as rbl
+
+    gnn_forward_fixtures(rdata, rgnn)
+    graph_spmv_fixtures(rbl)
 
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)

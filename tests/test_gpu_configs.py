@@ -1,7 +1,8 @@
 """GPU parity at BASELINE.json's configurations (full sizes), through the product's API.
 
-C1  synthetic N=10240, unpreconditioned CG, rtol 1e-8: iteration count inside the band of
-    admissible dot orderings (the reference's own count moves with the BLAS thread count)
+C1  synthetic N=10240, unpreconditioned CG, rtol 1e-8: the correctly-rounded-dot count (default)
+    and the reference's recorded counts in the parity dot order (its own count moves with the
+    OpenBLAS thread count: 3236 at 1 thread, 3229 at 8)
 C2  Poisson-2D 256x256 (N=65,536) fp64, GNN-inferred L, ext_spai PCG rtol 1e-8: GNN output vs
     the torch restatement (fp32, 1e-5), iteration count equal to the oracle's, solution 1e-12
 C3  heat on the voxelised bunny (6,310 vertices, 5 % Dirichlet, F_in = 5) fp32, GNN + PCG to 1e-6:
@@ -54,13 +55,22 @@ def _solve(A, L, b, eps, rtol, max_iter=0, dtype=np.float64):
     return it, conv, x.cpu().numpy(), hist
 
 
-def test_c1_synthetic_cg_count_in_band(gpu_ctx):
+def test_c1_synthetic_cg_counts(gpu_ctx):
+    """Config 1 built by the product's generator (== the reference's, golden synthetic.npz): the
+    default order gives the correctly-rounded-dot count, the parity order the reference's recorded
+    counts (3236 at 1 OpenBLAS thread, 3229 at 8; tests/golden/pcg_traj.npz)."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+    from tests.test_gpu_traj import Z
+
     A = P.synthetic_c1()
     b = A @ np.ones(A.shape[0])
-    lo, hi = O.count_spread(A, b, None, 1e-8)
     it, conv, x, _ = _solve(A, None, b, 0.0, 1e-8)
-    assert conv and lo <= it <= hi, (it, lo, hi)
+    assert conv and it == int(Z["synthetic10240__none__oracle_exact_count"]), it
     assert np.linalg.norm(b - A @ x) / np.linalg.norm(b) < 1e-7
+    for th, want in ((1, 3236), (8, 3229)):
+        s = PreconditionedConjugateGradient(A, device="cuda", dot_order="openblas", dot_threads=th)
+        it, _, _ = s(b, np.zeros(A.shape[0]), 1e-8)
+        assert it == want == int(Z[f"synthetic10240__none__t{th}__count"]), (th, it)
 
 
 def test_c2_poisson_gnn_spai_pcg(gpu_ctx):

@@ -128,3 +128,18 @@ def test_inference_step_batch_equals_single_forwards(gpu_ctx):
         a, b = L1.to_scipy().tocsr(), Lb.to_scipy().tocsr()
         assert np.array_equal(a.indptr, b.indptr) and np.array_equal(a.indices, b.indices)
         assert np.array_equal(a.data, b.data)
+
+
+@pytest.mark.parametrize("case", ["poisson", "synthetic", "bunny", "elast"])
+def test_gnn_forward_matches_reference_fixture(gpu_ctx, case):
+    """HIP forward vs the REFERENCE's own NodeEdgeProcessing.forward output (gnn_forward.npz,
+    made by tests/golden/make_golden.py from gnns.py / basic_layers.py over PyG's dispatch), with
+    the reference's parameters loaded through state_dict: fp32 within 1e-5."""
+    from learningsparsepreconditioner4gpu_amd.nn import build_gnn
+    from tests.test_oracle_golden import _load, gnn_fixture
+
+    x, ei, ea, bs, seed, sd, want = gnn_fixture(_load("gnn_forward.npz"), case)
+    gpu = build_gnn(x.shape[1], ea.shape[1], bs, seed=None)
+    gpu.load_state_dict(sd, strict=True)
+    _, got = gpu(x.cuda(), ei.cuda(), ea.cuda())
+    _close(got.cpu().numpy(), want)

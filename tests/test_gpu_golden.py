@@ -1,6 +1,8 @@
 """GPU vs the reference's own outputs (tests/golden, produced by tests/golden/make_golden.py):
-device to_csr_cpu bit-exact, PCG iteration counts exact (well-conditioned) / inside the
-rounding band (ill-conditioned synthetic), for every preconditioner and both tolerances."""
+device to_csr_cpu bit-exact; PCG iteration counts for every preconditioner and both tolerances:
+in the reference's dot order (parity mode) equal on every system, in the default compensated
+order equal on the well-conditioned ones and equal to the correctly-rounded-dot count on the
+ill-conditioned synthetic one."""
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -57,11 +59,16 @@ def test_pcg_counts_match_reference(gpu_ctx, method, small_n, monkeypatch):
             it, _, _ = s(b, x, 10.0 ** -rtol, 0, ext_spai=(L, eps) if method.startswith("ext") else None)
             if name in WELL_CONDITIONED:
                 assert it == want, (name, rtol, method, it, want)
-            else:
+            else:  # ill-conditioned: the count of the correctly rounded dots (the default's contract)
                 ps = {"none": None, "diagonal": O.diagonal_operator(A), "ext_spai": O.spai_operator(L, eps),
                       "ext_spai_scaled": O.spai_scaled_operator(A, L, eps)}[method]
-                lo, hi = O.count_spread(A, b, ps, 10.0 ** -rtol)
-                assert lo <= it <= hi, (name, rtol, method, lo, it, hi, want)
+                it_o = O.pcg(A, b, ps, rtol=10.0 ** -rtol, dot="exact")[0]
+                assert it == it_o, (name, rtol, method, it, it_o, want)
+            # parity mode: the reference's own dot order -> the reference's count, every system
+            s.set_dot_order("openblas", 1)
+            x = np.zeros(n)
+            it, _, _ = s(b, x, 10.0 ** -rtol, 0, ext_spai=(L, eps) if method.startswith("ext") else None)
+            assert it == want, ("openblas", name, rtol, method, it, want)
 
 
 def test_infer_driver_end_to_end(gpu_ctx, tmp_path):

@@ -94,3 +94,30 @@ def test_graph_empty_and_out_of_range(gpu_ctx):
     assert torch.equal(y, torch.zeros_like(X))
     with pytest.raises(_lib.LspcgError):
         GraphSpmv()(X, torch.tensor([[0, 7], [1, 2]], device="cuda"), torch.ones(2, 1, 1, device="cuda"))
+
+
+@pytest.mark.parametrize("bs", [1, 3])
+@pytest.mark.parametrize("dn", ["f64", "f32"])
+def test_graph_ops_match_reference_fixture(gpu_ctx, bs, dn):
+    """GraphSpmv / AATPE / LLT on the HIP kernels vs the REFERENCE's own modules' outputs
+    (graph_spmv.npz: basic_layers.py:112-142, 228-275 over PyG's dispatch, run in the same
+    dtype): fp64 within 1e-12, fp32 within 1e-5."""
+    from learningsparsepreconditioner4gpu_amd.nn import AATPE, LLT, GraphSpmv
+    from tests.test_oracle_golden import _load, graph_fixture
+
+    z = _load("graph_spmv.npz")
+    dt = torch.float64 if dn == "f64" else torch.float32
+    X, ei, A, m, d = (t.cuda() for t in graph_fixture(z, bs))
+    X, A, m, d = X.to(dt), A.to(dt), m.to(dt), d.to(dt)
+    eps = float(z["epsilon"])
+    got = {
+        "spmv_t0": GraphSpmv()(X, ei, A), "spmv_t1": GraphSpmv(True)(X, ei, A),
+        "spmv_t0_mask": GraphSpmv()(X, ei, A, m), "spmv_t1_mask": GraphSpmv(True)(X, ei, A, m),
+        "aatpe": AATPE(eps)(X, ei, A), "aatpe_mask": AATPE(eps)(X, ei, A, m),
+        "aatpe_mask_diag": AATPE(eps)(X, ei, A, m, d), "llt_mask": LLT()(X, ei, A, m),
+    }
+    tol = TOL[dt]
+    for k, y in got.items():
+        assert y.dtype == dt
+        err = _rel(y, z[f"b{bs}__{dn}__{k}"])
+        assert err <= tol, (k, err)

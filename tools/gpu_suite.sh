@@ -1,0 +1,31 @@
+#!/bin/bash
+# GPU evidence run: full GPU suite, smoke, default bench (optionally rocprofv3 kernel stats and
+# the roofline SpMV's PMC traffic).  Usage (on the box, via gpurun):
+#   bash tools/gpu_suite.sh TAG [tests] [bench] [prof] [traffic]
+# Every GPU step runs under its own time limit; the script stops at the first failing step.
+set -o pipefail
+tag=$1; shift
+steps=${*:-tests bench}
+cd "$GRAFT_REPO_ROOT"
+out=gpurun_out/$tag
+mkdir -p "$out"
+for s in $steps; do
+  case $s in
+    tests)
+      LSPCG_PARITY_LOG=$out/parity_traj.jsonl timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > "$out/gpu_tests.txt" 2>&1
+      rc=$?; echo "tests rc=$rc"; tail -3 "$out/gpu_tests.txt"; [ $rc -eq 0 ] || exit $rc
+      timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.txt" 2>&1 || exit $?
+      grep smoke "$out/smoke.txt" ;;
+    bench)
+      timeout -k 10 300 python -u bench.py > "$out/bench.json" 2> "$out/bench.err" || exit $?
+      python3 -c "
+import json; d=json.load(open('$out/bench.json')); print(d['value'], d['pcg_iter_us'], d['gnn_precond_ms'], d['roofline']['frac'])" ;;
+    prof)
+      bash tools/prof_bench.sh "$tag" || exit $?
+      f=$(find "gpurun_out/prof_$tag" -name "*kernel_stats.csv" | head -1); cp "$f" "$out/kernel_stats.csv" ;;
+    traffic)
+      bash tools/spmv_traffic.sh "$tag" || exit $?
+      cat "gpurun_out/traffic_$tag/summary.json" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
