@@ -131,9 +131,11 @@ int lspcg_ic0(const lspcg_mat* A, lspcg_mat** L, double* t_ms);
 /* AINV(0): *L = Z D^{-1/2} (Z unit upper, pattern triu(A)) so that L L^T = Z D^{-1} Z^T ~ A^{-1};
  * use it as an ext_spai factor with epsilon = 0 */
 int lspcg_ainv0(const lspcg_mat* A, lspcg_mat** L, double* t_ms);
-/* x = T^{-1} b, T triangular (lower != 0: diagonal stored last in each row; else first): one
- * sync-free launch over the level-ordered rows (LSPCG_TRSV_LEVELS=1: one launch per level, same
- * bits); b, x device vectors of T's dtype */
+/* x = T^{-1} b, T triangular (lower != 0: diagonal stored last in each row; else first), in the
+ * arithmetic of scipy's spsolve_triangular on csc(T) -- the reference's IC apply
+ * (validate.py:359-365): column-scaled unit solve, updates in SuperLU's column order, diagonal
+ * scaling after; one sync-free launch over the level-ordered rows; b, x device vectors of T's
+ * dtype */
 int lspcg_trsv(const lspcg_mat* T, int lower, const void* b, void* x);
 /* compensated, deterministic dot product of two device vectors; result to host */
 int lspcg_dot(lspcg_ctx* ctx, int64_t n, int dtype, const void* x, const void* y, double* out);
@@ -146,6 +148,11 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
 /* LSPCG_PRECOND_IC solvers: IC(0) factorization of A on the device (pymathprim "ic" setup;
  * the reference's scipy twin is validate.py:344-429); t_prec_ms = setup time */
 int lspcg_solver_set_ic(lspcg_solver* s, double* t_prec_ms);
+/* LSPCG_PRECOND_IC solvers: install a given lower-triangular factor L (scalar CSR of the solver's
+ * size and dtype, sorted rows, diagonal stored last) and apply M^-1 = L^-T L^-1 -- the
+ * reference's IncompleteCholeskyPreconditioner(L) of get_pcg_iter_time_scipy_ichol
+ * (validate.py:344-419, which takes an external L).  L is copied. */
+int lspcg_solver_set_ic_factor(lspcg_solver* s, const lspcg_mat* L, double* t_prec_ms);
 /* Solve A x = b from x (x0, in/out).  Semantics of scipy.sparse.linalg.cg (iterative.py
  * 359-418): atol = rtol*||b||, ||r|| checked at the top of each iteration, iters = number
  * of completed iterations, max_iter <= 0 means n.  res_hist (host, nullable, length

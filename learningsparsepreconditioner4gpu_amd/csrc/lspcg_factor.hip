@@ -186,6 +186,10 @@ void Levels::release() {
   (void)hipFree(order);
   (void)hipFree(pad);
   (void)hipFree(head);
+  (void)hipFree(sv);
+  (void)hipFree(inv);
+  (void)hipFree(c);
+  sv = inv = c = nullptr;
   ptr = order = pad = nullptr;
   head = nullptr;
   npad = 0;
@@ -258,7 +262,8 @@ int build_levels(lspcg_ctx* ctx, int64_t n, const int32_t* rp, const int32_t* ci
   LSPCG_HIP(hipMalloc(&out->pad, sizeof(int32_t) * pptr[maxl + 1]));
   LSPCG_HIP(hipMemsetAsync(out->pad, 0xFF, sizeof(int32_t) * pptr[maxl + 1], st));
   hipLaunchKernelGGL(k_pad_order, dim3(fgrid(n)), dim3(kThreads), 0, st, n, lev_s, ptr, dpptr, order, out->pad);
-  LSPCG_HIP(hipMalloc(&out->head, sizeof(unsigned)));
+  LSPCG_HIP(hipMalloc(&out->head, 2 * sizeof(unsigned)));  // [dequeue counter | timeout flag]
+  LSPCG_HIP(hipMemsetAsync(out->head, 0, 2 * sizeof(unsigned), st));
   LSPCG_HIP(hipStreamSynchronize(st));
   (void)hipFree(dpptr);
   out->npad = pptr[maxl + 1];
@@ -310,40 +315,24 @@ __global__ void k_ic0_level(const int32_t* __restrict__ order, int32_t beg, int3
 }
 
 // ---------------------------------------------------------------------------
-// triangular solves: one thread per row of the level (LOWER: diagonal last, UPPER: first)
+// triangular solves (LOWER: diagonal stored last in each row, UPPER: first)
 // ---------------------------------------------------------------------------
-template <typename T, bool LOWER>
-__global__ void k_trsv_level(const int32_t* __restrict__ order, int32_t beg, int32_t cnt,
-                             const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
-                             const T* __restrict__ v, const T* __restrict__ b, T* __restrict__ x,
-                             const int32_t* done) {
-  if (done && *done) return;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= cnt) return;
-  const int i = order[beg + t];
-  T s = b[i];
-  if constexpr (LOWER) {
-    const int pd = rp[i + 1] - 1;
-    for (int p = rp[i]; p < pd; ++p) s = s - v[p] * x[ci[p]];
-    x[i] = s / v[pd];
-  } else {
-    const int pd = rp[i];
-    for (int p = pd + 1; p < rp[i + 1]; ++p) s = s - v[p] * x[ci[p]];
-    x[i] = s / v[pd];
-  }
-}
-
 // Sync-free solve: ONE launch for the whole triangular solve instead of one per level.  A
 // resident grid (1 workgroup per CU: few polling waves per CU, short hand-offs) takes 256-position
 // blocks of the wave-padded level order from a dequeue counter, in order, so a block only ever
 // waits for blocks that running workgroups hold; thread t of block B owns position B*256 + t,
 // waits for its dependencies' values (all still-missing ones re-read together per poll round,
-// the row's values loaded beforehand) and runs k_trsv_level's arithmetic.  The
+// the row's values loaded beforehand) and runs scipy spsolve_triangular's arithmetic (the
+// reference's IC apply, validate.py:359-365; oracle/precond.py restates it): a unit solve on the
+// column-scaled factor, the row's updates in SuperLU's column order, then k_trsv_post.  The
 // hand-off is the value itself: x is first filled with a NaN pattern no arithmetic produces, each
 // row publishes its result with one 4- / 8-byte sc1 store (a self-validating granule,
 // MI355X_MICROARCH.md R2) and waiters poll with sc1 loads.  A wave never holds rows of two
-// levels, so no lane waits for a lane of its own wave.  A row whose wait exceeds ~0.1 s (never in a
-// finished solve: the chain is one hop per level) takes NaN, so the PCG stops as non-finite.
+// levels, so no lane waits for a lane of its own wave.  Forward progress: a block waits only for
+// blocks dequeued before it, which resident workgroups hold.  Every wave still has an exit: a row
+// whose wait exceeds 2 s (a finished solve's chain is ~2 us per level) raises the levels' error
+// word (head[1]) and takes NaN; lspcg_solver_solve / lspcg_trsv then fail with LSPCG_ERR_HIP
+// instead of returning a result.
 template <typename T>
 struct TrsvBits;
 template <>
@@ -376,7 +365,7 @@ __global__ void k_trsv_wait_fill(int64_t n, T* __restrict__ x, const int32_t* do
 template <typename T, bool LOWER>
 __global__ void __launch_bounds__(256) k_trsv_syncfree(int64_t npad, const int32_t* __restrict__ pad,
                                                        const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
-                                                       const T* __restrict__ v, const T* __restrict__ b, T* x,
+                                                       const T* __restrict__ sv, const T* __restrict__ b, T* x,
                                                        const int32_t* done, unsigned* head) {
   using U = typename TrsvBits<T>::U;
   __shared__ unsigned s_blk;
@@ -396,31 +385,32 @@ __global__ void __launch_bounds__(256) k_trsv_syncfree(int64_t npad, const int32
     const int i = t < npad ? pad[t] : -1;
     if (i >= 0) {
       T s = b[i];
-      const int pd = LOWER ? rp[i + 1] - 1 : rp[i];
-      const int p0 = LOWER ? rp[i] : pd + 1;
-      const int p1 = LOWER ? pd : rp[i + 1];
-      const T diag = v[pd];
+      // the off-diagonal entries of row i, visited in spsolve_triangular's update order:
+      // increasing column (lower, diagonal last) / decreasing column (upper, diagonal first)
+      const int cnt = rp[i + 1] - rp[i] - 1;
+      auto entry = [&](int k) { return LOWER ? rp[i] + k : rp[i + 1] - 1 - k; };
       // the dependencies' values are loaded kTrsvBatch at a time, and every poll round re-reads ALL
       // still-waiting ones together: one memory latency per round, not one per entry; the sum
-      // then runs in row order
-      for (int pb = p0; pb < p1; pb += kTrsvBatch) {
+      // then runs in update order
+      for (int kb = 0; kb < cnt; kb += kTrsvBatch) {
         U u[kTrsvBatch];
-        T w[kTrsvBatch];  // the row's values, loaded before the wait (not after the last hand-off)
+        T w[kTrsvBatch];  // the row's scaled values, loaded before the wait (not after the last hand-off)
         const U* src[kTrsvBatch];
 #pragma unroll
         for (int k = 0; k < kTrsvBatch; ++k) {
-          const int q = pb + k < p1 ? pb + k : p0;
+          const int q = entry(kb + k < cnt ? kb + k : 0);
           src[k] = xu + ci[q];
-          w[k] = v[q];
+          w[k] = sv[q];
         }
 #pragma unroll
         for (int k = 0; k < kTrsvBatch; ++k) u[k] = trsv_poll(src[k]);
         for (;;) {
           bool wait = false;
 #pragma unroll
-          for (int k = 0; k < kTrsvBatch; ++k) wait |= (pb + k < p1) && u[k] == TrsvBits<T>::kWait;
+          for (int k = 0; k < kTrsvBatch; ++k) wait |= (kb + k < cnt) && u[k] == TrsvBits<T>::kWait;
           if (!wait) break;
-          if (wall_clock64() - t0 > 10000000ull) {  // 0.1 s at the 100 MHz constant clock
+          if (wall_clock64() - t0 > 200000000ull) {  // 2 s at the 100 MHz constant clock
+            __hip_atomic_store(head + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
             for (int k = 0; k < kTrsvBatch; ++k)
               if (u[k] == TrsvBits<T>::kWait) u[k] = __builtin_bit_cast(U, T(NAN));
@@ -433,82 +423,126 @@ __global__ void __launch_bounds__(256) k_trsv_syncfree(int64_t npad, const int32
         }
 #pragma unroll
         for (int k = 0; k < kTrsvBatch; ++k)
-          if (pb + k < p1) s = s - w[k] * __builtin_bit_cast(T, u[k]);
+          if (kb + k < cnt) s = s - __builtin_bit_cast(T, u[k]) * w[k];
       }
-      __hip_atomic_store(xu + i, __builtin_bit_cast(U, s / diag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // unit triangular solve: the published value is y_i itself (k_trsv_post scales it)
+      __hip_atomic_store(xu + i, __builtin_bit_cast(U, s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
-static bool trsv_levels_env() {
-  static const bool v = [] { const char* e = std::getenv("LSPCG_TRSV_LEVELS"); return e && e[0] == '1'; }();
-  return v;
+// spsolve_triangular's column scaling: inv_i = 1 / d_i, c_i = d_i inv_i (the scaled diagonal the
+// lower solve's U phase divides by), then sv_p = v_p inv_{col p}
+template <typename T, bool LOWER>
+__global__ void k_trsv_inv(int64_t n, const int32_t* __restrict__ rp, const T* __restrict__ v, T* __restrict__ inv,
+                           T* __restrict__ c) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const T d = v[LOWER ? rp[i + 1] - 1 : rp[i]];
+    const T iv = T(1) / d;
+    inv[i] = iv;
+    c[i] = d * iv;
+  }
 }
 
-int trsv_launches(const Levels& lv) { return trsv_levels_env() ? lv.nlev : 3; }
+template <typename T>
+__global__ void k_trsv_scale(int64_t nnz, const int32_t* __restrict__ ci, const T* __restrict__ v,
+                             const T* __restrict__ inv, T* __restrict__ sv) {
+  for (int64_t p = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; p < nnz; p += int64_t(gridDim.x) * blockDim.x)
+    sv[p] = v[p] * inv[ci[p]];
+}
+
+// x_i = (y_i / c_i) inv_i (lower: SuperLU's U phase divides by the scaled diagonal) or y_i inv_i
+// (upper: its L phase divides by the identity's 1)
+template <typename T, bool LOWER>
+__global__ void k_trsv_post(int64_t n, T* __restrict__ x, const T* __restrict__ c, const T* __restrict__ inv,
+                            const int32_t* done) {
+  if (done && *done) return;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    if constexpr (LOWER) x[i] = (x[i] / c[i]) * inv[i];
+    else x[i] = x[i] * inv[i];
+  }
+}
+
+int trsv_prepare(const lspcg_mat* T_, bool lower, Levels* lv) {
+  LSPCG_CHECK(T_->block_size == 1 && T_->storage_dtype() == T_->dtype, LSPCG_ERR_UNSUPPORTED,
+              "trsv: scalar CSR with plain storage required");
+  hipStream_t st = T_->ctx->stream;
+  const int64_t n = T_->n, nnz = T_->nnzb;
+  const size_t es = T_->dtype == LSPCG_F64 ? 8 : 4;
+  (void)hipFree(lv->sv);
+  (void)hipFree(lv->inv);
+  (void)hipFree(lv->c);
+  lv->sv = lv->inv = lv->c = nullptr;
+  LSPCG_HIP(hipMalloc(&lv->sv, es * std::max<int64_t>(nnz, 1)));
+  LSPCG_HIP(hipMalloc(&lv->inv, es * std::max<int64_t>(n, 1)));
+  LSPCG_HIP(hipMalloc(&lv->c, es * std::max<int64_t>(n, 1)));
+  if (n == 0) return LSPCG_OK;
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    auto v = static_cast<const T*>(T_->vals);
+    if (lower)
+      hipLaunchKernelGGL((k_trsv_inv<T, true>), dim3(fgrid(n)), dim3(kThreads), 0, st, n, T_->rowptr, v,
+                         static_cast<T*>(lv->inv), static_cast<T*>(lv->c));
+    else
+      hipLaunchKernelGGL((k_trsv_inv<T, false>), dim3(fgrid(n)), dim3(kThreads), 0, st, n, T_->rowptr, v,
+                         static_cast<T*>(lv->inv), static_cast<T*>(lv->c));
+    if (nnz)
+      hipLaunchKernelGGL(k_trsv_scale<T>, dim3(fgrid(nnz)), dim3(kThreads), 0, st, nnz, T_->colind, v,
+                         static_cast<const T*>(lv->inv), static_cast<T*>(lv->sv));
+  };
+  if (T_->dtype == LSPCG_F64) go(double{});
+  else go(float{});
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
 
 int enqueue_trsv(const lspcg_mat* T_, const Levels& lv, bool lower, const void* b, void* x, const int32_t* done,
                  hipStream_t st) {
-  if (!trsv_levels_env() && lv.pad && lv.npad > 0) {
-    const int64_t n = T_->n;
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    static const int64_t per_cu = [] {
-      const char* e = std::getenv("LSPCG_TRSV_WG_PER_CU");
-      return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1);
-    }();
-    const dim3 g(unsigned(std::min<int64_t>((lv.npad + 255) / 256, per_cu * int64_t(cus)))), blk(256);
-    LSPCG_HIP(hipMemsetAsync(lv.head, 0, sizeof(unsigned), st));
-    if (T_->dtype == LSPCG_F64) {
-      auto vx = static_cast<double*>(x);
-      hipLaunchKernelGGL(k_trsv_wait_fill<double>, dim3(fgrid(n)), dim3(kThreads), 0, st, n, vx, done);
-      if (lower)
-        hipLaunchKernelGGL((k_trsv_syncfree<double, true>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind,
-                           static_cast<const double*>(T_->vals), static_cast<const double*>(b), vx, done, lv.head);
-      else
-        hipLaunchKernelGGL((k_trsv_syncfree<double, false>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind,
-                           static_cast<const double*>(T_->vals), static_cast<const double*>(b), vx, done, lv.head);
+  if (lv.npad <= 0) return LSPCG_OK;
+  LSPCG_CHECK(lv.sv && lv.inv && lv.c, LSPCG_ERR_ARG, "trsv: levels not prepared (trsv_prepare)");
+  const int64_t n = T_->n;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  // 1 workgroup per CU (2 or 4 measured slower: more polling waves)
+  const dim3 g(unsigned(std::min<int64_t>((lv.npad + 255) / 256, int64_t(cus)))), blk(256);
+  LSPCG_HIP(hipMemsetAsync(lv.head, 0, sizeof(unsigned), st));
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    auto vx = static_cast<T*>(x);
+    auto sv = static_cast<const T*>(lv.sv);
+    auto vb = static_cast<const T*>(b);
+    hipLaunchKernelGGL(k_trsv_wait_fill<T>, dim3(fgrid(n)), dim3(kThreads), 0, st, n, vx, done);
+    if (lower) {
+      hipLaunchKernelGGL((k_trsv_syncfree<T, true>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind, sv, vb,
+                         vx, done, lv.head);
+      hipLaunchKernelGGL((k_trsv_post<T, true>), dim3(fgrid(n)), dim3(kThreads), 0, st, n, vx,
+                         static_cast<const T*>(lv.c), static_cast<const T*>(lv.inv), done);
     } else {
-      auto vx = static_cast<float*>(x);
-      hipLaunchKernelGGL(k_trsv_wait_fill<float>, dim3(fgrid(n)), dim3(kThreads), 0, st, n, vx, done);
-      if (lower)
-        hipLaunchKernelGGL((k_trsv_syncfree<float, true>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind,
-                           static_cast<const float*>(T_->vals), static_cast<const float*>(b), vx, done, lv.head);
-      else
-        hipLaunchKernelGGL((k_trsv_syncfree<float, false>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind,
-                           static_cast<const float*>(T_->vals), static_cast<const float*>(b), vx, done, lv.head);
+      hipLaunchKernelGGL((k_trsv_syncfree<T, false>), g, blk, 0, st, lv.npad, lv.pad, T_->rowptr, T_->colind, sv, vb,
+                         vx, done, lv.head);
+      hipLaunchKernelGGL((k_trsv_post<T, false>), dim3(fgrid(n)), dim3(kThreads), 0, st, n, vx,
+                         static_cast<const T*>(lv.c), static_cast<const T*>(lv.inv), done);
     }
-    LSPCG_HIP(hipGetLastError());
-    return LSPCG_OK;
-  }
-  for (int l = 0; l < lv.nlev; ++l) {
-    const int beg = lv.hptr[l], cnt = lv.hptr[l + 1] - lv.hptr[l];
-    if (cnt <= 0) continue;
-    const dim3 g((cnt + 127) / 128), blk(128);
-    if (T_->dtype == LSPCG_F64) {
-      auto vb = static_cast<const double*>(b);
-      auto vx = static_cast<double*>(x);
-      auto vv = static_cast<const double*>(T_->vals);
-      if (lower)
-        hipLaunchKernelGGL((k_trsv_level<double, true>), g, blk, 0, st, lv.order, beg, cnt, T_->rowptr, T_->colind,
-                           vv, vb, vx, done);
-      else
-        hipLaunchKernelGGL((k_trsv_level<double, false>), g, blk, 0, st, lv.order, beg, cnt, T_->rowptr, T_->colind,
-                           vv, vb, vx, done);
-    } else {
-      auto vb = static_cast<const float*>(b);
-      auto vx = static_cast<float*>(x);
-      auto vv = static_cast<const float*>(T_->vals);
-      if (lower)
-        hipLaunchKernelGGL((k_trsv_level<float, true>), g, blk, 0, st, lv.order, beg, cnt, T_->rowptr, T_->colind,
-                           vv, vb, vx, done);
-      else
-        hipLaunchKernelGGL((k_trsv_level<float, false>), g, blk, 0, st, lv.order, beg, cnt, T_->rowptr, T_->colind,
-                           vv, vb, vx, done);
-    }
-  }
+  };
+  if (T_->dtype == LSPCG_F64) go(double{});
+  else go(float{});
   LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+int trsv_check_timeout(const Levels& lv, hipStream_t st) {
+  if (!lv.head) return LSPCG_OK;
+  unsigned h = 0;
+  LSPCG_HIP(hipMemcpyAsync(&h, lv.head + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  LSPCG_HIP(hipStreamSynchronize(st));
+  if (h) {
+    LSPCG_HIP(hipMemsetAsync(lv.head + 1, 0, sizeof(unsigned), st));
+    LSPCG_HIP(hipStreamSynchronize(st));
+    set_error("triangular solve: a row waited more than 2 s for a dependency (sync-free hand-off timed out); "
+              "the result is invalid");
+    return LSPCG_ERR_HIP;
+  }
   return LSPCG_OK;
 }
 
@@ -804,11 +838,13 @@ int lspcg_trsv(const lspcg_mat* T, int lower, const void* b, void* x) {
   LSPCG_HIP(hipSetDevice(T->ctx->device));
   Levels lv;
   int rc = build_levels(T->ctx, T->n, T->rowptr, T->colind, lower != 0, &lv);
+  if (!rc) rc = trsv_prepare(T, lower != 0, &lv);
   if (!rc) rc = enqueue_trsv(T, lv, lower != 0, b, x, nullptr, T->ctx->stream);
   if (!rc && hipStreamSynchronize(T->ctx->stream) != hipSuccess) {
     set_error("trsv: stream synchronize failed");
     rc = LSPCG_ERR_HIP;
   }
+  if (!rc) rc = trsv_check_timeout(lv, T->ctx->stream);
   lv.release();
   return rc;
 }

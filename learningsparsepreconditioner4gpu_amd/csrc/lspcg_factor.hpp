@@ -20,22 +20,31 @@ struct Levels {
   std::vector<int32_t> hptr;
   // sync-free solve (lspcg_factor.hip k_trsv_syncfree): `order` with every level padded to whole
   // wave64s (-1 = no row), so no wave holds two rows of which one waits for the other; npad
-  // positions; head = the launch's block dequeue counter
+  // positions; head[0] = the launch's block dequeue counter, head[1] = timeout flag
   int32_t* pad = nullptr;
   int64_t npad = 0;
   unsigned* head = nullptr;
+  // the triangular factor's column-scaled values sv_p = v_p / d_col and per row inv = 1 / d,
+  // c = d inv (trsv_prepare: spsolve_triangular's scaling)
+  void* sv = nullptr;
+  void* inv = nullptr;
+  void* c = nullptr;
   void release();
 };
 
 // lower: row i depends on the columns j < i of its row; upper: on the columns j > i.
 int build_levels(lspcg_ctx* ctx, int64_t n, const int32_t* rp, const int32_t* ci, bool lower, Levels* out);
-// x = T⁻¹ b (lower: diagonal stored last in each row, upper: first); `done` (nullable) is the
-// solver's device done flag -- every launch returns at once when it is set.  One sync-free launch
-// (rows wait for their dependencies' values) or, with LSPCG_TRSV_LEVELS=1, one launch per level.
-// Same bits either way.  launches_per_solve: graph nodes one enqueue_trsv adds.
+// scaled values of T for enqueue_trsv (after build_levels), enqueued on T's context stream
+int trsv_prepare(const lspcg_mat* T, bool lower, Levels* lv);
+// x = T⁻¹ b in scipy spsolve_triangular's arithmetic (lower: diagonal stored last in each row,
+// upper: first); `done` (nullable) is the solver's device done flag -- every launch returns at
+// once when it is set.  Counter reset + fill + one sync-free launch (rows wait for their
+// dependencies' values) + the diagonal scaling.
 int enqueue_trsv(const lspcg_mat* T, const Levels& lv, bool lower, const void* b, void* x, const int32_t* done,
                  hipStream_t st);
-int trsv_launches(const Levels& lv);
+constexpr int kTrsvLaunches = 4;  // graph nodes one enqueue_trsv adds
+// LSPCG_ERR_HIP (and clears the flag) when a sync-free solve on these levels timed out
+int trsv_check_timeout(const Levels& lv, hipStream_t st);
 int ic0_factor(const lspcg_mat* A, lspcg_mat** L);
 int ainv0_factor(const lspcg_mat* A, lspcg_mat** L);
 

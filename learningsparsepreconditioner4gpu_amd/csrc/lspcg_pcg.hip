@@ -555,7 +555,6 @@ struct CsrView {
 
 constexpr int kSmallThreads = 512;  // 2 waves per SIMD: the compensated reductions are VALU work
 constexpr int kSmallThreadsBig = 1024;  // n > 1024: 4 waves per SIMD keep rows per thread <= 3
-constexpr int kSmallRows = 5;       // largest rows per thread (template R = 1, 2 or 5 at 512 threads)
 constexpr int64_t kSmallLds = 61440;  // dynamic LDS: 3 gathered vectors
 constexpr int kSmallQB = 2;  // SELL groups (4 entries each) loaded per wait (4 measured slower: 13.0 vs 9.8 us per iteration)
 
@@ -587,7 +586,7 @@ __device__ __forceinline__ T sell_row(const CsrView& M, int32_t b, int32_t e, in
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             ok[4 * u + j] = o[j] != kSellPad16 && q0 + u < e;
-            c[4 * u + j] = ok[4 * u + j] ? base + o[j] : 0;
+            c[4 * u + j] = ok[4 * u + j] ? base + o[j] : i;  // masked slots gather the row's own entry
           }
         } else {
           const i32x4 cc = *(const __attribute__((address_space(1))) i32x4*)(static_cast<const int32_t*>(M.scol) + off);
@@ -595,7 +594,7 @@ __device__ __forceinline__ T sell_row(const CsrView& M, int32_t b, int32_t e, in
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             ok[4 * u + j] = o[j] >= 0 && q0 + u < e;
-            c[4 * u + j] = ok[4 * u + j] ? o[j] : 0;
+            c[4 * u + j] = ok[4 * u + j] ? o[j] : i;
           }
         }
       }
@@ -1009,7 +1008,6 @@ struct lspcg_solver {
   void* own_L = nullptr;
   void* own_LT = nullptr;
   int* flag = nullptr;
-  bool compact = true;
   // IC(0): factor, its explicit transpose and their level sets
   lspcg_mat* icL = nullptr;
   lspcg_mat* icU = nullptr;
@@ -1017,7 +1015,6 @@ struct lspcg_solver {
   // SELL-64 copies of the scalar iteration views A (0), L (1), Lᵀ (2) (lspcg_sell.hpp); sp[w]
   // is null where the CSR kernel is used (block size 3, irregular rows, LSPCG_NO_SELL=1)
   bool use_sell = true;
-  bool sell16 = true;  // 16-bit column offsets where they fit (LSPCG_SELL32=1 disables)
   SellPattern spat[3];
   const SellPattern* sp[3] = {nullptr, nullptr, nullptr};
   void* sv[3] = {nullptr, nullptr, nullptr};
@@ -1063,7 +1060,7 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   if (w > 0 && s->sp[0] && view->rowptr == s->Av.rowptr && view->colind == s->Av.colind) {
     P = s->sp[0];
   } else {
-    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(), s->sell16, st,
+    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(), true, st,
                                       &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: CSR kernel
     if (rc) return rc;
@@ -1085,7 +1082,7 @@ static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view) {
   if (shared) {
     P = s->sp[0];
   } else {
-    const int rc = bsell_build_pattern(view->nb, view->nnzb, view->rowptr, view->colind, sell_max_pad(), s->sell16, st,
+    const int rc = bsell_build_pattern(view->nb, view->nnzb, view->rowptr, view->colind, sell_max_pad(), true, st,
                                        &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: the staged block kernel
     if (rc) return rc;
@@ -1143,7 +1140,7 @@ static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const
   }
   *view = *M;
   const int64_t ne = M->nnzb * M->block_size * M->block_size;
-  const bool try_compact = s->compact && M->dtype == LSPCG_F64 && M->storage_dtype() == LSPCG_F64 && ne > 0;
+  const bool try_compact = M->dtype == LSPCG_F64 && M->storage_dtype() == LSPCG_F64 && ne > 0;
   const bool try_share = base && base != M && base->nb == M->nb && base->nnzb == M->nnzb &&
                          base->block_size == M->block_size;
   int f = 3;
@@ -1337,16 +1334,10 @@ static int enqueue_fixup(lspcg_solver* s, hipStream_t st) {
   return LSPCG_OK;
 }
 
-// LSPCG_SMALL_BIG=0: n in (1024, 2560] on the previous 512-thread, 5-row one-workgroup kernel
-static bool small_big() {
-  static const bool v = [] { const char* e = std::getenv("LSPCG_SMALL_BIG"); return !(e && e[0] == '0'); }();
-  return v;
-}
-
 static bool small_path(const lspcg_solver* s) {
   if (s->dot_order != LSPCG_DOT_COMPENSATED) return false;  // parity mode: the multi-kernel schedule
   if (s->n <= 0 || s->n > s->small_n || s->precond == LSPCG_PRECOND_IC || s->Av.block_size != 1) return false;
-  if (s->n > (small_big() ? int64_t(kSmallThreadsBig) * 3 : int64_t(kSmallThreads) * kSmallRows) || 3 * s->n * (s->dtype == LSPCG_F32 ? 4 : 8) > kSmallLds) return false;
+  if (s->n > int64_t(kSmallThreadsBig) * 3 || 3 * s->n * (s->dtype == LSPCG_F32 ? 4 : 8) > kSmallLds) return false;
   if (s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED)
     return s->Lv.block_size == 1 && s->LTv.block_size == 1;
   return true;
@@ -1407,11 +1398,9 @@ static int launch_small(lspcg_solver* s, hipStream_t st) {
   using T512 = std::integral_constant<int, kSmallThreads>;
   using T1024 = std::integral_constant<int, kSmallThreadsBig>;
   // n <= 1024: 512 threads, <= 2 rows each (the measured best there); above: 1024 threads, 2-3 rows
-  // (LSPCG_SMALL_BIG=0: the previous 512-thread, 5-row variant)
-  const bool big = small_big();
+  // (512 threads x 5 rows measured 20.5-28.2 vs 16.3-21.7 us per iteration)
   if (n <= kSmallThreads) go(I{}, T512{});
   else if (n <= 2 * kSmallThreads) go(I2{}, T512{});
-  else if (!big) go(std::integral_constant<int, kSmallRows>{}, T512{});
   else if (n <= 2 * kSmallThreadsBig) go(I2{}, T1024{});
   else go(I3{}, T1024{});
   LSPCG_HIP(hipGetLastError());
@@ -1478,9 +1467,7 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   LSPCG_HIP(hipEventCreate(&s->ev_t0));
   LSPCG_HIP(hipEventCreate(&s->ev_t1));
   LSPCG_HIP(hipMalloc(&s->flag, sizeof(int)));
-  if (const char* e = std::getenv("LSPCG_NO_COMPACT")) s->compact = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
-  if (const char* e = std::getenv("LSPCG_SELL32")) s->sell16 = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SMALL_N")) s->small_n = std::max<int64_t>(0, std::atoll(e));
   if (const char* e = std::getenv("LSPCG_SMALL_SELL")) s->small_sell = e[0] != '0';
   if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
@@ -1506,46 +1493,23 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   LSPCG_CHECK(L->n == s->n, LSPCG_ERR_ARG, "set_spai: L has a different size than A");
   LSPCG_CHECK(L->dtype == s->dtype, LSPCG_ERR_ARG, "set_spai: L dtype differs from A dtype");
   hipStream_t cst = s->ctx->stream;
-  // LSPCG_SETUP_PROFILE=1: host wall time of each setup phase (device drained after each) on stderr
-  static const bool prof = [] { const char* e = std::getenv("LSPCG_SETUP_PROFILE"); return e && e[0] == '1'; }();
-  std::vector<std::pair<const char*, double>> phases;
-  auto t_last = std::chrono::steady_clock::now();
-  auto phase = [&](const char* name) {
-    if (!prof) return;
-    (void)hipDeviceSynchronize();
-    const auto t = std::chrono::steady_clock::now();
-    phases.emplace_back(name, std::chrono::duration<double, std::milli>(t - t_last).count());
-    t_last = t;
-  };
-  phase("enter");
   LSPCG_HIP(hipEventRecord(s->ev_t0, cst));
   if (s->LT) {
     lspcg_mat_destroy(s->LT);
     s->LT = nullptr;
   }
-  phase("free old Lt");
   bool lt_same = false;
   int rc = mat_transpose(L, &s->LT, &lt_same);
   if (rc) return rc;
-  phase(lt_same ? "transpose (symmetric pattern)" : "transpose (general)");
   if (s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) {
     rc = lspcg_mat_diagonal(s->A, s->d);
     if (rc) return rc;
   }
   int lflag = 3;
   if ((rc = make_view(s, L, &s->Lv, &s->Av, &s->own_L, nullptr, &lflag))) return rc;
-  phase("view L");
   if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT, lt_same ? &lflag : nullptr))) return rc;
-  phase("view Lt");
   if ((rc = build_sell(s, 1, &s->Lv))) return rc;
-  phase("sell L");
   if ((rc = build_sell(s, 2, &s->LTv))) return rc;
-  phase("sell Lt");
-  if (prof) {
-    std::fprintf(stderr, "[lspcg setup] n=%lld lflag=%d", (long long)s->n, lflag);
-    for (auto& p : phases) std::fprintf(stderr, " | %s %.3f ms", p.first, p.second);
-    std::fprintf(stderr, "\n");
-  }
   s->split_ok = s->allow_split && s->sp[0] && s->sp[1] && s->sp[2];
   s->split = s->split_ok && s->dot_order == LSPCG_DOT_COMPENSATED;
   if (s->split_ok) {
@@ -1580,21 +1544,43 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   return LSPCG_OK;
 }
 
-int lspcg_solver_set_ic(lspcg_solver* s, double* t_prec_ms) {
+// IC preconditioner: factor (given, or IC(0) of A computed on the device), its explicit transpose
+// and both level orders
+static int install_ic(lspcg_solver* s, const lspcg_mat* given, double* t_prec_ms) {
   LSPCG_CHECK(s, LSPCG_ERR_ARG, "set_ic: NULL");
   LSPCG_CHECK(s->precond == LSPCG_PRECOND_IC, LSPCG_ERR_ARG, "set_ic: solver was not created with LSPCG_PRECOND_IC");
   LSPCG_HIP(hipSetDevice(s->ctx->device));
   LSPCG_HIP(hipStreamSynchronize(s->stream));
+  if (given) {
+    LSPCG_CHECK(given->n == s->n && given->block_size == 1 && given->dtype == s->dtype &&
+                    given->storage_dtype() == given->dtype,
+                LSPCG_ERR_ARG, "set_ic_factor: L must be a scalar CSR of the solver's size and dtype");
+    // lower triangular with the diagonal stored last in every row (host check of the pattern)
+    std::vector<int32_t> rp(size_t(s->n) + 1), ci(size_t(std::max<int64_t>(given->nnzb, 1)));
+    if (int rc = lspcg_mat_copy_out(given, rp.data(), ci.data(), nullptr)) return rc;
+    for (int64_t i = 0; i < s->n; ++i) {
+      bool ok = rp[i + 1] > rp[i] && ci[rp[i + 1] - 1] == i;
+      for (int32_t p = rp[i]; ok && p < rp[i + 1] - 1; ++p) ok = ci[p] < ci[p + 1];
+      LSPCG_CHECK(ok, LSPCG_ERR_FORMAT,
+                  "set_ic_factor: row " + std::to_string(i) + " is not lower triangular with its diagonal last");
+    }
+  }
   hipStream_t cst = s->ctx->stream;
   LSPCG_HIP(hipEventRecord(s->ev_t0, cst));
   for (lspcg_mat** m : {&s->icL, &s->icU}) {
     if (*m) lspcg_mat_destroy(*m);
     *m = nullptr;
   }
-  int rc = ic0_factor(s->A, &s->icL);
+  s->levL.release();
+  s->levU.release();
+  int rc = given ? lspcg_mat_create_csr(s->ctx, given->n, given->nnzb, given->rowptr, given->colind, given->vals,
+                                        given->dtype, &s->icL)
+                 : ic0_factor(s->A, &s->icL);
   if (!rc) rc = lspcg_mat_transpose(s->icL, &s->icU);
   if (!rc) rc = build_levels(s->ctx, s->n, s->icL->rowptr, s->icL->colind, true, &s->levL);
   if (!rc) rc = build_levels(s->ctx, s->n, s->icU->rowptr, s->icU->colind, false, &s->levU);
+  if (!rc) rc = trsv_prepare(s->icL, true, &s->levL);
+  if (!rc) rc = trsv_prepare(s->icU, false, &s->levU);
   if (rc) return rc;
   LSPCG_HIP(hipEventRecord(s->ev_t1, cst));
   LSPCG_HIP(hipEventSynchronize(s->ev_t1));
@@ -1606,6 +1592,13 @@ int lspcg_solver_set_ic(lspcg_solver* s, double* t_prec_ms) {
   s->graphs.clear();
   s->graph_defs.clear();
   return LSPCG_OK;
+}
+
+int lspcg_solver_set_ic(lspcg_solver* s, double* t_prec_ms) { return install_ic(s, nullptr, t_prec_ms); }
+
+int lspcg_solver_set_ic_factor(lspcg_solver* s, const lspcg_mat* L, double* t_prec_ms) {
+  LSPCG_CHECK(L, LSPCG_ERR_ARG, "set_ic_factor: NULL factor");
+  return install_ic(s, L, t_prec_ms);
 }
 
 int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int64_t max_iter, int64_t* iters,
@@ -1654,7 +1647,7 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   // decay minus the iterations already in flight, so that at most a few early-exit launches trail
   // the converged iteration (every launch is predicated on the device `done` flag).
   // graphs hold <= ~4096 nodes (IC: one launch per level of each triangular solve)
-  const int kpi = s->precond == LSPCG_PRECOND_IC ? trsv_launches(s->levL) + trsv_launches(s->levU) + 4 : 5;
+  const int kpi = s->precond == LSPCG_PRECOND_IC ? 2 * kTrsvLaunches + 4 : 5;
   const int max_chunk = std::max(1, std::min(32, 4096 / kpi));
   PcgState* const hs[2] = {s->hS, s->hS + 1};
   const hipEvent_t evp[2] = {s->ev_poll, s->ev_poll2};
@@ -1735,6 +1728,10 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   LSPCG_HIP(hipEventRecord(s->ev_out, st));
   LSPCG_HIP(hipStreamWaitEvent(s->ctx->stream, s->ev_out, 0));
   LSPCG_HIP(hipEventSynchronize(s->ev_t1));
+  if (s->precond == LSPCG_PRECOND_IC) {  // a timed-out sync-free hand-off fails the solve loudly
+    if (int r2 = trsv_check_timeout(s->levL, st)) return r2;
+    if (int r2 = trsv_check_timeout(s->levU, st)) return r2;
+  }
   float ms = 0.f;
   LSPCG_HIP(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1));
   if (t_solve_ms) *t_solve_ms = ms;
@@ -2127,13 +2124,16 @@ __global__ void __launch_bounds__(kThreads) k_batch_update_p_sums(BatchMap m, Pc
                                                              T* __restrict__ x) {
   const int sys = m.etile_sys[blockIdx.x];
   PcgState* St = S + sys;
-  if (St->done) return;
+  // `done` is loaded once and tested only after the group sums: group_sum_dd may hold workgroup
+  // barriers, and this system's first workgroup can write `done` during this launch
+  const int32_t done = St->done;
   const int64_t i = int64_t(blockIdx.x) * kThreads + threadIdx.x;
   const T zi = z[i], pi = p[i], xi = x[i];
   const int t0 = m.tile0[sys], t1 = m.tile0[sys + 1];
   const int64_t k = St->iter;
   double v[2];
   group_sum_dd<2>(gz + size_t(t0) * 4, t1 - t0, v);
+  if (done) return;
   const double rho = round_to<T>(v[0]);
   const double rr = k > 0 ? round_to<T>(v[1]) : St->rr;
   int code = 0;
@@ -2344,7 +2344,6 @@ static int launch_batch_small(lspcg_batch* bt, hipStream_t st) {
   using T1024 = std::integral_constant<int, kSmallThreadsBig>;
   if (n <= kSmallThreads) go(std::integral_constant<int, 1>{}, T512{});
   else if (n <= 2 * kSmallThreads) go(std::integral_constant<int, 2>{}, T512{});
-  else if (!small_big()) go(std::integral_constant<int, kSmallRows>{}, T512{});
   else if (n <= 2 * kSmallThreadsBig) go(std::integral_constant<int, 2>{}, T1024{});
   else go(std::integral_constant<int, 3>{}, T1024{});
   LSPCG_HIP(hipGetLastError());
@@ -2494,7 +2493,7 @@ int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, cons
   for (int k = 0; k < nsys; ++k) bt->max_n = std::max<int64_t>(bt->max_n, bt->n[k]);
   {
     const char* e = std::getenv("LSPCG_BATCH_SMALL");
-    const int64_t row_cap = small_big() ? int64_t(kSmallThreadsBig) * 3 : int64_t(kSmallThreads) * kSmallRows;
+    const int64_t row_cap = int64_t(kSmallThreadsBig) * 3;
     bt->small = !(e && e[0] == '0') && bt->bs == 1 && bt->max_n <= std::min<int64_t>(row_cap, bt->s->small_n) &&
                 3 * bt->max_n * int64_t(esize(bt->dtype)) <= kSmallLds;
   }

@@ -300,23 +300,18 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_bsell3(SellArgs<VT, CT> a, Pr
 
 // Reducing launches use a resident grid: 6 workgroups per CU (the compact-value kernels'
 // __launch_bounds__ guarantee), i.e. 1536 on MI355X -- one wave of workgroups, each walking its
-// row tiles, so no straggler round delays the ticket (8 per CU / 2048 measured the same).  Capped by the solver's 4096
-// partial slots.  Knobs LSPCG_SELL_RCAP / LSPCG_SELL_NCAP (read once) for experiments.
+// row tiles, so no straggler round delays the ticket (8 per CU / 2048 measured the same; caps of
+// 1024 / 1342 / 2013 / 4025 measured no better).  Capped by the solver's 4096
+// partial slots.  Non-reducing launches take one workgroup per row tile.
 inline int64_t sell_cap(bool reducing) {
   static const int64_t rcap = [] {
-    const char* e = std::getenv("LSPCG_SELL_RCAP");
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    const int64_t v = e ? std::atoll(e) : int64_t(6) * cus;
-    return std::max<int64_t>(1, std::min<int64_t>(v, 4096));
+    return std::max<int64_t>(1, std::min<int64_t>(int64_t(6) * cus, 4096));
   }();
-  static const int64_t ncap = [] {
-    const char* e = std::getenv("LSPCG_SELL_NCAP");
-    return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1) << 40;
-  }();
-  return reducing ? rcap : ncap;
+  return reducing ? rcap : int64_t(1) << 40;
 }
 
 // largest padded-slots / nnz ratio for which a SELL view is built (LSPCG_SELL_MAXPAD, read once)

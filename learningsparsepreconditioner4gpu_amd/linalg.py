@@ -80,6 +80,17 @@ class PreconditionedConjugateGradient:
         if dot_order != "compensated":
             self.set_dot_order(dot_order, dot_threads)
 
+    def set_ic_factor(self, L) -> float:
+        """``preconditioner="ic"`` with a given lower factor L (M⁻¹ = L⁻ᵀ L⁻¹; the reference's
+        ``IncompleteCholeskyPreconditioner(L)``, validate.py:344-419).  Returns the setup time (s)."""
+        if self.preconditioner != "ic":
+            raise ValueError("set_ic_factor needs preconditioner='ic'")
+        Ld = _as_device_matrix(L, self.dtype, 1, self.ctx)
+        ms = C.c_double()
+        _lib.call("lspcg_solver_set_ic_factor", self.handle, Ld.handle, C.byref(ms))
+        self.setup_time = ms.value / 1e3
+        return self.setup_time
+
     def set_dot_order(self, order: str = "compensated", threads: int = 1):
         """Summation order of the loop's dots and norms (include/lspcg.h lspcg_solver_set_dot_order).
         ``"compensated"`` (default): compensated dots in a fixed tree (~correctly rounded) on the

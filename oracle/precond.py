@@ -5,9 +5,10 @@ The reference calls pymathprim's ``ic`` and ``ainv`` preconditioners (``infer.py
 **parity unpinned** (SURVEY.md 8(c)).  This module fixes the published algorithms the GPU
 implements, with an explicit operation order, so the HIP factors can be checked bit for bit:
 
-* IC(0) -- incomplete Cholesky with the sparsity of tril(A) (row-oriented "up-looking" form;
-  the reference's own scipy restatement ``IncompleteCholeskyPreconditioner``,
-  validate.py:344-369, applies ``L Lᵀ`` by two triangular solves, as here).
+* IC(0) -- incomplete Cholesky with the sparsity of tril(A) (row-oriented "up-looking" form).
+  Its APPLY is the reference's own scipy restatement ``IncompleteCholeskyPreconditioner``
+  (validate.py:344-369: two spsolve_triangular calls), restated bit for bit below and pinned
+  against the reference's get_pcg_iter_time_scipy_ichol trajectories (ic_traj.npz).
 * AINV(0) -- Benzi & Tůma's factorized approximate inverse A⁻¹ ≈ Z D⁻¹ Zᵀ by incomplete
   A-biconjugation (symmetric case), Z unit upper triangular restricted to the pattern of
   triu(A) (left-looking form; identical arithmetic to the right-looking one).  Applied as
@@ -75,42 +76,50 @@ def ic0(A: sp.csr_matrix) -> sp.csr_matrix:
     return sp.csr_matrix((np.array(data), np.array(indices, dtype=np.int32), indptr), shape=(n, n))
 
 
+# The reference's IC apply (validate.py:359-365) is scipy.sparse.linalg.spsolve_triangular on
+# csc(L) then csc(Lᵀ).  scipy 1.15's arithmetic (scipy/sparse/linalg/_dsolve/linsolve.py
+# spsolve_triangular -> SuperLU gstrs), restated: the columns are scaled by inv = 1/diag
+# (A @ diags(inv)); the unit triangular solve then runs column by column, x_i -= x_j * A'_ij, so
+# row i receives its updates in increasing j for the lower solve and in DECREASING j for the
+# upper one; the lower solve's U phase divides by the scaled diagonal c = d * inv (not always
+# exactly 1), the upper's L phase by 1; finally x *= inv.  Verified bit for bit against
+# spsolve_triangular (tests/test_oracle_golden.py::test_trsv_is_spsolve_triangular).
 def trsv_lower(L: sp.csr_matrix, r: np.ndarray) -> np.ndarray:
-    """y_i = r_i; y_i -= L_ik y_k (increasing k < i); y_i = y_i / L_ii."""
+    """spsolve_triangular(csc(L), r, lower=True): y_i = r_i - Σ_{k<i, increasing} y_k (L_ik inv_k);
+    x_i = (y_i / (d_i inv_i)) inv_i."""
     rows = _rows(L)
+    d = np.asarray(sp.csr_matrix(L).diagonal(), dtype=np.float64)
+    inv = 1.0 / d
     y = np.zeros(len(r))
     for i, (cols, vals) in enumerate(rows):
         s = float(r[i])
-        d = None
         for k, v in zip(cols.tolist(), vals.tolist()):
             if k < i:
-                s = s - v * y[k]
-            elif k == i:
-                d = v
-        y[i] = s / d
-    return y
+                s = s - y[k] * (v * inv[k])
+        y[i] = s
+    return (y / (d * inv)) * inv
 
 
 def trsv_upper(U: sp.csr_matrix, r: np.ndarray) -> np.ndarray:
-    """z_i = r_i; z_i -= U_ij z_j (increasing j > i); z_i = z_i / U_ii, rows from the last."""
+    """spsolve_triangular(csc(U), r, lower=False): rows from the last, y_i = r_i - Σ_{j>i,
+    DECREASING j} y_j (U_ij inv_j); x_i = y_i inv_i."""
     rows = _rows(U)
-    z = np.zeros(len(r))
+    d = np.asarray(sp.csr_matrix(U).diagonal(), dtype=np.float64)
+    inv = 1.0 / d
+    y = np.zeros(len(r))
     for i in range(len(r) - 1, -1, -1):
         cols, vals = rows[i]
         s = float(r[i])
-        d = None
-        for j, v in zip(cols.tolist(), vals.tolist()):
+        for j, v in zip(reversed(cols.tolist()), reversed(vals.tolist())):
             if j > i:
-                s = s - v * z[j]
-            elif j == i:
-                d = v
-        z[i] = s / d
-    return z
+                s = s - y[j] * (v * inv[j])
+        y[i] = s
+    return y * inv
 
 
 def ic_operator(L: sp.csr_matrix) -> Callable[[np.ndarray], np.ndarray]:
-    """z = L⁻ᵀ L⁻¹ r (validate.py:358-365 IncompleteCholeskyPreconditioner._matvec), Lᵀ as an
-    explicit CSR."""
+    """z = L⁻ᵀ L⁻¹ r (validate.py:358-365 IncompleteCholeskyPreconditioner._matvec: two
+    spsolve_triangular calls), Lᵀ as an explicit CSR."""
     L = sp.csr_matrix(L)
     U = sp.csr_matrix(L.T)
     U.sort_indices()

@@ -30,6 +30,7 @@ Fixtures (inputs and the reference's outputs, data only):
   gnn_forward.npz  -- the reference's NodeEdgeProcessing.forward (seeded) on make_data inputs of
                       the BASELINE configs' layouts (F_in 1 / 2 / 5 / 9), with its state_dict
   graph_spmv.npz   -- the reference's GraphSpmv / AATPE / LLT on random edge lists (fp32, fp64)
+  ic_traj.npz      -- the reference's get_pcg_iter_time_scipy_ichol on the oracle's IC(0) factor
   ../../learningsparsepreconditioner4gpu_amd/meshes/bunny_grid.npz
                    -- voxelised interior of data/objs/bunny_low_res.obj (winding numbers of a
                       regular grid's vertices), input of the C3 heat stand-in (problems.heat_bunny);
@@ -43,6 +44,7 @@ Fixtures (inputs and the reference's outputs, data only):
     python tests/golden/make_golden.py            # every fixture
     python tests/golden/make_golden.py traj       # pcg_traj.npz only
     python tests/golden/make_golden.py gnn        # gnn_forward.npz + graph_spmv.npz only
+    python tests/golden/make_golden.py ichol      # ic_traj.npz only
     python tests/golden/make_golden.py bunny      # bunny_grid.npz only
 """
 from __future__ import annotations
@@ -341,6 +343,51 @@ def traj_fixtures(rval):
     np.savez_compressed(OUT / "pcg_traj.npz", **out)
 
 
+def ichol_fixtures(rval):
+    """ic_traj.npz: the reference's PCG-IC entry point get_pcg_iter_time_scipy_ichol
+    (validate.py:372-419: IncompleteCholeskyPreconditioner(L), two spsolve_triangular calls per
+    apply) on the oracle's IC(0) factor (ilupp, the reference's own factorization, is absent:
+    the factor arithmetic stays parity-unpinned, the apply and the loop are pinned), recording
+    count, every ‖r_k‖ and x at 1 OpenBLAS thread."""
+    import threadpoolctl
+
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from oracle import linalg as O
+    from oracle import precond as OP
+
+    rec = RecordingCG()
+    rval.cg = rec
+
+    def masked(A, m):
+        M = O.apply_dbc_masking(sp.csr_matrix(A), m).tocsr()
+        M.eliminate_zeros()
+        M.sort_indices()
+        return M
+
+    A1, m1, _ = P.poisson2d_grid(16, 16)
+    A3, m3, _ = P.poisson2d_grid(64, 64)
+    systems = {"poisson16": (masked(A1, m1), m1.ravel()), "kuhn7": (sp.csr_matrix(P.kuhn_laplacian(7)), None),
+               "poisson64": (masked(A3, m3), m3.ravel())}
+    out = {"blas_info": np.array(blas_info())}
+    for name, (A, m) in systems.items():
+        A.sort_indices()
+        gt = np.ones(A.shape[0]) if m is None else m.astype(np.float64)
+        L = OP.ic0(A)
+        out[f"{name}__indptr"], out[f"{name}__indices"], out[f"{name}__data"] = A.indptr, A.indices, A.data
+        out[f"{name}__L_indptr"], out[f"{name}__L_indices"], out[f"{name}__L_data"] = L.indptr, L.indices, L.data
+        out[f"{name}__gt"] = gt
+        for rtol in (1e-6, 1e-8):
+            with threadpoolctl.threadpool_limits(1):
+                cnt = rval.get_pcg_iter_time_scipy_ichol(A, L, gt, rtol=rtol)
+            assert cnt == rec.count and len(rec.hist) == cnt
+            t = f"{name}__rtol{int(-np.log10(rtol))}"
+            out[f"{t}__count"] = np.array(cnt)
+            out[f"{t}__hist"] = np.array(rec.hist)
+            out[f"{t}__x"] = rec.x.copy()
+            print("ichol", name, rtol, cnt, flush=True)
+    np.savez_compressed(OUT / "ic_traj.npz", **out)
+
+
 def _gnn_cfg():
     ff = lambda norm: {"pre_norm": norm, "hidden_channels": 16, "num_layers": 2}
     return dict(node_encoder=ff("none"), edge_encoder=ff("none"), node_decoder=ff("none"), edge_decoder=ff("none"),
@@ -478,6 +525,12 @@ def main():
 
         sys.path.insert(0, str(ROOT))
         traj_fixtures(rval)
+        return
+    if sys.argv[1:] == ["ichol"]:
+        from neural_cg.utils import validate as rval
+
+        sys.path.insert(0, str(ROOT))
+        ichol_fixtures(rval)
         return
     if sys.argv[1:] == ["gnn"]:
         from neural_cg import data as rdata
@@ -642,6 +695,7 @@ def main():
 
     gnn_forward_fixtures(rdata, rgnn)
     graph_spmv_fixtures(rbl)
+    ichol_fixtures(rval)
 
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)

@@ -91,6 +91,12 @@ def test_batch_fp32(gpu_ctx):
         it1, conv1, x1, h1 = _single(A, L, b, eps, 1e-5, dtype=np.float32)
         assert (it, conv) == (it1, conv1)
         assert _rel(x.astype(np.float64), x1.astype(np.float64)) <= 1e-5
+        # the oracle's fp32 scipy cg with correctly rounded dots (scalars rounded to fp32 like
+        # numpy's float32 dots): the same count, x within the fp32 tolerance
+        it_o, x_o, _ = O.pcg(sp.csr_matrix(A), b, O.spai_operator(sp.csr_matrix(L), np.float32(eps)), rtol=1e-5,
+                             dot="exact", dtype=np.float32)
+        assert it == it_o, (A.shape, it, it_o)
+        assert _rel(x.astype(np.float64), x_o.astype(np.float64)) <= 1e-5
 
 
 @pytest.mark.parametrize("reduce", ["0", "1"])

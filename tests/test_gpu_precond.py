@@ -56,7 +56,7 @@ def test_ainv0_factor_bitwise(gpu_ctx, name):
 @pytest.mark.parametrize("name", ["kuhn7", "kuhn31", "poisson100"])
 def test_trsv_bitwise(gpu_ctx, name):
     """The sync-free one-launch solve (many blocks waiting on each other across 90-200 levels)
-    gives the oracle's bits, as the per-level launches do."""
+    gives the oracle's bits."""
     if name == "kuhn31":
         A = sp.csr_matrix(P.kuhn_laplacian(31))
     elif name == "poisson100":
@@ -112,3 +112,64 @@ def test_ic0_breakdown_is_reported(gpu_ctx):
     with pytest.raises(_lib.LspcgError) as e:
         _dm(A).ic0()
     assert e.value.code == _lib.ERR_BREAKDOWN
+
+
+def test_ic_concurrent_solves_match_sequential(gpu_ctx):
+    """Sync-free IC triangular solves under contention: four PCG-IC solves in flight on separate
+    streams (linalg.solve_many: the solves' resident grids share the CUs and the hardware queues,
+    so hand-offs wait behind other work) give the sequential results bit for bit -- a delayed
+    dependency only waits longer (a wait beyond 2 s would fail the solve loudly, never silently)."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient, solve_many
+
+    A = sp.csr_matrix(P.kuhn_laplacian(31, 1e-3))
+    n = A.shape[0]
+    b = torch.from_numpy(A @ np.ones(n)).cuda()
+    solvers = [PreconditionedConjugateGradient(A, device="cuda", preconditioner="ic") for _ in range(4)]
+    xs = [torch.zeros(n, dtype=torch.float64, device="cuda") for _ in solvers]
+    seq = solvers[0].solve(b, xs[0].clone(), rtol=1e-8)
+    x_seq = xs[0].clone()
+    solvers[0].solve(b, x_seq, rtol=1e-8)
+    res = solve_many([(s, b, x) for s, x in zip(solvers, xs)], rtol=1e-8, concurrency=4)
+    for (it, conv, _), x in zip(res, xs):
+        assert conv and it == seq[0]
+        assert torch.equal(x, x_seq)
+
+
+@pytest.mark.parametrize("dot_order", ["compensated", "openblas"])
+@pytest.mark.parametrize("name", ["poisson16", "kuhn7", "poisson64"])
+def test_pcg_ic_apply_matches_reference_ichol(gpu_ctx, name, dot_order):
+    """PCG-IC with a GIVEN factor (lspcg_solver_set_ic_factor) vs the REFERENCE's
+    get_pcg_iter_time_scipy_ichol on that factor (tests/golden/ic_traj.npz; validate.py:372-419,
+    IncompleteCholeskyPreconditioner = two spsolve_triangular calls, whose arithmetic the device
+    solves reproduce): counts equal, ‖r_k‖ within 1e-12 of max ‖r_k‖, x within 1e-12; in the recorded
+    run's dot order, count, history and x bit for bit.  The factor is the oracle's IC(0) (the reference's ilupp
+    factorization is absent: its arithmetic stays parity-unpinned; the device IC(0) equals the
+    oracle's bit for bit, test_ic0_factor_bitwise)."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+    from tests.test_oracle_golden import _load, hist_dev, ic_system
+
+    z = _load("ic_traj.npz")
+    A, L, gt = ic_system(z, name)
+    b = A @ gt
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ic", dot_order=dot_order)
+    assert s.set_ic_factor(L) > 0
+    for rtol in (6, 8):
+        t = f"{name}__rtol{rtol}"
+        x = np.zeros_like(b)
+        it, _, _, h = s(b, x, 10.0 ** -rtol, return_history=True)
+        assert it == int(z[f"{t}__count"]), (name, rtol, it)
+        if dot_order == "openblas":  # the recorded run's own dot order: the same bits
+            assert np.array_equal(h[:it], z[f"{t}__hist"]) and np.array_equal(x, z[f"{t}__x"])
+        assert hist_dev(h, z[f"{t}__hist"]) <= 1e-12
+        assert np.linalg.norm(x - z[f"{t}__x"]) <= 1e-12 * np.linalg.norm(z[f"{t}__x"])
+
+
+def test_set_ic_factor_rejects_non_lower(gpu_ctx):
+    from learningsparsepreconditioner4gpu_amd import _lib
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    A = sp.csr_matrix(P.kuhn_laplacian(4))
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ic")
+    with pytest.raises(_lib.LspcgError) as e:
+        s.set_ic_factor(sp.csr_matrix(sp.triu(A)))
+    assert e.value.code == _lib.ERR_FORMAT

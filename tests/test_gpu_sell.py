@@ -78,12 +78,11 @@ def test_sell_skips_padding_with_inf(gpu_ctx):
         assert np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(y[~np.isnan(y)], ref[~np.isnan(ref)])
 
 
-def _v(no_sell="0", sell32="0", split="1", small="0"):
-    return {"LSPCG_NO_SELL": no_sell, "LSPCG_SELL32": sell32, "LSPCG_SPLIT_REDUCE": split, "LSPCG_SMALL_N": small}
+def _v(no_sell="0", split="1", small="0"):
+    return {"LSPCG_NO_SELL": no_sell, "LSPCG_SPLIT_REDUCE": split, "LSPCG_SMALL_N": small}
 
 
-VARIANTS = [_v(no_sell="1"), _v(sell32="1"), _v(), _v(split="0"),
-            _v(small="1000000"), _v(sell32="1", small="1000000"), _v(no_sell="1", small="1000000")]
+VARIANTS = [_v(no_sell="1"), _v(), _v(split="0"), _v(small="1000000"), _v(no_sell="1", small="1000000")]
 
 
 @pytest.mark.parametrize("precond", ["none", "diagonal", "ext_spai", "ext_spai_scaled"])
@@ -96,10 +95,9 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
     n = A.shape[0]
     b = torch.from_numpy(A @ np.ones(n)).cuda()
     out = []
-    # CSR views (5 kernels); SELL int32 columns / 16-bit offsets (+ split group reductions vs
-    # last-arriver reductions on the SELL 16-bit views); then the one-workgroup solve
-    # (k_pcg_small) on the SELL copies and on the CSR views (LSPCG_NO_SELL=1), which every other
-    # variant has switched off
+    # CSR views (5 kernels); SELL views (split group reductions vs last-arriver reductions);
+    # then the one-workgroup solve (k_pcg_small) on the SELL copies and on the CSR views
+    # (LSPCG_NO_SELL=1), which every other variant has switched off
     for env in VARIANTS:
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -114,6 +112,33 @@ def test_pcg_sell_equals_csr_views(gpu_ctx, precond, case, monkeypatch):
         assert out[0][0] == o[0], (name, out[0][0], o[0])
         assert np.array_equal(out[0][1], o[1]), name
         assert np.array_equal(out[0][2], o[2]), name
+
+
+@pytest.mark.parametrize("precond", ["none", "ext_spai"])
+def test_pcg_sell_int32_columns_equals_csr_views(gpu_ctx, precond, monkeypatch):
+    """A randomly renumbered 3-D grid (n = 42,875): columns up to n rows away from their slice, so
+    the loop's SELL views carry int32 columns (16-bit offsets do not fit); same bits as the CSR
+    views."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    K = sp.csr_matrix(P.kuhn_laplacian(35, 1e-2))
+    perm = np.random.default_rng(2).permutation(K.shape[0])
+    A = sp.csr_matrix(K[perm][:, perm])
+    A.sort_indices()
+    assert _expected_kind(A) == 32
+    n = A.shape[0]
+    b = torch.from_numpy(A @ np.ones(n)).cuda()
+    out = []
+    for no_sell in ("1", "0"):
+        monkeypatch.setenv("LSPCG_NO_SELL", no_sell)
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
+        if precond == "ext_spai":
+            s.set_spai(_cases.spai_like(A), 1e-3)
+        x = torch.zeros(n, dtype=torch.float64, device="cuda")
+        it, conv, _, hist = s.solve(b, x, rtol=1e-8, return_history=True)
+        out.append((it, x.cpu().numpy(), hist))
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
 
 
 @pytest.mark.parametrize("grid", [11, 13])

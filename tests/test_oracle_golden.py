@@ -158,20 +158,26 @@ def test_oracle_gnn_forward_shapes_and_message_direction():
     assert torch.equal(out, out2)
 
 
-def test_oracle_ic_operator_matches_scipy_triangular_solves():
-    """oracle.precond.ic_operator vs the reference's own IncompleteCholeskyPreconditioner
-    arithmetic (validate.py:344-369: two scipy spsolve_triangular calls)."""
+def test_trsv_is_spsolve_triangular():
+    """oracle.precond.trsv_lower / trsv_upper / ic_operator == the reference's own
+    IncompleteCholeskyPreconditioner arithmetic (validate.py:344-369: scipy spsolve_triangular on
+    csc(L) and csc(Lᵀ)), bit for bit."""
     import scipy.sparse as sp
     from scipy.sparse.linalg import spsolve_triangular
 
     from learningsparsepreconditioner4gpu_amd import problems as P
     from oracle import precond as OP
 
-    A = sp.csr_matrix(P.kuhn_laplacian(5, 1e-2))
-    L = OP.ic0(A)
-    r = np.random.default_rng(0).normal(size=A.shape[0])
-    ref = spsolve_triangular(sp.csc_matrix(L.T), spsolve_triangular(sp.csc_matrix(L), r, lower=True), lower=False)
-    np.testing.assert_allclose(OP.ic_operator(L)(r), ref, rtol=1e-12, atol=1e-14)
+    for A in (sp.csr_matrix(P.kuhn_laplacian(5, 1e-2)), sp.csr_matrix(P.kuhn_laplacian(8)),
+              sp.csr_matrix(P.poisson2d_grid(20, 17)[0])):
+        L = OP.ic0(A)
+        U = sp.csr_matrix(L.T)
+        for seed in range(3):
+            r = np.random.default_rng(seed).normal(size=A.shape[0])
+            y = spsolve_triangular(sp.csc_matrix(L), r, lower=True)
+            assert np.array_equal(OP.trsv_lower(L, r), y)
+            assert np.array_equal(OP.trsv_upper(U, r), spsolve_triangular(sp.csc_matrix(L.T), r, lower=False))
+            assert np.array_equal(OP.ic_operator(L)(r), spsolve_triangular(sp.csc_matrix(L.T), y, lower=False))
     # IC(0) reproduces A on its pattern; AINV(0) is exact when the inverse factor's pattern fits
     # triu(A) (2x2 diagonal blocks)
     R = (L @ L.T - A).multiply(sp.csr_matrix(A != 0))
@@ -310,3 +316,38 @@ def test_oracle_graph_ops_match_reference(bs, dn):
         ref = z[f"{t}__{k}"]
         err = float(np.abs(w.numpy() - ref).max()) / float(np.abs(ref).max())
         assert err <= tol, (k, err)
+
+
+def ic_system(z, name):
+    """One system of ic_traj.npz: (A, L, gt)."""
+    ip = z[f"{name}__indptr"]
+    n = ip.size - 1
+    A = sp.csr_matrix((z[f"{name}__data"], z[f"{name}__indices"], ip), shape=(n, n))
+    L = sp.csr_matrix((z[f"{name}__L_data"], z[f"{name}__L_indices"], z[f"{name}__L_indptr"]), shape=(n, n))
+    return A, L, z[f"{name}__gt"]
+
+
+def hist_dev(h, h_ref):
+    """largest |‖r_k‖ - ‖r_k‖_ref| relative to the largest ‖r_k‖_ref (late residuals of a fast
+    solve are tiny, so a per-entry relative measure would only weigh rounding of ~1e-16 ‖b‖
+    against ~1e-8 ‖b‖)."""
+    k = min(len(h), len(h_ref))
+    return float(np.max(np.abs(np.asarray(h[:k]) - np.asarray(h_ref[:k]))) / np.max(h_ref))
+
+
+@pytest.mark.parametrize("name", ["poisson16", "kuhn7", "poisson64"])
+def test_oracle_ic_apply_matches_reference_ichol(name):
+    """The oracle's IC apply (spsolve_triangular's order restated, oracle/precond.py) in scipy cg vs the
+    REFERENCE's get_pcg_iter_time_scipy_ichol on the same factor (ic_traj.npz: its
+    IncompleteCholeskyPreconditioner, validate.py:344-419), with the recorded run's OpenBLAS dot
+    order: count, every ‖r_k‖ and x bit for bit."""
+    from oracle import precond as OP
+
+    z = _load("ic_traj.npz")
+    A, L, gt = ic_system(z, name)
+    for rtol in (6, 8):
+        t = f"{name}__rtol{rtol}"
+        it, x, h = O.pcg(A, A @ gt, OP.ic_operator(L), rtol=10.0 ** -rtol, dot="blas1")
+        assert it == int(z[f"{t}__count"]), (name, rtol, it)
+        assert np.array_equal(np.asarray(h[:it]), z[f"{t}__hist"])
+        assert np.array_equal(x, z[f"{t}__x"])
