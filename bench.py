@@ -194,20 +194,27 @@ def cpu_rate(A, b, M, rtol: float, max_iter: int, threads: int, reps: int = 5) -
             "threads": threads}
 
 
-def cpu_baseline(A, L, eps, gt, max_iter: int, rtol: float) -> dict:
-    """ext_spai on the bench system, bounded to max_iter iterations per solve, at BLAS threads =
-    nproc and = 1."""
+def cpu_baseline(A, L, eps, gt, max_iter: int, rtol: float, all_threads: bool = False) -> dict:
+    """ext_spai on the bench system, bounded to max_iter iterations per solve, at 1 BLAS thread
+    (and at nproc threads with --cpu-all-threads: measured slower on the 256-thread box host, 7.3
+    vs 43.4 iterations/s, profiles/r3_bench_v2.json -- scipy's CSR matvec is single-threaded and
+    256 BLAS threads only add overhead to the dots)."""
     from oracle import linalg as O
 
     Aop = A.astype(np.float64)
     M = O._Op(O.spai_operator(L.astype(np.float64), eps), A.shape, np.float64)
     b = Aop @ gt
-    return {"nproc": cpu_rate(Aop, b, M, rtol, max_iter, os.cpu_count() or 1), "1": cpu_rate(Aop, b, M, rtol, max_iter, 1)}
+    out = {"1": cpu_rate(Aop, b, M, rtol, max_iter, 1)}
+    if all_threads:
+        out["nproc"] = cpu_rate(Aop, b, M, rtol, max_iter, os.cpu_count() or 1)
+    return out
 
 
-def c1_rows(rtol: float) -> dict:
+def c1_rows(rtol: float, all_threads: bool = False) -> dict:
     """BASELINE config 1 (datagen/synthetic.py N = 10240, CG, b = A·1): the reference's CPU path
-    (scipy cg, full solve, 1 warm-up + median of 5) beside the HIP solver on the same system."""
+    (scipy cg, full solve, 1 warm-up + median of 5, 1 BLAS thread; nproc threads with
+    --cpu-all-threads) beside the HIP solver on the same system, in the default dot order and in
+    the parity order (the reference's own count at 1 OpenBLAS thread, 3236)."""
     import scipy.sparse as sp
     import torch
 
@@ -217,19 +224,23 @@ def c1_rows(rtol: float) -> dict:
     A = sp.csr_matrix(P.synthetic_c1())
     n = A.shape[0]
     b = A @ np.ones(n)
-    cpu = {"nproc": cpu_rate(A, b, None, rtol, n, os.cpu_count() or 1), "1": cpu_rate(A, b, None, rtol, n, 1)}
-    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="none")
+    cpu = {"1": cpu_rate(A, b, None, rtol, n, 1)}
+    if all_threads:
+        cpu["nproc"] = cpu_rate(A, b, None, rtol, n, os.cpu_count() or 1)
     bt = torch.from_numpy(b).cuda()
     x = torch.zeros_like(bt)
-    ts = []
-    for _ in range(6):
-        x.zero_()
-        it, conv, t = s.solve(bt, x, rtol=rtol)
-        ts.append(t)
-    med = float(np.median(ts[1:]))
+    gpu = {}
+    for order in ("compensated", "openblas"):
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="none", dot_order=order, dot_threads=1)
+        ts = []
+        for _ in range(6):
+            x.zero_()
+            it, conv, t = s.solve(bt, x, rtol=rtol)
+            ts.append(t)
+        med = float(np.median(ts[1:]))
+        gpu[order] = {"iters": it, "time_to_rtol_ms": med * 1e3, "it_per_s": it / med}
     return {"workload": "synthetic C1 n=10240 nnz=%d, CG (none), b = A·1, rtol %g" % (A.nnz, rtol),
-            "gpu": {"iters": it, "time_to_rtol_ms": med * 1e3, "it_per_s": it / med, "reference_iters": 3229},
-            "cpu": cpu}
+            "gpu": gpu, "reference_iters": {"1_openblas_thread": 3236, "8_openblas_threads": 3229}, "cpu": cpu}
 
 
 def c5_rows(rtol: float, concurrency: int = 4) -> dict:
@@ -362,6 +373,8 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=60,
                     help="iterations per bounded CPU baseline solve (1 warm-up + median of 5, at nproc and 1 BLAS threads)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-all-threads", action="store_true",
+                    help="also time the CPU legs at nproc BLAS threads (slower than 1 thread on the box host)")
     ap.add_argument("--no-variants", action="store_true", help="skip the none / diagonal / random-rhs time-to-rtol rows")
     ap.add_argument("--spmv-reps", type=int, default=30)
     ap.add_argument("--configs", action="store_true",
@@ -526,20 +539,21 @@ def main():
                 A_h = A_h.tocsr()
             gt_h = gt.cpu().numpy()
             log(f"cpu baseline: scipy cg, <= {args.cpu_iters} iterations per solve, 1 warm-up + median of 5, "
-                f"BLAS threads {hc['nproc']} and 1")
-            cb = cpu_baseline(A_h, L_h, args.epsilon, gt_h, args.cpu_iters, args.rtol)
+                f"1 BLAS thread" + (f" and {hc['nproc']}" if args.cpu_all_threads else ""))
+            cb = cpu_baseline(A_h, L_h, args.epsilon, gt_h, args.cpu_iters, args.rtol, args.cpu_all_threads)
             best = max(cb.values(), key=lambda r: r["it_per_s"])
             cpu = {"value": best["it_per_s"], "unit": "CG iters/s", "cores": best["threads"], "kind": "port",
                    "cpu_model": hc["model"], "nproc": hc["nproc"], "by_threads": cb,
                    "sample": f"ext_spai PCG on the same system (scipy {__import__('scipy').__version__} cg + explicit-Lᵀ "
                              f"SPAI LinearOperator, validate.py:163-201), solves bounded to {args.cpu_iters} "
-                             f"iterations, 1 warm-up + median of 5, BLAS threads = nproc ({hc['nproc']}) and 1 "
-                             "(value = the faster; scipy's CSR matvec is single-threaded either way)"}
+                             f"iterations, 1 warm-up + median of 5, 1 BLAS thread (scipy's CSR matvec is "
+                             f"single-threaded; nproc = {hc['nproc']} BLAS threads measured slower, "
+                             "--cpu-all-threads)"}
         except Exception as e:  # pragma: no cover - reported, not fatal
             cpu = {"value": None, "unit": "CG iters/s", "cores": 1, "kind": "port", "sample": f"failed: {e}",
                    "cpu_model": hc["model"], "nproc": hc["nproc"]}
         try:
-            c1 = c1_rows(1e-8)
+            c1 = c1_rows(1e-8, args.cpu_all_threads)
         except Exception as e:  # pragma: no cover
             c1 = {"failed": str(e)}
     c5 = None

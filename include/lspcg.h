@@ -227,6 +227,11 @@ typedef struct lspcg_gnn_desc {
  * (pack_weights); host or device pointer */
 int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* weights,
                      int64_t nweights, lspcg_gnn** out);
+/* Structure analysis of a graph (its CSC by destination), like a sparse library's analysis step:
+ * lspcg_gnn_forward reuses it while it is called with the same (edge_index pointer, N, E) -- the
+ * reference runs `repeat` forwards of one sample (infer.py:290-293) -- and rebuilds it for any
+ * other graph.  Call it again after changing edge_index's contents in place. */
+int lspcg_gnn_set_graph(lspcg_gnn* g, int64_t N, int64_t E, const int64_t* edge_index);
 /* x [N,node_in], edge_index device int64 [2,E], edge_attr [E,edge_in] -> out [E,edge_out]
  * (all fp32 device).  Message aggregation order is deterministic. */
 int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const int64_t* edge_index,

@@ -136,6 +136,7 @@ class NodeEdgeProcessing(nn.Module):
         self._handle = None
         self._ctx = None
         self._packed_version = None
+        self._graph = None  # (key, edge_index tensor) of the structure analysed by lspcg_gnn_set_graph
 
     @staticmethod
     def _check_supported(nf, ef, *ffs):
@@ -183,6 +184,7 @@ class NodeEdgeProcessing(nn.Module):
         if self._handle is not None and self._ctx is ctx and self._packed_version == self._version():
             return
         self._free()
+        self._graph = None
         blob = self.pack_weights()
         desc = _lib.lspcg_gnn_desc(node_in=self.node_in_features, edge_in=self.edge_in_features, hidden=self.hidden,
                                    mlp_layers=2, num_mp_layers=self.num_mp_layers,
@@ -223,6 +225,12 @@ class NodeEdgeProcessing(nn.Module):
         assert x.shape[1] == self.node_in_features, (x.shape, self.node_in_features)
         assert ea.shape == (E, self.edge_in_features), (ea.shape, self.edge_in_features)
         out = torch.empty(E, self.edge_out_features, dtype=torch.float32, device=dev)
+        # the graph's CSC is analysed once per edge_index (the tensor is held, so its address cannot
+        # be reused by another one while cached; an in-place change bumps its version)
+        key = (ei.data_ptr(), ei._version, N, E)
+        if self._graph is None or self._graph[0] != key or self._graph[1].data_ptr() != ei.data_ptr():
+            _lib.call("lspcg_gnn_set_graph", self._handle, N, E, _ptr(ei))
+            self._graph = (key, ei)
         _lib.call("lspcg_gnn_forward", self._handle, N, E, _ptr(x), _ptr(ei), _ptr(ea), _ptr(out))
         return None, out
 

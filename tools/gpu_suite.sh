@@ -26,6 +26,13 @@ import json; d=json.load(open('$out/bench.json')); print(d['value'], d['pcg_iter
     traffic)
       bash tools/spmv_traffic.sh "$tag" || exit $?
       cat "gpurun_out/traffic_$tag/summary.json" ;;
+    gnn)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_gnn.py -x -q --timeout 200 --timeout-method thread > "$out/gnn_tests.txt" 2>&1
+      rc=$?; tail -2 "$out/gnn_tests.txt"; [ $rc -eq 0 ] || exit $rc
+      timeout -k 10 120 python -u tools/gnn_run.py --reps 5 > "$out/gnn_run.json" 2> "$out/gnn_run.err" || exit $?
+      cat "$out/gnn_run.json"
+      (cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/gnn_prof" -o gnn -- python3 tools/gnn_run.py --reps 5 > "$out/gnn_prof.log" 2>&1) || exit $?
+      f=$(find "$out/gnn_prof" -name "*kernel_stats.csv" | head -1); python3 tools/stats.py "$f" 2>/dev/null | head -20 || head -20 "$f" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -34,12 +34,12 @@ gt = ds.mask.reshape(-1).to(torch.float64)
 b = A.matvec(gt)
 print(f"{wl}: n={A.n} nnz={A.nnz}", flush=True)
 
-VARIANTS = [("csr", {"LSPCG_NO_SELL": "1"}), ("sell32", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "1"}),
-            ("ticket16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "0"}),
-            ("split16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "1"})]
+VARIANTS = [("csr", {"LSPCG_NO_SELL": "1"}),
+            ("ticket16", {"LSPCG_NO_SELL": "0", "LSPCG_SPLIT_REDUCE": "0"}),
+            ("split16", {"LSPCG_NO_SELL": "0", "LSPCG_SPLIT_REDUCE": "1"})]
 if os.environ.get("PROBE_VARIANTS") == "cap":
-    VARIANTS = [("ticket16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "0"}),
-                ("split16", {"LSPCG_NO_SELL": "0", "LSPCG_SELL32": "0", "LSPCG_SPLIT_REDUCE": "1"})]
+    VARIANTS = [("ticket16", {"LSPCG_NO_SELL": "0", "LSPCG_SPLIT_REDUCE": "0"}),
+                ("split16", {"LSPCG_NO_SELL": "0", "LSPCG_SPLIT_REDUCE": "1"})]
 ref = None
 for name, env in VARIANTS:
     os.environ.update(env)
