@@ -100,6 +100,33 @@ def build_plan(mats: Sequence[sp.csr_matrix], bounds: List[int], rank: int) -> H
     return HaloPlan(rank, list(bounds), halo.astype(np.int64), recv_counts, send_idx, send_counts)
 
 
+def build_plan_exchanged(rows: Sequence[sp.csr_matrix], bounds: List[int], rank: int, group=None) -> HaloPlan:
+    """build_plan from this rank's OWN rows only (``rows``: the rank's row blocks, global column
+    numbers): the halo comes from its own columns, and what it must send is what the other ranks
+    ask for -- one all-to-all of request counts and one of the requested global indices
+    (torch.distributed; O(own nnz) per rank instead of every rank rescanning every other rank's
+    rows).  Equal to build_plan on the same matrices."""
+    world = len(bounds) - 1
+    r0, r1 = bounds[rank], bounds[rank + 1]
+    cols = [M.indices for M in rows]
+    need = np.unique(np.concatenate(cols)) if cols else np.zeros(0, np.int64)
+    halo = need[(need < r0) | (need >= r1)].astype(np.int64)
+    ho = np.searchsorted(bounds, halo, side="right") - 1
+    recv_counts = [int(np.count_nonzero(ho == s)) for s in range(world)]
+    if world == 1 or _backend(group) is None:
+        send_counts = [0] * world
+        return HaloPlan(rank, list(bounds), halo, recv_counts, np.zeros(0, np.int32), send_counts)
+    # my requests to owner s = my halo block owned by s (ascending); their counts first
+    req_counts = torch.tensor(recv_counts, dtype=torch.int64)
+    got_counts = torch.empty(world, dtype=torch.int64)
+    dist.all_to_all_single(got_counts, req_counts, group=group)
+    send_counts = [int(c) for c in got_counts]
+    got = torch.empty(int(sum(send_counts)), dtype=torch.int64)
+    dist.all_to_all_single(got, torch.from_numpy(halo), send_counts, recv_counts, group=group)
+    send_idx = (got.numpy() - r0).astype(np.int32)
+    return HaloPlan(rank, list(bounds), halo, recv_counts, send_idx, send_counts)
+
+
 def local_matrix(M: sp.csr_matrix, plan: HaloPlan) -> sp.csr_matrix:
     """The rank's rows of M over its extended numbering [own | halo], as a square n_ext matrix
     whose halo rows are empty.  Entries stay in GLOBAL column order inside each row (the local
@@ -107,7 +134,7 @@ def local_matrix(M: sp.csr_matrix, plan: HaloPlan) -> sp.csr_matrix:
     the SpMV kernels sum a row in stored order, so every row sum is scipy's csr_matvec order,
     the single-GPU solver's bits."""
     r0, r1 = plan.bounds[plan.rank], plan.bounds[plan.rank + 1]
-    rows = M[r0:r1].tocsr()
+    rows = (M if M.shape[0] == r1 - r0 else M[r0:r1]).tocsr()  # the global matrix or its row block
     rows.sort_indices()
     g = rows.indices.astype(np.int64)
     own = (g >= r0) & (g < r1)
@@ -188,30 +215,53 @@ class DistributedPCG:
 
     def __init__(self, A, L=None, epsilon: float = 0.0, dtype=np.float64, group=None,
                  device: Optional[torch.device] = None):
-        self.group = group
-        if dist.is_available() and dist.is_initialized():
-            self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
-        else:
-            self.rank, self.world = 0, 1
+        """A, L: the global matrices (every rank passes the same ones; only this rank's rows of
+        A, L and Lᵀ are kept -- Lᵀ's row block is built from L's column block, never the whole
+        transpose).  For systems whose global matrices do not fit one host, use from_row_blocks."""
+        rank, world = self._rank_world(group)
         A = sp.csr_matrix(A, dtype=np.float64)
-        A.sort_indices()
-        mats = [A]
-        LT = None
+        bounds = partition_rows(A.indptr, world)
+        r0, r1 = bounds[rank], bounds[rank + 1]
+        blocks = [A[r0:r1]]
         if L is not None:
             L = sp.csr_matrix(L, dtype=np.float64)
-            L.sort_indices()
-            LT = L.T.tocsr()
-            LT.sort_indices()
-            mats += [L, LT]
-        self.n = A.shape[0]
+            blocks += [L[r0:r1], sp.csc_matrix(L[:, r0:r1]).T.tocsr()]
+        self._setup(blocks, A.shape[0], bounds, L is not None, epsilon, dtype, group, device)
+
+    @classmethod
+    def from_row_blocks(cls, A_rows, L_rows=None, LT_rows=None, n: int = 0, bounds: Optional[List[int]] = None,
+                        epsilon: float = 0.0, dtype=np.float64, group=None, device: Optional[torch.device] = None):
+        """Each rank passes only ITS row blocks (global column numbers) of A, L and Lᵀ for the row
+        partition ``bounds`` (partition_rows of the global row pointer): no rank ever holds the
+        global system; the halo plan is exchanged (build_plan_exchanged)."""
+        self = cls.__new__(cls)
+        self._setup([A_rows] + ([L_rows, LT_rows] if L_rows is not None else []), int(n), list(bounds),
+                    L_rows is not None, epsilon, dtype, group, device)
+        return self
+
+    @staticmethod
+    def _rank_world(group):
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(group), dist.get_world_size(group)
+        return 0, 1
+
+    def _setup(self, blocks, n, bounds, has_L, epsilon, dtype, group, device):
+        self.group = group
+        self.rank, self.world = self._rank_world(group)
+        blocks = [sp.csr_matrix(M, dtype=np.float64) for M in blocks]
+        for M in blocks:
+            M.sort_indices()
+        self.n = int(n)
         self.eps = float(epsilon)
         self.np_dtype = np.dtype(dtype)
         self.tdtype = torch.float64 if self.np_dtype == np.float64 else torch.float32
         self.ctx = Context.get(device)
-        self.bounds = partition_rows(A.indptr, self.world)
-        if any(b1 <= b0 for b0, b1 in zip(self.bounds, self.bounds[1:])):
+        self.bounds = list(bounds)
+        if len(self.bounds) != self.world + 1 or any(b1 <= b0 for b0, b1 in zip(self.bounds, self.bounds[1:])):
             raise ValueError(f"{self.world} ranks for {self.n} rows: every rank must own at least one row")
-        self.plan = build_plan(mats, self.bounds, self.rank)
+        self.plan = build_plan_exchanged(blocks, self.bounds, self.rank, group)
+        mats = blocks
+        L = blocks[1] if has_L else None
         p = self.plan
         self._mats = [DeviceMatrix.from_scipy(local_matrix(M, p), dtype=dtype, ctx=self.ctx, keep_order=True)
                       for M in mats]
@@ -329,7 +379,11 @@ class DistributedPCG:
         iters = mi if code == 3 else k
         out = (iters, code == 1, self.x[:no].clone())
         if return_history:
-            out = out + (np.array(hist),)
+            # a non-finite stop reports max_iter (pymathprim's count): NaN-padded to iters + 1
+            # entries, as lspcg_solver_solve does
+            h = np.full(iters + 1, np.nan)
+            h[:len(hist)] = hist[:iters + 1]
+            out = out + (h,)
         return out
 
     def gather_solution(self, x_own: torch.Tensor) -> np.ndarray:

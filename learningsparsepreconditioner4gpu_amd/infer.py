@@ -186,7 +186,7 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
     def finish_batch(jobs) -> List[SolveRecord]:
         infos = [{} for _ in jobs]
         out = get_pcg_iter_time_batch([j[1] for j in jobs], [j[3] for j in jobs], [j[2] for j in jobs], ws.epsilon,
-                                      rtol=rtol, infos=infos)
+                                      rtol=rtol, infos=infos, repeat=repeat)
         return [SolveRecord(index=j[0], iters=it, rel_res=info["rel_res"], t_prec=j[4], t_solve=sol, n=j[1].n,
                             nnz=j[1].nnz, converged=info["converged"]) for j, (it, _, sol), info in zip(jobs, out, infos)]
 

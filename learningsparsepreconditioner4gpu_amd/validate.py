@@ -132,12 +132,13 @@ def get_pcg_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat
 
 
 def get_pcg_iter_time_batch(As, gts, spais, epsilon: float, rtol=1e-6, max_iter=0, dtype=np.float64,
-                            infos: Optional[list] = None) -> List[Tuple[float, float, float]]:
+                            infos: Optional[list] = None, repeat: int = 1) -> List[Tuple[float, float, float]]:
     """get_pcg_iter_time over a window of independent systems solved as ONE lockstep batch
     (linalg.BatchedConjugateGradient; the reference calls get_pcg_iter_time once per sample,
     infer.py:322).  Per system ``(iters, prec_s, solve_s)``: the batch's setup (block-diagonal
-    copy, Lᵀ and views: host wall) and device solve time split evenly over its systems.  A window
-    without a SELL view (irregular rows) is solved one system at a time instead, on the GPU."""
+    copy, Lᵀ and views: host wall) and device solve time split evenly over its systems, the solve
+    averaged over ``repeat`` solves from x0 = 0 like get_pcg_iter_time (validate.py:111-121).  A
+    window without a SELL view (irregular rows) is solved one system at a time instead, on the GPU."""
     Ads = [_prepare(A, dtype) for A in As]
     Lds = [L if isinstance(L, DeviceMatrix) else _prepare(L, dtype) for L in spais]
     bs = [_device_rhs(A, gt) for A, gt in zip(Ads, gts)]
@@ -152,12 +153,16 @@ def get_pcg_iter_time_batch(As, gts, spais, epsilon: float, rtol=1e-6, max_iter=
         out = []
         for j in range(k):
             info = {} if infos is not None else None
-            out.append(get_pcg_iter_time(Ads[j], gts[j], Lds[j], epsilon, rtol, max_iter, 1, dtype, info=info))
+            out.append(get_pcg_iter_time(Ads[j], gts[j], Lds[j], epsilon, rtol, max_iter, repeat, dtype, info=info))
             if infos is not None:
                 infos[j].update(info)
         return out
-    xs = [torch.zeros_like(b) for b in bs]
-    res, t = B.solve(bs, xs, rtol, max_iter)
+    t = 0.0
+    for _ in range(max(1, int(repeat))):
+        xs = [torch.zeros_like(b) for b in bs]
+        res, dt = B.solve(bs, xs, rtol, max_iter)
+        t += dt
+    t /= max(1, int(repeat))
     out = []
     for j, (it, conv) in enumerate(res):
         if infos is not None:

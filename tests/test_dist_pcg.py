@@ -1,6 +1,7 @@
 """CPU: the host side of the row-partitioned single-system PCG (dist_pcg.py, SURVEY.md §8(f)
 rank 4): partition, halo plans, extended local matrices, the compensated cross-rank sum, and the
-exchange / gather plumbing over gloo with world sizes 2 and 3 (127.0.0.1)."""
+exchange / gather plumbing over gloo with world sizes 2 and 3 (127.0.0.1), and the plan built
+from each rank's own rows by two all-to-alls (build_plan_exchanged) equal to the global one."""
 import os
 import socket
 
@@ -12,8 +13,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from learningsparsepreconditioner4gpu_amd import problems as P
-from learningsparsepreconditioner4gpu_amd.dist_pcg import (GROUPS, build_plan, dd_add, exchange, gather_rows,
-                                                          local_matrix, partition_rows, sum_groups)
+from learningsparsepreconditioner4gpu_amd.dist_pcg import (GROUPS, build_plan, build_plan_exchanged, dd_add, exchange,
+                                                          gather_rows, local_matrix, partition_rows, sum_groups)
 
 
 def _mats():
@@ -87,6 +88,12 @@ def _worker(rank, world, port, q):
     n = mats[0].shape[0]
     bounds = partition_rows(mats[0].indptr, world)
     p = build_plan(mats, bounds, rank)
+    # the same plan from this rank's own rows and two all-to-alls
+    r0, r1 = bounds[rank], bounds[rank + 1]
+    pe = build_plan_exchanged([M[r0:r1] for M in mats], bounds, rank)
+    ok_plan = (np.array_equal(pe.halo, p.halo) and pe.recv_counts == p.recv_counts
+               and pe.send_counts == p.send_counts and np.array_equal(pe.send_idx, p.send_idx)
+               and all((local_matrix(M[r0:r1], pe) != local_matrix(M, p)).nnz == 0 for M in mats))
     x = np.random.default_rng(3).standard_normal(n)
     own = torch.from_numpy(x[bounds[rank]:bounds[rank + 1]].copy())
     ext = torch.zeros(p.n_ext, dtype=torch.float64)
@@ -97,7 +104,7 @@ def _worker(rank, world, port, q):
     red = torch.zeros(GROUPS * 2, dtype=torch.float64)
     red[2 * rank] = float(rank + 1)  # group `rank` of this rank's buffer
     tot = sum_groups(gather_rows(red), 1)[0]
-    q.put((rank, ok_halo, tot))
+    q.put((rank, ok_halo and ok_plan, tot))
     dist.barrier()
     dist.destroy_process_group()
 

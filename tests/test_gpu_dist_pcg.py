@@ -83,16 +83,23 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, kind, q):
+def _rank(rank, world, port, kind, q, blocks=False):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from learningsparsepreconditioner4gpu_amd.dist_pcg import DistributedPCG
+    from learningsparsepreconditioner4gpu_amd.dist_pcg import DistributedPCG, partition_rows
 
     A, L, b = _system(kind)
-    d = DistributedPCG(A, L, EPS)
+    if blocks:  # every rank hands over only its own rows of A, L and Lᵀ
+        bounds = partition_rows(sp.csr_matrix(A).indptr, world)
+        r0, r1 = bounds[rank], bounds[rank + 1]
+        LT = sp.csr_matrix(L).T.tocsr()
+        d = DistributedPCG.from_row_blocks(sp.csr_matrix(A)[r0:r1], sp.csr_matrix(L)[r0:r1], LT[r0:r1], n=A.shape[0],
+                                           bounds=bounds, epsilon=EPS)
+    else:
+        d = DistributedPCG(A, L, EPS)
     it, conv, x, hist = d.solve(b, rtol=1e-8, return_history=True)
     xg = d.gather_solution(x)
     q.put((rank, it, bool(conv), xg, hist, d.plan.n_own, len(d.plan.halo)))
@@ -100,13 +107,14 @@ def _rank(rank, world, port, kind, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_multi_rank_matches_oracle(gpu_ctx, world):
+@pytest.mark.parametrize("world,blocks", [(2, False), (3, False), (3, True)])
+def test_multi_rank_matches_oracle(gpu_ctx, world, blocks):
+    """blocks: DistributedPCG.from_row_blocks -- no rank holds the global system."""
     kind = "kuhn"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, kind, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, kind, q, blocks)) for r in range(world)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=100) for _ in range(world)], key=lambda o: o[0])

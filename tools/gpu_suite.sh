@@ -22,7 +22,10 @@ for s in $steps; do
 import json; d=json.load(open('$out/bench.json')); print(d['value'], d['pcg_iter_us'], d['gnn_precond_ms'], d['roofline']['frac'])" ;;
     prof)
       bash tools/prof_bench.sh "$tag" || exit $?
-      f=$(find "gpurun_out/prof_$tag" -name "*kernel_stats.csv" | head -1); cp "$f" "$out/kernel_stats.csv" ;;
+      f=$(find "gpurun_out/prof_$tag" -name "*kernel_stats.csv" | head -1); cp "$f" "$out/kernel_stats.csv"
+      # the per-dispatch trace is tens of MB: keep the roofline SpMV's launches and the loop's
+      python3 tools/trace_split.py "$(find "gpurun_out/prof_$tag" -name "*kernel_trace.csv" | head -1)" > "$out/trace_split.json" 2>&1 || true
+      find "gpurun_out/prof_$tag" -name "*kernel_trace.csv" -delete ;;
     traffic)
       bash tools/spmv_traffic.sh "$tag" || exit $?
       cat "gpurun_out/traffic_$tag/summary.json" ;;
@@ -32,7 +35,8 @@ import json; d=json.load(open('$out/bench.json')); print(d['value'], d['pcg_iter
       timeout -k 10 120 python -u tools/gnn_run.py --reps 5 > "$out/gnn_run.json" 2> "$out/gnn_run.err" || exit $?
       cat "$out/gnn_run.json"
       (cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/gnn_prof" -o gnn -- python3 tools/gnn_run.py --reps 5 > "$out/gnn_prof.log" 2>&1) || exit $?
-      f=$(find "$out/gnn_prof" -name "*kernel_stats.csv" | head -1); python3 tools/stats.py "$f" 2>/dev/null | head -20 || head -20 "$f" ;;
+      f=$(find "$out/gnn_prof" -name "*kernel_stats.csv" | head -1); python3 tools/stats.py "$f" 2>/dev/null | head -20 || head -20 "$f"
+      find "$out/gnn_prof" -name "*kernel_trace.csv" -delete ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
