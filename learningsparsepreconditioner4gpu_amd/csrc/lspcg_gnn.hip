@@ -103,6 +103,27 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
 }
 __device__ __forceinline__ float comp(f4 v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
 
+// One FeedForward's fragment block held in this lane's registers (the fused edge encoder of the
+// first MP layer: its ~21 floats per lane fit beside the layer, whose occupancy is LDS-bound, so
+// the per-tile weight reads leave the dependency chain)
+template <int S1>
+struct FragRegs {
+  float a1[S1], a2[4], a3[4];
+  f4 c1, c2, c3;
+  __device__ __forceinline__ void load(const float* fr, int lane) {
+#pragma unroll
+    for (int s = 0; s < S1; ++s) a1[s] = fr[s * 64 + lane];
+    const float* p = fr + S1 * 64;
+    c1 = *reinterpret_cast<const f4*>(p + lane * 4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) a2[s] = p[256 + s * 64 + lane];
+    c2 = *reinterpret_cast<const f4*>(p + 512 + lane * 4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) a3[s] = p[768 + s * 64 + lane];
+    c3 = *reinterpret_cast<const f4*>(p + 1024 + lane * 4);
+  }
+};
+
 // layers 2 and 3 of an FF on the layer-1 pre-activation `h` (in accumulator layout)
 __device__ __forceinline__ f4 ff_tail(const float* fr, int s1, f4 h, int lane) {
   const float* a2 = fr + s1 * 64 + 256;
@@ -154,6 +175,22 @@ __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const f
 }
 
 template <int S1>
+__device__ __forceinline__ f4 ff_tile_regs(const FragRegs<S1>& w, const float (&in)[S1]) {
+  f4 h = w.c1;
+#pragma unroll
+  for (int s = 0; s < S1; ++s) h = mfma(w.a1[s], in[s], h);
+  h = gelu4(h);
+  f4 h2 = w.c2;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) h2 = mfma(w.a2[s], comp(h, s), h2);
+  h2 = gelu4(h2);
+  f4 o = w.c3;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) o = mfma(w.a3[s], comp(h2, s), o);
+  return o;
+}
+
+template <int S1>
 __device__ __forceinline__ f4 ff_tile(const float* fr, const float (&in)[S1], int lane) {
   f4 h = *reinterpret_cast<const f4*>(fr + S1 * 64 + lane * 4);
 #pragma unroll
@@ -162,6 +199,8 @@ __device__ __forceinline__ f4 ff_tile(const float* fr, const float (&in)[S1], in
 }
 
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
 // Sum over the 4 K-quarters of an item (lanes l, l^16, l^32, l^48), every lane gets the total:
@@ -310,6 +349,11 @@ __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __rest
                                                  const int64_t* __restrict__ ei, const int32_t* __restrict__ inv,
                                                  const float* __restrict__ ecsc, const float* __restrict__ x,
                                                  float* __restrict__ out) {
+  // the decoder's fragment block in LDS (8 KiB): the per-tile weight reads stay off the gathers'
+  // memory queue
+  __shared__ __attribute__((aligned(16))) float wd[frag_size(12)];
+  for (int i = threadIdx.x; i < frag_size(12) / 4; i += 256) reinterpret_cast<f4*>(wd)[i] = ld4(fr + 4 * i);
+  __syncthreads();
   const int lane = threadIdx.x & 63, it = lane & 15, q = lane >> 4;
   const int64_t ntiles = (E + 15) / 16;
   for (int64_t t = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); t < ntiles; t += int64_t(gridDim.x) * 4) {
@@ -318,7 +362,7 @@ __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __rest
     const int64_t ee = valid ? e : E - 1;
     float in[12];
     pack12(ld4(ecsc + int64_t(inv[ee]) * H + 4 * q), ld4(x + ei[ee] * H + 4 * q), ld4(x + ei[E + ee] * H + 4 * q), in);
-    const f4 o = ff_tile<12>(fr, in, lane);
+    const f4 o = ff_tile<12>(wd, in, lane);
     if (valid) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -350,22 +394,26 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, it = lane & 15, q = lane >> 4;
   for (int i = tid; i < kLayerFrag / 4; i += 256) reinterpret_cast<f4*>(wl)[i] = ld4(frag + 4 * i);
   __syncthreads();
+  FragRegs<SE> wenc;
+  if constexpr (S1E > 0) wenc.load(fenc, lane);
   const float* fmsg = wl;
   const float* fedge = wl + kFrag48;
   const float* fnode = wl + 2 * kFrag48;
-  const int64_t n0 = int64_t(blockIdx.x) * 256;
-  const int64_t n1 = n0 + 256 < N ? n0 + 256 : N;
-  const int64_t k0 = ptr[n0], k1 = ptr[n1];
+  const int n0 = blockIdx.x * 256;
+  const int n1 = n0 + 256 < N ? n0 + 256 : int(N);
+  const int k0 = ptr[n0], k1 = ptr[n1];
   f4 agg[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) agg[j] = f4{0.f, 0.f, 0.f, 0.f};
 
   // Edge tiles T = 0..NT-1 of this workgroup (16 CSC edges each); wave w takes T = w, w+4, ...
-  // Software pipeline: while tile T is computed, the gathers of tile T+4 and the index
-  // loads of tile T+8 are in flight (registers carry across the chunk barriers).
-  const int NT = int((k1 - k0 + 15) / 16);
-  const int64_t klast = k1 - 1;
-  auto edge_of = [&](int T) { const int64_t k = k0 + int64_t(T) * 16 + it; return k < k1 ? k : klast; };
+  // Software pipeline: while tile T is computed, the gathers of tile T+4 and the index loads of
+  // tile T+8 are in flight.  Prefetches past the last tile are clamped to the last edge (issued
+  // unconditionally: no exec-mask branches), indices are 32-bit (E < 2^31, checked by the host),
+  // and the 4 tiles of a chunk are unrolled so the prefetch registers rotate without moves.
+  const int NT = (k1 - k0 + 15) / 16;
+  const int klast = k1 - 1;
+  auto edge_of = [&](int T) { const int k = k0 + T * 16 + it; return k < k1 ? k : klast; };
   int qd = 0, qs = 0, qe = 0;
   f4 pxd{}, pxs{}, pea{};
   float pin[SE];  // fused encoder: this lane's raw input features of the prefetched edge
@@ -373,33 +421,31 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
 #pragma unroll
     for (int s = 0; s < SE; ++s) {
       const int f = 4 * s + q;
-      pin[s] = f < fin ? eattr[int64_t(row) * fin + f] : 0.f;
+      pin[s] = f < fin ? eattr[row * fin + f] : 0.f;
     }
   };
   if (wave < NT) {
-    const int64_t kk = edge_of(wave);
+    const int kk = edge_of(wave);
     qd = dst[kk];
     qs = src[kk];
-    pxd = ld4(x + int64_t(qd) * H + 4 * q);
-    pxs = ld4(x + int64_t(qs) * H + 4 * q);
+    pxd = ld4(x + qd * H + 4 * q);
+    pxs = ld4(x + qs * H + 4 * q);
     if constexpr (S1E > 0) load_in(perm[kk]);
-    else pea = ld4(e + kk * H + 4 * q);
-    if (wave + 4 < NT) {
-      const int64_t kn = edge_of(wave + 4);
-      qd = dst[kn];
-      qs = src[kn];
-      if constexpr (S1E > 0) qe = perm[kn];
-    }
+    else pea = ld4(e + int64_t(kk) * H + 4 * q);
+    const int kn = edge_of(wave + 4);
+    qd = dst[kn];
+    qs = src[kn];
+    if constexpr (S1E > 0) qe = perm[kn];
   }
   const int nchunk = (NT + 15) / 16;
   for (int c = 0; c < nchunk; ++c) {
-    const int64_t c0 = k0 + int64_t(c) * CE;
-    const int64_t c1 = c0 + CE < k1 ? c0 + CE : k1;
-#pragma unroll 1
+    const int c0 = k0 + c * CE;
+    const int c1 = c0 + CE < k1 ? c0 + CE : k1;
+#pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int T = c * 16 + wave + 4 * i;
       if (T >= NT) break;  // wave-uniform: MFMA needs EXEC all ones
-      const int64_t k = k0 + int64_t(T) * 16 + it;
+      const int k = k0 + T * 16 + it;
       const bool valid = k < k1;
       const f4 xd = pxd, xs = pxs;  // x_i (target), x_j (source)
       f4 ea;                         // edge attr
@@ -407,21 +453,19 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
         float iv[SE];
 #pragma unroll
         for (int s = 0; s < SE; ++s) iv[s] = pin[s];
-        ea = ff_tile<SE>(fenc, iv, lane);  // k_encode<true>'s MLP on this edge
+        ea = ff_tile_regs<SE>(wenc, iv);  // k_encode<true>'s MLP on this edge
       } else {
         ea = pea;
       }
-      if (T + 4 < NT) {
-        pxd = ld4(x + int64_t(qd) * H + 4 * q);
-        pxs = ld4(x + int64_t(qs) * H + 4 * q);
+      {  // prefetch tile T+4 (clamped), indices of tile T+8 (clamped)
+        pxd = ld4(x + qd * H + 4 * q);
+        pxs = ld4(x + qs * H + 4 * q);
         if constexpr (S1E > 0) load_in(qe);
-        else pea = ld4(e + edge_of(T + 4) * H + 4 * q);
-        if (T + 8 < NT) {
-          const int64_t kn = edge_of(T + 8);
-          qd = dst[kn];
-          qs = src[kn];
-          if constexpr (S1E > 0) qe = perm[kn];
-        }
+        else pea = ld4(e + int64_t(edge_of(T + 4)) * H + 4 * q);
+        const int kn = edge_of(T + 8);
+        qd = dst[kn];
+        qs = src[kn];
+        if constexpr (S1E > 0) qe = perm[kn];
       }
       // LayerNorm(48) statistics: 12 values per lane, 4 lanes per edge, packed fp32 pairs
       f2 w[6] = {(f2){xd.x, xd.y}, (f2){xd.z, xd.w}, (f2){xs.x, xs.y},
@@ -446,18 +490,18 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
       ff2_48(fmsg, fedge, v, lane, m, u);
       if (edge_res) u += ea;
       if (valid) {
-        st4(e + k * H + 4 * q, u);
+        st4(e + int64_t(k) * H + 4 * q, u);
         st4(msg + (k - c0) * H + 4 * q, m);
       }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int64_t i = n0 + (wave + 4 * j) * 16 + it;
+      const int i = n0 + (wave + 4 * j) * 16 + it;
       if (i < n1) {
-        const int64_t kb = ptr[i] > c0 ? ptr[i] : c0;
-        const int64_t ke = ptr[i + 1] < c1 ? ptr[i + 1] : c1;
-        for (int64_t kq = kb; kq < ke; ++kq) agg[j] += ld4(msg + (kq - c0) * H + 4 * q);
+        const int kb = ptr[i] > c0 ? ptr[i] : c0;
+        const int ke = ptr[i + 1] < c1 ? ptr[i + 1] : c1;
+        for (int kq = kb; kq < ke; ++kq) agg[j] += ld4(msg + (kq - c0) * H + 4 * q);
       }
     }
     __syncthreads();
@@ -465,7 +509,7 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
   // update(): node_mlp(aggr) with LayerNorm(16) pre-norm; residual (basic_layers.py:203-206, 224-225)
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int64_t i = n0 + (wave + 4 * j) * 16 + it;
+    const int i = n0 + (wave + 4 * j) * 16 + it;
     const f4 a = agg[j];
     const float mean = quad_sum((a.x + a.y) + (a.z + a.w)) * (1.0f / 16.0f);
     float v[4] = {a.x - mean, a.y - mean, a.z - mean, a.w - mean};
@@ -475,8 +519,8 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
     for (int r = 0; r < 4; ++r) v[r] *= rstd;
     f4 o = ff_tile<4>(fnode, v, lane);
     if (i < n1) {
-      if (node_res) o += ld4(x + i * H + 4 * q);
-      st4(xout + i * H + 4 * q, o);
+      if (node_res) o += ld4(x + int64_t(i) * H + 4 * q);
+      st4(xout + int64_t(i) * H + 4 * q, o);
     }
   }
 }
