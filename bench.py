@@ -98,6 +98,11 @@ def reduce_timing(elapsed: float, iters: float, device) -> tuple:
     return float(mx[0]), float(sm[0])
 
 
+KIND_NAME = {4: "uint16", 16: "int16", 32: "int32"}
+KIND_TEXT = {4: "4-bit dictionary column codes (<= 15 row-relative offsets per 64-row slice)",
+             16: "16-bit column offsets", 32: "int32 columns"}
+
+
 def sell_slots(indptr: np.ndarray) -> int:
     """Stored slots of the SELL-64 layout (csrc/lspcg_sell.hpp): per 64-row slice, 64 x the
     slice's longest row rounded up to a multiple of 4."""
@@ -108,10 +113,32 @@ def sell_slots(indptr: np.ndarray) -> int:
     return int(256 * ((pad.reshape(ns, 64).max(axis=1) + 3) // 4).sum())
 
 
-def pcg_loop_spmv(A, p, q, reps: int) -> dict:
+def sell_kind(indptr: np.ndarray, indices: np.ndarray) -> int:
+    """Column storage the SELL-64 build picks (csrc/lspcg_sell.hip, sorted rows): 4 = dictionary
+    codes (<= 15 distinct offsets col - row per 64-row slice), 16 = 16-bit offsets from the
+    slice's first row, 32 = int32 columns."""
+    n = indptr.size - 1
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
+    if rows.size == 0:
+        return 32
+    key = np.unique((rows // 64) * (1 << 33) + (indices.astype(np.int64) - rows + (1 << 32)))
+    if np.bincount(key >> 33).max() <= 15:
+        return 4
+    return 16 if np.all(np.abs(indices.astype(np.int64) - (rows // 64) * 64) <= 32767) else 32
+
+
+def sell_format_bytes(indptr: np.ndarray, kind: int, value_bytes: int) -> int:
+    """Matrix bytes one SELL-64 SpMV streams: every stored slot's value and column (0.5 B code,
+    2 B offset or 4 B index) + the dictionaries (64 B per slice) for kind 4."""
+    slots = sell_slots(indptr)
+    col = {4: 0.5, 16: 2, 32: 4}[kind]
+    return int(slots * (value_bytes + col)) + (64 * ((indptr.size + 62) // 64) if kind == 4 else 0)
+
+
+def pcg_loop_spmv(A, p, q, reps: int, kind: int) -> dict:
     """The SpMV the PCG loop runs (fp32-stored values -- exact for the reference's fp32-born
-    matrices -- and 16-bit column offsets) timed cold / warm on the same matrix, against the
-    bytes of its own format: 6 B per stored slot + x read + y written."""
+    matrices -- and the loop's column storage `kind`) timed cold / warm on the same matrix,
+    against the bytes of its own format: stored slots + x read + y written."""
     import ctypes as C
 
     from learningsparsepreconditioner4gpu_amd import _lib
@@ -119,13 +146,13 @@ def pcg_loop_spmv(A, p, q, reps: int) -> dict:
     out = {}
     for label, flush in (("cold", FLUSH_BYTES), ("warm", 0)):
         ms = C.c_double()
-        _lib.call("lspcg_spmv_sell_timed", A.ctx.handle, A.handle, 3, C.c_void_p(p.data_ptr()), C.c_void_p(q.data_ptr()),
-                  reps if flush else 3 * reps, flush, C.byref(ms))
+        _lib.call("lspcg_spmv_sell_timed", A.ctx.handle, A.handle, 3 | (8 if kind == 4 else 0), C.c_void_p(p.data_ptr()),
+                  C.c_void_p(q.data_ptr()), reps if flush else 3 * reps, flush, C.byref(ms))
         out[label] = ms.value
     indptr = A.to_scipy().indptr
-    fmt = 6 * sell_slots(indptr) + 16 * A.n
-    return {"kernel": "k_spmv_sell<double,float,int16> as in the PCG loop (values stored as fp32 -- lossless for the "
-                      "reference's fp32-born A and L -- 16-bit column offsets)",
+    fmt = sell_format_bytes(indptr, kind, 4) + 16 * A.n
+    return {"kernel": f"k_spmv_sell<double,float,{KIND_NAME[kind]}> as in the PCG loop (values stored as fp32 -- lossless "
+                      f"for the reference's fp32-born A and L -- {KIND_TEXT[kind]})",
             "format_bytes": fmt, "avg_launch_ms_cold": out["cold"], "avg_launch_ms_warm": out["warm"],
             "achieved_format_GBs_cold": fmt / (out["cold"] * 1e-3) / 1e9,
             "frac_format_cold": fmt / (out["cold"] * 1e-3) / 1e9 / HBM_PEAK_GBS}
@@ -140,13 +167,15 @@ def loop_dominant(kernels: dict, A, n: int, nnz_l: int) -> dict:
     * SURVEY 8(d) bytes: fp64 / int32 CSR of the matrix + the vectors -- NOT what the loop moves
       (compact format, part of the working set served by the Infinity Cache), so this fraction
       can exceed 1 and is reported for reference only."""
-    slots = sell_slots(A.to_scipy().indptr) if A.block_size == 1 else None
     vec = {"KA t=L^T r": 2, "KB z=L t+eps r, rho": 3, "UP p, x": 5, "KC q=A p, pi": 2, "UR r": 3}
     name = max(kernels, key=kernels.get)
     t = kernels[name]
     out = {"kernel": name, "us": t * 1e6, "all_us": {k: v * 1e6 for k, v in kernels.items()}}
-    if slots is not None:
-        fmt = (6 * slots if name.startswith("K") else 0) + 8 * n * vec[name]
+    if A.block_size == 1:
+        As = A.to_scipy()
+        kind = sell_kind(As.indptr, As.indices)
+        out["format"] = f"SELL-64, fp32 values, {KIND_TEXT[kind]}"
+        fmt = (sell_format_bytes(As.indptr, kind, 4) if name.startswith("K") else 0) + 8 * n * vec[name]
         out.update({"format_bytes": fmt, "achieved_GBs_format": fmt / t / 1e9,
                     "frac_format": fmt / t / 1e9 / HBM_PEAK_GBS})
         survey = ((spmv_bytes(n, nnz_l) - 16 * n) if name.startswith("K") else 0) + 8 * n * vec[name]
@@ -156,7 +185,8 @@ def loop_dominant(kernels: dict, A, n: int, nnz_l: int) -> dict:
     tpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pcg_loop_traffic.json")
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
-        if tj.get("n") == n and name in tj.get("kernels", {}):
+        kind_ok = A.block_size != 1 or tj.get("column_kind", 16) == sell_kind(A.to_scipy().indptr, A.to_scipy().indices)
+        if tj.get("n") == n and kind_ok and name in tj.get("kernels", {}):
             tb = tj["kernels"][name]["traffic_bytes"]
             out.update({"counter_bytes": tb, "frac_counter_bytes": tb / t / 1e9 / HBM_PEAK_GBS,
                         "counter_bytes_source": "profiles/pcg_loop_traffic.json"})
@@ -506,12 +536,13 @@ def main():
         alg = bsr3_bytes(n // 3, A.nnzb)
         alg_formula = "(72+4)·nnzb + 4·(N_b+1) + 24·N_b + 24·N_b (SURVEY.md 8(d), BSR b=3)"
     else:
-        kernel = (f"k_spmv_sell<double,double,int{kind}> SELL-64 copy of the fp64 CSR A ({kind}-bit column offsets, "
+        kernel = (f"k_spmv_sell<double,double,{KIND_NAME[kind]}> SELL-64 copy of the fp64 CSR A ({KIND_TEXT[kind]}, "
                   "fp64 values), bit-exact scipy order" if kind else
                   "k_spmv<double,1> staged scalar CSR SpMV of A, bit-exact scipy order")
         alg = spmv_bytes(n, nnz_a)
         alg_formula = "12·nnz + 20·n + 4 (SURVEY.md 8(d), scalar CSR fp64)"
-    pcg_spmv = pcg_loop_spmv(A, p, q, args.spmv_reps) if A.block_size == 1 else None  # BSR: scalar SELL views only
+    # BSR: scalar SELL views only; the loop's views share A's pattern and column storage
+    pcg_spmv = pcg_loop_spmv(A, p, q, args.spmv_reps, kind) if A.block_size == 1 and kind else None
     gbs_cold = alg / (ms_cold * 1e-3) / 1e9
     gbs_warm = alg / (ms_warm * 1e-3) / 1e9
     it_per_solve = iters[-1]

@@ -550,7 +550,8 @@ struct CsrView {
   const void* scol;
   const void* sv;
   int sf32;
-  int c16;
+  int cmode;             // SELL column storage: 0 int32, 1 16-bit offsets, 2 dictionary codes (sdict)
+  const int32_t* sdict;
 };
 
 constexpr int kSmallThreads = 512;  // 2 waves per SIMD: the compensated reductions are VALU work
@@ -580,7 +581,15 @@ __device__ __forceinline__ T sell_row(const CsrView& M, int32_t b, int32_t e, in
           for (int j = 0; j < 4; ++j) v[4 * u + j] = gld(static_cast<const T*>(M.sv) + off + j);
         }
         int o[4];
-        if (M.c16) {
+        if (M.cmode == 2) {
+          const unsigned cw = gld(static_cast<const uint16_t*>(M.scol) + 64 * size_t(min(q0 + u, e - 1)) + lane);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int code = int(cw >> (4 * j)) & 15;
+            ok[4 * u + j] = code != kSellDictPad && q0 + u < e;
+            c[4 * u + j] = ok[4 * u + j] ? i + gld(M.sdict + kSellDictCodes * (i >> 6) + code) : i;
+          }
+        } else if (M.cmode == 1) {
           const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(static_cast<const int16_t*>(M.scol) + off);
           o[0] = cc.x; o[1] = cc.y; o[2] = cc.z; o[3] = cc.w;
 #pragma unroll
@@ -1060,7 +1069,10 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   if (w > 0 && s->sp[0] && view->rowptr == s->Av.rowptr && view->colind == s->Av.colind) {
     P = s->sp[0];
   } else {
-    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(), true, st,
+    // dictionary columns only above the one-workgroup bound (its row loads are L2 hits, and the
+    // dictionary lookup would add a dependent load there)
+    const int cols = kSellCol16 | (view->n > std::min<int64_t>(s->small_n, int64_t(kSmallThreadsBig) * 3) ? kSellColDict : 0);
+    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(), cols, st,
                                       &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: CSR kernel
     if (rc) return rc;
@@ -1344,14 +1356,15 @@ static bool small_path(const lspcg_solver* s) {
 }
 
 static CsrView csr_view(const lspcg_solver* s, int w, const lspcg_mat& M) {
-  CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, nullptr, nullptr, nullptr, 0, 0};
+  CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, nullptr, nullptr, nullptr, 0, 0, nullptr};
   if (const SellPattern* P = s->sp[w]) {
     if (s->small_sell && s->sv[w] && P->bs == 1 && P->groups > 0) {
       v.gp = P->gp;
       v.scol = P->col;
       v.sv = s->sv[w];
       v.sf32 = s->svd[w] == LSPCG_F32 ? 1 : 0;
-      v.c16 = P->col_bits == 16 ? 1 : 0;
+      v.cmode = P->col_bits == 4 ? 2 : (P->col_bits == 16 ? 1 : 0);
+      v.sdict = P->dict;
     }
   }
   return v;

@@ -3,6 +3,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <climits>
 
 #include "lspcg_sell.hpp"
 
@@ -52,9 +53,9 @@ __global__ void __launch_bounds__(256) k_sell_fill(int64_t n, int64_t ns, const 
   }
 }
 
-// flag |= some column is more than 32767 away from its slice's first row
+// flag |= bit when some column is more than 32767 away from its slice's first row
 __global__ void k_sell_fit16(int64_t n, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
-                             int* __restrict__ flag) {
+                             int* __restrict__ flag, int bit) {
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     const int32_t base = int32_t((i / kSellC) * kSellC);
     const int32_t b = rowptr[i], e = rowptr[i + 1];
@@ -64,7 +65,85 @@ __global__ void k_sell_fit16(int64_t n, const int32_t* __restrict__ rowptr, cons
       const int32_t o = colind[k] - base;
       far |= o < -32767 || o > 32767;
     }
-    if (far) atomicOr(flag, 1);
+    if (far) atomicOr(flag, bit);
+  }
+}
+
+// Dictionary of slice s (col_bits 4): one wave per slice merges its 64 rows' row-relative offsets
+// col - row (each row's list in storage order): every round takes the wave minimum m of the lanes'
+// current heads, appends it, and advances the lanes whose head equals m.  Every entry becomes a head
+// and is emitted when it is the minimum, so the dictionary holds every offset of the slice (rows
+// with unsorted columns can only add duplicates).  More than 15 rounds: flag bit 0, no dictionary.
+__global__ void k_sell_dict(int64_t n, int64_t ns, const int32_t* __restrict__ rowptr,
+                            const int32_t* __restrict__ colind, int32_t* __restrict__ dict, int* __restrict__ flag) {
+  const int64_t s = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= ns) return;  // wave-uniform
+  const int64_t i = s * kSellC + lane;
+  int32_t k = 0, e = 0;
+  if (i < n) {
+    k = rowptr[i];
+    e = rowptr[i + 1];
+  }
+  int cnt = 0, mine = 0;
+  bool over = false;
+  for (;;) {
+    const int h = k < e ? int(int64_t(colind[k]) - i) : INT_MAX;
+    int m = h;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) m = min(m, __shfl_xor(m, d, 64));
+    if (m == INT_MAX) break;
+    if (cnt == kSellDictPad) {
+      over = true;
+      break;
+    }
+    if (lane == cnt) mine = m;
+    ++cnt;
+    if (h == m) ++k;
+  }
+  if (over) {
+    if (lane == 0) atomicOr(flag, 1);
+    return;
+  }
+  if (lane < kSellDictCodes) dict[kSellDictCodes * s + lane] = lane < cnt ? mine : 0;
+}
+
+// code words of the dictionary layout: one workgroup per slice, a thread per (group q, lane) word;
+// the 4 codes are the dictionary positions of the row's entries 4q .. 4q + 3 (padding: code 15)
+__global__ void __launch_bounds__(256) k_sell_fill_dict(int64_t n, int64_t ns, const int32_t* __restrict__ gp,
+                                                        const int32_t* __restrict__ rowptr,
+                                                        const int32_t* __restrict__ colind,
+                                                        const int32_t* __restrict__ dict, uint16_t* __restrict__ col) {
+  for (int64_t s = blockIdx.x; s < ns; s += gridDim.x) {
+    __shared__ int32_t sd[kSellDictCodes];
+    __syncthreads();
+    if (threadIdx.x < kSellDictCodes) sd[threadIdx.x] = dict[kSellDictCodes * s + threadIdx.x];
+    __syncthreads();
+    const int64_t g0 = gp[s];
+    const int32_t words = 64 * (gp[s + 1] - gp[s]);
+    for (int32_t p = threadIdx.x; p < words; p += blockDim.x) {
+      const int lane = p & 63;
+      const int32_t q = p >> 6;
+      const int64_t i = s * kSellC + lane;
+      int32_t b = 0, len = 0;
+      if (i < n) {
+        b = rowptr[i];
+        len = rowptr[i + 1] - b;
+      }
+      unsigned w = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int32_t k = 4 * q + j;
+        unsigned code = kSellDictPad;
+        if (k < len) {
+          const int off = int(int64_t(colind[b + k]) - i);
+          for (int t = kSellDictPad - 1; t >= 0; --t)
+            if (sd[t] == off) code = unsigned(t);  // first match (duplicates are possible)
+        }
+        w |= code << (4 * j);
+      }
+      col[64 * g0 + p] = uint16_t(w);
+    }
   }
 }
 
@@ -121,7 +200,7 @@ __global__ void __launch_bounds__(256) k_bsell_fill(int64_t nb, int64_t ns, cons
 }
 
 int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
-                       bool allow16, hipStream_t st, SellPattern* out);
+                       int cols, hipStream_t st, SellPattern* out);
 
 int bsell_build_pattern(int64_t nb, int64_t nnzb, const int32_t* rowptr, const int32_t* colind, double max_pad,
                         bool allow16, hipStream_t st, SellPattern* out) {
@@ -169,7 +248,7 @@ int bsell_build_pattern(int64_t nb, int64_t nnzb, const int32_t* rowptr, const i
     e = hipMalloc(&flag, sizeof(int));
     if (e == hipSuccess) e = hipMemsetAsync(flag, 0, sizeof(int), st);
     if (e == hipSuccess)
-      hipLaunchKernelGGL(k_sell_fit16, dim3(fill_grid(nb)), dim3(kThreads), 0, st, nb, rowptr, colind, flag);
+      hipLaunchKernelGGL(k_sell_fit16, dim3(fill_grid(nb)), dim3(kThreads), 0, st, nb, rowptr, colind, flag, 1);
     if (e == hipSuccess) e = hipMemcpyAsync(&fit, flag, sizeof(int), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(flag);
@@ -224,7 +303,7 @@ int bsell_fill_values(const SellPattern& P, const void* src, int src_dtype, int 
 }
 
 int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
-                       bool allow16, hipStream_t st, SellPattern* out) {
+                       int cols, hipStream_t st, SellPattern* out) {
   SellPattern P;
   P.n = n;
   P.nb = n;
@@ -262,24 +341,39 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
     set_error("sell: padding exceeds the limit (irregular row lengths)");
     return LSPCG_ERR_UNSUPPORTED;
   }
-  int fit = 1;  // 0 = 16-bit offsets fit
-  if (allow16 && n) {
+  // one host read decides the column storage: bit 0 = some slice has > 15 offsets (no dictionary),
+  // bit 1 = some column is out of 16-bit offset range
+  int fit = 3;
+  if ((cols & (kSellCol16 | kSellColDict)) && n) {
     int* flag = nullptr;
     e = hipMalloc(&flag, sizeof(int));
-    if (e == hipSuccess) e = hipMemsetAsync(flag, 0, sizeof(int), st);
-    if (e == hipSuccess)
-      hipLaunchKernelGGL(k_sell_fit16, dim3(fill_grid(n)), dim3(kThreads), 0, st, n, rowptr, colind, flag);
+    if (e == hipSuccess && (cols & kSellColDict)) e = hipMalloc(&P.dict, sizeof(int32_t) * kSellDictCodes * P.ns);
+    if (e == hipSuccess) e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flag), (cols & kSellColDict) ? 0 : 1, 1, st);
+    if (e == hipSuccess && (cols & kSellColDict))
+      hipLaunchKernelGGL(k_sell_dict, dim3(unsigned((P.ns + 3) / 4)), dim3(256), 0, st, n, P.ns, rowptr, colind, P.dict,
+                         flag);
+    if (e == hipSuccess && (cols & kSellCol16))
+      hipLaunchKernelGGL(k_sell_fit16, dim3(fill_grid(n)), dim3(kThreads), 0, st, n, rowptr, colind, flag, 2);
     if (e == hipSuccess) e = hipMemcpyAsync(&fit, flag, sizeof(int), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(flag);
     if (e != hipSuccess) return fail(e);
+    if (!(cols & kSellCol16)) fit |= 2;
   }
-  P.col_bits = fit == 0 ? 16 : 32;
+  P.col_bits = !(fit & 1) ? 4 : (!(fit & 2) ? 16 : 32);
+  if (P.col_bits != 4) {
+    (void)hipFree(P.dict);
+    P.dict = nullptr;
+  }
   // the fill writes every slot (padding included)
-  const size_t cbytes = size_t(P.col_bits / 8) * size_t(std::max<int64_t>(256 * P.groups, 1));
+  const size_t cbytes = P.col_bits == 4 ? sizeof(uint16_t) * size_t(std::max<int64_t>(64 * P.groups, 1))
+                                        : size_t(P.col_bits / 8) * size_t(std::max<int64_t>(256 * P.groups, 1));
   e = hipMalloc(&P.col, cbytes);
   if (e != hipSuccess) return fail(e);
-  if (P.ns)
+  if (P.ns && P.col_bits == 4)
+    hipLaunchKernelGGL(k_sell_fill_dict, dim3(slice_grid(P.ns)), dim3(256), 0, st, n, P.ns, P.gp, rowptr, colind, P.dict,
+                       static_cast<uint16_t*>(P.col));
+  else if (P.ns)
     hipLaunchKernelGGL((k_sell_fill<float, float>), dim3(slice_grid(P.ns)), dim3(256), 0, st, n, P.ns, P.gp, rowptr, colind,
                        static_cast<const float*>(nullptr), P.col_bits == 32 ? static_cast<int32_t*>(P.col) : nullptr,
                        P.col_bits == 16 ? static_cast<int16_t*>(P.col) : nullptr, static_cast<float*>(nullptr));

@@ -30,6 +30,19 @@ constexpr int kSellC = 64;  // rows per slice = one wave64
 // needs no row lengths (no dependent rowptr load before the entry loads).
 constexpr int16_t kSellPad16 = -32768;
 
+// Dictionary columns (col_bits == 4; structured-grid orderings: Kuhn-tet / Poisson / elasticity
+// grids have <= 15 distinct row-relative offsets col - row per 64-row slice): each slice keeps its
+// offsets in dict[16 s + j] (j < 15) and entry j of group q of lane r is a 4-bit code (bits 4j..4j+3
+// of the uint16 col[64 (gp[s] + q) + r]) into it; code 15 marks padding.  0.5 B per slot instead
+// of 2 (16-bit offsets): the column stream of the PCG loop's three SpMVs drops from 2 / 6 to
+// 0.5 / 4.5 of a slot's bytes.  The lane looks its offset up with ds_bpermute from the lane that
+// holds that dictionary entry (one VGPR per slice), so decoding costs no memory access.
+constexpr int kSellDictCodes = 16;
+constexpr int kSellDictPad = 15;
+// column-storage choices for sell_build_pattern (bit mask); int32 columns are always possible
+constexpr int kSellCol16 = 1;
+constexpr int kSellColDict = 2;
+
 // Pattern shared by every matrix with the same CSR (rowptr, colind).
 //
 // Block variant (bs == 3, "BSELL-64"; BSR 3x3 matrices): a wave owns 64
@@ -50,14 +63,18 @@ struct SellPattern {
   int64_t ns = 0;                  // slices
   int64_t groups = 0;              // gp[ns]: 4-entry groups (bs 1) / block slots (bs 3) per lane, summed over slices
   int32_t* gp = nullptr;           // [ns+1] exclusive prefix of per-slice groups-per-row
-  void* col = nullptr;             // [256*groups] (bs 1) / [64*groups] (bs 3) int32 columns or int16 offsets (col_bits)
+  void* col = nullptr;             // [256*groups] (bs 1) / [64*groups] (bs 3) int32 columns or int16 offsets, or
+                                   // [64*groups] uint16 code words (col_bits 4, bs 1)
   int col_bits = 32;
+  int32_t* dict = nullptr;         // [16*ns] row-relative offsets per slice (col_bits 4)
   const int32_t* rowptr = nullptr; // CSR row pointer (row lengths), not owned
   void release() {
     (void)hipFree(gp);
     (void)hipFree(col);
+    (void)hipFree(dict);
     gp = nullptr;
     col = nullptr;
+    dict = nullptr;
   }
 };
 
@@ -69,6 +86,7 @@ struct SellArgs {
   const CT* col;
   const int32_t* rowptr;
   const VT* vals;
+  const int32_t* dict;  // col_bits 4 only
 };
 
 // ---- the SpMV ----------------------------------------------------------------
@@ -110,7 +128,8 @@ struct epi_prefetch<E, std::void_t<decltype(E::PREFETCH)>> : std::bool_constant<
 template <typename T, typename VT, typename CT, int QB, int TH, int MINW, class Pro, class Gx, class Epi>
 __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
-  constexpr bool C16 = sizeof(CT) == 2;
+  constexpr bool D4 = std::is_same<CT, uint16_t>::value;  // dictionary codes (col_bits 4)
+  constexpr bool C16 = std::is_same<CT, int16_t>::value;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int64_t ntiles = (a.n + TH - 1) / TH;
@@ -139,7 +158,9 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
       const int nq = gb[1] - g0;
       const int32_t base = int32_t(s * kSellC);
       const VT* vp = a.vals + 256 * int64_t(g0) + 4 * lane;
-      const CT* cp = a.col + 256 * int64_t(g0) + 4 * lane;
+      const CT* cp = a.col + (D4 ? 64 * int64_t(g0) + lane : 256 * int64_t(g0) + 4 * lane);
+      int dv = 0;  // D4: lane j < 16 holds the slice's dictionary entry j
+      if constexpr (D4) dv = lane < kSellDictCodes ? gld(a.dict + kSellDictCodes * s + lane) : 0;
       T acc = T(0);
       T pf = T(0);
       if constexpr (epi_prefetch<Epi>::value) {
@@ -153,7 +174,16 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
         for (int u = 0; u < QB; ++u) {
           const int q = min(q0 + u, nq - 1);
           Vec4Ld<VT>::load(vp + 256 * q, v[u]);
-          if constexpr (C16) {
+          if constexpr (D4) {
+            const unsigned cw = gld(cp + 64 * q);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int code = int(cw >> (4 * j)) & 15;
+              const int off = __builtin_amdgcn_ds_bpermute(code << 2, dv);
+              m[u][j] = (code != kSellDictPad) && (q0 + u < nq);
+              c[u][j] = m[u][j] ? base + lane + off : base;
+            }
+          } else if constexpr (C16) {
             const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(cp + 256 * q);
             const int o[4] = {cc.x, cc.y, cc.z, cc.w};
 #pragma unroll
@@ -338,14 +368,16 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
   // that tile's and its prologue may test the tile's own system
   if (!one_tile_per_wg) grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
-  SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
+  SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals), P.dict};
   // compact-value kernels: registers for 6 workgroups per CU (the resident reducing grid)
   constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? (TH <= 1536 ? 1536 / TH : 1) : 1;
-  if (P.bs == 3) {
-    // 2 block slots (18 values, 6 gathers) per batch
-    hipLaunchKernelGGL((k_spmv_bsell3<T, VT, CT, 2, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a,
-                       pro, gx, epi);
-    return;
+  if constexpr (!std::is_same<CT, uint16_t>::value) {  // BSELL-64 has no dictionary columns
+    if (P.bs == 3) {
+      // 2 block slots (18 values, 6 gathers) per batch
+      hipLaunchKernelGGL((k_spmv_bsell3<T, VT, CT, 2, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st,
+                         a, pro, gx, epi);
+      return;
+    }
   }
   // 2 groups of 4 entries per batch for fp32-stored values (fewer registers in flight: 89.6-90.7
   // vs 91.2 us per PCG iteration, 25.0 vs 27.0 us cold SpMV), 4 for fp64 values
@@ -357,7 +389,8 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
                                  bool one_tile_per_wg = false) {
-  if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
+  if (P.col_bits == 4) launch_spmv_sell_th<T, VT, uint16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
+  else if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else launch_spmv_sell_th<T, VT, int32_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
 }
 
@@ -378,9 +411,10 @@ namespace lspcg {
 // Host-side construction (lspcg_sell.hip), enqueued on `st`.
 // Builds the SELL-64 pattern of a scalar CSR (n rows); fails with LSPCG_ERR_UNSUPPORTED when the
 // padded size exceeds max_pad x nnz (irregular row lengths: the CSR kernel is used instead).
-// allow16: store 16-bit column offsets when they fit.
+// cols (kSellCol16 | kSellColDict): the column storages allowed besides int32; the most compact
+// one that fits is taken (dictionary codes, then 16-bit offsets).
 int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
-                       bool allow16, hipStream_t st, SellPattern* out);
+                       int cols, hipStream_t st, SellPattern* out);
 // Allocates and fills the SELL value array of a CSR with the same pattern.  src_dtype /
 // dst_dtype: LSPCG_F32 or LSPCG_F64 (fp64 -> fp32 only for exactly representable values).
 int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* src, int src_dtype, int dst_dtype,

@@ -19,7 +19,7 @@ for s in $steps; do
     bench)
       timeout -k 10 300 python -u bench.py > "$out/bench.json" 2> "$out/bench.err" || exit $?
       python3 -c "
-import json; d=json.load(open('$out/bench.json')); print(d['value'], d['pcg_iter_us'], d['gnn_precond_ms'], d['roofline']['frac'])" ;;
+import json; d=json.load(open('$out/bench.json')); print(d['value'], d['pcg_iter_us'], d['gnn_precond_ms'], d['roofline']['frac'], d['roofline']['kernel'][:40], d['pcg_loop_kernels']['all_us'])" ;;
     prof)
       bash tools/prof_bench.sh "$tag" || exit $?
       f=$(find "gpurun_out/prof_$tag" -name "*kernel_stats.csv" | head -1); cp "$f" "$out/kernel_stats.csv"
@@ -37,6 +37,10 @@ import json; d=json.load(open('$out/bench.json')); print(d['value'], d['pcg_iter
       (cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/gnn_prof" -o gnn -- python3 tools/gnn_run.py --reps 5 > "$out/gnn_prof.log" 2>&1) || exit $?
       f=$(find "$out/gnn_prof" -name "*kernel_stats.csv" | head -1); python3 tools/stats.py "$f" 2>/dev/null | head -20 || head -20 "$f"
       find "$out/gnn_prof" -name "*kernel_trace.csv" -delete ;;
+    t=*)  # a subset of the GPU tests: t=tests/test_gpu_sell.py[,tests/...]
+      files=$(echo "${s#t=}" | tr ',' ' ')
+      timeout -k 10 600 python -u -m pytest $files -m gpu -x -q --timeout 200 --timeout-method thread > "$out/subset_tests.txt" 2>&1
+      rc=$?; echo "subset tests rc=$rc"; tail -3 "$out/subset_tests.txt"; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
