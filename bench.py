@@ -98,8 +98,8 @@ def reduce_timing(elapsed: float, iters: float, device) -> tuple:
     return float(mx[0]), float(sm[0])
 
 
-KIND_NAME = {4: "uint16", 16: "int16", 32: "int32"}
-KIND_TEXT = {4: "4-bit dictionary column codes (<= 15 row-relative offsets per 64-row slice)",
+KERNEL_NAME = {1: "k_spmv_sdia", 16: "k_spmv_sell<int16 columns>", 32: "k_spmv_sell<int32 columns>"}
+KIND_TEXT = {1: "SELL-DIA: one slot per distinct row-relative offset of the 64-row slice, 2-B row masks, no columns",
              16: "16-bit column offsets", 32: "int32 columns"}
 
 
@@ -113,26 +113,36 @@ def sell_slots(indptr: np.ndarray) -> int:
     return int(256 * ((pad.reshape(ns, 64).max(axis=1) + 3) // 4).sum())
 
 
+def dia_counts(indptr: np.ndarray, indices: np.ndarray) -> np.ndarray:
+    """Distinct row-relative offsets col - row per 64-row slice (SELL-DIA slots per row)."""
+    n = indptr.size - 1
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
+    key = np.unique((rows // 64) * (1 << 33) + (indices.astype(np.int64) - rows + (1 << 32)))
+    return np.bincount(key >> 33, minlength=(n + 63) // 64)
+
+
 def sell_kind(indptr: np.ndarray, indices: np.ndarray) -> int:
-    """Column storage the SELL-64 build picks (csrc/lspcg_sell.hip, sorted rows): 4 = dictionary
-    codes (<= 15 distinct offsets col - row per 64-row slice), 16 = 16-bit offsets from the
-    slice's first row, 32 = int32 columns."""
+    """Column storage the SELL-64 build picks (csrc/lspcg_sell.hip, sorted rows): 1 = SELL-DIA
+    (<= 16 distinct offsets col - row per 64-row slice, no more slots than 4-entry groups), 16 =
+    16-bit offsets from the slice's first row, 32 = int32 columns."""
     n = indptr.size - 1
     rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
     if rows.size == 0:
         return 32
-    key = np.unique((rows // 64) * (1 << 33) + (indices.astype(np.int64) - rows + (1 << 32)))
-    if np.bincount(key >> 33).max() <= 15:
-        return 4
+    d = dia_counts(indptr, indices)
+    if d.max() <= 16 and 64 * d.sum() <= sell_slots(indptr):
+        return 1
     return 16 if np.all(np.abs(indices.astype(np.int64) - (rows // 64) * 64) <= 32767) else 32
 
 
-def sell_format_bytes(indptr: np.ndarray, kind: int, value_bytes: int) -> int:
-    """Matrix bytes one SELL-64 SpMV streams: every stored slot's value and column (0.5 B code,
-    2 B offset or 4 B index) + the dictionaries (64 B per slice) for kind 4."""
-    slots = sell_slots(indptr)
-    col = {4: 0.5, 16: 2, 32: 4}[kind]
-    return int(slots * (value_bytes + col)) + (64 * ((indptr.size + 62) // 64) if kind == 4 else 0)
+def sell_format_bytes(indptr: np.ndarray, indices: np.ndarray, kind: int, value_bytes: int) -> int:
+    """Matrix bytes one SELL-64 SpMV streams.  SELL-DIA: 64 x D_s value slots per slice + a 2-B row
+    mask + the slice's dictionary (64 B) and transposed-slot map (32 B); otherwise every stored
+    slot's value and column (2 B offset or 4 B index)."""
+    if kind == 1:
+        ns = (indptr.size + 62) // 64
+        return int(64 * dia_counts(indptr, indices).sum() * value_bytes) + ns * (128 + 64 + 32)
+    return int(sell_slots(indptr) * (value_bytes + {16: 2, 32: 4}[kind]))
 
 
 def pcg_loop_spmv(A, p, q, reps: int, kind: int) -> dict:
@@ -146,12 +156,12 @@ def pcg_loop_spmv(A, p, q, reps: int, kind: int) -> dict:
     out = {}
     for label, flush in (("cold", FLUSH_BYTES), ("warm", 0)):
         ms = C.c_double()
-        _lib.call("lspcg_spmv_sell_timed", A.ctx.handle, A.handle, 3 | (8 if kind == 4 else 0), C.c_void_p(p.data_ptr()),
+        _lib.call("lspcg_spmv_sell_timed", A.ctx.handle, A.handle, 3 | (8 if kind == 1 else 0), C.c_void_p(p.data_ptr()),
                   C.c_void_p(q.data_ptr()), reps if flush else 3 * reps, flush, C.byref(ms))
         out[label] = ms.value
-    indptr = A.to_scipy().indptr
-    fmt = sell_format_bytes(indptr, kind, 4) + 16 * A.n
-    return {"kernel": f"k_spmv_sell<double,float,{KIND_NAME[kind]}> as in the PCG loop (values stored as fp32 -- lossless "
+    As = A.to_scipy()
+    fmt = sell_format_bytes(As.indptr, As.indices, kind, 4) + 16 * A.n
+    return {"kernel": f"{KERNEL_NAME[kind]}<double,float> as in the PCG loop (values stored as fp32 -- lossless "
                       f"for the reference's fp32-born A and L -- {KIND_TEXT[kind]})",
             "format_bytes": fmt, "avg_launch_ms_cold": out["cold"], "avg_launch_ms_warm": out["warm"],
             "achieved_format_GBs_cold": fmt / (out["cold"] * 1e-3) / 1e9,
@@ -175,7 +185,7 @@ def loop_dominant(kernels: dict, A, n: int, nnz_l: int) -> dict:
         As = A.to_scipy()
         kind = sell_kind(As.indptr, As.indices)
         out["format"] = f"SELL-64, fp32 values, {KIND_TEXT[kind]}"
-        fmt = (sell_format_bytes(As.indptr, kind, 4) if name.startswith("K") else 0) + 8 * n * vec[name]
+        fmt = (sell_format_bytes(As.indptr, As.indices, kind, 4) if name.startswith("K") else 0) + 8 * n * vec[name]
         out.update({"format_bytes": fmt, "achieved_GBs_format": fmt / t / 1e9,
                     "frac_format": fmt / t / 1e9 / HBM_PEAK_GBS})
         survey = ((spmv_bytes(n, nnz_l) - 16 * n) if name.startswith("K") else 0) + 8 * n * vec[name]
@@ -536,7 +546,7 @@ def main():
         alg = bsr3_bytes(n // 3, A.nnzb)
         alg_formula = "(72+4)·nnzb + 4·(N_b+1) + 24·N_b + 24·N_b (SURVEY.md 8(d), BSR b=3)"
     else:
-        kernel = (f"k_spmv_sell<double,double,{KIND_NAME[kind]}> SELL-64 copy of the fp64 CSR A ({KIND_TEXT[kind]}, "
+        kernel = (f"{KERNEL_NAME[kind]}<double,double> SELL-64 copy of the fp64 CSR A ({KIND_TEXT[kind]}, "
                   "fp64 values), bit-exact scipy order" if kind else
                   "k_spmv<double,1> staged scalar CSR SpMV of A, bit-exact scipy order")
         alg = spmv_bytes(n, nnz_a)

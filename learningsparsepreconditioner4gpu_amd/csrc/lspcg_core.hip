@@ -496,7 +496,7 @@ int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind) {
   std::unique_ptr<SellCopy> c(new SellCopy());
   const bool blk = A->block_size == 3;  // BSR 3x3: the BSELL-64 block layout
   int rc = blk ? bsell_build_pattern(A->nb, A->nnzb, A->rowptr, A->colind, sell_max_pad(), true, st, &c->P)
-               : sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, sell_max_pad(), kSellCol16 | kSellColDict, st,
+               : sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, sell_max_pad(), kSellCol16 | kSellColDia, st,
                                     &c->P);
   if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // irregular rows: the CSR / BSR kernel stays
   if (rc) return rc;
@@ -646,8 +646,8 @@ int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int compact, const
               LSPCG_ERR_ARG, "spmv_sell_timed: fp64 scalar CSR required");
   hipStream_t st = ctx->stream;
   SellPattern P;
-  // any padding; compact bit 1: 16-bit offsets allowed, bit 3: dictionary codes allowed
-  const int cols = ((compact & 2) ? kSellCol16 : 0) | ((compact & 8) ? kSellColDict : 0);
+  // any padding; compact bit 1: 16-bit offsets allowed, bit 3: SELL-DIA allowed
+  const int cols = ((compact & 2) ? kSellCol16 : 0) | ((compact & 8) ? kSellColDia : 0);
   int rc = sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, 1e30, cols, st, &P);
   if (rc) return rc;
   void* v = nullptr;

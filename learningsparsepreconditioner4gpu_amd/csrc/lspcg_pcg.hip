@@ -550,13 +550,13 @@ struct CsrView {
   const void* scol;
   const void* sv;
   int sf32;
-  int cmode;             // SELL column storage: 0 int32, 1 16-bit offsets, 2 dictionary codes (sdict)
-  const int32_t* sdict;
+  int cmode;             // SELL column storage: 0 int32, 1 16-bit offsets
 };
 
 constexpr int kSmallThreads = 512;  // 2 waves per SIMD: the compensated reductions are VALU work
 constexpr int kSmallThreadsBig = 1024;  // n > 1024: 4 waves per SIMD keep rows per thread <= 3
 constexpr int64_t kSmallLds = 61440;  // dynamic LDS: 3 gathered vectors
+constexpr int64_t kSmallNDefault = 3072;  // LSPCG_SMALL_N default
 constexpr int kSmallQB = 2;  // SELL groups (4 entries each) loaded per wait (4 measured slower: 13.0 vs 9.8 us per iteration)
 
 // row i; [b, e): its CSR entry range, or (SELL) its slice's group range; gx(c) reads the
@@ -581,15 +581,7 @@ __device__ __forceinline__ T sell_row(const CsrView& M, int32_t b, int32_t e, in
           for (int j = 0; j < 4; ++j) v[4 * u + j] = gld(static_cast<const T*>(M.sv) + off + j);
         }
         int o[4];
-        if (M.cmode == 2) {
-          const unsigned cw = gld(static_cast<const uint16_t*>(M.scol) + 64 * size_t(min(q0 + u, e - 1)) + lane);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int code = int(cw >> (4 * j)) & 15;
-            ok[4 * u + j] = code != kSellDictPad && q0 + u < e;
-            c[4 * u + j] = ok[4 * u + j] ? i + gld(M.sdict + kSellDictCodes * (i >> 6) + code) : i;
-          }
-        } else if (M.cmode == 1) {
+        if (M.cmode == 1) {
           const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(static_cast<const int16_t*>(M.scol) + off);
           o[0] = cc.x; o[1] = cc.y; o[2] = cc.z; o[3] = cc.w;
 #pragma unroll
@@ -1030,10 +1022,11 @@ struct lspcg_solver {
   int svd[3] = {0, 0, 0};
   double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
   int64_t dhist_cap = 0;
-  int64_t small_n = 3072;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it; also bounded by
+  int64_t small_n = kSmallNDefault;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it; also bounded by
                            // 3 rows per thread at 1024 threads and the LDS of 3 vectors: 2560 in fp64)
   bool small_sell = true;  // k_pcg_small reads the SELL copies (LSPCG_SMALL_SELL=0: the CSR views)
   bool split_ok = false;   // set_spai found SELL views for the split schedule
+  bool dia_ok = true;      // SELL-DIA views allowed (a batch of one-workgroup solves turns them off)
   int dot_order = LSPCG_DOT_COMPENSATED;  // lspcg_solver_set_dot_order
   int dot_threads = 1;
 };
@@ -1069,11 +1062,11 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   if (w > 0 && s->sp[0] && view->rowptr == s->Av.rowptr && view->colind == s->Av.colind) {
     P = s->sp[0];
   } else {
-    // dictionary columns only above the one-workgroup bound (its row loads are L2 hits, and the
-    // dictionary lookup would add a dependent load there)
-    const int cols = kSellCol16 | (view->n > std::min<int64_t>(s->small_n, int64_t(kSmallThreadsBig) * 3) ? kSellColDict : 0);
-    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(), cols, st,
-                                      &s->spat[w]);
+    // SELL-DIA except for systems the one-workgroup solve takes (its per-thread rows load 4-entry
+    // groups with one 16-B load; slot-by-slot loads measured 16.0 vs 9.8 us per iteration at n = 900)
+    const bool dia = s->dia_ok && view->n > std::min<int64_t>(s->small_n, int64_t(kSmallThreadsBig) * 3);
+    const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(),
+                                      kSellCol16 | (dia ? kSellColDia : 0), st, &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: CSR kernel
     if (rc) return rc;
     P = &s->spat[w];
@@ -1356,15 +1349,15 @@ static bool small_path(const lspcg_solver* s) {
 }
 
 static CsrView csr_view(const lspcg_solver* s, int w, const lspcg_mat& M) {
-  CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, nullptr, nullptr, nullptr, 0, 0, nullptr};
+  CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, nullptr, nullptr, nullptr, 0, 0};
   if (const SellPattern* P = s->sp[w]) {
-    if (s->small_sell && s->sv[w] && P->bs == 1 && P->groups > 0) {
+    // (SELL-DIA views are never built for systems this kernel solves: build_sell / lspcg_batch_create)
+    if (s->small_sell && s->sv[w] && P->bs == 1 && P->groups > 0 && P->col_bits != 1) {
       v.gp = P->gp;
       v.scol = P->col;
       v.sv = s->sv[w];
       v.sf32 = s->svd[w] == LSPCG_F32 ? 1 : 0;
-      v.cmode = P->col_bits == 4 ? 2 : (P->col_bits == 16 ? 1 : 0);
-      v.sdict = P->dict;
+      v.cmode = P->col_bits == 16 ? 1 : 0;
     }
   }
   return v;
@@ -1447,7 +1440,13 @@ static size_t esize(int dtype) { return dtype == LSPCG_F32 ? 4 : 8; }
 
 extern "C" {
 
+static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool dia_ok, lspcg_solver** out);
+
 int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_solver** out) {
+  return solver_create(ctx, A, precond, true, out);
+}
+
+static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool dia_ok, lspcg_solver** out) {
   LSPCG_CHECK(ctx && A && out, LSPCG_ERR_ARG, "solver_create: NULL argument");
   LSPCG_CHECK(precond >= LSPCG_PRECOND_NONE && precond <= LSPCG_PRECOND_IC, LSPCG_ERR_ARG,
               "solver_create: unknown preconditioner " + std::to_string(precond));
@@ -1455,12 +1454,20 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   std::unique_ptr<lspcg_solver> s(new lspcg_solver());
   s->ctx = ctx;
   s->A = A;
+  s->dia_ok = dia_ok;
   s->precond = precond;
   s->dtype = A->dtype;
   s->n = A->n;
   const size_t vb = esize(s->dtype) * std::max<int64_t>(s->n, 1);
   LSPCG_HIP(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+  // q (KC -> UR) and t (KA -> KB; the IC solve's intermediate) are never live together: one
+  // buffer, 8 B per row less in the loop's working set (kuhn101: 78 vs 84 us per iteration with
+  // two buffers, profiles/r3_tq_probe_v7.txt -- the loop sits at the Infinity Cache's size)
   for (void** v : {&s->x, &s->b, &s->r, &s->z, &s->t, &s->p, &s->q, &s->d}) {
+    if (v == &s->q) {
+      s->q = s->t;
+      continue;
+    }
     LSPCG_HIP(hipMalloc(v, vb));
     LSPCG_HIP(hipMemsetAsync(*v, 0, vb, s->stream));
   }
@@ -1832,7 +1839,8 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipStreamSynchronize(s->stream);
   for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
-  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->q, s->d}) (void)hipFree(v);
+  for (void* v : {s->x, s->b, s->r, s->z, s->t, s->p, s->d}) (void)hipFree(v);
+  if (s->q != s->t) (void)hipFree(s->q);
   (void)hipFree(s->S);
   (void)hipHostFree(s->hS);
   (void)hipFree(s->partials);
@@ -2466,7 +2474,19 @@ int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, cons
   bt->ntot = brow[nsys] * bt->bs;
   if (int rc = cat_matrices(ctx, nsys, A, brow, &bt->Acat)) return rc;
   if (int rc = cat_matrices(ctx, nsys, L, brow, &bt->Lcat)) return rc;
-  if (int rc = lspcg_solver_create(ctx, bt->Acat, LSPCG_PRECOND_EXT_SPAI, &bt->s)) return rc;
+  // one workgroup per system when every system fits the one-workgroup solve (scalar views; its
+  // row and LDS bounds, small_path); LSPCG_BATCH_SMALL=0 keeps the lockstep phases.  Decided before
+  // the views are built: that mode reads 4-entry-group SELL copies, not SELL-DIA
+  for (int k = 0; k < nsys; ++k) bt->max_n = std::max<int64_t>(bt->max_n, bt->n[k]);
+  {
+    const char* e = std::getenv("LSPCG_BATCH_SMALL");
+    const char* en = std::getenv("LSPCG_SMALL_N");
+    const int64_t small_n = en ? std::max<int64_t>(0, std::atoll(en)) : kSmallNDefault;
+    const int64_t row_cap = int64_t(kSmallThreadsBig) * 3;
+    bt->small = !(e && e[0] == '0') && bt->bs == 1 && bt->max_n <= std::min<int64_t>(row_cap, small_n) &&
+                3 * bt->max_n * int64_t(esize(bt->dtype)) <= kSmallLds;
+  }
+  if (int rc = solver_create(ctx, bt->Acat, LSPCG_PRECOND_EXT_SPAI, !bt->small, &bt->s)) return rc;
   if (int rc = lspcg_solver_set_spai(bt->s, bt->Lcat, epsilon, nullptr)) return rc;
   LSPCG_CHECK(bt->s->sp[0] && bt->s->sp[1] && bt->s->sp[2], LSPCG_ERR_UNSUPPORTED,
               "batch_create: no SELL view of the block-diagonal system (irregular rows): solve one by one");
@@ -2501,15 +2521,6 @@ int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, cons
   if (const char* e = std::getenv("LSPCG_BATCH_REDUCE")) bt->sums = e[0] == '1';
   bt->ntiles = ntiles;
   LSPCG_HIP(hipMalloc(&bt->gsum, sizeof(double) * 10 * ntiles));
-  // one workgroup per system when every system fits the one-workgroup solve (scalar views; its
-  // row and LDS bounds, small_path); LSPCG_BATCH_SMALL=0 keeps the lockstep phases
-  for (int k = 0; k < nsys; ++k) bt->max_n = std::max<int64_t>(bt->max_n, bt->n[k]);
-  {
-    const char* e = std::getenv("LSPCG_BATCH_SMALL");
-    const int64_t row_cap = int64_t(kSmallThreadsBig) * 3;
-    bt->small = !(e && e[0] == '0') && bt->bs == 1 && bt->max_n <= std::min<int64_t>(row_cap, bt->s->small_n) &&
-                3 * bt->max_n * int64_t(esize(bt->dtype)) <= kSmallLds;
-  }
   if (bt->small) {
     std::vector<int32_t> ho(nsys), hn(nsys);
     for (int k = 0; k < nsys; ++k) {

@@ -69,13 +69,14 @@ __global__ void k_sell_fit16(int64_t n, const int32_t* __restrict__ rowptr, cons
   }
 }
 
-// Dictionary of slice s (col_bits 4): one wave per slice merges its 64 rows' row-relative offsets
-// col - row (each row's list in storage order): every round takes the wave minimum m of the lanes'
-// current heads, appends it, and advances the lanes whose head equals m.  Every entry becomes a head
-// and is emitted when it is the minimum, so the dictionary holds every offset of the slice (rows
-// with unsorted columns can only add duplicates).  More than 15 rounds: flag bit 0, no dictionary.
-__global__ void k_sell_dict(int64_t n, int64_t ns, const int32_t* __restrict__ rowptr,
-                            const int32_t* __restrict__ colind, int32_t* __restrict__ dict, int* __restrict__ flag) {
+// ---- SELL-DIA (layout: lspcg_sell.hpp kSdiaMax) ----------------------------------------------
+// Dictionary of slice s: one wave merges its 64 rows' row-relative offsets col - row: every round
+// takes the wave minimum m of the lanes' current heads, appends it and advances the lanes whose head
+// equals m, so with sorted rows the dictionary comes out ascending and duplicate-free.  cnt[s] =
+// D_s.  flag bit 0: some slice has more than 16 offsets, or some row is not sorted (a lane's next
+// head not above the value it just consumed) -- no SELL-DIA.
+__global__ void k_sdia_dict(int64_t n, int64_t ns, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                            int32_t* __restrict__ dict, int32_t* __restrict__ cnt, int* __restrict__ flag) {
   const int64_t s = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (s >= ns) return;  // wave-uniform
@@ -85,64 +86,70 @@ __global__ void k_sell_dict(int64_t n, int64_t ns, const int32_t* __restrict__ r
     k = rowptr[i];
     e = rowptr[i + 1];
   }
-  int cnt = 0, mine = 0;
-  bool over = false;
+  int nd = 0, mine = 0;
+  bool bad = false;
+  int prev = INT_MIN;
   for (;;) {
     const int h = k < e ? int(int64_t(colind[k]) - i) : INT_MAX;
+    bad |= k < e && h <= prev;  // unsorted (or duplicate) column in this row
     int m = h;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) m = min(m, __shfl_xor(m, d, 64));
     if (m == INT_MAX) break;
-    if (cnt == kSellDictPad) {
-      over = true;
+    if (nd == kSdiaMax) {
+      bad = true;
       break;
     }
-    if (lane == cnt) mine = m;
-    ++cnt;
-    if (h == m) ++k;
+    if (lane == nd) mine = m;
+    ++nd;
+    if (h == m) {
+      prev = h;
+      ++k;
+    }
   }
-  if (over) {
+  if (__any(bad)) {
     if (lane == 0) atomicOr(flag, 1);
     return;
   }
-  if (lane < kSellDictCodes) dict[kSellDictCodes * s + lane] = lane < cnt ? mine : 0;
+  if (lane < kSdiaMax) dict[kSdiaMax * s + lane] = lane < nd ? mine : 0;
+  if (lane == 0) cnt[s] = nd;
 }
 
-// code words of the dictionary layout: one workgroup per slice, a thread per (group q, lane) word;
-// the 4 codes are the dictionary positions of the row's entries 4q .. 4q + 3 (padding: code 15)
-__global__ void __launch_bounds__(256) k_sell_fill_dict(int64_t n, int64_t ns, const int32_t* __restrict__ gp,
-                                                        const int32_t* __restrict__ rowptr,
-                                                        const int32_t* __restrict__ colind,
-                                                        const int32_t* __restrict__ dict, uint16_t* __restrict__ col) {
+// row masks: bit j of row i <=> the row has the offset dict[16 s + j]
+__global__ void k_sdia_mask(int64_t n, int64_t ns, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                            const int32_t* __restrict__ dict, const int32_t* __restrict__ gp, uint16_t* __restrict__ mask) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < ns * kSellC; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t s = i / kSellC;
+    unsigned m = 0;
+    if (i < n) {
+      const int nd = gp[s + 1] - gp[s];
+      int j = 0;
+      for (int32_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        const int off = int(int64_t(colind[k]) - i);
+        while (j < nd && dict[kSdiaMax * s + j] != off) ++j;  // both ascending
+        m |= 1u << j;
+        ++j;
+      }
+    }
+    mask[i] = uint16_t(m);
+  }
+}
+
+// values: slot j of row i holds the row's entry number popcount(mask & (2^j - 1)) when bit j is set
+template <typename VS, typename VD>
+__global__ void k_sdia_fill(int64_t n, int64_t ns, const int32_t* __restrict__ gp, const uint16_t* __restrict__ mask,
+                            const int32_t* __restrict__ rowptr, const VS* __restrict__ src, VD* __restrict__ dst) {
   for (int64_t s = blockIdx.x; s < ns; s += gridDim.x) {
-    __shared__ int32_t sd[kSellDictCodes];
-    __syncthreads();
-    if (threadIdx.x < kSellDictCodes) sd[threadIdx.x] = dict[kSellDictCodes * s + threadIdx.x];
-    __syncthreads();
     const int64_t g0 = gp[s];
-    const int32_t words = 64 * (gp[s + 1] - gp[s]);
-    for (int32_t p = threadIdx.x; p < words; p += blockDim.x) {
+    const int32_t slots = kSellC * (gp[s + 1] - gp[s]);
+    for (int32_t p = threadIdx.x; p < slots; p += blockDim.x) {
       const int lane = p & 63;
-      const int32_t q = p >> 6;
+      const int j = p >> 6;
       const int64_t i = s * kSellC + lane;
-      int32_t b = 0, len = 0;
-      if (i < n) {
-        b = rowptr[i];
-        len = rowptr[i + 1] - b;
-      }
-      unsigned w = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int32_t k = 4 * q + j;
-        unsigned code = kSellDictPad;
-        if (k < len) {
-          const int off = int(int64_t(colind[b + k]) - i);
-          for (int t = kSellDictPad - 1; t >= 0; --t)
-            if (sd[t] == off) code = unsigned(t);  // first match (duplicates are possible)
-        }
-        w |= code << (4 * j);
-      }
-      col[64 * g0 + p] = uint16_t(w);
+      const unsigned m = mask[i];
+      VD v = VD(0);
+      if (i < n && ((m >> j) & 1u)) v = VD(src[rowptr[i] + __builtin_popcount(m & ((1u << j) - 1u))]);
+      dst[kSellC * g0 + p] = v;
     }
   }
 }
@@ -341,39 +348,74 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
     set_error("sell: padding exceeds the limit (irregular row lengths)");
     return LSPCG_ERR_UNSUPPORTED;
   }
-  // one host read decides the column storage: bit 0 = some slice has > 15 offsets (no dictionary),
-  // bit 1 = some column is out of 16-bit offset range
-  int fit = 3;
-  if ((cols & (kSellCol16 | kSellColDict)) && n) {
-    int* flag = nullptr;
-    e = hipMalloc(&flag, sizeof(int));
-    if (e == hipSuccess && (cols & kSellColDict)) e = hipMalloc(&P.dict, sizeof(int32_t) * kSellDictCodes * P.ns);
-    if (e == hipSuccess) e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flag), (cols & kSellColDict) ? 0 : 1, 1, st);
-    if (e == hipSuccess && (cols & kSellColDict))
-      hipLaunchKernelGGL(k_sell_dict, dim3(unsigned((P.ns + 3) / 4)), dim3(256), 0, st, n, P.ns, rowptr, colind, P.dict,
-                         flag);
+  // SELL-DIA: dictionaries and slot counts first; one host read of (flag, DIA slot total) decides
+  int fit16 = 0;  // 1 = some column out of 16-bit offset range
+  int flag_h[2] = {1, 0};  // [flags (bit 0: no DIA, bit 1: no 16-bit, bit 2: not symmetric), DIA slots]
+  int32_t* dgp = nullptr;  // DIA slot prefix
+  int* flag = nullptr;
+  if (n) {
+    e = hipMalloc(&flag, 2 * sizeof(int));
+    if (e == hipSuccess) e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flag), (cols & kSellColDia) ? 0 : 1, 1, st);
+    if (e == hipSuccess) e = hipMemsetAsync(flag + 1, 0, sizeof(int), st);
+    if (e == hipSuccess && (cols & kSellColDia)) {
+      e = hipMalloc(&P.dict, sizeof(int32_t) * kSdiaMax * P.ns);
+      if (e == hipSuccess) e = hipMalloc(&cnt, sizeof(int32_t) * (P.ns + 1));
+      if (e == hipSuccess) e = hipMalloc(&dgp, sizeof(int32_t) * (P.ns + 1));
+      if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (P.ns + 1), st);
+      if (e == hipSuccess)
+        hipLaunchKernelGGL(k_sdia_dict, dim3(unsigned((P.ns + 3) / 4)), dim3(256), 0, st, n, P.ns, rowptr, colind, P.dict,
+                           cnt, flag);
+      size_t tb2 = 0;
+      if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, cnt, dgp, int(P.ns + 1), st);
+      if (e == hipSuccess) e = hipMalloc(&tmp, tb2);
+      if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb2, cnt, dgp, int(P.ns + 1), st);
+      if (e == hipSuccess) e = hipMemcpyAsync(flag + 1, dgp + P.ns, sizeof(int), hipMemcpyDeviceToDevice, st);
+    }
     if (e == hipSuccess && (cols & kSellCol16))
       hipLaunchKernelGGL(k_sell_fit16, dim3(fill_grid(n)), dim3(kThreads), 0, st, n, rowptr, colind, flag, 2);
-    if (e == hipSuccess) e = hipMemcpyAsync(&fit, flag, sizeof(int), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(flag_h, flag, 2 * sizeof(int), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(cnt);
+    (void)hipFree(tmp);
+    cnt = nullptr;
+    tmp = nullptr;
+    if (e != hipSuccess) {
+      (void)hipFree(flag);
+      (void)hipFree(dgp);
+      return fail(e);
+    }
+    fit16 = (!(cols & kSellCol16) || (flag_h[0] & 2)) ? 1 : 0;
+  } else {
+    fit16 = (cols & kSellCol16) ? 0 : 1;
+  }
+  // SELL-DIA when it fits and stores no more slots than the 4-entry groups
+  const bool dia = n && !(flag_h[0] & 1) && int64_t(flag_h[1]) <= 4 * P.groups;
+  if (dia) {
+    (void)hipFree(P.gp);
+    P.gp = dgp;
+    dgp = nullptr;
+    P.groups = flag_h[1];
+    P.col_bits = 1;
+    e = hipMalloc(&P.col, sizeof(uint16_t) * kSellC * std::max<int64_t>(P.ns, 1));
     (void)hipFree(flag);
     if (e != hipSuccess) return fail(e);
-    if (!(cols & kSellCol16)) fit |= 2;
+    hipLaunchKernelGGL(k_sdia_mask, dim3(fill_grid(P.ns * kSellC)), dim3(kThreads), 0, st, n, P.ns, rowptr, colind, P.dict,
+                       P.gp, static_cast<uint16_t*>(P.col));
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(e);
+    *out = P;
+    return LSPCG_OK;
   }
-  P.col_bits = !(fit & 1) ? 4 : (!(fit & 2) ? 16 : 32);
-  if (P.col_bits != 4) {
-    (void)hipFree(P.dict);
-    P.dict = nullptr;
-  }
+  (void)hipFree(flag);
+  (void)hipFree(dgp);
+  (void)hipFree(P.dict);
+  P.dict = nullptr;
+  P.col_bits = fit16 ? 32 : 16;
   // the fill writes every slot (padding included)
-  const size_t cbytes = P.col_bits == 4 ? sizeof(uint16_t) * size_t(std::max<int64_t>(64 * P.groups, 1))
-                                        : size_t(P.col_bits / 8) * size_t(std::max<int64_t>(256 * P.groups, 1));
+  const size_t cbytes = size_t(P.col_bits / 8) * size_t(std::max<int64_t>(256 * P.groups, 1));
   e = hipMalloc(&P.col, cbytes);
   if (e != hipSuccess) return fail(e);
-  if (P.ns && P.col_bits == 4)
-    hipLaunchKernelGGL(k_sell_fill_dict, dim3(slice_grid(P.ns)), dim3(256), 0, st, n, P.ns, P.gp, rowptr, colind, P.dict,
-                       static_cast<uint16_t*>(P.col));
-  else if (P.ns)
+  if (P.ns)
     hipLaunchKernelGGL((k_sell_fill<float, float>), dim3(slice_grid(P.ns)), dim3(256), 0, st, n, P.ns, P.gp, rowptr, colind,
                        static_cast<const float*>(nullptr), P.col_bits == 32 ? static_cast<int32_t*>(P.col) : nullptr,
                        P.col_bits == 16 ? static_cast<int16_t*>(P.col) : nullptr, static_cast<float*>(nullptr));
@@ -387,9 +429,24 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
                      hipStream_t st, void** out) {
   const size_t es = dst_dtype == LSPCG_F32 ? 4 : 8;
   void* v = nullptr;
-  LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(256 * P.groups, 1)));
+  const int64_t slots = P.col_bits == 1 ? kSellC * P.groups : 256 * P.groups;
+  LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(slots, 1)));
   const dim3 g(slice_grid(P.ns)), b(256);
-  if (P.ns) {
+  if (P.ns && P.col_bits == 1) {
+    const auto* m = static_cast<const uint16_t*>(P.col);
+    if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F64)
+      hipLaunchKernelGGL((k_sdia_fill<double, double>), g, b, 0, st, P.n, P.ns, P.gp, m, P.rowptr,
+                         static_cast<const double*>(src), static_cast<double*>(v));
+    else if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F32)
+      hipLaunchKernelGGL((k_sdia_fill<double, float>), g, b, 0, st, P.n, P.ns, P.gp, m, P.rowptr,
+                         static_cast<const double*>(src), static_cast<float*>(v));
+    else if (src_dtype == LSPCG_F32 && dst_dtype == LSPCG_F32)
+      hipLaunchKernelGGL((k_sdia_fill<float, float>), g, b, 0, st, P.n, P.ns, P.gp, m, P.rowptr,
+                         static_cast<const float*>(src), static_cast<float*>(v));
+    else
+      hipLaunchKernelGGL((k_sdia_fill<float, double>), g, b, 0, st, P.n, P.ns, P.gp, m, P.rowptr,
+                         static_cast<const float*>(src), static_cast<double*>(v));
+  } else if (P.ns) {
     if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F64)
       hipLaunchKernelGGL((k_sell_fill<double, double>), g, b, 0, st, P.n, P.ns, P.gp, P.rowptr, colind,
                          static_cast<const double*>(src), static_cast<int32_t*>(nullptr), static_cast<int16_t*>(nullptr), static_cast<double*>(v));

@@ -30,18 +30,20 @@ constexpr int kSellC = 64;  // rows per slice = one wave64
 // needs no row lengths (no dependent rowptr load before the entry loads).
 constexpr int16_t kSellPad16 = -32768;
 
-// Dictionary columns (col_bits == 4; structured-grid orderings: Kuhn-tet / Poisson / elasticity
-// grids have <= 15 distinct row-relative offsets col - row per 64-row slice): each slice keeps its
-// offsets in dict[16 s + j] (j < 15) and entry j of group q of lane r is a 4-bit code (bits 4j..4j+3
-// of the uint16 col[64 (gp[s] + q) + r]) into it; code 15 marks padding.  0.5 B per slot instead
-// of 2 (16-bit offsets): the column stream of the PCG loop's three SpMVs drops from 2 / 6 to
-// 0.5 / 4.5 of a slot's bytes.  The lane looks its offset up with ds_bpermute from the lane that
-// holds that dictionary entry (one VGPR per slice), so decoding costs no memory access.
-constexpr int kSellDictCodes = 16;
-constexpr int kSellDictPad = 15;
+// Slice-diagonal layout ("SELL-DIA", col_bits == 1; structured-grid orderings: the Kuhn-tet
+// stencil has 15 distinct row-relative offsets col - row per 64-row slice, the 2-D 5-point stencil
+// 5, boundary rows use subsets).  Each slice s keeps its D_s <= 16 distinct offsets, ascending, in
+// dict[16 s + j] and stores its rows' values slot-major, ONE slot per dictionary entry:
+//     vals[64 (gp[s] + j) + lane]   (row 64 s + lane, column row + dict[16 s + j]),
+// with bit j of mask[64 s + lane] set where the row has that entry (absent entries: value 0, bit
+// clear, never added).  Rows are sorted, so slot order = the row's column order = scipy's sum
+// order.  No column storage at all: the offset of slot j is wave-uniform (a scalar register), the
+// x / r / t / p "gather" of slot j is one contiguous 64-entry load, and a row costs D_s values +
+// 2 bytes of mask (Kuhn: 15 slots per row where SELL-64's 4-entry groups store 16).
+constexpr int kSdiaMax = 16;       // slots (distinct offsets) per slice
 // column-storage choices for sell_build_pattern (bit mask); int32 columns are always possible
 constexpr int kSellCol16 = 1;
-constexpr int kSellColDict = 2;
+constexpr int kSellColDia = 2;
 
 // Pattern shared by every matrix with the same CSR (rowptr, colind).
 //
@@ -61,12 +63,12 @@ struct SellPattern {
   int64_t nb = 0;                  // rows of the pattern: scalar rows (bs 1) or block rows (bs 3)
   int bs = 1;
   int64_t ns = 0;                  // slices
-  int64_t groups = 0;              // gp[ns]: 4-entry groups (bs 1) / block slots (bs 3) per lane, summed over slices
-  int32_t* gp = nullptr;           // [ns+1] exclusive prefix of per-slice groups-per-row
-  void* col = nullptr;             // [256*groups] (bs 1) / [64*groups] (bs 3) int32 columns or int16 offsets, or
-                                   // [64*groups] uint16 code words (col_bits 4, bs 1)
+  int64_t groups = 0;              // gp[ns]: 4-entry groups (bs 1) / block slots (bs 3) / DIA slots per lane, summed
+  int32_t* gp = nullptr;           // [ns+1] exclusive prefix of per-slice groups (slots) per row
+  void* col = nullptr;             // [256*groups] (bs 1) / [64*groups] (bs 3) int32 columns or int16 offsets;
+                                   // SELL-DIA (col_bits 1): [64*ns] uint16 row masks
   int col_bits = 32;
-  int32_t* dict = nullptr;         // [16*ns] row-relative offsets per slice (col_bits 4)
+  int32_t* dict = nullptr;         // SELL-DIA: [16*ns] ascending row-relative offsets per slice
   const int32_t* rowptr = nullptr; // CSR row pointer (row lengths), not owned
   void release() {
     (void)hipFree(gp);
@@ -86,7 +88,16 @@ struct SellArgs {
   const CT* col;
   const int32_t* rowptr;
   const VT* vals;
-  const int32_t* dict;  // col_bits 4 only
+};
+
+template <typename VT>
+struct SdiaArgs {
+  int64_t n;
+  int64_t ns;
+  const int32_t* gp;
+  const uint16_t* mask;
+  const int32_t* dict;
+  const VT* vals;
 };
 
 // ---- the SpMV ----------------------------------------------------------------
@@ -128,7 +139,6 @@ struct epi_prefetch<E, std::void_t<decltype(E::PREFETCH)>> : std::bool_constant<
 template <typename T, typename VT, typename CT, int QB, int TH, int MINW, class Pro, class Gx, class Epi>
 __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
-  constexpr bool D4 = std::is_same<CT, uint16_t>::value;  // dictionary codes (col_bits 4)
   constexpr bool C16 = std::is_same<CT, int16_t>::value;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -158,9 +168,7 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
       const int nq = gb[1] - g0;
       const int32_t base = int32_t(s * kSellC);
       const VT* vp = a.vals + 256 * int64_t(g0) + 4 * lane;
-      const CT* cp = a.col + (D4 ? 64 * int64_t(g0) + lane : 256 * int64_t(g0) + 4 * lane);
-      int dv = 0;  // D4: lane j < 16 holds the slice's dictionary entry j
-      if constexpr (D4) dv = lane < kSellDictCodes ? gld(a.dict + kSellDictCodes * s + lane) : 0;
+      const CT* cp = a.col + 256 * int64_t(g0) + 4 * lane;
       T acc = T(0);
       T pf = T(0);
       if constexpr (epi_prefetch<Epi>::value) {
@@ -174,16 +182,7 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
         for (int u = 0; u < QB; ++u) {
           const int q = min(q0 + u, nq - 1);
           Vec4Ld<VT>::load(vp + 256 * q, v[u]);
-          if constexpr (D4) {
-            const unsigned cw = gld(cp + 64 * q);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int code = int(cw >> (4 * j)) & 15;
-              const int off = __builtin_amdgcn_ds_bpermute(code << 2, dv);
-              m[u][j] = (code != kSellDictPad) && (q0 + u < nq);
-              c[u][j] = m[u][j] ? base + lane + off : base;
-            }
-          } else if constexpr (C16) {
+          if constexpr (C16) {
             const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(cp + 256 * q);
             const int o[4] = {cc.x, cc.y, cc.z, cc.w};
 #pragma unroll
@@ -211,6 +210,65 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             if (m[u][j]) acc = acc + T(v[u][j]) * xv[u][j];
+      }
+      if constexpr (epi_prefetch<Epi>::value) {
+        if (i < a.n) epi.row_pf(i, acc, d, pf);
+      } else {
+        if (i < a.n) epi.row(i, acc, d);
+      }
+    }
+  }
+  finish_epi_dots<Epi>(d, epi);
+}
+
+// SELL-DIA SpMV (layout: see kSdiaMax): one wave = one 64-row slice of a 256-row tile, SB slots
+// per batch, every load of a batch issued before the first add (value loads and vector loads are
+// independent: the slot's offset is a scalar).
+template <typename T, typename VT, int SB, int TH, int MINW, class Pro, class Gx, class Epi>
+__global__ void __launch_bounds__(TH, MINW) k_spmv_sdia(SdiaArgs<VT> a, Pro pro, Gx gx, Epi epi) {
+  constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int64_t ntiles = (a.n + TH - 1) / TH;
+  if (pro.exit()) return;
+  gx.prepare();
+  epi.prepare();
+  DD d[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) d[j] = dd_zero();
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t s = tile * (TH / 64) + w;
+    const int64_t i = tile * TH + threadIdx.x;
+    if (s < a.ns) {  // wave-uniform
+      const int32_t g0 = a.gp[s];
+      const int nd = a.gp[s + 1] - g0;
+      const int32_t* dp = a.dict + kSdiaMax * s;
+      const unsigned msk = gld(a.mask + kSellC * s + lane);
+      const int32_t base = int32_t(s * kSellC);
+      const int32_t row = base + lane;
+      T acc = T(0);
+      T pf = T(0);
+      if constexpr (epi_prefetch<Epi>::value) {
+        if (i < a.n) pf = epi.prefetch(i);
+      }
+#pragma unroll
+      for (int j0 = 0; j0 < kSdiaMax; j0 += SB) {
+        if (j0 >= nd) break;  // wave-uniform
+        VT v[SB];
+        T xv[SB];
+        bool m[SB];
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+          const int j = min(j0 + u, nd - 1);
+          const int off = dp[j];  // scalar
+          m[u] = (j0 + u < nd) && ((msk >> (j0 + u)) & 1u);
+          const int32_t c = m[u] ? row + off : base;
+          v[u] = gld(a.vals + kSellC * int64_t(g0 + j) + lane);
+          xv[u] = gx(c);
+        }
+#pragma unroll
+        for (int u = 0; u < SB; ++u)
+          if (m[u]) acc = acc + T(v[u]) * xv[u];
       }
       if constexpr (epi_prefetch<Epi>::value) {
         if (i < a.n) epi.row_pf(i, acc, d, pf);
@@ -355,6 +413,7 @@ inline double sell_max_pad() {
 
 // grid of a SELL launch (the solver sizes the split-reduction groups from it)
 constexpr int kSellWG = 256;  // 4 slices per workgroup (512 / 1024 measured slower: DESIGN.md §5)
+constexpr int kSdiaSB = 8;    // SELL-DIA slots per batch
 
 inline int64_t sell_grid(const SellPattern& P, bool reducing) {
   return std::min<int64_t>((P.nb + kSellWG - 1) / kSellWG, sell_cap(reducing));
@@ -368,7 +427,7 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
   // that tile's and its prologue may test the tile's own system
   if (!one_tile_per_wg) grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
-  SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals), P.dict};
+  SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
   // compact-value kernels: registers for 6 workgroups per CU (the resident reducing grid)
   constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? (TH <= 1536 ? 1536 / TH : 1) : 1;
   if constexpr (!std::is_same<CT, uint16_t>::value) {  // BSELL-64 has no dictionary columns
@@ -379,17 +438,30 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
       return;
     }
   }
-  // 2 groups of 4 entries per batch for fp32-stored values (fewer registers in flight: 89.6-90.7
-  // vs 91.2 us per PCG iteration, 25.0 vs 27.0 us cold SpMV), 4 for fp64 values
-  constexpr int QB = sizeof(VT) == 4 ? 2 : 4;
+  // 2 groups of 4 entries per batch (tools/sell_sweep.py on kuhn101, dictionary columns, cold:
+  // fp64 values 32.2 us vs 33.8 with 4 groups and 46.0 with 8; fp32 values 22.7 vs 24.1 / 37.0)
+  constexpr int QB = 2;
   hipLaunchKernelGGL((k_spmv_sell<T, VT, CT, QB, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a,
                      pro, gx, epi);
+}
+
+// SELL-DIA launch
+template <typename T, typename VT, class Pro, class Gx, class Epi>
+inline void launch_spmv_sdia(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
+                             bool one_tile_per_wg = false) {
+  int64_t grid = (P.nb + kSellWG - 1) / kSellWG;
+  if (!one_tile_per_wg) grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
+  if (grid <= 0) return;
+  SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals)};
+  constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? 1536 / kSellWG : 1;
+  hipLaunchKernelGGL((k_spmv_sdia<T, VT, kSdiaSB, kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
+                     0, st, a, pro, gx, epi);
 }
 
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
                                  bool one_tile_per_wg = false) {
-  if (P.col_bits == 4) launch_spmv_sell_th<T, VT, uint16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
+  if (P.col_bits == 1) launch_spmv_sdia<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else launch_spmv_sell_th<T, VT, int32_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
 }
@@ -411,8 +483,9 @@ namespace lspcg {
 // Host-side construction (lspcg_sell.hip), enqueued on `st`.
 // Builds the SELL-64 pattern of a scalar CSR (n rows); fails with LSPCG_ERR_UNSUPPORTED when the
 // padded size exceeds max_pad x nnz (irregular row lengths: the CSR kernel is used instead).
-// cols (kSellCol16 | kSellColDict): the column storages allowed besides int32; the most compact
-// one that fits is taken (dictionary codes, then 16-bit offsets).
+// cols (kSellCol16 | kSellColDia): the column storages allowed besides int32; SELL-DIA is taken
+// when every slice has <= 16 distinct offsets, every row is sorted and it stores no more slots
+// than the 4-entry groups would, else 16-bit offsets when they fit.
 int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
                        int cols, hipStream_t st, SellPattern* out);
 // Allocates and fills the SELL value array of a CSR with the same pattern.  src_dtype /

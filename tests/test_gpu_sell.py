@@ -62,7 +62,7 @@ def test_sell_spmv_bitwise_vs_scipy(gpu_ctx, which):
     ref = A @ x
     Ad = _dm(A)
     xt = torch.from_numpy(x).cuda()
-    for flags in (0, 1, 2, 3, 8, 9, 10, 11):  # fp32 values x 16-bit column offsets x dictionary codes
+    for flags in (0, 1, 2, 3, 8, 9, 10, 11):  # fp32 values x 16-bit column offsets x SELL-DIA
         y = _sell_spmv(Ad, xt, flags)
         assert np.array_equal(y, ref), (which, flags, np.nanmax(np.abs(y - ref)))
 
@@ -165,20 +165,23 @@ def test_small_solve_1024_threads(gpu_ctx, grid, monkeypatch):
         assert np.array_equal(out[a][1], out[c][1]) and np.array_equal(out[a][2], out[c][2])
 
 
-def _max_offsets_per_slice(A):
-    """Largest number of distinct row-relative offsets col - row in a 64-row slice."""
+def _dia_slots(A):
+    """(max distinct row-relative offsets col - row in a 64-row slice, sum over slices of that count)
+    for a CSR with sorted rows."""
     n = A.shape[0]
     rows = np.repeat(np.arange(n), np.diff(A.indptr)).astype(np.int64)
     if rows.size == 0:
-        return 0
+        return 0, 0
     key = np.unique((rows // 64) * (1 << 33) + (A.indices.astype(np.int64) - rows + (1 << 32)))
-    return int(np.bincount(key >> 33).max())
+    cnt = np.bincount(key >> 33)
+    return int(cnt.max()), int(cnt.sum())
 
 
-def _expected_kind(A, max_pad=2.0, dictionary=True):
-    """lspcg_mat_prepare_spmv's rule: SELL-64 if the padded slots stay <= max_pad * nnz, with
-    4-bit dictionary codes if no 64-row slice has more than 15 distinct offsets col - row (sorted
-    rows), else 16-bit column offsets if every |col - 64*slice| <= 32767, else int32 columns."""
+def _expected_kind(A, max_pad=2.0, dia=True):
+    """lspcg_mat_prepare_spmv's rule: SELL-64 if the padded slots stay <= max_pad * nnz; then SELL-DIA
+    (kind 1) if every 64-row slice has <= 16 distinct offsets col - row and the slices' offset counts
+    sum to no more than the 4-entry groups' slots (sorted rows), else 16-bit column offsets if every
+    |col - 64*slice| <= 32767, else int32 columns."""
     n = A.shape[0]
     lens = np.diff(A.indptr)
     if n == 0 or A.nnz == 0:
@@ -186,11 +189,12 @@ def _expected_kind(A, max_pad=2.0, dictionary=True):
     ns = (n + 63) // 64
     pad = np.zeros(ns * 64, dtype=np.int64)
     pad[:n] = lens
-    slots = 256 * ((pad.reshape(ns, 64).max(axis=1) + 3) // 4).sum()
-    if slots > max_pad * A.nnz:
+    groups = ((pad.reshape(ns, 64).max(axis=1) + 3) // 4).sum()
+    if 256 * groups > max_pad * A.nnz:
         return 0
-    if dictionary and _max_offsets_per_slice(A) <= 15:
-        return 4
+    mx, tot = _dia_slots(A)
+    if dia and mx <= 16 and tot <= 4 * groups:
+        return 1
     rows = np.repeat(np.arange(n), lens)
     off = A.indices - (rows // 64) * 64
     return 16 if np.all(np.abs(off) <= 32767) else 32
@@ -213,7 +217,7 @@ def test_prepare_spmv_keeps_bits(gpu_ctx, which, dtype):
 def test_prepare_spmv_dropped_by_scale_columns(gpu_ctx):
     A = sp.csr_matrix(P.kuhn_laplacian(7))
     Ad = _dm(A)
-    assert Ad.prepare_spmv() == 4  # 15 stencil offsets: dictionary codes
+    assert Ad.prepare_spmv() == 1  # 15 stencil offsets: SELL-DIA
     d = np.random.default_rng(0).uniform(0.5, 2.0, size=A.shape[0])
     Ad.scale_columns_(torch.from_numpy(d).cuda())
     x = np.random.default_rng(1).normal(size=A.shape[0])
@@ -304,20 +308,25 @@ def _offset_matrix(n, offsets, seed=0):
     return A
 
 
-@pytest.mark.parametrize("case", ["15-offsets", "16-offsets", "tail-slice", "far-offsets", "2d-5pt"])
-def test_dictionary_columns_rule_and_bits(gpu_ctx, case):
-    """Dictionary codes are chosen exactly when every slice has <= 15 distinct offsets (15 = the
-    Kuhn-tet stencil; 16 falls back to 16-bit offsets); offsets far beyond the 16-bit range are
-    fine in a dictionary; a ragged last slice (n % 64 != 0) gathers in range."""
+@pytest.mark.parametrize("case", ["15-offsets", "16-offsets", "17-offsets", "tail-slice", "far-offsets", "2d-5pt",
+                                  "lower"])
+def test_dia_rule_and_bits(gpu_ctx, case):
+    """SELL-DIA is chosen exactly when every slice has <= 16 distinct offsets (15 = the Kuhn-tet
+    stencil; 17 falls back to 16-bit offsets); offsets far beyond the 16-bit range are fine; a
+    ragged last slice (n % 64 != 0) and a non-symmetric (lower-triangular) pattern give scipy's bits."""
     offs15 = [-4097, -4096, -65, -64, -63, -2, -1, 0, 1, 2, 63, 64, 65, 4096, 4097]
     A = {"15-offsets": lambda: _offset_matrix(20000, offs15),
          "16-offsets": lambda: _offset_matrix(20000, offs15 + [5000]),
+         "17-offsets": lambda: _offset_matrix(20000, offs15 + [5000, -5000]),
          "tail-slice": lambda: _offset_matrix(4099, offs15, 1),
          "far-offsets": lambda: _offset_matrix(150000, [-120000, -2, -1, 0, 1, 2, 120000], 2),
-         "2d-5pt": lambda: sp.csr_matrix(P.poisson2d_grid(70, 61)[0])}[case]()
-    kind_expected = {"15-offsets": 4, "16-offsets": 16, "tail-slice": 4, "far-offsets": 4, "2d-5pt": 4}[case]
+         "2d-5pt": lambda: sp.csr_matrix(P.poisson2d_grid(70, 61)[0]),
+         "lower": lambda: sp.csr_matrix(sp.tril(_offset_matrix(20000, offs15, 3)))}[case]()
+    A.sort_indices()
+    kind_expected = {"17-offsets": 16}.get(case, 1)
     assert _expected_kind(A) == kind_expected
     x = np.random.default_rng(3).normal(size=A.shape[0])
+    x[::13] = -0.0
     ref = A @ x
     Ad = _dm(A)
     assert Ad.prepare_spmv() == kind_expected
@@ -326,45 +335,42 @@ def test_dictionary_columns_rule_and_bits(gpu_ctx, case):
         assert np.array_equal(_sell_spmv(Ad, torch.from_numpy(x).cuda(), flags), ref), flags
 
 
-def test_dictionary_columns_unsorted_rows(gpu_ctx):
-    """Rows uploaded in a stored, unsorted order (keep_order): the dictionary merge may list an
-    offset twice but still holds every one, and the row sums keep the stored order."""
+def test_dia_unsorted_rows_fall_back(gpu_ctx):
+    """Rows uploaded in a stored, unsorted order (keep_order): SELL-DIA's slot order would not be the
+    row's order, so the build takes 16-bit offsets and the sums keep the stored order."""
     from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
 
     A = _offset_matrix(9000, [-300, -1, 0, 1, 300], 4)
-    rng = np.random.default_rng(5)
     B = A.copy()
-    for i in range(B.shape[0]):  # reverse every third row
+    for i in range(0, B.shape[0], 3):  # reverse every third row
         a, b = B.indptr[i], B.indptr[i + 1]
-        if i % 3 == 0:
-            B.indices[a:b] = B.indices[a:b][::-1].copy()
-            B.data[a:b] = B.data[a:b][::-1].copy()
+        B.indices[a:b] = B.indices[a:b][::-1].copy()
+        B.data[a:b] = B.data[a:b][::-1].copy()
     B.has_sorted_indices = False
-    x = rng.normal(size=B.shape[0])
+    x = np.random.default_rng(5).normal(size=B.shape[0])
     ref = B @ x  # scipy's csr_matvec sums each row in stored order
     Ad = DeviceMatrix.from_scipy(B, keep_order=True)
-    kind = Ad.prepare_spmv()
-    assert kind == 4
+    assert Ad.prepare_spmv() == 16
     assert np.array_equal(Ad.matvec(torch.from_numpy(x).cuda()).cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("precond", ["none", "ext_spai"])
-def test_pcg_dictionary_views_equal_csr_views(gpu_ctx, precond, monkeypatch):
-    """A Kuhn grid above the one-workgroup bound (n = 5832): the loop's SELL views carry dictionary
-    codes; count, history and iterate equal the CSR views' bit for bit, under both reduction forms."""
+@pytest.mark.parametrize("precond", ["none", "ext_spai", "ext_spai_scaled"])
+def test_pcg_dia_views_equal_csr_views(gpu_ctx, precond, monkeypatch):
+    """A Kuhn grid (n = 5832) on SELL-DIA views: count, history and iterate equal the CSR views' bit
+    for bit, under every reduction form and in the one-workgroup solve."""
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
 
     A = sp.csr_matrix(P.kuhn_laplacian(18, 1e-2))
     A.sort_indices()
-    assert _expected_kind(A) == 4
+    assert _expected_kind(A) == 1
     n = A.shape[0]
     b = torch.from_numpy(A @ np.ones(n)).cuda()
     out = []
-    for env in (_v(no_sell="1"), _v(), _v(split="0"), _v(split="2")):
+    for env in (_v(no_sell="1"), _v(), _v(split="0"), _v(split="2"), _v(small="1000000")):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
-        if precond == "ext_spai":
+        if precond.startswith("ext_spai"):
             s.set_spai(_cases.spai_like(A), 1e-3)
         x = torch.zeros(n, dtype=torch.float64, device="cuda")
         it, conv, _, hist = s.solve(b, x, rtol=1e-9, return_history=True)
@@ -373,3 +379,28 @@ def test_pcg_dictionary_views_equal_csr_views(gpu_ctx, precond, monkeypatch):
     for o in out[1:]:
         assert out[0][0] == o[0]
         assert np.array_equal(out[0][1], o[1]) and np.array_equal(out[0][2], o[2])
+
+
+def test_pcg_dia_nonsymmetric_L(gpu_ctx, monkeypatch):
+    """L with a lower-triangular pattern (not A's): L and its transpose get SELL-DIA views of their own
+    (offsets <= 0 / >= 0); same bits as the CSR views."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    A = sp.csr_matrix(P.kuhn_laplacian(17, 1e-2))
+    A.sort_indices()
+    L = sp.csr_matrix(sp.tril(_cases.spai_like(A)))
+    L.sort_indices()
+    n = A.shape[0]
+    b = torch.from_numpy(A @ np.ones(n)).cuda()
+    out = []
+    for env in (_v(no_sell="1"), _v()):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai")
+        s.set_spai(L, 1e-3)
+        x = torch.zeros(n, dtype=torch.float64, device="cuda")
+        it, conv, _, hist = s.solve(b, x, rtol=1e-9, max_iter=400, return_history=True)
+        out.append((it, x.cpu().numpy(), hist))
+        del s
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])

@@ -43,6 +43,9 @@ if os.environ.get("PROBE_VARIANTS") == "cap":
 ref = None
 for name, env in VARIANTS:
     os.environ.update(env)
+    for k, v in env.items():
+        if v == "":
+            os.environ.pop(k, None)
     solver = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", dtype=np.float64)
     solver.set_spai(L, 3e-3, block_size=L.block_size)
     ts = []

@@ -1,0 +1,111 @@
+// Diagnostics only (not part of liblspcg_hip.so): the SELL-DIA SpMV (csrc/lspcg_sell.hpp) under
+// other launch configurations -- slots loaded per batch (SB) x register budget (MINW, minimum
+// workgroups per CU in __launch_bounds__) -- timed cold / warm exactly like lspcg_spmv_timed, so a
+// sweep can pick the product's configuration.  Built and driven by tools/sell_sweep.py.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+#include "../learningsparsepreconditioner4gpu_amd/csrc/lspcg_sell.hpp"
+
+using namespace lspcg;
+
+namespace {
+
+__global__ void k_flush(const int4* __restrict__ buf, int64_t n, int* sink) {
+  int acc = 0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int4 v = buf[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x1234567) sink[0] = acc;
+}
+
+template <typename VT, int SB, int MINW>
+void launch(const SellPattern& P, const void* vals, const double* x, double* y, hipStream_t st) {
+  const int64_t grid = (P.nb + kSellWG - 1) / kSellWG;
+  SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals)};
+  hipLaunchKernelGGL((k_spmv_sdia<double, VT, SB, kSellWG, MINW, ProNone, GatherVec<double>, EpiStore<double>>),
+                     dim3(unsigned(grid)), dim3(kSellWG), 0, st, a, ProNone{}, GatherVec<double>{x}, EpiStore<double>{y});
+}
+
+using Fn = void (*)(const SellPattern&, const void*, const double*, double*, hipStream_t);
+
+// config id -> (value bytes, slots per batch SB, MINW, transposed)
+struct Cfg {
+  int vbytes, qb, minw, tr;
+  Fn fn;
+};
+const Cfg kCfgs[] = {
+    {8, 4, 1, 0, launch<double, 4, 1>},  {8, 8, 1, 0, launch<double, 8, 1>}, {8, 16, 1, 0, launch<double, 16, 1>},
+    {8, 8, 4, 0, launch<double, 8, 4>},  {4, 4, 6, 0, launch<float, 4, 6>},  {4, 8, 6, 0, launch<float, 8, 6>},
+    {4, 16, 6, 0, launch<float, 16, 6>}, {4, 8, 8, 0, launch<float, 8, 8>},  {4, 8, 1, 0, launch<float, 8, 1>},
+};
+
+}  // namespace
+
+extern "C" {
+
+int sweep_count() { return int(sizeof(kCfgs) / sizeof(kCfgs[0])); }
+
+int sweep_cfg(int id, int* vbytes, int* qb, int* minw, int* tr) {
+  if (id < 0 || id >= sweep_count()) return -1;
+  *tr = kCfgs[id].tr;
+  *vbytes = kCfgs[id].vbytes;
+  *qb = kCfgs[id].qb;
+  *minw = kCfgs[id].minw;
+  return 0;
+}
+
+// rowptr / colind (int32, device) / vals (fp64, device) of an n-row CSR with sorted rows; x, y device
+// fp64.  Times config `id` (dictionary columns required): ms_cold / ms_warm per launch.
+int sweep_run(int id, int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, const double* vals,
+              const double* x, double* y, int reps, int64_t flush_bytes, double* ms_cold, double* ms_warm) {
+  if (id < 0 || id >= sweep_count()) return -1;
+  hipStream_t st = nullptr;
+  SellPattern P;
+  if (sell_build_pattern(n, nnz, rowptr, colind, 1e30, kSellColDia, st, &P) || P.col_bits != 1) return -2;
+  void* v = nullptr;
+  const int vb = kCfgs[id].vbytes;
+  if (sell_fill_values(P, colind, vals, LSPCG_F64, vb == 4 ? LSPCG_F32 : LSPCG_F64, st, &v)) return -3;
+  int4* fl = nullptr;
+  int* sink = nullptr;
+  (void)hipMalloc(&fl, size_t(flush_bytes) + 64);
+  (void)hipMalloc(&sink, 64);
+  (void)hipMemset(fl, 1, size_t(flush_bytes));
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  auto run = [&]() { kCfgs[id].fn(P, v, x, y, st); };
+  auto flush = [&]() { hipLaunchKernelGGL(k_flush, dim3(4096), dim3(256), 0, st, fl, flush_bytes / 16, sink); };
+  float t = 0.f;
+  run();
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < 3 * reps; ++i) run();
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&t, e0, e1);
+  *ms_warm = t / (3 * reps);
+  float tp = 0.f, tf = 0.f;
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < reps; ++i) {
+    flush();
+    run();
+  }
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&tp, e0, e1);
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < reps; ++i) flush();
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&tf, e0, e1);
+  *ms_cold = (tp - tf) / reps;
+  const hipError_t e = hipDeviceSynchronize();
+  (void)hipFree(v);
+  (void)hipFree(fl);
+  (void)hipFree(sink);
+  P.release();
+  return e == hipSuccess ? 0 : -4;
+}
+}

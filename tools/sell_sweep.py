@@ -1,0 +1,69 @@
+"""Launch-configuration sweep of the SELL-DIA SpMV (tools/sell_sweep.hip; diagnostics, not the product):
+every (value type, slots per batch, MINW) configuration on the bench matrix, cold and warm, checked bit for bit
+against the product's lspcg_spmv on the same SELL copy.
+
+    python tools/sell_sweep.py --build          # in the container: hipcc -> tools/_sweep/libsellsweep.so
+    python tools/sell_sweep.py [workload]       # on the GPU box: one JSON line per configuration
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "tools", "_sweep", "libsellsweep.so")
+
+
+def build():
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    pkg = os.path.join(ROOT, "learningsparsepreconditioner4gpu_amd")
+    cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950", "-ffp-contract=off",
+           "-I" + os.path.join(ROOT, "include"), os.path.join(ROOT, "tools", "sell_sweep.hip"), "-L" + pkg, "-llspcg_hip",
+           "-Wl,-rpath," + pkg, "-o", LIB]
+    print(" ".join(cmd))
+    subprocess.check_call(cmd)
+
+
+def main(wl):
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import scipy.sparse as sp
+    import torch
+
+    from bench import FLUSH_BYTES, spmv_bytes
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    A_raw, mask, _, _, _ = P.workload(wl)
+    A = sp.csr_matrix(A_raw)
+    A.sort_indices()
+    A.data = A.data.astype(np.float32).astype(np.float64)  # fp32-exact, like the reference's matrices
+    Ad = DeviceMatrix.from_scipy(A)
+    lib = C.CDLL(LIB)
+    rp = torch.from_numpy(A.indptr.astype(np.int32)).cuda()
+    ci = torch.from_numpy(A.indices.astype(np.int32)).cuda()
+    va = torch.from_numpy(A.data).cuda()
+    x = torch.randn(A.shape[0], dtype=torch.float64, device="cuda")
+    y = torch.empty_like(x)
+    ref = Ad.matvec(x)
+    alg = spmv_bytes(A.shape[0], A.nnz)
+    p = lambda t: C.c_void_p(t.data_ptr())
+    for cid in range(lib.sweep_count()):
+        vb, qb, mw, tr = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        lib.sweep_cfg(cid, C.byref(vb), C.byref(qb), C.byref(mw), C.byref(tr))
+        cold, warm = C.c_double(), C.c_double()
+        y.fill_(float("nan"))
+        rc = lib.sweep_run(cid, C.c_int64(A.shape[0]), C.c_int64(A.nnz), p(rp), p(ci), p(va), p(x), p(y), 20,
+                           C.c_int64(FLUSH_BYTES), C.byref(cold), C.byref(warm))
+        print(json.dumps({"workload": wl, "values": "fp64" if vb.value == 8 else "fp32", "SB": qb.value,
+                          "MINW": mw.value, "rc": rc, "cold_us": cold.value * 1e3, "warm_us": warm.value * 1e3,
+                          "frac_alg_cold": alg / (cold.value * 1e-3) / 8e12, "bitexact": bool(torch.equal(y, ref))}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    if "--build" in sys.argv:
+        build()
+    else:
+        main(sys.argv[1] if len(sys.argv) > 1 else "kuhn101")

@@ -16,7 +16,7 @@ def per_dispatch(d, counter):
     for f in glob.glob(f"{d}/{counter}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name", "")
-            roof = "k_spmv<double, double, 1" in name or "k_spmv_sell<double, double" in name
+            roof = "k_spmv<double, double, 1" in name or "k_spmv_sell<double, double" in name or "k_spmv_sdia<double, double" in name
             if roof and "EpiStore" in name and r["Counter_Name"] == counter:
                 vals.setdefault(r["Dispatch_Id"], 0.0)
                 vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
