@@ -34,17 +34,27 @@ def main(path):
             "KB z=L t+eps r, rho": r"k_spmv_s(?:ell|dia)<double, float.*EpiZG<double, false>",
             "UP p, x": r"k_update_p_g<double>", "KC q=A p, pi": r"k_spmv_s(?:ell|dia)<double, float.*EpiQG<double>",
             "UR r": r"k_update_r_g<double>"}
+    # the bench system's launches only: the largest grid of each kind (smaller systems -- C1, C5 --
+    # launch smaller grids), without the predicated launches that exit at once after convergence
+    # (chunk tails: < 1/3 of that grid's median)
+    def grid(r):
+        for key in ("Grid_Size", "Grid_Size_X"):
+            if key in r and r[key]:
+                return int(r[key])
+        return 0
     lk = {}
     for r in rows:
         for k, pat in loop.items():
             if re.search(pat, r["Kernel_Name"]):
-                lk.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)
-    # the bench system's launches only: drop the predicated launches that exit at once (chunk tails
-    # after convergence) and smaller systems' launches -- keep those >= half the 90th percentile
-    def big(v):
-        p90 = sorted(v)[int(0.9 * (len(v) - 1))]
-        return [d for d in v if d >= 0.5 * p90]
-    res["pcg_loop_kernels_us"] = {k: {"n": len(big(v)), "avg": avg(big(v)), "median": med(big(v))} for k, v in lk.items()}
+                lk.setdefault(k, []).append((grid(r), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3))
+    out = {}
+    for k, v in lk.items():
+        g = max(x[0] for x in v)
+        d = [x[1] for x in v if x[0] == g]
+        m = med(d)
+        d = [x for x in d if x >= m / 3]
+        out[k] = {"grid": g, "n": len(d), "avg": avg(d), "median": med(d)}
+    res["pcg_loop_kernels_us"] = out
     print(json.dumps(res, indent=1))
 
 
