@@ -29,6 +29,26 @@ void launch(const SellPattern& P, const void* vals, const double* x, double* y, 
                      dim3(unsigned(grid)), dim3(kSellWG), 0, st, a, ProNone{}, GatherVec<double>{x}, EpiStore<double>{y});
 }
 
+// the fused-update cost model: the vector entry of a slot recomputed from two vectors,
+// p_new[c] = p_old[c] * beta + z[c] (what a KC with UP folded in would load)
+struct GatherFused {
+  const double* z;
+  const double* p;
+  double beta;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ double operator()(int64_t j) const { return (gld(p + j) * beta) + gld(z + j); }
+};
+
+template <typename VT, int SB, int MINW>
+void launch_fused(const SellPattern& P, const void* vals, const double* x, double* y, hipStream_t st) {
+  const int64_t grid = (P.nb + kSellWG - 1) / kSellWG;
+  SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals)};
+  // z = x, p = y's second half is not available: use x for both streams at distinct offsets (x + 0 / x + 1)
+  hipLaunchKernelGGL((k_spmv_sdia<double, VT, SB, kSellWG, MINW, ProNone, GatherFused, EpiStore<double>>),
+                     dim3(unsigned(grid)), dim3(kSellWG), 0, st, a, ProNone{}, GatherFused{x, x + P.n, 0.5},
+                     EpiStore<double>{y});
+}
+
 using Fn = void (*)(const SellPattern&, const void*, const double*, double*, hipStream_t);
 
 // config id -> (value bytes, slots per batch SB, MINW, transposed)
@@ -40,11 +60,85 @@ const Cfg kCfgs[] = {
     {8, 4, 1, 0, launch<double, 4, 1>},  {8, 8, 1, 0, launch<double, 8, 1>}, {8, 16, 1, 0, launch<double, 16, 1>},
     {8, 8, 4, 0, launch<double, 8, 4>},  {4, 4, 6, 0, launch<float, 4, 6>},  {4, 8, 6, 0, launch<float, 8, 6>},
     {4, 16, 6, 0, launch<float, 16, 6>}, {4, 8, 8, 0, launch<float, 8, 8>},  {4, 8, 1, 0, launch<float, 8, 1>},
+    {4, 8, 6, 1, launch_fused<float, 8, 6>}, {4, 16, 6, 1, launch_fused<float, 16, 6>},
+};
+
+template <typename VT, int QB, int MINW>
+void launch_bsr(const SellPattern& P, const void* vals, const double* x, double* y, hipStream_t st) {
+  const int64_t grid = (P.nb + kSellWG - 1) / kSellWG;
+  SellArgs<VT, int16_t> a{P.n, P.ns, P.gp, static_cast<const int16_t*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
+  hipLaunchKernelGGL((k_spmv_bsell3<double, VT, int16_t, QB, kSellWG, MINW, ProNone, GatherVec<double>, EpiStore<double>>),
+                     dim3(unsigned(grid)), dim3(kSellWG), 0, st, a, ProNone{}, GatherVec<double>{x}, EpiStore<double>{y});
+}
+
+// BSELL-64 (BSR 3x3) configurations: (value bytes, block slots per batch QB, MINW)
+const Cfg kBsrCfgs[] = {
+    {8, 1, 1, 0, launch_bsr<double, 1, 1>}, {8, 2, 1, 0, launch_bsr<double, 2, 1>}, {8, 4, 1, 0, launch_bsr<double, 4, 1>},
+    {8, 8, 1, 0, launch_bsr<double, 8, 1>}, {4, 2, 1, 0, launch_bsr<float, 2, 1>},  {4, 4, 1, 0, launch_bsr<float, 4, 1>},
+    {4, 8, 1, 0, launch_bsr<float, 8, 1>},
 };
 
 }  // namespace
 
 extern "C" {
+
+int sweep_bsr_count() { return int(sizeof(kBsrCfgs) / sizeof(kBsrCfgs[0])); }
+
+int sweep_bsr_cfg(int id, int* vbytes, int* qb) {
+  if (id < 0 || id >= sweep_bsr_count()) return -1;
+  *vbytes = kBsrCfgs[id].vbytes;
+  *qb = kBsrCfgs[id].qb;
+  return 0;
+}
+
+// BSR 3x3: nb block rows, nnzb blocks, rowptr / colind (int32, device), vals [nnzb][3][3] fp64 (device)
+int sweep_bsr_run(int id, int64_t nb, int64_t nnzb, const int32_t* rowptr, const int32_t* colind, const double* vals,
+                  const double* x, double* y, int reps, int64_t flush_bytes, double* ms_cold, double* ms_warm) {
+  if (id < 0 || id >= sweep_bsr_count()) return -1;
+  hipStream_t st = nullptr;
+  SellPattern P;
+  if (bsell_build_pattern(nb, nnzb, rowptr, colind, 1e30, true, st, &P) || P.col_bits != 16) return -2;
+  void* v = nullptr;
+  if (bsell_fill_values(P, vals, LSPCG_F64, kBsrCfgs[id].vbytes == 4 ? LSPCG_F32 : LSPCG_F64, st, &v)) return -3;
+  int4* fl = nullptr;
+  int* sink = nullptr;
+  (void)hipMalloc(&fl, size_t(flush_bytes) + 64);
+  (void)hipMalloc(&sink, 64);
+  (void)hipMemset(fl, 1, size_t(flush_bytes));
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  auto run = [&]() { kBsrCfgs[id].fn(P, v, x, y, st); };
+  auto flush = [&]() { hipLaunchKernelGGL(k_flush, dim3(4096), dim3(256), 0, st, fl, flush_bytes / 16, sink); };
+  float t = 0.f, tp = 0.f, tf = 0.f;
+  run();
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < 3 * reps; ++i) run();
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&t, e0, e1);
+  *ms_warm = t / (3 * reps);
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < reps; ++i) {
+    flush();
+    run();
+  }
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&tp, e0, e1);
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < reps; ++i) flush();
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&tf, e0, e1);
+  *ms_cold = (tp - tf) / reps;
+  const hipError_t e = hipDeviceSynchronize();
+  (void)hipFree(v);
+  (void)hipFree(fl);
+  (void)hipFree(sink);
+  P.release();
+  return e == hipSuccess ? 0 : -4;
+}
 
 int sweep_count() { return int(sizeof(kCfgs) / sizeof(kCfgs[0])); }
 

@@ -25,6 +25,45 @@ def build():
     subprocess.check_call(cmd)
 
 
+def main_bsr():
+    """BSELL-64 block slots per batch on the C4 elasticity system (BSR 3x3)."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import scipy.sparse as sp
+    import torch
+
+    from bench import FLUSH_BYTES, bsr3_bytes
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    A_raw, _, _, _, _ = P.workload("elast")
+    B = sp.bsr_matrix(sp.csr_matrix(A_raw), blocksize=(3, 3))
+    B.sort_indices()
+    B.data = B.data.astype(np.float32).astype(np.float64)
+    ref = DeviceMatrix.from_scipy(sp.csr_matrix(B)).matvec
+    lib = C.CDLL(LIB)
+    rp = torch.from_numpy(B.indptr.astype(np.int32)).cuda()
+    ci = torch.from_numpy(B.indices.astype(np.int32)).cuda()
+    va = torch.from_numpy(np.ascontiguousarray(B.data)).cuda()
+    n = B.shape[0]
+    x = torch.randn(n, dtype=torch.float64, device="cuda")
+    y = torch.empty_like(x)
+    want = ref(x)
+    alg = bsr3_bytes(n // 3, B.indices.size)
+    p = lambda t: C.c_void_p(t.data_ptr())
+    for cid in range(lib.sweep_bsr_count()):
+        vb, qb = C.c_int(), C.c_int()
+        lib.sweep_bsr_cfg(cid, C.byref(vb), C.byref(qb))
+        cold, warm = C.c_double(), C.c_double()
+        y.fill_(float("nan"))
+        rc = lib.sweep_bsr_run(cid, C.c_int64(n // 3), C.c_int64(B.indices.size), p(rp), p(ci), p(va), p(x), p(y), 20,
+                               C.c_int64(FLUSH_BYTES), C.byref(cold), C.byref(warm))
+        print(json.dumps({"workload": "elast BSR3", "values": "fp64" if vb.value == 8 else "fp32", "QB": qb.value,
+                          "rc": rc, "cold_us": cold.value * 1e3, "warm_us": warm.value * 1e3,
+                          "frac_alg_cold": alg / (cold.value * 1e-3) / 8e12, "bitexact": bool(torch.equal(y, want))}),
+              flush=True)
+
+
 def main(wl):
     sys.path.insert(0, ROOT)
     import numpy as np
@@ -44,9 +83,10 @@ def main(wl):
     rp = torch.from_numpy(A.indptr.astype(np.int32)).cuda()
     ci = torch.from_numpy(A.indices.astype(np.int32)).cuda()
     va = torch.from_numpy(A.data).cuda()
-    x = torch.randn(A.shape[0], dtype=torch.float64, device="cuda")
-    y = torch.empty_like(x)
-    ref = Ad.matvec(x)
+    x = torch.randn(2 * A.shape[0], dtype=torch.float64, device="cuda")  # [z | p] for the fused configs
+    y = torch.empty(A.shape[0], dtype=torch.float64, device="cuda")
+    ref = Ad.matvec(x[: A.shape[0]].contiguous())
+    reff = Ad.matvec((x[A.shape[0]:] * 0.5 + x[: A.shape[0]]).contiguous())
     alg = spmv_bytes(A.shape[0], A.nnz)
     p = lambda t: C.c_void_p(t.data_ptr())
     for cid in range(lib.sweep_count()):
@@ -57,13 +97,15 @@ def main(wl):
         rc = lib.sweep_run(cid, C.c_int64(A.shape[0]), C.c_int64(A.nnz), p(rp), p(ci), p(va), p(x), p(y), 20,
                            C.c_int64(FLUSH_BYTES), C.byref(cold), C.byref(warm))
         print(json.dumps({"workload": wl, "values": "fp64" if vb.value == 8 else "fp32", "SB": qb.value,
-                          "MINW": mw.value, "rc": rc, "cold_us": cold.value * 1e3, "warm_us": warm.value * 1e3,
-                          "frac_alg_cold": alg / (cold.value * 1e-3) / 8e12, "bitexact": bool(torch.equal(y, ref))}),
+                          "MINW": mw.value, "fused_gather": bool(tr.value), "rc": rc, "cold_us": cold.value * 1e3, "warm_us": warm.value * 1e3,
+                          "frac_alg_cold": alg / (cold.value * 1e-3) / 8e12, "bitexact": bool(torch.equal(y, reff if tr.value else ref))}),
               flush=True)
 
 
 if __name__ == "__main__":
     if "--build" in sys.argv:
         build()
+    elif "--bsr" in sys.argv:
+        main_bsr()
     else:
         main(sys.argv[1] if len(sys.argv) > 1 else "kuhn101")
