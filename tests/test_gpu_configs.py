@@ -151,3 +151,28 @@ def test_c5_heat_batch8_counts(gpu_ctx):
         it_o = O.pcg(A_h, b, O.spai_operator(L_h, ws.epsilon), rtol=1e-6, dot="exact")[0]
         it, conv, _, _ = _solve(A, L, b, ws.epsilon, 1e-6)
         assert conv and it == it_o, (A.n, it, it_o)
+
+
+def test_bench_system_views_bitwise(gpu_ctx, monkeypatch):
+    """The headline system (kuhn101: 1,030,301 rows, SELL-DIA views, GNN-inferred L, ext_spai to
+    1e-8) at full size through size-independent properties: the count, every ‖r_k‖ and the iterate
+    are bit-identical on SELL-DIA views (split group reductions and last-arriver reductions) and
+    on the staged CSR views (LSPCG_NO_SELL=1, scipy's row order by construction), and the true
+    residual ‖b - A x‖ / ‖b‖ is below the requested rtol (within the recurrence's drift)."""
+    A_raw, mask, _, _, _ = P.workload("kuhn101")
+    s, ws, A, L = _system(A_raw, mask)
+    assert A.n == 1030301
+    gt = s.mask.to("cuda").reshape(-1).to(torch.float64)
+    b = A.matvec(gt).cpu().numpy()
+    out = []
+    for env in ({"LSPCG_NO_SELL": "0", "LSPCG_SPLIT_REDUCE": "1"}, {"LSPCG_NO_SELL": "0", "LSPCG_SPLIT_REDUCE": "0"},
+                {"LSPCG_NO_SELL": "1", "LSPCG_SPLIT_REDUCE": "1"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        out.append(_solve(A, L, b, ws.epsilon, 1e-8))
+    it, conv, x, h = out[0]
+    assert conv and it == 212, it
+    for o in out[1:]:
+        assert o[0] == it and np.array_equal(o[2], x) and np.array_equal(o[3], h)
+    A_h = _csr(A)
+    assert np.linalg.norm(b - A_h @ x) / np.linalg.norm(b) <= 2e-8
