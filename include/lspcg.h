@@ -100,10 +100,11 @@ int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y);
 /* analysis step (cf. rocSPARSE csrmv_analysis): attach a SELL-64 copy of a scalar CSR matrix, or
  * the BSELL-64 block copy of a BSR 3x3 (one column per block, block values in 16-B lane chunks), with the
  * same values and dtype and 16-bit column offsets where they fit, that lspcg_spmv then uses -- the
- * results keep the same bits.  *kind (nullable) = the column storage: 4 (scalar CSR whose 64-row
- * slices have <= 15 distinct row-relative offsets col - row: 4-bit codes into a per-slice
- * dictionary), 16 (16-bit offsets from the slice's first row), 32 (int32 columns), or 0 when the
- * matrix stays on the CSR / BSR kernel (irregular row lengths).  lspcg_mat_scale_columns drops it. */
+ * results keep the same bits.  *kind (nullable) = the column storage: 1 (SELL-DIA: a sorted scalar
+ * CSR whose 64-row slices have <= 16 distinct row-relative offsets col - row, one value slot per
+ * offset and a row mask, no column array), 16 (16-bit offsets from the slice's first row), 32
+ * (int32 columns), or 0 when the matrix stays on the CSR / BSR kernel (irregular row lengths).
+ * lspcg_mat_scale_columns drops it. */
 int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind);
 /* average device ms of one SpMV launch, HIP events on the ctx stream.  flush_bytes == 0:
  * reps back-to-back launches (warm caches); > 0: before every launch a read of a flush_bytes
@@ -118,7 +119,7 @@ int lspcg_spmv_variant_timed(lspcg_ctx* ctx, const lspcg_mat* A, int variant, co
 /* diagnostics: the same timing for the SELL-64 kernel the PCG loop uses (csrc/lspcg_sell.hpp) on a
  * SELL copy of A built inside the call (fp64 scalar CSR).  flags bit 0: store the values as fp32
  * (lossless only when every value is fp32-representable); bit 1: 16-bit column offsets where they
- * fit; bit 3: dictionary column codes where they fit (tried before bit 1); bit 2 (experiment): gather x from an interleaved (x, x) pair array with one 16-B load per
+ * fit; bit 3: SELL-DIA where it fits (tried before bit 1); bit 2 (experiment): gather x from an interleaved (x, x) pair array with one 16-B load per
  * entry, the cost model of a fused update evaluated in the gather.  y = A x, same bits as
  * lspcg_spmv */
 int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int flags, const void* x, void* y,

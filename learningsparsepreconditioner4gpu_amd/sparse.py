@@ -209,7 +209,7 @@ class DeviceMatrix:
 
     def prepare_spmv(self) -> int:
         """Analysis step: attach a SELL-64 copy that :meth:`matvec` then uses (same bits).
-        Returns the column storage (4 = dictionary codes, 16 = 16-bit offsets, 32 = int32) or 0
+        Returns the column storage (1 = SELL-DIA, 16 = 16-bit offsets, 32 = int32) or 0
         when the CSR kernel stays in use."""
         kind = C.c_int()
         _lib.call("lspcg_mat_prepare_spmv", self.handle, C.byref(kind))
