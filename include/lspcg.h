@@ -119,9 +119,9 @@ int lspcg_spmv_variant_timed(lspcg_ctx* ctx, const lspcg_mat* A, int variant, co
 /* diagnostics: the same timing for the SELL-64 kernel the PCG loop uses (csrc/lspcg_sell.hpp) on a
  * SELL copy of A built inside the call (fp64 scalar CSR).  flags bit 0: store the values as fp32
  * (lossless only when every value is fp32-representable); bit 1: 16-bit column offsets where they
- * fit; bit 3: SELL-DIA where it fits (tried before bit 1); bit 2 (experiment): gather x from an interleaved (x, x) pair array with one 16-B load per
- * entry, the cost model of a fused update evaluated in the gather.  y = A x, same bits as
- * lspcg_spmv */
+ * fit; bit 3: SELL-DIA where it fits (tried before bit 1); bit 2 (experiment): gather x from an
+ * interleaved (x, x) pair array with one 16-B load per entry, the cost model of a fused update
+ * evaluated in the gather.  y = A x, same bits as lspcg_spmv */
 int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int flags, const void* x, void* y,
                           int reps, int64_t flush_bytes, double* avg_ms);
 /* calibration: the same cold / warm timing for a plain streaming read of `bytes` (16-B loads, 8
