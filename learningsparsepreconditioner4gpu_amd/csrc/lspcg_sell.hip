@@ -350,7 +350,7 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
   }
   // SELL-DIA: dictionaries and slot counts first; one host read of (flag, DIA slot total) decides
   int fit16 = 0;  // 1 = some column out of 16-bit offset range
-  int flag_h[2] = {1, 0};  // [flags (bit 0: no DIA, bit 1: no 16-bit, bit 2: not symmetric), DIA slots]
+  int flag_h[2] = {1, 0};  // [flags (bit 0: no SELL-DIA, bit 1: no 16-bit offsets), SELL-DIA slots]
   int32_t* dgp = nullptr;  // DIA slot prefix
   int* flag = nullptr;
   if (n) {
