@@ -404,3 +404,35 @@ def test_pcg_dia_nonsymmetric_L(gpu_ctx, monkeypatch):
         del s
     assert out[0][0] == out[1][0]
     assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_dia_randomized_structured(gpu_ctx, seed):
+    """Randomized SELL-DIA cases: a random offset set (3..16 offsets, some far apart), random n
+    (not a multiple of 64), ~30 % of the entries dropped (ragged rows inside a slice, empty rows),
+    explicit zeros kept, fp64 and fp32 values: the analysis step takes SELL-DIA exactly when the rule
+    says so and the SpMV gives scipy's bits; x carries -0.0 and a few huge values."""
+    rng = np.random.default_rng(100 + seed)
+    n = int(rng.integers(200, 40000))
+    k = int(rng.integers(3, 17))
+    offs = sorted(set(int(o) for o in rng.choice(np.r_[np.arange(-70, 71), [-9000, -4096, 4096, 9000]], k,
+                                                 replace=False)) | {0})[:16]
+    A = _offset_matrix(n, offs, seed)
+    drop = rng.random(A.nnz) < 0.3
+    A.data[rng.random(A.nnz) < 0.05] = 0.0  # explicit zeros stay stored
+    A = sp.csr_matrix((A.data[~drop], A.indices[~drop],
+                       np.r_[0, np.cumsum(np.add.reduceat(~drop, A.indptr[:-1]) * (np.diff(A.indptr) > 0))]),
+                      shape=A.shape)
+    A.sort_indices()
+    for dtype in (np.float64, np.float32):
+        B = A.astype(dtype)
+        x = rng.normal(size=n).astype(dtype)
+        x[::11] = -0.0
+        x[5::997] = dtype(1e30)
+        ref = B @ x
+        Ad = _dm(B, dtype)
+        kind = Ad.prepare_spmv()
+        assert kind == _expected_kind(B), (n, offs, kind)
+        y = Ad.matvec(torch.from_numpy(x).cuda()).cpu().numpy()
+        assert np.array_equal(y, ref) or np.array_equal(np.isnan(y), np.isnan(ref)) and np.array_equal(
+            y[~np.isnan(y)], ref[~np.isnan(ref)]), (n, offs, dtype)
