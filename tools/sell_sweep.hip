@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <vector>
 
 #include "../learningsparsepreconditioner4gpu_amd/csrc/lspcg_sell.hpp"
 
@@ -78,9 +79,123 @@ const Cfg kBsrCfgs[] = {
     {4, 8, 1, 0, launch_bsr<float, 8, 1>},
 };
 
+// SELL-DIA with the values of a slice stored in quads (the experiment: 16-B value loads, one per 4
+// slots, D_s padded to a multiple of 4): vals[64 gq[s] * 4 + 256 (j / 4) + 4 lane + j % 4]
+template <typename T, int QPB>
+__global__ void __launch_bounds__(256, 6) k_sdia_quad(int64_t n, int64_t ns, const int32_t* __restrict__ gp,
+                                                      const int32_t* __restrict__ gq, const uint16_t* __restrict__ mask,
+                                                      const int32_t* __restrict__ dict, const float* __restrict__ vals,
+                                                      const T* __restrict__ x, T* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int64_t s = int64_t(blockIdx.x) * 4 + w;
+  if (s >= ns) return;
+  const int nd = gp[s + 1] - gp[s];
+  const int nq = gq[s + 1] - gq[s];
+  const int32_t* dp = dict + kSdiaMax * s;
+  const unsigned msk = mask[kSellC * s + lane];
+  const int32_t base = int32_t(s * kSellC), row = base + lane;
+  const float* vp = vals + 256 * int64_t(gq[s]) + 4 * lane;
+  T acc = T(0);
+#pragma unroll
+  for (int j0 = 0; j0 < kSdiaMax; j0 += 4 * QPB) {
+    if (j0 >= nd) break;
+    float v[4 * QPB];
+    T xv[4 * QPB];
+    bool m[4 * QPB];
+#pragma unroll
+    for (int u = 0; u < QPB; ++u) {
+      const int g = min(j0 / 4 + u, nq - 1);
+      const f32x4 a = *(const __attribute__((address_space(1))) f32x4*)(vp + 256 * g);
+      v[4 * u] = a.x; v[4 * u + 1] = a.y; v[4 * u + 2] = a.z; v[4 * u + 3] = a.w;
+    }
+#pragma unroll
+    for (int u = 0; u < 4 * QPB; ++u) {
+      const int j = min(j0 + u, nd - 1);
+      m[u] = (j0 + u < nd) && ((msk >> (j0 + u)) & 1u);
+      xv[u] = gld(x + (m[u] ? row + dp[j] : base));
+    }
+#pragma unroll
+    for (int u = 0; u < 4 * QPB; ++u)
+      if (m[u]) acc = acc + T(v[u]) * xv[u];
+  }
+  if (row < n) y[row] = acc;
+}
+
 }  // namespace
 
 extern "C" {
+
+// the quad-layout experiment: builds the SELL-DIA pattern, re-lays its fp32 values into quads on the
+// host and times k_sdia_quad (QPB quads per batch: 2 or 4) like sweep_run
+int sweep_quad_run(int qpb, int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, const double* vals,
+                   const double* x, double* y, int reps, int64_t flush_bytes, double* ms_cold, double* ms_warm) {
+  hipStream_t st = nullptr;
+  SellPattern P;
+  if (sell_build_pattern(n, nnz, rowptr, colind, 1e30, kSellColDia, st, &P) || P.col_bits != 1) return -2;
+  void* v = nullptr;
+  if (sell_fill_values(P, colind, vals, LSPCG_F64, LSPCG_F32, st, &v)) return -3;
+  (void)hipDeviceSynchronize();
+  std::vector<int32_t> gp(P.ns + 1), gq(P.ns + 1, 0);
+  (void)hipMemcpy(gp.data(), P.gp, sizeof(int32_t) * (P.ns + 1), hipMemcpyDeviceToHost);
+  for (int64_t s = 0; s < P.ns; ++s) gq[s + 1] = gq[s] + (gp[s + 1] - gp[s] + 3) / 4;
+  std::vector<float> sv(size_t(64) * gp[P.ns]), qv(size_t(256) * gq[P.ns], 0.f);
+  (void)hipMemcpy(sv.data(), v, sizeof(float) * sv.size(), hipMemcpyDeviceToHost);
+  for (int64_t s = 0; s < P.ns; ++s)
+    for (int j = 0; j < gp[s + 1] - gp[s]; ++j)
+      for (int l = 0; l < 64; ++l)
+        qv[size_t(256) * gq[s] + 256 * (j / 4) + 4 * l + j % 4] = sv[size_t(64) * (gp[s] + j) + l];
+  int32_t* dgq = nullptr;
+  float* dqv = nullptr;
+  (void)hipMalloc(&dgq, sizeof(int32_t) * gq.size());
+  (void)hipMalloc(&dqv, sizeof(float) * std::max<size_t>(qv.size(), 1));
+  (void)hipMemcpy(dgq, gq.data(), sizeof(int32_t) * gq.size(), hipMemcpyHostToDevice);
+  (void)hipMemcpy(dqv, qv.data(), sizeof(float) * qv.size(), hipMemcpyHostToDevice);
+  int4* fl = nullptr;
+  int* sink = nullptr;
+  (void)hipMalloc(&fl, size_t(flush_bytes) + 64);
+  (void)hipMalloc(&sink, 64);
+  (void)hipMemset(fl, 1, size_t(flush_bytes));
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  const dim3 g(unsigned((P.ns + 3) / 4)), b(256);
+  auto run = [&]() {
+    if (qpb == 4)
+      hipLaunchKernelGGL((k_sdia_quad<double, 4>), g, b, 0, st, P.n, P.ns, P.gp, dgq,
+                         static_cast<const uint16_t*>(P.col), P.dict, dqv, x, y);
+    else
+      hipLaunchKernelGGL((k_sdia_quad<double, 2>), g, b, 0, st, P.n, P.ns, P.gp, dgq,
+                         static_cast<const uint16_t*>(P.col), P.dict, dqv, x, y);
+  };
+  auto flush = [&]() { hipLaunchKernelGGL(k_flush, dim3(4096), dim3(256), 0, st, fl, flush_bytes / 16, sink); };
+  float t = 0.f, tp = 0.f, tf = 0.f;
+  run();
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < 3 * reps; ++i) run();
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&t, e0, e1);
+  *ms_warm = t / (3 * reps);
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < reps; ++i) {
+    flush();
+    run();
+  }
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&tp, e0, e1);
+  (void)hipEventRecord(e0, st);
+  for (int i = 0; i < reps; ++i) flush();
+  (void)hipEventRecord(e1, st);
+  (void)hipEventSynchronize(e1);
+  (void)hipEventElapsedTime(&tf, e0, e1);
+  *ms_cold = (tp - tf) / reps;
+  const hipError_t e = hipDeviceSynchronize();
+  for (void* p : {(void*)dgq, (void*)dqv, v, (void*)fl, (void*)sink}) (void)hipFree(p);
+  P.release();
+  return e == hipSuccess ? 0 : -4;
+}
 
 int sweep_bsr_count() { return int(sizeof(kBsrCfgs) / sizeof(kBsrCfgs[0])); }
 

@@ -64,6 +64,41 @@ def main_bsr():
               flush=True)
 
 
+def main_quad(wl):
+    """SELL-DIA with quad-interleaved fp32 values (16-B value loads) against the slot-major kernel."""
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import scipy.sparse as sp
+    import torch
+
+    from bench import FLUSH_BYTES, spmv_bytes
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    A_raw, _, _, _, _ = P.workload(wl)
+    A = sp.csr_matrix(A_raw)
+    A.sort_indices()
+    A.data = A.data.astype(np.float32).astype(np.float64)
+    lib = C.CDLL(LIB)
+    rp = torch.from_numpy(A.indptr.astype(np.int32)).cuda()
+    ci = torch.from_numpy(A.indices.astype(np.int32)).cuda()
+    va = torch.from_numpy(A.data).cuda()
+    x = torch.randn(A.shape[0], dtype=torch.float64, device="cuda")
+    y = torch.empty_like(x)
+    ref = DeviceMatrix.from_scipy(A).matvec(x)
+    alg = spmv_bytes(A.shape[0], A.nnz)
+    p = lambda t: C.c_void_p(t.data_ptr())
+    for qpb in (2, 4):
+        cold, warm = C.c_double(), C.c_double()
+        y.fill_(float("nan"))
+        rc = lib.sweep_quad_run(qpb, C.c_int64(A.shape[0]), C.c_int64(A.nnz), p(rp), p(ci), p(va), p(x), p(y), 20,
+                                C.c_int64(FLUSH_BYTES), C.byref(cold), C.byref(warm))
+        print(json.dumps({"workload": wl, "layout": "quad fp32", "quads_per_batch": qpb, "rc": rc,
+                          "cold_us": cold.value * 1e3, "warm_us": warm.value * 1e3,
+                          "frac_alg_cold": alg / (cold.value * 1e-3) / 8e12, "bitexact": bool(torch.equal(y, ref))}),
+              flush=True)
+
+
 def main(wl):
     sys.path.insert(0, ROOT)
     import numpy as np
@@ -107,5 +142,7 @@ if __name__ == "__main__":
         build()
     elif "--bsr" in sys.argv:
         main_bsr()
+    elif "--quad" in sys.argv:
+        main_quad("kuhn101")
     else:
         main(sys.argv[1] if len(sys.argv) > 1 else "kuhn101")
