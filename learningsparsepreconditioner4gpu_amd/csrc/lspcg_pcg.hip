@@ -828,7 +828,7 @@ __global__ void __launch_bounds__(kThreads) k_dot_rho(int64_t n, PcgState* S, co
 // time, lanes 0..31 its accumulators.  The launch follows the reducing launch whose scalars it
 // replaces (same predicate on `done`), so the loop's order of state updates is unchanged.
 constexpr int kObMaxThreads = 16;
-constexpr int kObBlock = 1024;
+constexpr int kObBlock = 512;  // 8 waves: <= 256 VGPRs for the two register buffers
 
 // chunk c of OpenBLAS's blas_level1_thread split of [0, n) (width = ceil(rest / threads left))
 __device__ __forceinline__ void ob_chunk(int64_t n, int nch, int c, int64_t* start, int64_t* width) {
@@ -843,26 +843,73 @@ __device__ __forceinline__ void ob_chunk(int64_t n, int nch, int c, int64_t* sta
   *width = w > 0 ? w : 0;
 }
 
-// dot_compute(w, x, y) of one chunk; the result is returned to every lane of the wave
-__device__ double ob_chunk_dot(const double* __restrict__ x, const double* __restrict__ y, int64_t w) {
+// dot_compute(w, x, y) of one chunk (ob_chains, then ob_finish); the result is returned to every
+// lane of the wave.  Each accumulator's FMA chain is sequential, so the loads set the time: groups
+// of kObU 32-element steps are double-buffered in registers (group g + 1's loads in flight while group g's
+// FMAs run; prefetch addresses are clamped instead of branched, so the compiler's in-order vmcnt
+// waits never drain the other buffer), and the remainder and tail are loaded at once.  BASELINE
+// config 1 (n = 10,240): 8.7 us per launch against 15-16 with flat loads and one 8-step batch
+// (~18 GB/s: one wave's loads in flight); a third buffer measured the same, and staging tiles
+// through LDS with every wave loading (one barrier per 16-step tile) measured slower (~19 us).
+constexpr int kObU = 16;
+
+__device__ __forceinline__ void ob_load(const double* __restrict__ x, const double* __restrict__ y, int64_t i,
+                                        double (&xv)[kObU], double (&yv)[kObU]) {
+#pragma unroll
+  for (int u = 0; u < kObU; ++u) {
+    xv[u] = x[i + 32 * u];
+    yv[u] = y[i + 32 * u];
+  }
+}
+
+__device__ __forceinline__ double ob_fma(const double (&xv)[kObU], const double (&yv)[kObU], double acc) {
+#pragma unroll
+  for (int u = 0; u < kObU; ++u) acc = __builtin_fma(xv[u], yv[u], acc);
+  return acc;
+}
+
+// the 32 accumulators over the 32-aligned prefix (lanes 0..31; one wave reads everything)
+__device__ __forceinline__ double ob_chains(const double* __restrict__ x, const double* __restrict__ y, int64_t w) {
+  const int lane = threadIdx.x & 63;
+  const int64_t n32 = (w & -int64_t(16)) & ~int64_t(31);
+  double acc = 0.0;
+  if (lane < 32) {
+    constexpr int64_t GW = 32 * kObU;  // elements per group
+    const int64_t G = n32 / GW;
+    double ax[kObU], ay[kObU], bx[kObU], by[kObU];
+    int64_t g = 0;
+    if (G > 0) ob_load(x, y, lane, ax, ay);
+    for (; g + 1 < G; g += 2) {
+      ob_load(x, y, (g + 1) * GW + lane, bx, by);
+      acc = ob_fma(ax, ay, acc);
+      ob_load(x, y, (g + 2 < G ? g + 2 : g + 1) * GW + lane, ax, ay);
+      acc = ob_fma(bx, by, acc);
+    }
+    if (g < G) acc = ob_fma(ax, ay, acc);
+    // the remaining < kObU steps, loaded at once and added in order
+    const int64_t base = G * GW;
+    const int rem = int((n32 - base) >> 5);
+    if (rem > 0) {
+#pragma unroll
+      for (int u = 0; u < kObU; ++u) {
+        const int64_t i = base + (u < rem ? 32 * u : 0) + lane;
+        bx[u] = x[i];
+        by[u] = y[i];
+      }
+#pragma unroll
+      for (int u = 0; u < kObU; ++u)
+        if (u < rem) acc = __builtin_fma(bx[u], by[u], acc);
+    }
+  }
+  return acc;
+}
+
+// fold, 16-element step, lane tree and sequential tail of one chunk from its accumulators
+__device__ __forceinline__ double ob_finish(const double* __restrict__ x, const double* __restrict__ y, int64_t w,
+                                            double acc) {
   const int lane = threadIdx.x & 63;
   const int64_t n1 = w & -int64_t(16);
   const int64_t n32 = n1 & ~int64_t(31);
-  double acc = 0.0;
-  if (lane < 32) {
-    int64_t i = lane;
-    for (; i + 7 * 32 < n32; i += 8 * 32) {  // loads of 8 steps issued before the FMA chain
-      double xv[8], yv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        xv[u] = x[i + 32 * u];
-        yv[u] = y[i + 32 * u];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc = __builtin_fma(xv[u], yv[u], acc);
-    }
-    for (; i < n32; i += 32) acc = __builtin_fma(x[i], y[i], acc);
-  }
   // fold the 512-bit accumulators: lane 8v + j (j < 4) <- acc[8v + j] + acc[8v + 4 + j]
   double a = acc + __shfl_down(acc, 4, 64);
   if (n1 > n32 && lane < 32 && (lane & 7) < 4) {
@@ -872,8 +919,19 @@ __device__ double ob_chunk_dot(const double* __restrict__ x, const double* __res
   const int j = lane & 3;
   const double s = ((__shfl(a, j, 64) + __shfl(a, 8 + j, 64)) + __shfl(a, 16 + j, 64)) + __shfl(a, 24 + j, 64);
   double dot = (__shfl(s, 0, 64) + __shfl(s, 2, 64)) + (__shfl(s, 1, 64) + __shfl(s, 3, 64));
-  for (int64_t i = n1; i < w; ++i) dot = __builtin_fma(y[i], x[i], dot);
+  // sequential tail of < 16 elements, loaded at once
+  const int nt = int(w - n1);
+  double tx = 0.0, ty = 0.0;
+  if (lane < nt) {
+    tx = x[n1 + lane];
+    ty = y[n1 + lane];
+  }
+  for (int t = 0; t < nt; ++t) dot = __builtin_fma(__shfl(ty, t, 64), __shfl(tx, t, 64), dot);
   return dot;
+}
+
+__device__ __forceinline__ double ob_chunk_dot(const double* __restrict__ x, const double* __restrict__ y, int64_t w) {
+  return ob_finish(x, y, w, ob_chains(x, y, w));
 }
 
 enum ObWhich { kObInit = 0, kObZ = 1, kObQ = 2, kObR = 3, kObRho = 4, kObRR = 5 };
@@ -891,15 +949,17 @@ __global__ void __launch_bounds__(kObBlock) k_dot_openblas(int64_t n, int nch, i
                                                            const double* x2, const double* y2) {
   __shared__ double part[3][kObMaxThreads];
   if (WHICH != kObInit && S->done) return;
-  const double* xs[3] = {x0, x1, x2};
-  const double* ys[3] = {y0, y1, y2};
   const int ch = (n > 10000 && nch > 1) ? nch : 1;
   const int nw = blockDim.x >> 6;
   for (int item = threadIdx.x >> 6; item < nd * ch; item += nw) {
     const int j = item / ch, c = item % ch;
     int64_t s = 0, w = n;
     if (ch > 1) ob_chunk(n, ch, c, &s, &w);
-    const double v = ob_chunk_dot(xs[j] + s, ys[j] + s, w);
+    // selects, not an array of pointers: the loads stay global_load (a flat load's lgkmcnt forces
+    // waits on ALL outstanding loads, which would serialise the two register buffers)
+    const double* xj = j == 0 ? x0 : j == 1 ? x1 : x2;
+    const double* yj = j == 0 ? y0 : j == 1 ? y1 : y2;
+    const double v = ob_chunk_dot(xj + s, yj + s, w);
     if ((threadIdx.x & 63) == 0) part[j][c] = v;
   }
   __syncthreads();

@@ -61,3 +61,29 @@ def test_random_spd_pcg_parity(gpu_ctx, seed, mode, monkeypatch):
     assert it == it_o, (n, seed, it, it_o)
     np.testing.assert_allclose(h, h_o, rtol=1e-12, atol=0)
     assert np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
+
+
+OB_SIZES = [37, 1000, 5000, 10001, 16417, 33000, 70000]
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+@pytest.mark.parametrize("n", OB_SIZES)
+def test_random_spd_openblas_order_bitexact(gpu_ctx, n, threads):
+    """Parity mode (dot_order="openblas") on random systems: k_dot_openblas's chains, register
+    double buffers (even / odd group counts, partial 16-element step, sequential tail) and the
+    OpenBLAS thread split for n > 10,000 against oracle/openblas_ddot.c: count, every ‖r_k‖ and x
+    bit for bit."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    rng = np.random.default_rng(7 * n + threads)
+    A = _random_spd(n, n + threads)
+    L = _cases.spai_like(A, seed=n)
+    b = A @ rng.uniform(-1.0, 1.0, size=n)
+    it_o, x_o, h_o = O.pcg(A, b, O.spai_operator(L, 3e-3), rtol=1e-8, max_iter=300, dot=f"blas{threads}")
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", dot_order="openblas",
+                                        dot_threads=threads)
+    x = np.zeros(n)
+    it, _, _, h = s(b.copy(), x, 1e-8, 300, ext_spai=(L, 3e-3), return_history=True)
+    assert it == it_o, (n, threads, it, it_o)
+    assert np.array_equal(np.asarray(h[:it]), np.asarray(h_o[:it])), (n, threads)
+    assert np.array_equal(x, x_o), (n, threads, float(np.abs(x - x_o).max()))

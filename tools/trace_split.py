@@ -55,6 +55,27 @@ def main(path):
         d = [x for x in d if x >= m / 3]
         out[k] = {"grid": g, "n": len(d), "avg": avg(d), "median": med(d)}
     res["pcg_loop_kernels_us"] = out
+    # the bench system's GNN forwards (largest grid of each GNN kernel): per-kernel average and the
+    # forward's kernel sum (num_mp_layers - 1 plain layers + the first layer + decoder + node encoder)
+    gnn = {"k_encode<false>": r"k_encode<false>", "k_mp_layer<0>": r"k_mp_layer<0>",
+           "k_mp_layer<S1E>": r"k_mp_layer<[123]>", "k_edge_dec": r"k_edge_dec<"}
+    gk = {}
+    for r in rows:
+        for k, pat in gnn.items():
+            if re.search(pat, r["Kernel_Name"]):
+                gk.setdefault(k, []).append((grid(r), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3))
+    g_out = {}
+    for k, v in gk.items():
+        g = max(x[0] for x in v)
+        d = [x[1] for x in v if x[0] == g]
+        g_out[k] = {"grid": g, "n": len(d), "avg": avg(d), "median": med(d), "min": min(d)}
+    if "k_mp_layer<0>" in g_out and "k_mp_layer<S1E>" in g_out:
+        per_fwd = g_out["k_mp_layer<0>"]["n"] // max(1, g_out["k_mp_layer<S1E>"]["n"])
+        fwd = per_fwd * g_out["k_mp_layer<0>"]["avg"] + g_out["k_mp_layer<S1E>"]["avg"] + \
+            g_out.get("k_edge_dec", {}).get("avg", 0.0) + g_out.get("k_encode<false>", {}).get("avg", 0.0)
+        g_out["forward_kernel_sum_us"] = fwd
+        g_out["plain_layers_per_forward"] = per_fwd
+    res["gnn_forward_us"] = g_out
     print(json.dumps(res, indent=1))
 
 
