@@ -17,6 +17,11 @@ namespace lspcg {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
+std::mutex& submit_mutex() {
+  static std::mutex mu;
+  return mu;
+}
+
 static size_t dtype_size(int dtype) { return dtype == LSPCG_F32 ? 4 : 8; }
 
 int mat_alloc_entries(lspcg_mat* m, int64_t nnzb) {

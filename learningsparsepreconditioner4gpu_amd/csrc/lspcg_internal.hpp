@@ -12,6 +12,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <mutex>
 #include <string>
 
 #include "../../include/lspcg.h"
@@ -40,6 +41,19 @@ void set_error(const std::string& msg);
       return (code);                   \
     }                                  \
   } while (0)
+
+// ---------------------------------------------------------------------------
+// Submission lock.  Independent solves may run on several host threads at once
+// (linalg.solve_many); each solver owns its stream, but with GPU_MAX_HW_QUEUES = 4 the
+// streams share hardware queues.  Every solve enqueues (launches, graph captures and
+// launches, async copies, event records) under this one process-wide lock and releases it
+// around each host wait, so no two threads of this library write packets into a queue at
+// the same time; the GPU still runs the solves concurrently.  Round 4 found a SIGSEGV in
+// the rocprofv3 kernel-trace packet interceptor (rocprofiler-sdk reading past the end of
+// the HSA intercept queue's ring, called from hipGraphLaunch) that fired only while four
+// threads submitted concurrently ("Concurrent solves").
+// ---------------------------------------------------------------------------
+std::mutex& submit_mutex();
 
 // ---------------------------------------------------------------------------
 // Launch geometry

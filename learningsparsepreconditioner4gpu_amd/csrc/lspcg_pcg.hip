@@ -1705,6 +1705,15 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     dhist = s->dhist;
   }
 
+  // every enqueue below runs under the process-wide submission lock, released around each host
+  // wait (lspcg_internal.hpp: concurrent solves from several host threads)
+  std::unique_lock<std::mutex> sub(submit_mutex());
+  auto wait = [&sub](hipEvent_t e) {
+    sub.unlock();
+    const hipError_t r = hipEventSynchronize(e);
+    sub.lock();
+    return r;
+  };
   LSPCG_HIP(hipEventRecord(s->ev_in, s->ctx->stream));
   LSPCG_HIP(hipStreamWaitEvent(st, s->ev_in, 0));
   LSPCG_HIP(hipEventRecord(s->ev_t0, st));
@@ -1755,7 +1764,7 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     rc = s->dtype == LSPCG_F64 ? launch_small<double>(s, st) : launch_small<float>(s, st);
     if (!rc) rc = post();
     if (rc) return rc;
-    LSPCG_HIP(hipEventSynchronize(evp[head]));
+    LSPCG_HIP(wait(evp[head]));
     cur = *hs[head];
   } else {
     rc = post();
@@ -1766,7 +1775,7 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   double last_rr = -1.0;
   int chunk = std::min(4, max_chunk);
   for (; !small;) {
-    LSPCG_HIP(hipEventSynchronize(evp[head]));
+    LSPCG_HIP(wait(evp[head]));
     cur = *hs[head];
     const int64_t inflight = queued[head];
     head ^= 1;
@@ -1807,7 +1816,7 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   LSPCG_HIP(hipEventRecord(s->ev_t1, st));
   LSPCG_HIP(hipEventRecord(s->ev_out, st));
   LSPCG_HIP(hipStreamWaitEvent(s->ctx->stream, s->ev_out, 0));
-  LSPCG_HIP(hipEventSynchronize(s->ev_t1));
+  LSPCG_HIP(wait(s->ev_t1));
   if (s->precond == LSPCG_PRECOND_IC) {  // a timed-out sync-free hand-off fails the solve loudly
     if (int r2 = trsv_check_timeout(s->levL, st)) return r2;
     if (int r2 = trsv_check_timeout(s->levU, st)) return r2;
@@ -2622,6 +2631,13 @@ int lspcg_batch_solve(lspcg_batch* bt, const void* const* b, void* const* x, dou
     LSPCG_HIP(hipMalloc(&bt->dhist, sizeof(double) * hoff[ns]));
     bt->dhist_cap = hoff[ns];
   }
+  std::unique_lock<std::mutex> sub(submit_mutex());  // as in lspcg_solver_solve
+  auto wait = [&sub](hipEvent_t e) {
+    sub.unlock();
+    const hipError_t r = hipEventSynchronize(e);
+    sub.lock();
+    return r;
+  };
   LSPCG_HIP(hipEventRecord(s->ev_in, bt->ctx->stream));
   LSPCG_HIP(hipStreamWaitEvent(st, s->ev_in, 0));
   LSPCG_HIP(hipEventRecord(s->ev_t0, st));
@@ -2671,7 +2687,7 @@ int lspcg_batch_solve(lspcg_batch* bt, const void* const* b, void* const* x, dou
     rc = bt->dtype == LSPCG_F64 ? launch_batch_small<double>(bt, st) : launch_batch_small<float>(bt, st);
     if (!rc) rc = post();
     if (rc) return rc;
-    LSPCG_HIP(hipEventSynchronize(evp[head]));
+    LSPCG_HIP(wait(evp[head]));
     std::copy(hs[head], hs[head] + ns, cur.begin());
   }
   if (!bt->small) {
@@ -2683,7 +2699,7 @@ int lspcg_batch_solve(lspcg_batch* bt, const void* const* b, void* const* x, dou
   std::vector<double> last_rr(ns, -1.0);
   int chunk = 4;
   for (; !bt->small;) {
-    LSPCG_HIP(hipEventSynchronize(evp[head]));
+    LSPCG_HIP(wait(evp[head]));
     std::copy(hs[head], hs[head] + ns, cur.begin());
     const int64_t inflight = queued[head];
     head ^= 1;
@@ -2741,7 +2757,7 @@ int lspcg_batch_solve(lspcg_batch* bt, const void* const* b, void* const* x, dou
   LSPCG_HIP(hipEventRecord(s->ev_t1, st));
   LSPCG_HIP(hipEventRecord(s->ev_out, st));
   LSPCG_HIP(hipStreamWaitEvent(bt->ctx->stream, s->ev_out, 0));
-  LSPCG_HIP(hipEventSynchronize(s->ev_t1));
+  LSPCG_HIP(wait(s->ev_t1));
   float ms = 0.f;
   LSPCG_HIP(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1));
   if (t_solve_ms) *t_solve_ms = ms;

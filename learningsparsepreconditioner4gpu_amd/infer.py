@@ -4,12 +4,18 @@ Mirrors ``/root/reference/infer.py``: warm-up of the GNN (:270-275), per sample 
 preconditioner time averaged over ``repeat`` inference steps (:288-293), rhs = mask /
 random / neighbour (:297-307), the Neural PCG row (:322-331) and the two CSVs with the
 reference schema (:372-384: ``Key, Total Time (ms), Solve Time (ms), Precond Time (ms),
-#Iteration`` and the per-sample ``all_*`` file with ``Matrix Size``).  Differences: the
-PCG runs on the MI355X (key ``Neural+HIP``); the pymathprim baseline rows (:310-321) are the
-``PCG-{none,diagonal,ainv,ic}-cuda`` rows of this framework's own GPU baselines (no ``-cpu``
-rows); ``Precond Time`` is the GNN time (the reference overwrites it with the last
-baseline's setup time).  Samples are sharded one-per-GPU under torchrun
-(``distributed.run_sharded``) with a single all-gather at the end.
+#Iteration`` and the per-sample ``all_*`` file with ``Matrix Size``), with the reference's row
+keys: the GPU PCG row is ``Neural+CUDA`` (:331; the reference's consumers key on it,
+misc/plot_bars.py:54-55, misc/tab_to_latex.py:79-126; ``--hip-key`` writes ``Neural+HIP``
+instead) and the GPU baselines are ``PCG-{none,diagonal,ainv,ic}-cuda`` (:310-321).  The host
+rows ``Neural`` (:330) and ``PCG-{none,diagonal}-cpu`` come with ``--cpu-rows`` from the
+reference's own scipy restatement (cpu_rows.py; pymathprim's CPU backend is absent, and so
+are ``PCG-{ainv,ic}-cpu``).  Differences kept on purpose: ``Neural+CUDA`` carries the GPU
+solve's own count (the reference copies the CPU run's, :330-331) and ``Precond Time`` is the
+GNN time (the reference overwrites it with the last baseline's setup time).
+``--dot-order openblas --dot-threads T`` runs every GPU row in parity mode (the reference's
+recorded scipy trajectories, T OpenBLAS threads).  Samples are sharded one-per-GPU under
+torchrun (``distributed.run_sharded``) with a single all-gather at the end.
 
     python -m learningsparsepreconditioner4gpu_amd.infer --dataset heat_batch8 --rtol 1e-8
     torchrun --nproc-per-node 8 -m learningsparsepreconditioner4gpu_amd.infer --dataset heat_batch8
@@ -146,7 +152,8 @@ def rhs_for(rhs: str, mask: np.ndarray, sample: Optional[GraphSample] = None) ->
 
 
 def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: float = 1e-6, repeat: int = 1,
-        rhs: str = "mask", warmup: int = 20, concurrency: int = 1, batch: int = 1) -> List[SolveRecord]:
+        rhs: str = "mask", warmup: int = 20, concurrency: int = 1, batch: int = 1, dot_order: str = "compensated",
+        dot_threads: int = 1) -> List[SolveRecord]:
     """The ``Neural+CUDA`` row of infer.py:278-331 (GNN -> L, A; ext_spai PCG).  ``concurrency``
     > 1 keeps that many solves of this rank in flight at once (run_sharded_concurrent): the same
     iterates and counts, a higher batch throughput on the reference's mid-size systems.  ``batch``
@@ -154,7 +161,10 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
     many (run_sharded_batched, validate.get_pcg_iter_time_batch) after ONE GNN forward over the
     window's graphs (workspace.inference_step_batch): the same L, counts and iterates, every launch
     covering the whole window; a record's t_prec / t_solve are its shares of the window's forward
-    / device solve time."""
+    / device solve time.  ``dot_order`` / ``dot_threads``: the loop's dot order (``"openblas"`` =
+    parity mode; not with ``batch`` > 1, whose lockstep schedule has the compensated order only)."""
+    if batch > 1 and dot_order != "compensated":
+        raise ValueError("batch > 1 runs the compensated dot order only; use batch=1 for dot_order='openblas'")
     pcg = get_pcg_scaled_iter_time if isinstance(ws, ScaledInferenceWorkspace) else get_pcg_iter_time
     dev = torch.device("cuda", torch.cuda.current_device())
     warmed = set()
@@ -178,7 +188,8 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
     def finish(job) -> SolveRecord:
         i, A, L, r, prec = job
         info = {}
-        it, _, sol = pcg(A, r, L, ws.epsilon, rtol=rtol, repeat=repeat, info=info)
+        it, _, sol = pcg(A, r, L, ws.epsilon, rtol=rtol, repeat=repeat, info=info, dot_order=dot_order,
+                         dot_threads=dot_threads)
         # the true ‖b − A x‖/‖b‖ of the solution (one device SpMV) and the solver's own verdict
         return SolveRecord(index=i, iters=it, rel_res=info["rel_res"], t_prec=prec, t_solve=sol, n=A.n, nnz=A.nnz,
                            converged=info["converged"])
@@ -216,7 +227,8 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
 
 
 def run_baseline(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, method: str, rtol: float = 1e-6,
-                 repeat: int = 1, rhs: str = "mask") -> List[SolveRecord]:
+                 repeat: int = 1, rhs: str = "mask", dot_order: str = "compensated",
+                 dot_threads: int = 1) -> List[SolveRecord]:
     """The ``PCG-{method}-cuda`` rows (infer.py:310-321: get_cg_iter_time with method none /
     diagonal / ainv / ic on the same A and rhs).  A non-converged solve raises RuntimeError in
     the reference (caught at :363); here its row is NaN and left out of the statistics."""
@@ -228,7 +240,8 @@ def run_baseline(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, m
         r = rhs_for(rhs, s.mask.cpu().numpy(), s)
         info = {}
         try:
-            it, prec, sol = get_cg_iter_time(A, r, rtol=rtol, repeat=repeat, method=method, info=info)
+            it, prec, sol = get_cg_iter_time(A, r, rtol=rtol, repeat=repeat, method=method, info=info,
+                                             dot_order=dot_order, dot_threads=dot_threads)
         except RuntimeError:
             return SolveRecord(index=i, iters=float("nan"), rel_res=float("nan"), t_prec=float("nan"),
                                t_solve=float("nan"), n=A.n, nnz=A.nnz, converged=False)
@@ -237,6 +250,53 @@ def run_baseline(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, m
 
     weights = [float(s.edge_index.shape[1]) for s in samples]
     return run_sharded(len(samples), weights, solve)
+
+
+def run_cpu_rows(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: float = 1e-6, repeat: int = 1,
+                 rhs: str = "mask", methods: Sequence[str] = ("none", "diagonal"),
+                 threads: Optional[int] = None) -> Dict[str, List[SolveRecord]]:
+    """The reference's host rows (infer.py:310-330 with device="cpu"): ``Neural`` (ext_spai or its
+    scaled variant on the host copies of A and of the GNN's L) and ``PCG-{method}-cpu`` for
+    ``methods`` (none / diagonal), each from cpu_rows (the reference's scipy restatement; its
+    pymathprim CPU backend is absent).  The GNN and the assembly run on the GPU as for the GPU
+    rows; ``Precond Time`` is the GNN time for ``Neural`` and 0 for the baselines (no setup).
+    A baseline that reaches max_iter is left out, as the reference's RuntimeError does (:363)."""
+    from . import cpu_rows
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    scaled = isinstance(ws, ScaledInferenceWorkspace)
+
+    def solve(i: int):
+        s = samples[i].to(dev)
+        prec = 0.0
+        for _ in range(repeat):
+            _, dt = ws.inference_step(s)
+            prec += dt
+        prec /= repeat
+        L, _ = ws.inference_step(s)
+        A = ws.system_matrix(s)
+        Ah, Lh = A.to_scipy().tocsr(), L.to_scipy().tocsr()
+        r = rhs_for(rhs, s.mask.cpu().numpy(), s)
+        it, sol = cpu_rows.neural_row(Ah, r, Lh, ws.epsilon, rtol, scaled=scaled, repeat=repeat, threads=threads)
+        recs = [SolveRecord(index=i, iters=it, rel_res=float("nan"), t_prec=prec, t_solve=sol, n=A.n, nnz=A.nnz,
+                            converged=it < A.n)]
+        for m in methods:
+            try:
+                it, sol = cpu_rows.baseline_row(Ah, r, m, rtol, repeat=repeat, threads=threads)
+                recs.append(SolveRecord(index=i, iters=it, rel_res=float("nan"), t_prec=0.0, t_solve=sol, n=A.n,
+                                        nnz=A.nnz, converged=True))
+            except RuntimeError:
+                recs.append(SolveRecord(index=i, iters=float("nan"), rel_res=float("nan"), t_prec=float("nan"),
+                                        t_solve=float("nan"), n=A.n, nnz=A.nnz, converged=False))
+        return recs
+
+    per = {}
+    for i in range(len(samples)):  # host rows: the rank-0 process's host, one sample at a time
+        per[i] = solve(i)
+    out = {"Neural": [per[i][0] for i in sorted(per)]}
+    for k, m in enumerate(methods):
+        out[f"PCG-{m}-cpu"] = [per[i][k + 1] for i in sorted(per)]
+    return out
 
 
 def main(argv=None):
@@ -265,6 +325,14 @@ def main(argv=None):
                     help="systems per lockstep batch per GPU (run_sharded_batched); 1 = one solve at a time")
     ap.add_argument("--baselines", default="none,diagonal,ainv,ic",
                     help="comma list of PCG-{method}-cuda rows (infer.py:310-321); '' for none")
+    ap.add_argument("--dot-order", default="compensated", choices=["compensated", "openblas"],
+                    help="dot order of every GPU row: openblas = parity mode (the reference's scipy trajectories)")
+    ap.add_argument("--dot-threads", type=int, default=1,
+                    help="OpenBLAS threads of the parity order (numpy splits dots of n > 10,000 over them)")
+    ap.add_argument("--hip-key", action="store_true", help="key the GPU PCG row Neural+HIP instead of Neural+CUDA")
+    ap.add_argument("--cpu-rows", action="store_true",
+                    help="also write the reference's host rows Neural and PCG-{none,diagonal}-cpu (scipy restatement)")
+    ap.add_argument("--cpu-threads", type=int, default=None, help="BLAS threads of the host rows (default: process)")
     args = ap.parse_args(argv)
 
     import torch.distributed as dist
@@ -291,11 +359,16 @@ def main(argv=None):
         ws = cls(node_features=s0.x.shape[1], edge_features=s0.edge_attr.shape[1], block_size=s0.block_size,
                  epsilon=args.epsilon, seed=0)
     rows = {}
+    dots = dict(dot_order=args.dot_order, dot_threads=args.dot_threads)
     for m in [b for b in args.baselines.split(",") if b]:
-        rows[f"PCG-{m}-cuda"] = run_baseline(samples, ws, m, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs)
-    rows["Neural+HIP"] = run(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, warmup=args.warmup,
-                             concurrency=args.concurrency, batch=args.batch)
-    recs = rows["Neural+HIP"]
+        rows[f"PCG-{m}-cuda"] = run_baseline(samples, ws, m, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, **dots)
+    key = "Neural+HIP" if args.hip_key else "Neural+CUDA"
+    rows[key] = run(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, warmup=args.warmup,
+                    concurrency=args.concurrency, batch=args.batch, **dots)
+    recs = rows[key]
+    if args.cpu_rows and (not dist.is_initialized() or dist.get_rank() == 0):
+        rows.update(run_cpu_rows(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs,
+                                 threads=args.cpu_threads))
     if not dist.is_initialized() or dist.get_rank() == 0:
         stats = Timestat()
         for key, rs in rows.items():

@@ -10,6 +10,10 @@ Same names, arguments, return values and error behaviour as the reference:
 * ``get_pcg_scaled_iter_time``   -- validate.py:124-160 (ext_spai_scaled)
 * ``get_pcg_iter_time_batch``    -- not in the reference: ``get_pcg_iter_time`` over a window
   of independent systems solved as one lockstep batch
+* ``get_pcg_iter_time_scipy`` / ``get_pcg_diagonal_iter_time_scipy`` /
+  ``get_pcg_scaled_iter_time_scipy`` / ``get_cg_iter_time_scipy`` -- validate.py:163-341, the
+  reference's host (scipy) restatements, re-exported from ``cpu_rows`` (host comparison rows
+  only; never called by the functions above)
 
 Matrices may be scipy CSR (uploaded) or :class:`DeviceMatrix` (already in HBM).
 
@@ -31,6 +35,8 @@ import scipy.sparse as sp
 import torch
 
 from . import _lib
+from .cpu_rows import (get_cg_iter_time_scipy, get_pcg_diagonal_iter_time_scipy,  # noqa: F401
+                       get_pcg_iter_time_scipy, get_pcg_scaled_iter_time_scipy)
 from .linalg import BatchedConjugateGradient, PreconditionedConjugateGradient
 from .sparse import Context, DeviceMatrix, assemble, dot, lspcg_dtype
 
@@ -71,9 +77,12 @@ def _prepare(A, dtype, block_size=1) -> DeviceMatrix:
 
 
 def get_cg_iter_time(A, gt, rtol=1e-6, max_iter=0, dtype=np.float64, repeat=1, device="cuda",
-                     method="ainv", info: Optional[dict] = None) -> Tuple[float, float, float]:
+                     method="ainv", info: Optional[dict] = None, dot_order: str = "compensated",
+                     dot_threads: int = 1) -> Tuple[float, float, float]:
     """validate.py:54-86: method none / diagonal / ic (IC(0), level-scheduled triangular solves) /
-    ainv (AINV(0) as L Lᵀ); the prec time is the device setup of the preconditioner."""
+    ainv (AINV(0) as L Lᵀ); the prec time is the device setup of the preconditioner.
+    ``dot_order`` / ``dot_threads`` (not in the reference's signature): the loop's dot order,
+    ``"openblas"`` = parity mode (linalg.PreconditionedConjugateGradient.set_dot_order)."""
     Ad = _prepare(A, dtype)
     rows = Ad.n
     max_iter = max_iter if max_iter > 0 else rows
@@ -81,7 +90,8 @@ def get_cg_iter_time(A, gt, rtol=1e-6, max_iter=0, dtype=np.float64, repeat=1, d
     iter_cnt, time_prec, time_elp = 0, 0.0, 0.0
     x = torch.zeros_like(b)
     for _ in range(repeat):
-        solver = PreconditionedConjugateGradient(Ad, device=device, preconditioner=method, dtype=dtype)
+        solver = PreconditionedConjugateGradient(Ad, device=device, preconditioner=method, dtype=dtype,
+                                                 dot_order=dot_order, dot_threads=dot_threads)
         xs = x.clone()
         this_iter, this_prec, this_solve = solver(b.clone(), xs, rtol, max_iter)
         iter_cnt += this_iter
@@ -102,7 +112,8 @@ def relative_residual(A: DeviceMatrix, x: torch.Tensor, b: torch.Tensor) -> floa
     return math.sqrt(dot(r, r) / bb) if bb > 0 else math.sqrt(dot(r, r))
 
 
-def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info=None):
+def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info=None,
+                 dot_order="compensated", dot_threads=1):
     Ad = _prepare(A, dtype)
     Ld = spai if isinstance(spai, DeviceMatrix) else _prepare(spai, dtype)
     rows = Ad.n
@@ -112,7 +123,8 @@ def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, de
     iter_cnt, time_elp, time_prec = 0, 0.0, 0.0
     x = torch.zeros_like(b)
     for _ in range(repeat):
-        solver = PreconditionedConjugateGradient(Ad, device=device, preconditioner=method, dtype=dtype)
+        solver = PreconditionedConjugateGradient(Ad, device=device, preconditioner=method, dtype=dtype,
+                                                 dot_order=dot_order, dot_threads=dot_threads)
         xs = x.clone()
         this_iter, this_prec, this_solve = solver(b.clone(), xs, rtol, max_iter, ext_spai=(Ld, epsilon))
         iter_cnt += this_iter
@@ -125,10 +137,14 @@ def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, de
 
 
 def get_pcg_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat=1, dtype=np.float64,
-                      device="cuda", info: Optional[dict] = None) -> Tuple[float, float, float]:
+                      device="cuda", info: Optional[dict] = None, dot_order: str = "compensated",
+                      dot_threads: int = 1) -> Tuple[float, float, float]:
     """validate.py:89-121: ext_spai PCG, M⁻¹ = L Lᵀ + εI.  ``info`` (optional dict, not in the
-    reference's signature) receives the last solve's x, true relative residual and convergence."""
-    return _pcg_generic("ext_spai", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info)
+    reference's signature) receives the last solve's x, true relative residual and convergence;
+    ``dot_order`` / ``dot_threads`` (not in the reference's signature) select the loop's dot order
+    (``"openblas"`` = parity mode: the reference's recorded scipy trajectories bit for bit)."""
+    return _pcg_generic("ext_spai", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info,
+                        dot_order, dot_threads)
 
 
 def get_pcg_iter_time_batch(As, gts, spais, epsilon: float, rtol=1e-6, max_iter=0, dtype=np.float64,
@@ -172,6 +188,8 @@ def get_pcg_iter_time_batch(As, gts, spais, epsilon: float, rtol=1e-6, max_iter=
 
 
 def get_pcg_scaled_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat=1, dtype=np.float64,
-                             device="cuda", info: Optional[dict] = None) -> Tuple[float, float, float]:
+                             device="cuda", info: Optional[dict] = None, dot_order: str = "compensated",
+                             dot_threads: int = 1) -> Tuple[float, float, float]:
     """validate.py:124-160: ext_spai_scaled PCG, M⁻¹ r = L((Lᵀr)/d) + εr/d, d = diag(A)."""
-    return _pcg_generic("ext_spai_scaled", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info)
+    return _pcg_generic("ext_spai_scaled", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info,
+                        dot_order, dot_threads)

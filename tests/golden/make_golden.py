@@ -31,6 +31,16 @@ Fixtures (inputs and the reference's outputs, data only):
                       the BASELINE configs' layouts (F_in 1 / 2 / 5 / 9), with its state_dict
   graph_spmv.npz   -- the reference's GraphSpmv / AATPE / LLT on random edge lists (fp32, fp64)
   ic_traj.npz      -- the reference's get_pcg_iter_time_scipy_ichol on the oracle's IC(0) factor
+  traj_kuhn101.npz, traj_elast.npz
+                   -- the reference's get_pcg_iter_time_scipy at FULL bench size (the headline
+                      kuhn101 system, n = 1,030,301, and the C4 elasticity box, n = 315,900) with
+                      the bench's own L (the HIP GNN's output, dumped on the GPU box by
+                      tools/dump_gnn_l.py; its sha256 is stored and re-checked by the GPU tests):
+                      counts at 1 / 2 / 4 / 8 OpenBLAS threads, every ‖r_k‖ and sha256(x) + a
+                      sample of x at 1 and 8 threads
+  infer_folder_free.npz
+                   -- the reference's infer rows (PCG-none / PCG-diagonal / Neural counts, mask
+                      rhs, rtol 1e-8) on folder_free, its FolderDataset samples and its seeded GNN
   ../../learningsparsepreconditioner4gpu_amd/meshes/bunny_grid.npz
                    -- voxelised interior of data/objs/bunny_low_res.obj (winding numbers of a
                       regular grid's vertices), input of the C3 heat stand-in (problems.heat_bunny);
@@ -45,6 +55,8 @@ Fixtures (inputs and the reference's outputs, data only):
     python tests/golden/make_golden.py traj       # pcg_traj.npz only
     python tests/golden/make_golden.py gnn        # gnn_forward.npz + graph_spmv.npz only
     python tests/golden/make_golden.py ichol      # ic_traj.npz only
+    python tests/golden/make_golden.py infer      # infer_folder_free.npz only
+    python tests/golden/make_golden.py headline kuhn101 gpurun_out/.../kuhn101.npy   # traj_kuhn101.npz
     python tests/golden/make_golden.py bunny      # bunny_grid.npz only
 """
 from __future__ import annotations
@@ -388,11 +400,134 @@ def ichol_fixtures(rval):
     np.savez_compressed(OUT / "ic_traj.npz", **out)
 
 
+def _sha(*arrs) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for a in arrs:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+HEADLINE_THREADS = (1, 2, 4, 8)
+X_STRIDE = 997  # sampled iterate entries stored beside the iterate's sha256
+
+
+def headline_fixtures(rval, workload: str, boo_path: str):
+    """traj_<workload>.npz: the reference's own ext_spai PCG on a bench workload at full size.
+
+    Inputs: the bench's system (problems.workload -> data.make_sample, pinned bit-equal to the
+    reference's make_data) and the HIP GNN's own output ``boo`` on it (tools/dump_gnn_l.py on the
+    GPU box: seeded init, the bench's forward), so the fixture's L is the bench's L.  The
+    reference then runs exactly its infer path: ``to_csr_cpu(edge_index, matrix_values, n, mask)``
+    for A (infer.py:282), ``to_csr_cpu(edge_index, boo, n, mask, float64)`` for L
+    (workspace.py:195-205), and ``get_pcg_iter_time_scipy(A, mask, L, eps, rtol=1e-8)``
+    (validate.py:163-201) through RecordingCG at 1 / 2 / 4 / 8 OpenBLAS threads.  Stored: every
+    count and true residual; for 1 and 8 threads every ‖r_k‖ and sha256(x) with every 997th entry
+    of x; sha256 of boo, A and L (the GPU test checks its inputs against them); labelled
+    ``oracle_exact_*``, the oracle's correctly-rounded-dot run.  A is not stored."""
+    import json
+
+    import threadpoolctl
+
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+    from oracle import linalg as O
+
+    meta = json.load(open(boo_path[:-4] + ".json"))
+    boo = np.load(boo_path)
+    assert boo.dtype == np.float32 and _sha(boo) == meta["sha256"], "boo file does not match its sha256"
+    A_raw, mask, feats, bs, e2n = P.workload(workload)
+    s = make_sample(A_raw, mask, node_features=feats, block_size=bs, use_edge_features_as_node_feature=e2n)
+    n = s.num_nodes * bs
+    assert boo.shape == (s.edge_index.shape[1], bs, bs), boo.shape
+    A = rval.to_csr_cpu(s.edge_index, s.matrix_values, n, s.mask)
+    L = rval.to_csr_cpu(s.edge_index, torch.from_numpy(boo), n, s.mask, dtype=np.float64)
+    gt = s.mask.numpy().reshape(-1).astype(np.float64)
+    eps, rtol = 3e-3, 1e-8
+    rec = RecordingCG()
+    rval.cg = rec
+    out = {"blas_info": np.array(blas_info()), "ref_threads": np.array(HEADLINE_THREADS),
+           "workload": np.array(workload), "n": np.array(n), "nnz_A": np.array(A.nnz), "nnz_L": np.array(L.nnz),
+           "block_size": np.array(bs), "eps": np.array(eps), "rtol": np.array(rtol),
+           "boo_sha256": np.array(meta["sha256"]), "A_sha256": np.array(_sha(A.indptr, A.indices, A.data)),
+           "L_sha256": np.array(_sha(L.indptr, L.indices, L.data)), "x_stride": np.array(X_STRIDE)}
+    b = A @ gt
+    nb = np.linalg.norm(b)
+    runs = {}
+    for th in HEADLINE_THREADS:
+        with threadpoolctl.threadpool_limits(th):
+            cnt = rval.get_pcg_iter_time_scipy(A, gt, L, eps, rtol=rtol)
+        assert cnt == rec.count and len(rec.hist) == cnt
+        runs[th] = (cnt, rec.x.copy(), np.array(rec.hist))
+        out[f"t{th}__count"] = np.array(cnt)
+        out[f"t{th}__true_res"] = np.array(np.linalg.norm(b - A @ rec.x) / nb)
+        if th in (1, 8):
+            out[f"t{th}__hist"] = np.array(rec.hist)
+            out[f"t{th}__x_sha256"] = np.array(_sha(rec.x))
+            out[f"t{th}__x_sample"] = rec.x[::X_STRIDE].copy()
+        print(workload, "threads", th, "count", cnt, "true res %.3e" % float(out[f"t{th}__true_res"]), flush=True)
+    out["ref_counts"] = np.array([runs[t][0] for t in HEADLINE_THREADS])
+    ps = O.spai_operator(L, eps)
+    for th in (1, 8):  # the oracle's OpenBLAS restatement reproduces the recorded runs bit for bit
+        it_b, x_b, h_b = O.pcg(A, b, ps, rtol=rtol, dot=f"blas{th}")
+        assert it_b == runs[th][0] and np.array_equal(x_b, runs[th][1]), (workload, th)
+        assert np.array_equal(np.asarray(h_b[:it_b]), runs[th][2]), (workload, th)
+    ex = O.pcg(A, b, ps, rtol=rtol, dot="exact")
+    out["oracle_exact_count"] = np.array(ex[0])
+    out["oracle_exact_hist"] = np.asarray(ex[2])
+    out["oracle_exact_x_sha256"] = np.array(_sha(ex[1]))
+    print(workload, "reference counts", out["ref_counts"].tolist(), "exact-dot", ex[0], flush=True)
+    np.savez_compressed(OUT / f"traj_{workload}.npz", **out)
+
+
 def _gnn_cfg():
     ff = lambda norm: {"pre_norm": norm, "hidden_channels": 16, "num_layers": 2}
     return dict(node_encoder=ff("none"), edge_encoder=ff("none"), node_decoder=ff("none"), edge_decoder=ff("none"),
                 num_mp_layers=4, node_residual=True, edge_residual=True, node_features=16, edge_features=16,
                 node_mlp=ff("layer"), edge_mlp=ff("layer"), msg_mlp=ff("layer"), msg_norm=True, aggr="add")
+
+
+def infer_fixtures(rdata, rgnn, rval):
+    """infer_folder_free.npz: the reference's infer.py rows (:278-331) on the on-disk folder_free
+    dataset, run from the reference's own modules: FolderDataset(**infer config).get(i), the seeded
+    NodeEdgeProcessing (torch.manual_seed(0), config/gnn.yaml -- what infer's
+    SimpleInferenceWorkspace(seed=0) builds), A = to_csr_cpu(edge_index, matrix_values, n, mask)
+    (:282), L = to_csr_cpu(edge_index, forward(...), n, mask) (workspace.py:195-205), r = mask
+    (:297-299), and the PCG-none / PCG-diagonal / Neural counts from get_cg_iter_time_scipy /
+    get_pcg_diagonal_iter_time_scipy / get_pcg_iter_time_scipy (the reference's CPU stand-ins,
+    validate.py:163-333) at 1 OpenBLAS thread, rtol 1e-8."""
+    import threadpoolctl
+
+    cfg = dict(is_fixed_topology=False, load_into_memory=False, block_size=1, has_shared_features=False,
+               use_node_features=True, use_matrix_as_edge_feature=True, use_mask_as_node_feature=True,
+               use_node_features_as_edge_feature=False, use_edge_features_as_node_feature="disable",
+               use_random_rhs=True, normalize_matrix="mean", prefix=str(OUT / "folder_free"))
+    ds = rdata.FolderDataset(**cfg)
+    out = {"rtol": np.array(1e-8), "eps": np.array(3e-3), "len": np.array(ds.len())}
+    for i in range(ds.len()):
+        torch.manual_seed(100 + i)
+        d = ds.get(i)
+        n = d.x.shape[0]
+        torch.manual_seed(0)
+        net = rgnn.NodeEdgeProcessing(node_in_features=d.x.shape[1], node_out_features=None,
+                                      edge_in_features=d.edge_attr.shape[1], edge_out_features=1, **_gnn_cfg())
+        net.eval()
+        with torch.no_grad():
+            boo = net(d.x, d.edge_index, d.edge_attr)[1].reshape(-1, 1, 1)
+        A = rval.to_csr_cpu(d.edge_index, d.matrix_values, n, d.mask)
+        L = rval.to_csr_cpu(d.edge_index, boo, n, d.mask, dtype=np.float64)
+        r = d.mask.numpy().reshape(-1).astype(np.float64)
+        with threadpoolctl.threadpool_limits(1):
+            out[f"{i}__none"] = np.array(rval.get_cg_iter_time_scipy(A, r, rtol=1e-8))
+            out[f"{i}__diagonal"] = np.array(rval.get_pcg_diagonal_iter_time_scipy(A, r, rtol=1e-8))
+            out[f"{i}__ext_spai"] = np.array(rval.get_pcg_iter_time_scipy(A, r, L, 3e-3, rtol=1e-8))
+        out[f"{i}__n"] = np.array(n)
+        for key in ("x", "edge_index", "edge_attr", "matrix_values", "mask"):
+            out[f"{i}__{key}"] = getattr(d, key).numpy()
+        print("infer folder_free", i, "n", n, {k: int(out[f"{i}__{k}"]) for k in ("none", "diagonal", "ext_spai")},
+              flush=True)
+    np.savez_compressed(OUT / "infer_folder_free.npz", **out)
 
 
 def gnn_forward_fixtures(rdata, rgnn):
@@ -525,6 +660,20 @@ def main():
 
         sys.path.insert(0, str(ROOT))
         traj_fixtures(rval)
+        return
+    if sys.argv[1:2] == ["headline"]:  # headline <workload> <boo .npy from tools/dump_gnn_l.py>
+        from neural_cg.utils import validate as rval
+
+        sys.path.insert(0, str(ROOT))
+        headline_fixtures(rval, sys.argv[2], sys.argv[3])
+        return
+    if sys.argv[1:] == ["infer"]:
+        from neural_cg import data as rdata
+        from neural_cg.nn import gnns as rgnn
+        from neural_cg.utils import validate as rval
+
+        sys.path.insert(0, str(ROOT))
+        infer_fixtures(rdata, rgnn, rval)
         return
     if sys.argv[1:] == ["ichol"]:
         from neural_cg.utils import validate as rval
@@ -696,6 +845,7 @@ def main():
     gnn_forward_fixtures(rdata, rgnn)
     graph_spmv_fixtures(rbl)
     ichol_fixtures(rval)
+    infer_fixtures(rdata, rgnn, rval)
 
     for f in sorted(OUT.glob("*.npz")):
         print(f.name, f.stat().st_size)

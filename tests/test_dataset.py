@@ -74,3 +74,18 @@ def test_edge_to_node_aggregation(reduce):
         if len(sel):
             exp[v] = {"sum": sel.sum(0), "mean": sel.mean(0), "max": sel.max(0), "min": sel.min(0)}[reduce]
     np.testing.assert_allclose(d.x.numpy(), exp, rtol=1e-6, atol=1e-7)
+
+
+def test_infer_folder_samples_equal_reference_infer_inputs():
+    """infer.folder_dataset (the --folder input of python -m ...infer) yields the GNN / solver inputs
+    the reference's own FolderDataset.get gave when infer_folder_free.npz was recorded."""
+    from learningsparsepreconditioner4gpu_amd.infer import folder_dataset
+
+    z = np.load(GOLDEN / "infer_folder_free.npz")
+    samples = folder_dataset(str(GOLDEN / "folder_free"))
+    assert len(samples) == int(z["len"])
+    for i, s in enumerate(samples):
+        for key in ("x", "edge_index", "edge_attr", "matrix_values", "mask"):
+            got = getattr(s, key).numpy()
+            ref = z[f"{i}__{key}"]
+            assert got.shape == ref.shape and np.array_equal(got, ref), (i, key)

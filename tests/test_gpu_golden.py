@@ -94,7 +94,7 @@ def test_infer_driver_end_to_end(gpu_ctx, tmp_path):
         rel_o = np.linalg.norm(b - A @ x_o) / np.linalg.norm(b)
         assert r.iters == it_o
         assert r.rel_res <= 1.05e-8 and abs(r.rel_res - rel_o) <= 1e-12, (r.rel_res, rel_o)
-        st.put("Neural+HIP", r.t_solve, r.t_prec, r.iters, r.n)
+        st.put("Neural+CUDA", r.t_solve, r.t_prec, r.iters, r.n)
     df = st.timestat_to_dataframe()
     assert list(df.columns) == ["Key", "Total Time (ms)", "Solve Time (ms)", "Precond Time (ms)", "#Iteration"]
 
@@ -157,9 +157,33 @@ def test_folder_dataset_through_hot_path(gpu_ctx, rhs):
         assert rec.iters == it_o, (rec.index, rec.iters, it_o)  # (tiny systems may need n iterations)
 
 
+def test_infer_main_parity_mode_reference_counts(gpu_ctx, tmp_path):
+    """python -m ...infer --dot-order openblas on folder_free: every row's count equals the count the
+    REFERENCE's infer rows recorded on the same samples (infer_folder_free.npz: its FolderDataset,
+    seeded GNN, to_csr_cpu and scipy PCG): PCG-none-cuda / PCG-diagonal-cuda and Neural+CUDA per
+    sample and as the CSV's #Iteration mean.  (The GNN-L of Neural+CUDA is the HIP forward, within
+    1e-7 of the reference's: on these 30- / 35-row systems both take the same count.)"""
+    import pandas as pd
+
+    from learningsparsepreconditioner4gpu_amd.infer import main
+
+    z = np.load(GOLDEN / "infer_folder_free.npz")
+    k = int(z["len"])
+    recs = main(["--folder", str(GOLDEN / "folder_free"), "--rtol", "1e-8", "--warmup", "1", "--out-dir",
+                 str(tmp_path), "--dot-order", "openblas", "--dot-threads", "1", "--baselines", "none,diagonal"])
+    assert [r.iters for r in sorted(recs, key=lambda r: r.index)] == [int(z[f"{i}__ext_spai"]) for i in range(k)]
+    df = pd.read_csv(tmp_path / "infer_folder_free_8.csv").set_index("Key")
+    for key, col in (("Neural+CUDA", "ext_spai"), ("PCG-none-cuda", "none"), ("PCG-diagonal-cuda", "diagonal")):
+        assert df.loc[key, "#Iteration"] == pytest.approx(np.mean([int(z[f"{i}__{col}"]) for i in range(k)]), abs=1e-9)
+    alls = pd.read_csv(tmp_path / "all_infer_folder_free_8.csv")
+    for key, col in (("PCG-none-cuda", "none"), ("PCG-diagonal-cuda", "diagonal")):
+        got = alls[alls["Key"] == key]["#Iteration"].tolist()
+        assert got == [float(z[f"{i}__{col}"]) for i in range(k)], key
+
+
 @pytest.mark.parametrize("batch", ["1", "4"])
 def test_infer_main_writes_baseline_rows(gpu_ctx, tmp_path, batch):
-    """infer CLI on an on-disk dataset: Neural+HIP and PCG-{none,diagonal,ainv,ic}-cuda rows (the
+    """infer CLI on an on-disk dataset: Neural+CUDA and PCG-{none,diagonal,ainv,ic}-cuda rows (the
     Neural rows solved one by one or, --batch 4, as one lockstep batch)."""
     import pandas as pd
 
@@ -170,7 +194,7 @@ def test_infer_main_writes_baseline_rows(gpu_ctx, tmp_path, batch):
     assert len(recs) == 4 and all(r.iters == r.iters for r in recs)
     df = pd.read_csv(tmp_path / "infer_folder_free_8.csv")
     keys = set(df["Key"])  # (a row whose every solve hit max_iter = n is left out, like the reference)
-    assert {"Neural+HIP", "PCG-ainv-cuda", "PCG-ic-cuda"} <= keys
-    assert keys <= {"Neural+HIP", "PCG-none-cuda", "PCG-diagonal-cuda", "PCG-ainv-cuda", "PCG-ic-cuda"}
+    assert {"Neural+CUDA", "PCG-ainv-cuda", "PCG-ic-cuda"} <= keys
+    assert keys <= {"Neural+CUDA", "PCG-none-cuda", "PCG-diagonal-cuda", "PCG-ainv-cuda", "PCG-ic-cuda"}
     alls = pd.read_csv(tmp_path / "all_infer_folder_free_8.csv")
     assert list(alls.columns) == ["Key", "Solve Time (ms)", "Precond Time (ms)", "#Iteration", "Matrix Size"]

@@ -285,3 +285,45 @@ def test_solve_many_matches_one_by_one(gpu_ctx):
     for (it, conv, x), (it2, conv2, _), (_, _, x2) in zip(ref, out, jobs):
         assert (it, conv) == (it2, conv2)
         assert torch.equal(x, x2)
+
+
+def test_solve_many_fresh_solvers_concurrent_capture(gpu_ctx):
+    """Round-4 regression (DESIGN.md §6 "Concurrent solves"): 8 FRESH solvers above the
+    one-workgroup bound (multi-kernel schedule, hipGraphs captured on first use) solved 4 at a
+    time, so graph capture, instantiation and launches of different solvers overlap on four host
+    threads, twice (the second pass captures the chunk lengths the first did not use).  Every
+    result equals a sequential solve on its own fresh solver, bit for bit."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient, solve_many
+
+    systems = []
+    for k in range(8):
+        if k % 2:
+            A, _m, _ = P.poisson2d_grid(56 + 8 * k, 48 + 4 * k)
+        else:
+            A = P.kuhn_laplacian(15 + 2 * k)
+        A = sp.csr_matrix(A)
+        assert A.shape[0] > 2560  # not the one-workgroup solve: graphs are captured
+        systems.append(A)
+
+    def fresh(A, precond):
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=precond)
+        if precond == "ext_spai":
+            s.set_spai(_cases.spai_like(A), 3e-3)
+        b = torch.from_numpy(A @ np.ones(A.shape[0])).cuda()
+        return s, b, torch.zeros_like(b)
+
+    precs = ["ext_spai", "diagonal", "ext_spai", "none"] * 2
+    ref = []
+    for A, pc in zip(systems, precs):
+        s, b, x = fresh(A, pc)
+        it, conv, _ = s.solve(b, x, rtol=1e-8)
+        ref.append((it, conv, x.clone()))
+    jobs = [fresh(A, pc) for A, pc in zip(systems, precs)]
+    for _pass in range(2):
+        for _, _, x in jobs:
+            x.zero_()
+        out = solve_many(jobs, rtol=1e-8, concurrency=4)
+        torch.cuda.synchronize()
+        for (it, conv, x), (it2, conv2, _), (_, _, x2) in zip(ref, out, jobs):
+            assert (it, conv) == (it2, conv2)
+            assert torch.equal(x, x2)

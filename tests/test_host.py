@@ -1,10 +1,14 @@
 """CPU: host-side logic -- generators, byte models, weight packing, sample building."""
+from pathlib import Path
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
 import torch
 
 from learningsparsepreconditioner4gpu_amd import problems as P
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
 
 
 def test_kuhn_roofline_target_sizes():
@@ -83,14 +87,72 @@ def test_timestat_csv_schema(tmp_path):
     from learningsparsepreconditioner4gpu_amd.infer import Timestat
 
     st = Timestat()
-    st.put("Neural+HIP", 0.010, 0.002, 113, 6276)
-    st.put("Neural+HIP", 0.020, 0.004, 115, 6300)
+    st.put("Neural+CUDA", 0.010, 0.002, 113, 6276)
+    st.put("Neural+CUDA", 0.020, 0.004, 115, 6300)
     df = st.timestat_to_dataframe()
     assert list(df.columns) == ["Key", "Total Time (ms)", "Solve Time (ms)", "Precond Time (ms)", "#Iteration"]
     assert df.iloc[0]["Total Time (ms)"] == 18.0 and df.iloc[0]["#Iteration"] == 114.0
     al = st.all_time_stat()
     assert list(al.columns) == ["Key", "Solve Time (ms)", "Precond Time (ms)", "#Iteration", "Matrix Size"]
     assert len(al) == 2
+
+
+# the rows misc/tab_to_latex.py:79-126 and misc/plot_bars.py:54-55 read from an infer CSV (the
+# reference's own consumers of infer.py:372-384); `read_csv_data` restates tab_to_latex.py:45-55
+TAB_TO_LATEX_KEYS = ("PCG-ic-cpu", "PCG-ainv-cpu", "PCG-diagonal-cpu", "Neural", "PCG-ic-cuda", "PCG-ainv-cuda",
+                     "PCG-diagonal-cuda", "Neural+CUDA")
+
+
+def _read_csv_data(path):
+    import csv
+
+    data = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            data[row["Key"]] = {"total": float(row["Total Time (ms)"]), "iter": float(row["#Iteration"]),
+                                "construction": float(row["Precond Time (ms)"])}
+    return data
+
+
+def test_infer_csv_reads_with_reference_consumer_keys(tmp_path):
+    """The infer CSV carries the row keys the reference's table / plot scripts key on: the GPU rows
+    (PCG-{diagonal,ic,ainv}-cuda, Neural+CUDA) from the device path, the host rows Neural and
+    PCG-diagonal-cpu from --cpu-rows (PCG-{ic,ainv}-cpu need pymathprim / ilupp, absent)."""
+    from learningsparsepreconditioner4gpu_amd import infer
+
+    assert "Neural+CUDA" in infer.__doc__ and "--hip-key" in infer.__doc__
+    st = infer.Timestat()
+    rows = {"PCG-none-cuda": 474, "PCG-diagonal-cuda": 265, "PCG-ainv-cuda": 172, "PCG-ic-cuda": 100,
+            "Neural+CUDA": 113, "Neural": 113, "PCG-none-cpu": 474, "PCG-diagonal-cpu": 265}
+    for k, it in rows.items():
+        st.put(k, 0.02, 0.001, it, 6276)
+    f = tmp_path / "infer_heat_8.csv"
+    st.timestat_to_dataframe().to_csv(f, index=False)
+    data = _read_csv_data(f)
+    gpu = [k for k in TAB_TO_LATEX_KEYS if k.endswith("cuda") or k == "Neural+CUDA"]
+    for k in gpu + ["Neural", "PCG-diagonal-cpu"]:
+        assert data[k]["iter"] == rows[k] and data[k]["total"] == 21.0 and data[k]["construction"] == 1.0
+
+
+def test_cpu_rows_restate_reference_scipy_counts():
+    """cpu_rows (the --cpu-rows host rows) = the reference's scipy restatements: the recorded
+    counts of pcg_counts.npz (validate.py get_*_scipy run by make_golden.py)."""
+    import scipy.sparse as sp
+
+    from learningsparsepreconditioner4gpu_amd import cpu_rows
+
+    z = np.load(GOLDEN / "pcg_counts.npz")
+    for name in ("synthetic600", "poisson16", "kuhn7"):
+        A = sp.csr_matrix((z[f"{name}__data"], z[f"{name}__indices"], z[f"{name}__indptr"]))
+        L = A.copy()
+        L.data = z[f"{name}__L_data"]
+        gt, eps = z[f"{name}__gt"], float(z[f"{name}__eps"])
+        for rtol in (1e-6, 1e-8):
+            tag = f"{name}__rtol{int(-np.log10(rtol))}"
+            assert cpu_rows.get_cg_iter_time_scipy(A, gt, rtol=rtol) == int(z[f"{tag}__none"])
+            assert cpu_rows.get_pcg_diagonal_iter_time_scipy(A, gt, rtol=rtol) == int(z[f"{tag}__diagonal"])
+            assert cpu_rows.get_pcg_iter_time_scipy(A, gt, L, eps, rtol=rtol) == int(z[f"{tag}__ext_spai"])
+            assert cpu_rows.get_pcg_scaled_iter_time_scipy(A, gt, L, eps, rtol=rtol) == int(z[f"{tag}__ext_spai_scaled"])
 
 
 def test_heat_bunny_c3_stand_in():
