@@ -136,12 +136,12 @@ def sell_kind(indptr: np.ndarray, indices: np.ndarray) -> int:
 
 
 def sell_format_bytes(indptr: np.ndarray, indices: np.ndarray, kind: int, value_bytes: int) -> int:
-    """Matrix bytes one SELL-64 SpMV streams.  SELL-DIA: 64 x D_s value slots per slice + a 2-B row
-    mask + the slice's dictionary (64 B) and transposed-slot map (32 B); otherwise every stored
-    slot's value and column (2 B offset or 4 B index)."""
+    """Matrix bytes one SELL-64 SpMV streams.  SELL-DIA: 64 x D_s value slots per slice + the 2-B row
+    masks (128 B per slice) + the slice's 16-entry int32 offset dictionary (64 B); otherwise every
+    stored slot's value and column (2 B offset or 4 B index)."""
     if kind == 1:
         ns = (indptr.size + 62) // 64
-        return int(64 * dia_counts(indptr, indices).sum() * value_bytes) + ns * (128 + 64 + 32)
+        return int(64 * dia_counts(indptr, indices).sum() * value_bytes) + ns * (128 + 64)
     return int(sell_slots(indptr) * (value_bytes + {16: 2, 32: 4}[kind]))
 
 
@@ -250,6 +250,104 @@ def cpu_baseline(A, L, eps, gt, max_iter: int, rtol: float, all_threads: bool = 
     return out
 
 
+def reference_iters(workload: str, boo) -> dict:
+    """The REFERENCE's own count on this very system (tests/golden/traj_<workload>.npz, written by
+    tests/golden/make_golden.py: get_pcg_iter_time_scipy on the bench's A and GNN-L at 1 / 2 / 4 / 8
+    OpenBLAS threads), if the fixture exists and its GNN-output sha256 equals this run's."""
+    import hashlib
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", f"traj_{workload}.npz")
+    if not os.path.exists(path):
+        return None
+    z = np.load(path)
+    sha = hashlib.sha256(np.ascontiguousarray(boo.detach().cpu().numpy()).tobytes()).hexdigest()
+    return {"counts_by_openblas_threads": dict(zip([str(int(t)) for t in z["ref_threads"]],
+                                                   [int(c) for c in z["ref_counts"]])),
+            "oracle_correctly_rounded_count": int(z["oracle_exact_count"]), "same_L": sha == str(z["boo_sha256"]),
+            "source": f"tests/golden/traj_{workload}.npz (validate.py:163-201 run on this A and GNN-L)"}
+
+
+def parity_rows(A, L, eps: float, b, rtol: float, threads=(1, 8)) -> dict:
+    """The headline solve in the parity dot order (dot_order="openblas": numpy's ddot at T OpenBLAS
+    threads, the reference's recorded trajectory bit for bit): iterations and time, 1 warm-up +
+    median of 3."""
+    import torch
+
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    out = {}
+    for th in threads:
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", dtype=np.float64,
+                                            dot_order="openblas", dot_threads=th)
+        s.set_spai(L, eps, block_size=L.block_size)
+        x = torch.zeros_like(b)
+        ts = []
+        for _ in range(4):
+            x.zero_()
+            it, conv, t = s.solve(b, x, rtol=rtol)
+            ts.append(t)
+        med = float(np.median(ts[1:]))
+        out[f"openblas_{th}_threads"] = {"iters": it, "converged": bool(conv), "time_to_rtol_ms": med * 1e3,
+                                         "it_per_s": it / med}
+        del s
+    return out
+
+
+def irregular_row(workload: str, eps: float, rtol: float, reps: int) -> dict:
+    """An irregular ordering of the headline's 1M-row system (problems.renumber: a seeded random
+    symmetric permutation then reverse Cuthill-McKee -- banded like an RCM-ordered tet mesh, ~32
+    distinct row-relative offsets per 64-row slice, so the 16-bit SELL-64 views instead of
+    SELL-DIA): GNN-L on it, the PCG loop (1 warm-up + median of 3 solves) and the fp64 SpMV
+    against the SURVEY 8(d) CSR bytes, cold."""
+    import torch
+
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    A_raw, mask, feats, bs, e2n = P.workload(workload)
+    smp = make_sample(A_raw, mask, node_features=feats, block_size=bs, use_edge_features_as_node_feature=e2n)
+    ws = SimpleInferenceWorkspace(node_features=smp.x.shape[1], edge_features=smp.edge_attr.shape[1], block_size=bs,
+                                  epsilon=eps, seed=0)
+    d = smp.to("cuda")
+    L, _ = ws.inference_step(d)
+    A = ws.system_matrix(d)
+    b = A.matvec(d.mask.reshape(-1).to(torch.float64))
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", dtype=np.float64)
+    s.set_spai(L, eps, block_size=bs)
+    x = torch.zeros_like(b)
+    ts = []
+    for _ in range(4):
+        x.zero_()
+        it, conv, t = s.solve(b, x, rtol=rtol)
+        ts.append(t)
+    med = float(np.median(ts[1:]))
+    try:
+        loop = s.time_kernels(b, 40)
+    except RuntimeError:
+        loop = {}
+    Ah = A.to_scipy()
+    kind_loop = sell_kind(Ah.indptr, Ah.indices)
+    p = torch.randn(A.n, dtype=torch.float64, device="cuda")
+    q = torch.empty_like(p)
+    kind = A.prepare_spmv()
+    cold = A.spmv_timed(p, q, reps, flush_bytes=FLUSH_BYTES)
+    warm = A.spmv_timed(p, q, 3 * reps)
+    alg = spmv_bytes(A.n, A.nnz)
+    dc = dia_counts(Ah.indptr, Ah.indices)
+    return {"workload": f"{workload}: the headline system renumbered (random symmetric permutation + RCM), "
+                        f"n={A.n}, nnz={A.nnz}, ext_spai, rtol {rtol:g}",
+            "distinct_offsets_per_slice": {"mean": float(dc.mean()), "max": int(dc.max())},
+            "bandwidth": int(np.abs(Ah.indices - np.repeat(np.arange(A.n), np.diff(Ah.indptr))).max()),
+            "column_storage": KIND_TEXT[kind_loop], "iters": it, "converged": bool(conv),
+            "time_to_rtol_ms": med * 1e3, "pcg_iter_us": med / it * 1e6,
+            "loop_kernels_us": {k: v * 1e6 for k, v in loop.items()},
+            "spmv": {"kernel": f"{KERNEL_NAME.get(kind, 'k_spmv')}<double,double>", "avg_launch_ms_cold": cold,
+                     "avg_launch_ms_warm": warm, "alg_bytes": alg, "achieved_GBs_cold": alg / (cold * 1e-3) / 1e9,
+                     "frac_cold": alg / (cold * 1e-3) / 1e9 / HBM_PEAK_GBS}}
+
+
 def c1_rows(rtol: float, all_threads: bool = False) -> dict:
     """BASELINE config 1 (datagen/synthetic.py N = 10240, CG, b = A·1): the reference's CPU path
     (scipy cg, full solve, 1 warm-up + median of 5, 1 BLAS thread; nproc threads with
@@ -270,15 +368,17 @@ def c1_rows(rtol: float, all_threads: bool = False) -> dict:
     bt = torch.from_numpy(b).cuda()
     x = torch.zeros_like(bt)
     gpu = {}
-    for order in ("compensated", "openblas"):
-        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="none", dot_order=order, dot_threads=1)
+    for label, order, threads in (("compensated", "compensated", 1), ("openblas", "openblas", 1),
+                                  ("openblas_8_threads", "openblas", 8)):
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="none", dot_order=order,
+                                            dot_threads=threads)
         ts = []
         for _ in range(6):
             x.zero_()
             it, conv, t = s.solve(bt, x, rtol=rtol)
             ts.append(t)
         med = float(np.median(ts[1:]))
-        gpu[order] = {"iters": it, "time_to_rtol_ms": med * 1e3, "it_per_s": it / med}
+        gpu[label] = {"iters": it, "time_to_rtol_ms": med * 1e3, "it_per_s": it / med}
     return {"workload": "synthetic C1 n=10240 nnz=%d, CG (none), b = A·1, rtol %g" % (A.nnz, rtol),
             "gpu": gpu, "reference_iters": {"1_openblas_thread": 3236, "8_openblas_threads": 3229}, "cpu": cpu}
 
@@ -460,6 +560,7 @@ def main():
     log(f"rank {rank}: GNN forward ms {[round(t * 1e3, 3) for t in gnn_times]}")
     gnn_fl = gnn_flops(sample.x.shape[0], sample.edge_index.shape[1], sample.x.shape[1], sample.edge_attr.shape[1],
                        bs * bs)
+    ref_iters = reference_iters(args.workload, ws.forward(dev_sample.x, dev_sample.edge_index, dev_sample.edge_attr))
     A = ws.system_matrix(dev_sample)
     n, nnz_a, nnz_l = A.n, A.nnz, L.nnz
     gt = dev_sample.mask.reshape(-1).to(torch.float64)
@@ -598,11 +699,22 @@ def main():
         except Exception as e:  # pragma: no cover
             c1 = {"failed": str(e)}
     c5 = None
+    parity = None
+    irregular = None
     if rank == 0 and world == 1 and not args.no_variants:
         try:
             c5 = c5_rows(args.rtol)
         except Exception as e:  # pragma: no cover
             c5 = {"failed": str(e)}
+        try:
+            parity = parity_rows(A, L, args.epsilon, b, args.rtol)
+        except Exception as e:  # pragma: no cover
+            parity = {"failed": str(e)}
+        if args.workload == "kuhn101":
+            try:
+                irregular = irregular_row("kuhn101rcm", args.epsilon, args.rtol, args.spmv_reps)
+            except Exception as e:  # pragma: no cover
+                irregular = {"failed": str(e)}
 
     if rank == 0:
         value = total_iters / elapsed
@@ -626,6 +738,7 @@ def main():
                 "rtol": args.rtol, "iters_per_solve": it_per_solve, "systems_per_gpu": 1,
                 "parallelism": f"independent systems, 1 per GPU x {world}",
             },
+            "reference_iters": ref_iters,
             "time_to_rtol_ms": float(np.median(solve_times)) * 1e3,
             "time_to_rtol_variants": variants,
             "gnn_tflops": gnn_fl / float(np.median(gnn_times)) / 1e12,
@@ -660,6 +773,8 @@ def main():
             "cpu_baseline": cpu,
             "c1_synthetic": c1,
             "c5_heat_batch": c5,
+            "parity_mode": parity,
+            "irregular_1m": irregular,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -42,6 +42,7 @@ extern "C" {
 #define LSPCG_ERR_UNSUPPORTED (-3)
 #define LSPCG_ERR_FORMAT (-4)
 #define LSPCG_ERR_BREAKDOWN (-5) /* incomplete factorization hit a non-positive pivot */
+#define LSPCG_ERR_SINGULAR (-6)  /* a given triangular factor has a zero diagonal entry */
 
 #define LSPCG_F32 0
 #define LSPCG_F64 1
@@ -285,6 +286,21 @@ int lspcg_part_a(lspcg_part* p, const void* p_ext, void* q, double* red);
 int lspcg_part_update_p(lspcg_part* p, const void* z, void* p_ext, double beta, int first);
 /* x += alpha p ; r -= alpha q */
 int lspcg_part_update_xr(lspcg_part* p, double alpha, const void* p_ext, const void* q, void* x, void* r_ext);
+/* Device-side scalar recurrence (no host round trip per iteration; dist_pcg.DistributedPCG):
+ * the part's device state holds scipy cg's scalars (rtol, atol, ‖r‖², ρ, ρ_prev, π, α, β, the
+ * iteration count and a done code: 1 converged, 2 max_iter, 3 non-finite, 4 ‖b‖ = 0).
+ * state_init: reset it (hist: device buffer of max_iter + 2 doubles receiving ‖r_k‖, or NULL).
+ * scalars: one single-thread launch summing the all-gathered [world][64][nd][2] group pairs
+ * rank-major and applying phase 0 init (nd 2: ‖r_0‖², ‖b‖²), 1 after part_l (nd 2: ρ, ‖r_k‖²;
+ * then the top-of-loop test and β), 2 the same for plain CG (no gathered data), 3 after part_a
+ * (nd 1: π; α), 4 plain CG after part_norms of r (nd 2: ‖r_{k+1}‖²).  update_p_dev /
+ * update_xr_dev: update_p / update_xr with β, α from the state, skipped once done (update_xr_dev
+ * also advances the iteration).  status: the iteration count and done code (synchronises). */
+int lspcg_part_state_init(lspcg_part* p, double rtol, int64_t max_iter, double* hist);
+int lspcg_part_scalars(lspcg_part* p, const double* gathered, int world, int phase);
+int lspcg_part_update_p_dev(lspcg_part* p, const void* z, void* p_ext);
+int lspcg_part_update_xr_dev(lspcg_part* p, const void* p_ext, const void* q, void* x, void* r_ext);
+int lspcg_part_status(lspcg_part* p, int64_t* iter, int* done);
 
 #ifdef __cplusplus
 }

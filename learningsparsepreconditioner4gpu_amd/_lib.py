@@ -14,7 +14,7 @@ PKG = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("LSPCG_LIB", PKG / "liblspcg_hip.so"))
 
 OK, NOT_CONVERGED = 0, 1
-ERR_ARG, ERR_HIP, ERR_UNSUPPORTED, ERR_FORMAT, ERR_BREAKDOWN = -1, -2, -3, -4, -5
+ERR_ARG, ERR_HIP, ERR_UNSUPPORTED, ERR_FORMAT, ERR_BREAKDOWN, ERR_SINGULAR = -1, -2, -3, -4, -5, -6
 F32, F64 = 0, 1
 PRECOND = {"none": 0, "diagonal": 1, "ext_spai": 2, "ext_spai_scaled": 3, "ic": 4}
 DOT_ORDER = {"compensated": 0, "openblas": 1}
@@ -87,6 +87,11 @@ SIGNATURES = {
     "lspcg_part_a": (C.c_int, [vp, vp, vp, vp]),
     "lspcg_part_update_p": (C.c_int, [vp, vp, vp, C.c_double, C.c_int]),
     "lspcg_part_update_xr": (C.c_int, [vp, C.c_double, vp, vp, vp, vp]),
+    "lspcg_part_state_init": (C.c_int, [vp, C.c_double, C.c_int64, vp]),
+    "lspcg_part_scalars": (C.c_int, [vp, vp, C.c_int, C.c_int]),
+    "lspcg_part_update_p_dev": (C.c_int, [vp, vp, vp]),
+    "lspcg_part_update_xr_dev": (C.c_int, [vp, vp, vp, vp, vp]),
+    "lspcg_part_status": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
 }
 
 

@@ -128,6 +128,118 @@ __global__ void __launch_bounds__(kThreads) k_part_norms(int64_t n, const T* __r
   grid_partial_groups<2>(d, partials, ticket, part_gsz(), group_out);
 }
 
+// ---- device-side scalar recurrence (round 4): the dot totals, scipy's scalars and its top-of-loop
+// test computed on the device from the all-gathered group pairs, so an iteration needs no host
+// round trip (the host polls the state once per chunk of iterations).  One thread sums every
+// rank's 64 group pairs in rank-major order with dd_add -- dist_pcg.sum_groups' order, so the
+// scalars are the host recurrence's bits -- and every later kernel of the iteration reads them.
+struct PartState {
+  double rtol, atol, rr, rho, rho_prev, pq, alpha, beta, bb;
+  int64_t iter, max_iter;
+  int32_t done;  // 0 running, 1 converged, 2 max_iter, 3 non-finite residual, 4 ‖b‖ = 0
+  int32_t pad;
+  double* hist;  // ‖r_k‖, k = 0 .. iter (device, caller-owned; may be NULL)
+};
+
+template <typename T>
+__device__ __forceinline__ T part_sqrt(T v) { return sqrt(v); }
+
+// total j of the gathered [world][64 groups][nd][2] pairs, rank-major (sum_groups' order)
+__device__ double part_total(const double* g, int world, int nd, int j) {
+  DD acc = dd_zero();
+  for (int r = 0; r < world; ++r)
+    for (int k = 0; k < kPartGroups; ++k) {
+      const double* e = g + (size_t(r) * kPartGroups * nd + size_t(k) * nd + j) * 2;
+      acc = dd_add(acc, DD{e[0], e[1]});
+    }
+  return acc.s + acc.c;
+}
+
+// top-of-loop test (k_update_p_g's): sets done, returns true when the loop stops here
+template <typename T>
+__device__ __forceinline__ bool part_test(PartState* S) {
+  int code = 0;
+  if (S->iter >= S->max_iter) {
+    code = 2;
+  } else {
+    const double rn = double(part_sqrt<T>(T(S->rr)));
+    if (rn < S->atol) code = 1;
+    else if (!(rn == rn) || rn == INFINITY) code = 3;
+  }
+  if (code) S->done = code;
+  return code != 0;
+}
+
+enum PartPhase { kPartInit = 0, kPartZ = 1, kPartZcg = 2, kPartQ = 3, kPartR = 4 };
+
+template <typename T>
+__global__ void k_part_scalars(PartState* S, const double* __restrict__ g, int world, int phase) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (phase == kPartInit) {  // rr0 = r·r, bb = b·b (r = b); atol = max(0, rtol ‖b‖)
+    const double rr0 = round_to<T>(part_total(g, world, 2, 0));
+    const double bb = round_to<T>(part_total(g, world, 2, 1));
+    const double bn = double(part_sqrt<T>(T(bb)));
+    S->rr = rr0;
+    S->bb = bb;
+    S->atol = fmax(0.0, S->rtol * bn);
+    S->iter = 0;
+    S->done = bn == 0.0 ? 4 : 0;
+    if (S->hist) S->hist[0] = double(part_sqrt<T>(T(rr0)));
+    return;
+  }
+  if (S->done) return;
+  if (phase == kPartZ || phase == kPartZcg) {
+    const int64_t k = S->iter;
+    double rho;
+    if (phase == kPartZ) {  // ρ = r·z and ‖r_k‖² from L's launch
+      rho = round_to<T>(part_total(g, world, 2, 0));
+      const double rr_k = round_to<T>(part_total(g, world, 2, 1));
+      if (k > 0) S->rr = rr_k;
+    } else {  // CG: z = r, ρ = ‖r_k‖² (from the init or the previous kPartR)
+      rho = S->rr;
+    }
+    if (k > 0 && S->hist) S->hist[k] = double(part_sqrt<T>(T(S->rr)));
+    S->rho = rho;
+    if (part_test<T>(S)) return;
+    S->beta = k == 0 ? 0.0 : double(T(rho) / T(S->rho_prev));
+  } else if (phase == kPartQ) {  // π = p·q ; α = ρ/π
+    const double pq = round_to<T>(part_total(g, world, 1, 0));
+    S->pq = pq;
+    S->alpha = double(T(S->rho) / T(pq));
+  } else {  // kPartR (CG): ‖r_{k+1}‖² for the next test
+    S->rr = round_to<T>(part_total(g, world, 2, 0));
+  }
+}
+
+// p = z (k = 0) or p β + z, scalars from the device state
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_part_update_p_dev(int64_t n, const PartState* S, const T* __restrict__ z,
+                                                                T* __restrict__ p) {
+  if (S->done) return;
+  const bool first = S->iter == 0;
+  const T beta = T(S->beta);
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    p[i] = first ? z[i] : (p[i] * beta) + z[i];
+}
+
+// x += α p ; r -= α q ; then ρ_prev = ρ and the iteration count (workgroup 0, thread 0: the
+// other workgroups read only α and done, which it does not write)
+template <typename T>
+__global__ void __launch_bounds__(kThreads) k_part_update_xr_dev(int64_t n, PartState* S, const T* __restrict__ p,
+                                                                 const T* __restrict__ q, T* __restrict__ x,
+                                                                 T* __restrict__ r) {
+  if (S->done) return;
+  const T alpha = T(S->alpha);
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    x[i] = x[i] + alpha * p[i];
+    r[i] = r[i] - alpha * q[i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    S->rho_prev = S->rho;
+    S->iter = S->iter + 1;
+  }
+}
+
 static int part_grid(int64_t n) {
   const int64_t g = (n + kThreads - 1) / kThreads;
   return int(g < 1 ? 1 : (g > 1024 ? 1024 : g));
@@ -147,6 +259,7 @@ struct lspcg_part {
   int32_t* send_idx = nullptr;  // owned device copy
   double* partials = nullptr;
   unsigned* ticket = nullptr;
+  PartState* S = nullptr;  // device state of the device-side recurrence
 };
 
 namespace {
@@ -201,6 +314,8 @@ int lspcg_part_create(lspcg_ctx* ctx, const lspcg_mat* A, const lspcg_mat* L, co
   LSPCG_HIP(hipMalloc(&p->partials, sizeof(double) * 2 * 2 * (kReduceBlocksMax + 1)));
   LSPCG_HIP(hipMalloc(&p->ticket, sizeof(unsigned) * kTicketWords));
   LSPCG_HIP(hipMemsetAsync(p->ticket, 0, sizeof(unsigned) * kTicketWords, st));
+  LSPCG_HIP(hipMalloc(&p->S, sizeof(PartState)));
+  LSPCG_HIP(hipMemsetAsync(p->S, 0, sizeof(PartState), st));
   LSPCG_HIP(hipStreamSynchronize(st));
   *out = p.release();
   return LSPCG_OK;
@@ -210,7 +325,7 @@ int lspcg_part_destroy(lspcg_part* p) {
   if (!p) return LSPCG_OK;
   (void)hipSetDevice(p->ctx->device);
   (void)hipStreamSynchronize(p->ctx->stream);
-  for (void* v : {(void*)p->send_idx, (void*)p->partials, (void*)p->ticket}) (void)hipFree(v);
+  for (void* v : {(void*)p->send_idx, (void*)p->partials, (void*)p->ticket, (void*)p->S}) (void)hipFree(v);
   delete p;
   return LSPCG_OK;
 }
@@ -317,6 +432,69 @@ int lspcg_part_update_xr(lspcg_part* p, double alpha, const void* p_ext, const v
                        static_cast<const float*>(p_ext), static_cast<const float*>(q), static_cast<float*>(x),
                        static_cast<float*>(r_ext));
   LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+int lspcg_part_state_init(lspcg_part* p, double rtol, int64_t max_iter, double* hist) {
+  LSPCG_CHECK(p && max_iter > 0, LSPCG_ERR_ARG, "part_state_init: bad argument");
+  PartState h{};
+  h.rtol = rtol;
+  h.max_iter = max_iter;
+  h.hist = hist;
+  LSPCG_HIP(hipMemcpyAsync(p->S, &h, sizeof(PartState), hipMemcpyHostToDevice, p->ctx->stream));
+  LSPCG_HIP(hipStreamSynchronize(p->ctx->stream));  // h is a stack copy
+  return LSPCG_OK;
+}
+
+int lspcg_part_scalars(lspcg_part* p, const double* gathered, int world, int phase) {
+  LSPCG_CHECK(p && world >= 1 && phase >= kPartInit && phase <= kPartR && (gathered || phase == kPartZcg),
+              LSPCG_ERR_ARG, "part_scalars: bad argument");
+  hipStream_t st = p->ctx->stream;
+  if (p->dtype == LSPCG_F64)
+    hipLaunchKernelGGL(k_part_scalars<double>, dim3(1), dim3(64), 0, st, p->S, gathered, world, phase);
+  else
+    hipLaunchKernelGGL(k_part_scalars<float>, dim3(1), dim3(64), 0, st, p->S, gathered, world, phase);
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+int lspcg_part_update_p_dev(lspcg_part* p, const void* z, void* p_ext) {
+  LSPCG_CHECK(p && z && p_ext, LSPCG_ERR_ARG, "part_update_p_dev: NULL argument");
+  hipStream_t st = p->ctx->stream;
+  const int g = part_grid(p->n_own);
+  if (p->dtype == LSPCG_F64)
+    hipLaunchKernelGGL(k_part_update_p_dev<double>, dim3(g), dim3(kThreads), 0, st, p->n_own, p->S,
+                       static_cast<const double*>(z), static_cast<double*>(p_ext));
+  else
+    hipLaunchKernelGGL(k_part_update_p_dev<float>, dim3(g), dim3(kThreads), 0, st, p->n_own, p->S,
+                       static_cast<const float*>(z), static_cast<float*>(p_ext));
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+int lspcg_part_update_xr_dev(lspcg_part* p, const void* p_ext, const void* q, void* x, void* r_ext) {
+  LSPCG_CHECK(p && p_ext && q && x && r_ext, LSPCG_ERR_ARG, "part_update_xr_dev: NULL argument");
+  hipStream_t st = p->ctx->stream;
+  const int g = part_grid(p->n_own);
+  if (p->dtype == LSPCG_F64)
+    hipLaunchKernelGGL(k_part_update_xr_dev<double>, dim3(g), dim3(kThreads), 0, st, p->n_own, p->S,
+                       static_cast<const double*>(p_ext), static_cast<const double*>(q), static_cast<double*>(x),
+                       static_cast<double*>(r_ext));
+  else
+    hipLaunchKernelGGL(k_part_update_xr_dev<float>, dim3(g), dim3(kThreads), 0, st, p->n_own, p->S,
+                       static_cast<const float*>(p_ext), static_cast<const float*>(q), static_cast<float*>(x),
+                       static_cast<float*>(r_ext));
+  LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+int lspcg_part_status(lspcg_part* p, int64_t* iter, int* done) {
+  LSPCG_CHECK(p && iter && done, LSPCG_ERR_ARG, "part_status: NULL argument");
+  PartState h{};
+  LSPCG_HIP(hipMemcpyAsync(&h, p->S, sizeof(PartState), hipMemcpyDeviceToHost, p->ctx->stream));
+  LSPCG_HIP(hipStreamSynchronize(p->ctx->stream));
+  *iter = h.iter;
+  *done = h.done;
   return LSPCG_OK;
 }
 

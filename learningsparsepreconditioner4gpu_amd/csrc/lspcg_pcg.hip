@@ -410,7 +410,7 @@ struct EpiQG {
 
 // UP.  The first chunk's vector loads are issued before the group sums, so their latency overlaps
 // the scalar reduction instead of following it.
-template <typename T>
+template <typename T, bool NTX = false>
 __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S, const double* __restrict__ gz, int ngz,
                                                          const T* __restrict__ z, T* __restrict__ p,
                                                          T* __restrict__ x) {
@@ -427,46 +427,55 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
       if (j < nv) {
         zz[u] = reinterpret_cast<const V*>(z)[j];
         pp[u] = reinterpret_cast<const V*>(p)[j];
-        xx[u] = reinterpret_cast<const V*>(x)[j];
+        if constexpr (NTX) xx[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(x) + j);
+        else xx[u] = reinterpret_cast<const V*>(x)[j];
       }
     }
   };
-  // the first chunk, the group totals and the state line are all loaded before the first test:
-  // one memory latency instead of a state read followed by the loads
+  // the first chunk, the group totals and every state field are all loaded before the first test:
+  // one memory latency instead of a state read followed by the loads (the state fields are read
+  // into registers up front -- workgroup 0's state stores below would otherwise order the later
+  // ρ_{k-1} / α_{k-1} reads after them, a second scalar round trip for every wave)
   load(jt);
   const int32_t done = S->done;
   const int64_t k = S->iter;
+  const int64_t max_iter = S->max_iter;
+  const double atol = S->atol, rr0 = S->rr, rho_prev = S->rho, alpha_prev = S->alpha;
+  double* const hist = S->hist;
   double v[2];
   group_sum_dd<2>(gz, ngz, v);
   if (done) return;
   const double rho = round_to<T>(v[0]);
-  const double rr = k > 0 ? round_to<T>(v[1]) : S->rr;  // ‖r_0‖² from the init launch
+  const double rr = k > 0 ? round_to<T>(v[1]) : rr0;  // ‖r_0‖² from the init launch
   int code = 0;  // scipy's top-of-loop test (ProCheck)
-  if (k >= S->max_iter) {
+  if (k >= max_iter) {
     code = 2;
   } else {
     const double rn = double(tsqrt<T>(T(rr)));
-    if (rn < S->atol) code = 1;
+    if (rn < atol) code = 1;
     else if (!(rn == rn) || rn == INFINITY) code = 3;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (k > 0) {
       S->rr = rr;
-      if (S->hist) S->hist[k] = double(tsqrt<T>(T(rr)));
+      if (hist) hist[k] = double(tsqrt<T>(T(rr)));
     }
     if (code) S->done = code;
   }
   if (code) return;
   const bool first = k == 0;
-  const T beta = first ? T(0) : T(rho) / T(S->rho);  // S->rho = ρ_{k-1}
-  const T alpha = T(S->alpha);                        // α_{k-1}
+  const T beta = first ? T(0) : T(rho) / T(rho_prev);  // ρ_{k-1}
+  const T alpha = T(alpha_prev);                        // α_{k-1}
   for (int64_t j0 = jt; j0 < nv; j0 += ts * kElemUnroll) {
     if (j0 != jt) load(j0);
 #pragma unroll
     for (int u = 0; u < kElemUnroll; ++u) {
       const int64_t j = j0 + u * ts;
       if (j < nv) {
-        if (!first) reinterpret_cast<V*>(x)[j] = xx[u] + alpha * pp[u];
+        if (!first) {
+          if constexpr (NTX) __builtin_nontemporal_store(xx[u] + alpha * pp[u], reinterpret_cast<V*>(x) + j);
+          else reinterpret_cast<V*>(x)[j] = xx[u] + alpha * pp[u];
+        }
         reinterpret_cast<V*>(p)[j] = first ? zz[u] : (pp[u] * beta) + zz[u];
       }
     }
@@ -501,6 +510,8 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
   };
   load(jt);  // first chunk, group totals and state line together (as in UP)
   const int32_t done = S->done;
+  const int64_t k = S->iter;
+  const double rho_prev = S->rho;
   double vz[2], vq[1];
   group_sum_dd<2>(gz, ngz, vz);
   group_sum_dd<1>(gq, ngq, vq);
@@ -509,11 +520,11 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
   const double pq = round_to<T>(vq[0]);
   const T alpha = T(rho) / T(pq);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    S->rho_prev = S->rho;
+    S->rho_prev = rho_prev;
     S->rho = rho;
     S->pq = pq;
     S->alpha = double(alpha);
-    S->iter = S->iter + 1;
+    S->iter = k + 1;
   }
   for (int64_t j0 = jt; j0 < nv; j0 += ts * kElemUnroll) {
     if (j0 != jt) load(j0);
@@ -829,6 +840,7 @@ __global__ void __launch_bounds__(kThreads) k_dot_rho(int64_t n, PcgState* S, co
 // replaces (same predicate on `done`), so the loop's order of state updates is unchanged.
 constexpr int kObMaxThreads = 16;
 constexpr int kObBlock = 512;  // 8 waves: <= 256 VGPRs for the two register buffers
+constexpr int64_t kObSplitN = 131072;  // from this n the parity dots run one workgroup per (dot, chunk)
 
 // chunk c of OpenBLAS's blas_level1_thread split of [0, n) (width = ceil(rest / threads left))
 __device__ __forceinline__ void ob_chunk(int64_t n, int nch, int c, int64_t* start, int64_t* width) {
@@ -851,53 +863,57 @@ __device__ __forceinline__ void ob_chunk(int64_t n, int nch, int c, int64_t* sta
 // config 1 (n = 10,240): 8.7 us per launch against 15-16 with flat loads and one 8-step batch
 // (~18 GB/s: one wave's loads in flight); a third buffer measured the same, and staging tiles
 // through LDS with every wave loading (one barrier per 16-step tile) measured slower (~19 us).
-constexpr int kObU = 16;
+constexpr int kObU = 16;   // steps per register buffer, single-workgroup kernel (8 waves: <= 256 VGPRs)
+constexpr int kObU1 = 32;  // the split kernel's one-wave workgroups hold twice as many steps in flight
 
+template <int U>
 __device__ __forceinline__ void ob_load(const double* __restrict__ x, const double* __restrict__ y, int64_t i,
-                                        double (&xv)[kObU], double (&yv)[kObU]) {
+                                        double (&xv)[U], double (&yv)[U]) {
 #pragma unroll
-  for (int u = 0; u < kObU; ++u) {
+  for (int u = 0; u < U; ++u) {
     xv[u] = x[i + 32 * u];
     yv[u] = y[i + 32 * u];
   }
 }
 
-__device__ __forceinline__ double ob_fma(const double (&xv)[kObU], const double (&yv)[kObU], double acc) {
+template <int U>
+__device__ __forceinline__ double ob_fma(const double (&xv)[U], const double (&yv)[U], double acc) {
 #pragma unroll
-  for (int u = 0; u < kObU; ++u) acc = __builtin_fma(xv[u], yv[u], acc);
+  for (int u = 0; u < U; ++u) acc = __builtin_fma(xv[u], yv[u], acc);
   return acc;
 }
 
 // the 32 accumulators over the 32-aligned prefix (lanes 0..31; one wave reads everything)
+template <int U = kObU>
 __device__ __forceinline__ double ob_chains(const double* __restrict__ x, const double* __restrict__ y, int64_t w) {
   const int lane = threadIdx.x & 63;
   const int64_t n32 = (w & -int64_t(16)) & ~int64_t(31);
   double acc = 0.0;
   if (lane < 32) {
-    constexpr int64_t GW = 32 * kObU;  // elements per group
+    constexpr int64_t GW = 32 * U;  // elements per group
     const int64_t G = n32 / GW;
-    double ax[kObU], ay[kObU], bx[kObU], by[kObU];
+    double ax[U], ay[U], bx[U], by[U];
     int64_t g = 0;
-    if (G > 0) ob_load(x, y, lane, ax, ay);
+    if (G > 0) ob_load<U>(x, y, lane, ax, ay);
     for (; g + 1 < G; g += 2) {
-      ob_load(x, y, (g + 1) * GW + lane, bx, by);
-      acc = ob_fma(ax, ay, acc);
-      ob_load(x, y, (g + 2 < G ? g + 2 : g + 1) * GW + lane, ax, ay);
-      acc = ob_fma(bx, by, acc);
+      ob_load<U>(x, y, (g + 1) * GW + lane, bx, by);
+      acc = ob_fma<U>(ax, ay, acc);
+      ob_load<U>(x, y, (g + 2 < G ? g + 2 : g + 1) * GW + lane, ax, ay);
+      acc = ob_fma<U>(bx, by, acc);
     }
-    if (g < G) acc = ob_fma(ax, ay, acc);
-    // the remaining < kObU steps, loaded at once and added in order
+    if (g < G) acc = ob_fma<U>(ax, ay, acc);
+    // the remaining < U steps, loaded at once and added in order
     const int64_t base = G * GW;
     const int rem = int((n32 - base) >> 5);
     if (rem > 0) {
 #pragma unroll
-      for (int u = 0; u < kObU; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t i = base + (u < rem ? 32 * u : 0) + lane;
         bx[u] = x[i];
         by[u] = y[i];
       }
 #pragma unroll
-      for (int u = 0; u < kObU; ++u)
+      for (int u = 0; u < U; ++u)
         if (u < rem) acc = __builtin_fma(bx[u], by[u], acc);
     }
   }
@@ -930,8 +946,9 @@ __device__ __forceinline__ double ob_finish(const double* __restrict__ x, const 
   return dot;
 }
 
+template <int U = kObU>
 __device__ __forceinline__ double ob_chunk_dot(const double* __restrict__ x, const double* __restrict__ y, int64_t w) {
-  return ob_finish(x, y, w, ob_chains(x, y, w));
+  return ob_finish(x, y, w, ob_chains<U>(x, y, w));
 }
 
 enum ObWhich { kObInit = 0, kObZ = 1, kObQ = 2, kObR = 3, kObRho = 4, kObRR = 5 };
@@ -943,33 +960,9 @@ enum ObWhich { kObInit = 0, kObZ = 1, kObQ = 2, kObR = 3, kObRho = 4, kObRR = 5 
 //   kObR     rr = r·r ; rho = (DIAG ? r·z : rr) ; hist[k]           (after CG / Jacobi k_update_r)
 //   kObRho   rho = r·z                                             (after IC's k_dot_rho)
 //   kObRR    rr = r·r ; hist[k]                                    (after IC's k_update_r)
+// thread 0's scalar update of phase WHICH from the dot values v[0..nd)
 template <int WHICH, bool DIAG>
-__global__ void __launch_bounds__(kObBlock) k_dot_openblas(int64_t n, int nch, int nd, PcgState* S, const double* x0,
-                                                           const double* y0, const double* x1, const double* y1,
-                                                           const double* x2, const double* y2) {
-  __shared__ double part[3][kObMaxThreads];
-  if (WHICH != kObInit && S->done) return;
-  const int ch = (n > 10000 && nch > 1) ? nch : 1;
-  const int nw = blockDim.x >> 6;
-  for (int item = threadIdx.x >> 6; item < nd * ch; item += nw) {
-    const int j = item / ch, c = item % ch;
-    int64_t s = 0, w = n;
-    if (ch > 1) ob_chunk(n, ch, c, &s, &w);
-    // selects, not an array of pointers: the loads stay global_load (a flat load's lgkmcnt forces
-    // waits on ALL outstanding loads, which would serialise the two register buffers)
-    const double* xj = j == 0 ? x0 : j == 1 ? x1 : x2;
-    const double* yj = j == 0 ? y0 : j == 1 ? y1 : y2;
-    const double v = ob_chunk_dot(xj + s, yj + s, w);
-    if ((threadIdx.x & 63) == 0) part[j][c] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  double v[3] = {0.0, 0.0, 0.0};
-  for (int j = 0; j < nd; ++j) {
-    double d = 0.0;
-    for (int c = 0; c < ch; ++c) d = d + part[j][c];
-    v[j] = ch > 1 ? d : part[j][0];
-  }
+__device__ __forceinline__ void ob_epilogue(PcgState* S, const double (&v)[3]) {
   const int64_t k = S->iter;
   if constexpr (WHICH == kObInit) {
     S->rr = v[0];
@@ -998,6 +991,70 @@ __global__ void __launch_bounds__(kObBlock) k_dot_openblas(int64_t n, int nch, i
     S->rr = v[0];
     if (S->hist) S->hist[k] = sqrt(v[0]);
   }
+}
+
+// the chunk totals of dot j summed in chunk order (numpy's threads joined in order)
+__device__ __forceinline__ void ob_join(const double* part, int nd, int ch, double (&v)[3]) {
+  for (int j = 0; j < 3; ++j) v[j] = 0.0;
+  for (int j = 0; j < nd; ++j) {
+    double d = 0.0;
+    for (int c = 0; c < ch; ++c) d = d + part[j * kObMaxThreads + c];
+    v[j] = ch > 1 ? d : part[j * kObMaxThreads];
+  }
+}
+
+template <int WHICH, bool DIAG>
+__global__ void __launch_bounds__(kObBlock) k_dot_openblas(int64_t n, int nch, int nd, PcgState* S, const double* x0,
+                                                           const double* y0, const double* x1, const double* y1,
+                                                           const double* x2, const double* y2) {
+  __shared__ double part[3 * kObMaxThreads];
+  if (WHICH != kObInit && S->done) return;
+  const int ch = (n > 10000 && nch > 1) ? nch : 1;
+  const int nw = blockDim.x >> 6;
+  for (int item = threadIdx.x >> 6; item < nd * ch; item += nw) {
+    const int j = item / ch, c = item % ch;
+    int64_t s = 0, w = n;
+    if (ch > 1) ob_chunk(n, ch, c, &s, &w);
+    // selects, not an array of pointers: the loads stay global_load (a flat load's lgkmcnt forces
+    // waits on ALL outstanding loads, which would serialise the two register buffers)
+    const double* xj = j == 0 ? x0 : j == 1 ? x1 : x2;
+    const double* yj = j == 0 ? y0 : j == 1 ? y1 : y2;
+    const double v = ob_chunk_dot(xj + s, yj + s, w);
+    if ((threadIdx.x & 63) == 0) part[j * kObMaxThreads + c] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double v[3];
+  ob_join(part, nd, ch, v);
+  ob_epilogue<WHICH, DIAG>(S, v);
+}
+
+// Large n (>= kObSplitN): one single-wave workgroup per (dot, chunk) item -- every chunk of every
+// dot on its own CU, with twice the steps in flight per register buffer (kObU1) -- writing its
+// chunk total to a scratch slot; k_dot_openblas_fin then joins them in order and updates the
+// scalars (one more launch; the same bits).
+template <int WHICH>
+__global__ void __launch_bounds__(64) k_dot_openblas_item(int64_t n, int nch, const PcgState* S, double* part,
+                                                          const double* x0, const double* y0, const double* x1,
+                                                          const double* y1, const double* x2, const double* y2) {
+  if (WHICH != kObInit && S->done) return;
+  const int ch = (n > 10000 && nch > 1) ? nch : 1;
+  const int j = int(blockIdx.x) / ch, c = int(blockIdx.x) % ch;
+  int64_t s = 0, w = n;
+  if (ch > 1) ob_chunk(n, ch, c, &s, &w);
+  const double* xj = j == 0 ? x0 : j == 1 ? x1 : x2;
+  const double* yj = j == 0 ? y0 : j == 1 ? y1 : y2;
+  const double v = ob_chunk_dot<kObU1>(xj + s, yj + s, w);
+  if (threadIdx.x == 0) part[j * kObMaxThreads + c] = v;
+}
+
+template <int WHICH, bool DIAG>
+__global__ void k_dot_openblas_fin(int64_t n, int nch, int nd, PcgState* S, const double* part) {
+  if (threadIdx.x != 0 || (WHICH != kObInit && S->done)) return;
+  const int ch = (n > 10000 && nch > 1) ? nch : 1;
+  double v[3];
+  ob_join(part, nd, ch, v);
+  ob_epilogue<WHICH, DIAG>(S, v);
 }
 
 // after the loop: the deferred x += α_{k-1} p_{k-1} of the last completed iteration
@@ -1049,6 +1106,7 @@ struct lspcg_solver {
   void *x = nullptr, *b = nullptr, *r = nullptr, *z = nullptr, *t = nullptr, *p = nullptr, *q = nullptr,
        *d = nullptr;
   bool split = false;   // current ext_spai schedule uses the split reductions (set_spai decides)
+  int exp = 0;          // LSPCG_EXP: bit mask of measurement-only kernel variants
   bool allow_split = true;  // LSPCG_SPLIT_REDUCE=0 keeps the last-arriver reductions
   int split_mode = -1;  // -1 auto (by grid size), 1 groups, 2 no groups (LSPCG_SPLIT_REDUCE)
   double* groups = nullptr;  // [GZ: <= 4096 x 2 dots x DD | GQ: <= 4096 x DD]
@@ -1089,6 +1147,7 @@ struct lspcg_solver {
   bool dia_ok = true;      // SELL-DIA views allowed (a batch of one-workgroup solves turns them off)
   int dot_order = LSPCG_DOT_COMPENSATED;  // lspcg_solver_set_dot_order
   int dot_threads = 1;
+  double* ob_part = nullptr;  // [3 dots x kObMaxThreads chunks] parity-mode chunk totals (k_dot_openblas_item)
 };
 
 // parity mode: every reducing launch is followed by k_dot_openblas, which rewrites its scalars
@@ -1098,10 +1157,22 @@ static void enqueue_ob(lspcg_solver* s, hipStream_t st, int nd, const void* x0, 
                        const void* y2 = nullptr) {
   if (s->dot_order != LSPCG_DOT_OPENBLAS) return;
   const int ch = (s->n > 10000 && s->dot_threads > 1) ? s->dot_threads : 1;
+  const auto* X0 = static_cast<const double*>(x0);
+  const auto* Y0 = static_cast<const double*>(y0);
+  const auto* X1 = static_cast<const double*>(x1);
+  const auto* Y1 = static_cast<const double*>(y1);
+  const auto* X2 = static_cast<const double*>(x2);
+  const auto* Y2 = static_cast<const double*>(y2);
+  if (s->n >= kObSplitN) {  // large n: one CU per (dot, chunk), then the ordered join
+    hipLaunchKernelGGL(k_dot_openblas_item<WHICH>, dim3(nd * ch), dim3(64), 0, st, s->n, s->dot_threads, s->S,
+                       s->ob_part, X0, Y0, X1, Y1, X2, Y2);
+    hipLaunchKernelGGL((k_dot_openblas_fin<WHICH, DIAG>), dim3(1), dim3(64), 0, st, s->n, s->dot_threads, nd, s->S,
+                       static_cast<const double*>(s->ob_part));
+    return;
+  }
   const int waves = std::min(kObBlock / 64, std::max(1, nd * ch));
   hipLaunchKernelGGL((k_dot_openblas<WHICH, DIAG>), dim3(1), dim3(64 * waves), 0, st, s->n, s->dot_threads, nd, s->S,
-                     static_cast<const double*>(x0), static_cast<const double*>(y0), static_cast<const double*>(x1),
-                     static_cast<const double*>(y1), static_cast<const double*>(x2), static_cast<const double*>(y2));
+                     X0, Y0, X1, Y1, X2, Y2);
 }
 
 // (Re)build the SELL copy of iteration view w (0 = A, 1 = L, 2 = Lᵀ); L and Lᵀ reuse A's
@@ -1271,8 +1342,12 @@ static int enqueue_iteration_split(lspcg_solver* s, hipStream_t st) {
                     EpiZG<T, SC>{z, r, d, T(s->eps), s->partials, s->ticket, gz, s->gsz_l}, st);
   if (rc) return rc;
   mark(s, st);
-  hipLaunchKernelGGL(k_update_p_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
-                     static_cast<const T*>(z), p, x);
+  if (s->exp & 1)  // experiment switch (LSPCG_EXP bit 0): x streamed with non-temporal loads / stores
+    hipLaunchKernelGGL((k_update_p_g<T, true>), dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz),
+                       s->ng_l, static_cast<const T*>(z), p, x);
+  else
+    hipLaunchKernelGGL(k_update_p_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
+                       static_cast<const T*>(z), p, x);
   mark(s, st);
   rc = launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQG<T>{q, p, s->partials, s->ticket, gq, s->gsz_a},
                     st);
@@ -1547,9 +1622,11 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
   LSPCG_HIP(hipEventCreate(&s->ev_t0));
   LSPCG_HIP(hipEventCreate(&s->ev_t1));
   LSPCG_HIP(hipMalloc(&s->flag, sizeof(int)));
+  LSPCG_HIP(hipMalloc(&s->ob_part, sizeof(double) * 3 * kObMaxThreads));
   if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SMALL_N")) s->small_n = std::max<int64_t>(0, std::atoll(e));
   if (const char* e = std::getenv("LSPCG_SMALL_SELL")) s->small_sell = e[0] != '0';
+  if (const char* e = std::getenv("LSPCG_EXP")) s->exp = std::atoi(e);
   if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
     s->allow_split = e[0] != '0';
     s->split_mode = std::atoi(e);
@@ -1635,14 +1712,23 @@ static int install_ic(lspcg_solver* s, const lspcg_mat* given, double* t_prec_ms
     LSPCG_CHECK(given->n == s->n && given->block_size == 1 && given->dtype == s->dtype &&
                     given->storage_dtype() == given->dtype,
                 LSPCG_ERR_ARG, "set_ic_factor: L must be a scalar CSR of the solver's size and dtype");
-    // lower triangular with the diagonal stored last in every row (host check of the pattern)
+    // lower triangular with the diagonal stored last in every row, and a nonzero diagonal (host
+    // check; scipy's spsolve_triangular, the reference's apply, raises LinAlgError "A is singular:
+    // zero entry on diagonal" there -- validate.py:344-419)
     std::vector<int32_t> rp(size_t(s->n) + 1), ci(size_t(std::max<int64_t>(given->nnzb, 1)));
-    if (int rc = lspcg_mat_copy_out(given, rp.data(), ci.data(), nullptr)) return rc;
+    std::vector<double> vd(given->dtype == LSPCG_F64 ? ci.size() : 0);
+    std::vector<float> vf(given->dtype == LSPCG_F32 ? ci.size() : 0);
+    void* vals = given->dtype == LSPCG_F64 ? static_cast<void*>(vd.data()) : static_cast<void*>(vf.data());
+    if (int rc = lspcg_mat_copy_out(given, rp.data(), ci.data(), vals)) return rc;
     for (int64_t i = 0; i < s->n; ++i) {
       bool ok = rp[i + 1] > rp[i] && ci[rp[i + 1] - 1] == i;
       for (int32_t p = rp[i]; ok && p < rp[i + 1] - 1; ++p) ok = ci[p] < ci[p + 1];
       LSPCG_CHECK(ok, LSPCG_ERR_FORMAT,
                   "set_ic_factor: row " + std::to_string(i) + " is not lower triangular with its diagonal last");
+      const int32_t dp = rp[i + 1] - 1;
+      const double dv = given->dtype == LSPCG_F64 ? vd[dp] : double(vf[dp]);
+      LSPCG_CHECK(dv != 0.0, LSPCG_ERR_SINGULAR,
+                  "set_ic_factor: A is singular: zero entry on diagonal (row " + std::to_string(i) + ")");
     }
   }
   hipStream_t cst = s->ctx->stream;
@@ -1927,6 +2013,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
     s->spat[w].release();
   }
   (void)hipFree(s->flag);
+  (void)hipFree(s->ob_part);
   (void)hipFree(s->dhist);
   (void)hipStreamDestroy(s->stream);
   delete s;

@@ -14,11 +14,15 @@ The device phases are the native ``lspcg_part_*`` calls (csrc/lspcg_part.hip: th
 kernels with own-row epilogues).  Exchanges go through ``torch.distributed``: the halo of a
 vector is ONE ``all_to_all_single`` whose receive buffer is the tail of the rank's extended
 vector (halo entries ordered by owner rank, so nothing is unpacked), and a dot product is an
-all-gather of every rank's 64 per-group compensated (sum, correction) pairs, summed on the host
-in rank-major order with the device's own double-double addition, then rounded -- every rank
-takes the same scalar, hence the same convergence decision.  With backend ``nccl`` (RCCL over
-xGMI) device buffers are exchanged directly; with ``gloo`` (tests: several ranks on one GPU)
-they are staged through host memory.  With one rank there is no exchange at all.
+all-gather of every rank's 64 per-group compensated (sum, correction) pairs into a device
+buffer, summed by one single-thread kernel in rank-major order with double-double addition
+(``lspcg_part_scalars``), then rounded -- every rank takes the same scalar, hence the same
+convergence decision.  The scalars, scipy's top-of-loop test and the iteration count live in
+the part's device state, so the host enqueues whole chunks of iterations and reads the state
+once per chunk (no device-to-host round trip per reduction; ``solve_host`` keeps the round-3
+host recurrence, bit-identical, for comparison).  With backend ``nccl`` (RCCL over xGMI) device
+buffers are exchanged directly; with ``gloo`` (tests: several ranks on one GPU) they are staged
+through host memory.  With one rank there is no exchange at all.
 """
 from __future__ import annotations
 
@@ -100,6 +104,14 @@ def build_plan(mats: Sequence[sp.csr_matrix], bounds: List[int], rank: int) -> H
     return HaloPlan(rank, list(bounds), halo.astype(np.int64), recv_counts, send_idx, send_counts)
 
 
+def plan_device(group=None) -> torch.device:
+    """Where the planning all-to-alls' tensors live: nccl (RCCL) moves device buffers only, so
+    this rank's GPU there; the host otherwise (gloo)."""
+    if _backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def build_plan_exchanged(rows: Sequence[sp.csr_matrix], bounds: List[int], rank: int, group=None) -> HaloPlan:
     """build_plan from this rank's OWN rows only (``rows``: the rank's row blocks, global column
     numbers): the halo comes from its own columns, and what it must send is what the other ranks
@@ -113,17 +125,19 @@ def build_plan_exchanged(rows: Sequence[sp.csr_matrix], bounds: List[int], rank:
     halo = need[(need < r0) | (need >= r1)].astype(np.int64)
     ho = np.searchsorted(bounds, halo, side="right") - 1
     recv_counts = [int(np.count_nonzero(ho == s)) for s in range(world)]
-    if world == 1 or _backend(group) is None:
+    be = _backend(group)
+    if world == 1 or be is None:
         send_counts = [0] * world
         return HaloPlan(rank, list(bounds), halo, recv_counts, np.zeros(0, np.int32), send_counts)
+    dev = plan_device(group)
     # my requests to owner s = my halo block owned by s (ascending); their counts first
-    req_counts = torch.tensor(recv_counts, dtype=torch.int64)
-    got_counts = torch.empty(world, dtype=torch.int64)
+    req_counts = torch.tensor(recv_counts, dtype=torch.int64, device=dev)
+    got_counts = torch.empty(world, dtype=torch.int64, device=dev)
     dist.all_to_all_single(got_counts, req_counts, group=group)
-    send_counts = [int(c) for c in got_counts]
-    got = torch.empty(int(sum(send_counts)), dtype=torch.int64)
-    dist.all_to_all_single(got, torch.from_numpy(halo), send_counts, recv_counts, group=group)
-    send_idx = (got.numpy() - r0).astype(np.int32)
+    send_counts = [int(c) for c in got_counts.cpu()]
+    got = torch.empty(int(sum(send_counts)), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(got, torch.from_numpy(halo).to(dev), send_counts, recv_counts, group=group)
+    send_idx = (got.cpu().numpy() - r0).astype(np.int32)
     return HaloPlan(rank, list(bounds), halo, recv_counts, send_idx, send_counts)
 
 
@@ -187,6 +201,23 @@ def exchange(recv: torch.Tensor, send: torch.Tensor, recv_counts: List[int], sen
     recv.copy_(rc)
 
 
+def gather_device(t: torch.Tensor, group=None) -> torch.Tensor:
+    """All ranks' copies of a small fixed-size device buffer, concatenated rank-major, on t's
+    device (nccl: one all-gather, no host copy; gloo: staged through the host)."""
+    be = _backend(group)
+    if be is None or dist.get_world_size(group) == 1:
+        return t.reshape(-1)
+    w = dist.get_world_size(group)
+    if be == "nccl" or not t.is_cuda:
+        out = torch.empty(w * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.reshape(-1), group=group)
+        return out
+    tc = t.reshape(-1).cpu()
+    parts = [torch.empty_like(tc) for _ in range(w)]
+    dist.all_gather(parts, tc, group=group)
+    return torch.cat(parts).to(t.device)
+
+
 def gather_rows(t: torch.Tensor, group=None) -> np.ndarray:
     """All ranks' copies of a small fixed-size buffer -> [world, t.numel()] on the host."""
     be = _backend(group)
@@ -229,11 +260,22 @@ class DistributedPCG:
         self._setup(blocks, A.shape[0], bounds, L is not None, epsilon, dtype, group, device)
 
     @classmethod
-    def from_row_blocks(cls, A_rows, L_rows=None, LT_rows=None, n: int = 0, bounds: Optional[List[int]] = None,
+    def from_row_blocks(cls, A_rows, L_rows=None, LT_rows=None, *, n: int, bounds: Sequence[int],
                         epsilon: float = 0.0, dtype=np.float64, group=None, device: Optional[torch.device] = None):
         """Each rank passes only ITS row blocks (global column numbers) of A, L and Lᵀ for the row
         partition ``bounds`` (partition_rows of the global row pointer): no rank ever holds the
-        global system; the halo plan is exchanged (build_plan_exchanged)."""
+        global system; the halo plan is exchanged (build_plan_exchanged).  ``n`` and ``bounds``
+        are required; L_rows and LT_rows come together; every block must be (own rows) x n."""
+        if (L_rows is None) != (LT_rows is None):
+            raise ValueError("from_row_blocks: pass both L_rows and LT_rows, or neither")
+        rank, world = cls._rank_world(group)
+        bounds = [int(b) for b in bounds]
+        if len(bounds) != world + 1 or bounds[0] != 0 or bounds[-1] != int(n):
+            raise ValueError(f"from_row_blocks: bounds must have {world + 1} entries from 0 to n = {n}")
+        shape = (bounds[rank + 1] - bounds[rank], int(n))
+        for name, M in (("A_rows", A_rows), ("L_rows", L_rows), ("LT_rows", LT_rows)):
+            if M is not None and tuple(M.shape) != shape:
+                raise ValueError(f"from_row_blocks: {name} has shape {tuple(M.shape)}, rank {rank} needs {shape}")
         self = cls.__new__(cls)
         self._setup([A_rows] + ([L_rows, LT_rows] if L_rows is not None else []), int(n), list(bounds),
                     L_rows is not None, epsilon, dtype, group, device)
@@ -287,6 +329,7 @@ class DistributedPCG:
         self.send = torch.zeros(max(int(sidx.size), 1), dtype=self.tdtype, device=dev)
         self.red = torch.zeros(GROUPS * 2 * 2, dtype=torch.float64, device=dev)
         self.has_L = L is not None
+        self.hist_dev = None
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -314,11 +357,87 @@ class DistributedPCG:
     def own_slice(self) -> slice:
         return slice(self.bounds[self.rank], self.bounds[self.rank + 1])
 
-    # ---- solve
-    def solve(self, b_global: np.ndarray, rtol: float = 1e-6, max_iter: int = 0,
-              return_history: bool = False):
+    # ---- solve (device-side scalar recurrence)
+    def _scalars(self, nd: int, phase: int):
+        g = gather_device(self.red[:GROUPS * nd * 2], self.group) if nd else None
+        _lib.call("lspcg_part_scalars", self.handle, _ptr(g) if g is not None else None, self.world, phase)
+        self._keep = g  # the gathered buffer stays alive until the kernel that reads it has run
+
+    def _iteration(self):
+        """One scipy cg iteration, enqueued without a host round trip; every scalar is read from and
+        written to the device state, and every update is skipped once the state says done."""
+        if self.has_L:
+            self._halo(self.r)
+            _lib.call("lspcg_part_lt", self.handle, _ptr(self.r), _ptr(self.t))
+            self._halo(self.t)
+            _lib.call("lspcg_part_l", self.handle, _ptr(self.t), _ptr(self.r), self.eps, _ptr(self.z), _ptr(self.red))
+            self._scalars(2, 1)  # ρ, ‖r_k‖², the top-of-loop test, β
+            z = self.z
+        else:
+            self._scalars(0, 2)
+            z = self.r
+        _lib.call("lspcg_part_update_p_dev", self.handle, _ptr(z), _ptr(self.p))
+        self._halo(self.p)
+        _lib.call("lspcg_part_a", self.handle, _ptr(self.p), _ptr(self.q), _ptr(self.red))
+        self._scalars(1, 3)  # π, α
+        _lib.call("lspcg_part_update_xr_dev", self.handle, _ptr(self.p), _ptr(self.q), _ptr(self.x), _ptr(self.r))
+        if not self.has_L:
+            _lib.call("lspcg_part_norms", self.handle, _ptr(self.r), _ptr(self.r), _ptr(self.red))
+            self._scalars(2, 4)
+
+    def _status(self):
+        it, done = C.c_int64(), C.c_int()
+        _lib.call("lspcg_part_status", self.handle, C.byref(it), C.byref(done))
+        return it.value, done.value
+
+    def solve(self, b_global: np.ndarray, rtol: float = 1e-6, max_iter: int = 0, return_history: bool = False,
+              max_chunk: int = 16):
         """scipy cg from x0 = 0 on the global rhs (every rank passes the same vector).  Returns
-        ``(iters, converged, x_own[, history])``; x_own: this rank's rows of the solution."""
+        ``(iters, converged, x_own[, history])``; x_own: this rank's rows of the solution.
+        Iterations are enqueued in chunks of 1, 2, 4, ... ``max_chunk`` with the device state read
+        once per chunk; iterations enqueued past convergence skip every update (predicated on the
+        state), so count, history and x are those of the converged iteration."""
+        p = self.plan
+        no = p.n_own
+        mi = int(max_iter) if max_iter and max_iter > 0 else self.n
+        b = torch.as_tensor(np.asarray(b_global)[self.own_slice()], dtype=self.tdtype).to(self.ctx.torch_device)
+        if self.hist_dev is None or self.hist_dev.numel() < mi + 2:
+            self.hist_dev = torch.empty(mi + 2, dtype=torch.float64, device=self.ctx.torch_device)
+        self.hist_dev.fill_(float("nan"))
+        self.x.zero_()
+        self.r.zero_()
+        self.r[:no] = b
+        self.p.zero_()
+        _lib.call("lspcg_part_state_init", self.handle, float(rtol), mi, _ptr(self.hist_dev))
+        _lib.call("lspcg_part_norms", self.handle, _ptr(self.r), _ptr(self.r), _ptr(self.red))
+        self._scalars(2, 0)
+        k, done = self._status()
+        if done == 4:  # ‖b‖ = 0: scipy returns b
+            self.x[:no] = b
+            out = (0, True, self.x[:no].clone())
+            return out + ((self.hist_dev[:1].cpu().numpy(),) if return_history else ())
+        chunk = 1
+        while not done:
+            for _ in range(chunk):
+                self._iteration()
+            k, done = self._status()
+            chunk = min(2 * chunk, int(max_chunk))
+        iters = mi if done == 3 else k
+        out = (iters, done == 1, self.x[:no].clone())
+        if return_history:
+            # a non-finite stop reports max_iter (pymathprim's count): NaN after the last written
+            # entry, iters + 1 entries, as lspcg_solver_solve does
+            h = np.full(iters + 1, np.nan)
+            got = self.hist_dev[: min(k, iters) + 1].cpu().numpy()
+            h[:got.size] = got
+            out = out + (h,)
+        return out
+
+    # ---- solve (host scalar recurrence: round 3's path, kept for comparison)
+    def solve_host(self, b_global: np.ndarray, rtol: float = 1e-6, max_iter: int = 0,
+                   return_history: bool = False):
+        """``solve`` with the scalars summed and tested on the host after every reduction (two
+        device-to-host round trips per iteration); the same bits as ``solve``."""
         p = self.plan
         no = p.n_own
         mi = int(max_iter) if max_iter and max_iter > 0 else self.n

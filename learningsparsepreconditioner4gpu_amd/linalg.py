@@ -87,7 +87,12 @@ class PreconditionedConjugateGradient:
             raise ValueError("set_ic_factor needs preconditioner='ic'")
         Ld = _as_device_matrix(L, self.dtype, 1, self.ctx)
         ms = C.c_double()
-        _lib.call("lspcg_solver_set_ic_factor", self.handle, Ld.handle, C.byref(ms))
+        try:
+            _lib.call("lspcg_solver_set_ic_factor", self.handle, Ld.handle, C.byref(ms))
+        except _lib.LspcgError as e:  # the reference's apply (spsolve_triangular) raises LinAlgError
+            if e.code == _lib.ERR_SINGULAR:
+                raise np.linalg.LinAlgError("A is singular: zero entry on diagonal.") from e
+            raise
         self.setup_time = ms.value / 1e3
         return self.setup_time
 

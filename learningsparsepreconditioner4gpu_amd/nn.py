@@ -210,6 +210,12 @@ class NodeEdgeProcessing(nn.Module):
         self._packed_version = None
         return res
 
+    def invalidate_graph(self):
+        """Forget the cached graph analysis and release the edge_index tensor it holds (the next
+        forward re-analyses).  Needed after an in-place change of edge_index that torch's version
+        counter does not see (.data, DLPack / CuPy views); also frees the held tensor."""
+        self._graph = None
+
     @torch.no_grad()
     def forward(self, node_attr: torch.Tensor, edge_index: torch.Tensor, edge_attr: torch.Tensor):
         """Returns ``(None, edge_out [E, b*b])``; the reference's node output is the identity
@@ -226,7 +232,9 @@ class NodeEdgeProcessing(nn.Module):
         assert ea.shape == (E, self.edge_in_features), (ea.shape, self.edge_in_features)
         out = torch.empty(E, self.edge_out_features, dtype=torch.float32, device=dev)
         # the graph's CSC is analysed once per edge_index (the tensor is held, so its address cannot
-        # be reused by another one while cached; an in-place change bumps its version)
+        # be reused by another one while cached; an in-place torch op bumps its version -- writes
+        # that bypass the version counter, through .data, DLPack or CuPy views, must be followed by
+        # invalidate_graph(), as lspcg_gnn.h asks for lspcg_gnn_set_graph)
         key = (ei.data_ptr(), ei._version, N, E)
         if self._graph is None or self._graph[0] != key or self._graph[1].data_ptr() != ei.data_ptr():
             _lib.call("lspcg_gnn_set_graph", self._handle, N, E, _ptr(ei))

@@ -377,11 +377,39 @@ def kuhn_dirichlet(n: int = 101, shift: float = 1e-4):
     return A, mask
 
 
+def renumber(A: sp.csr_matrix, mask: np.ndarray, order: str, seed: int = 0):
+    """``A`` and ``mask`` under a symmetric renumbering (P A Pᵀ, P mask): ``"rand"`` = a seeded random
+    permutation (no locality at all), ``"rcm"`` = that random permutation followed by reverse
+    Cuthill-McKee (scipy.sparse.csgraph) -- a banded but irregular ordering like an RCM-ordered
+    tet mesh's, with many distinct row-relative offsets per 64-row slice.  Same matrix, same nnz."""
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+
+    n = A.shape[0]
+    perm = np.random.default_rng(seed).permutation(n)
+    if order == "rcm":
+        Ar = sp.csr_matrix(A)[perm][:, perm]
+        perm = perm[reverse_cuthill_mckee(sp.csr_matrix(Ar), symmetric_mode=True)]
+    elif order != "rand":
+        raise ValueError(order)
+    B = sp.csr_matrix(sp.csr_matrix(A)[perm][:, perm])
+    B.sort_indices()
+    return B, mask[perm]
+
+
 def workload(name: str):
-    """Named systems: returns ``(A_raw, mask, node_features, block_size, edge_to_node)``."""
-    if name.startswith("kuhn"):
-        n = int(name[4:] or 101)
+    """Named systems: returns ``(A_raw, mask, node_features, block_size, edge_to_node)``.
+
+    ``kuhn<N>`` is the structured Kuhn-tet grid (N³ vertices, Dirichlet face); ``kuhn<N>rcm`` and
+    ``kuhn<N>rand`` are the same system renumbered (``renumber``): irregular orderings of the same
+    1M-row problem, the shape of the reference's tetgen meshes (datagen/heat_tetmesh.py)."""
+    import re
+
+    m = re.fullmatch(r"kuhn(\d*)(rcm|rand)?", name)
+    if m:
+        n = int(m.group(1) or 101)
         A, mask = kuhn_dirichlet(n)
+        if m.group(2):
+            A, mask = renumber(A, mask, m.group(2))
         return A, mask, None, 1, "disable"
     if name.startswith("poisson"):
         n = int(name[7:] or 256)

@@ -124,3 +124,35 @@ def test_gloo_halo_exchange_and_gather(world):
     for rank, ok_halo, tot in outs:
         assert ok_halo, rank
         assert tot == sum(range(1, world + 1))
+
+
+def test_plan_exchange_uses_device_tensors_on_nccl(monkeypatch):
+    """on a nccl (RCCL) group the planning all-to-alls move device tensors (RCCL has no
+    CPU backend), on gloo host tensors; the backend check is mocked (no GPU in the CPU suite), the
+    gloo path itself runs for real in test_gloo_plan_exchange."""
+    from learningsparsepreconditioner4gpu_amd import dist_pcg
+
+    monkeypatch.setattr(torch.cuda, "current_device", lambda: 3)
+    monkeypatch.setattr(dist_pcg, "_backend", lambda g: "nccl")
+    assert dist_pcg.plan_device() == torch.device("cuda", 3)
+    monkeypatch.setattr(dist_pcg, "_backend", lambda g: "gloo")
+    assert dist_pcg.plan_device() == torch.device("cpu")
+    src = open(dist_pcg.__file__).read().split("def build_plan_exchanged")[1].split("\ndef ")[0]
+    assert "dev = plan_device(group)" in src and src.count("device=dev") == 3 and ".to(dev)" in src
+
+
+def test_from_row_blocks_validates_its_blocks():
+    """n and bounds are required, L_rows needs LT_rows, and every block must be
+    (own rows) x n -- checked before any device work."""
+    from learningsparsepreconditioner4gpu_amd.dist_pcg import DistributedPCG
+
+    A = sp.csr_matrix(P.kuhn_laplacian(4))
+    n = A.shape[0]
+    with pytest.raises(TypeError):
+        DistributedPCG.from_row_blocks(A)  # n / bounds missing
+    with pytest.raises(ValueError, match="both L_rows and LT_rows"):
+        DistributedPCG.from_row_blocks(A, A, n=n, bounds=[0, n])
+    with pytest.raises(ValueError, match="bounds"):
+        DistributedPCG.from_row_blocks(A, n=n, bounds=[0, n - 1])
+    with pytest.raises(ValueError, match="shape"):
+        DistributedPCG.from_row_blocks(A[: n - 3], n=n, bounds=[0, n])

@@ -45,6 +45,8 @@ def test_world1_matches_oracle_and_single_gpu(gpu_ctx, kind, precond):
     L = L if precond == "ext_spai" else None
     d = DistributedPCG(A, L, EPS)
     it, conv, x, hist = d.solve(b, rtol=1e-8, return_history=True)
+    it_h, conv_h, x_h, hist_h = d.solve_host(b, rtol=1e-8, return_history=True)  # round 3's host recurrence
+    assert (it_h, conv_h) == (it, conv) and np.array_equal(hist_h, hist) and torch.equal(x_h, x)
     it_o, x_o, h_o = _oracle(A, L, b, 1e-8)
     assert conv and it == it_o
     np.testing.assert_allclose(hist, h_o[: it + 1], rtol=1e-12, atol=0)
@@ -68,6 +70,8 @@ def test_world1_fp32(gpu_ctx):
     A, L, b = _system("poisson")
     d = DistributedPCG(A, L, EPS, dtype=np.float32)
     it, conv, x = d.solve(b, rtol=1e-5)
+    it_h, conv_h, x_h = d.solve_host(b, rtol=1e-5)
+    assert (it_h, conv_h) == (it, conv) and torch.equal(x_h, x)
     ps = O.spai_operator(L.astype(np.float32), EPS)
     it_o, x_o, _ = O.pcg(A.astype(np.float32), b.astype(np.float32), ps, rtol=1e-5, dot="exact", dtype=np.float32)
     assert conv and it == it_o, (it, it_o)
@@ -101,8 +105,10 @@ def _rank(rank, world, port, kind, q, blocks=False):
     else:
         d = DistributedPCG(A, L, EPS)
     it, conv, x, hist = d.solve(b, rtol=1e-8, return_history=True)
+    it_h, conv_h, x_h, hist_h = d.solve_host(b, rtol=1e-8, return_history=True)
+    same = (it_h, conv_h) == (it, conv) and np.array_equal(hist_h, hist) and torch.equal(x_h, x)
     xg = d.gather_solution(x)
-    q.put((rank, it, bool(conv), xg, hist, d.plan.n_own, len(d.plan.halo)))
+    q.put((rank, it, bool(conv), xg, hist, d.plan.n_own, len(d.plan.halo), same))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -124,7 +130,8 @@ def test_multi_rank_matches_oracle(gpu_ctx, world, blocks):
     A, L, b = _system(kind)
     it_o, x_o, h_o = _oracle(A, L, b, 1e-8)
     assert sum(o[5] for o in outs) == A.shape[0] and all(o[6] > 0 for o in outs)
-    for rank, it, conv, xg, hist, _, _ in outs:
+    for rank, it, conv, xg, hist, _, _, same in outs:
+        assert same, rank  # device-side scalars = the host recurrence, bit for bit
         assert conv and it == it_o, (rank, it, it_o)
         np.testing.assert_allclose(hist, h_o[: it + 1], rtol=1e-12, atol=0)
         assert np.linalg.norm(xg - x_o) <= 1e-12 * np.linalg.norm(x_o)

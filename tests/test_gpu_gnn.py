@@ -59,6 +59,23 @@ def test_gnn_deterministic(gpu_ctx):
     assert torch.equal(a, b)
 
 
+def test_gnn_invalidate_graph_after_untracked_edit(gpu_ctx):
+    """ADVICE r3: edge_index edited in place through .data (no version bump) keeps the cached CSC;
+    invalidate_graph() makes the next forward re-analyse -- equal to a forward on a fresh copy."""
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+
+    A, mask, _ = P.poisson2d_grid(20, 17)
+    s = make_sample(A, mask).to("cuda")
+    _, gpu = _pair(s.x.shape[1], s.edge_attr.shape[1], 1, seed=2)
+    ei = s.edge_index.clone()
+    gpu(s.x, ei, s.edge_attr)
+    ei.data.copy_(s.edge_index.flip(0))  # the transposed graph: a different CSC, same tensor
+    gpu.invalidate_graph()
+    got = gpu(s.x, ei, s.edge_attr)[1]
+    want = gpu(s.x, s.edge_index.flip(0).contiguous(), s.edge_attr)[1]
+    assert torch.equal(got, want)
+
+
 def test_inference_step_and_pcg_end_to_end(gpu_ctx):
     """GNN -> device assembly of L (masked) -> ext_spai PCG vs oracle on the same L."""
     from learningsparsepreconditioner4gpu_amd.data import make_sample

@@ -173,3 +173,22 @@ def test_set_ic_factor_rejects_non_lower(gpu_ctx):
     with pytest.raises(_lib.LspcgError) as e:
         s.set_ic_factor(sp.csr_matrix(sp.triu(A)))
     assert e.value.code == _lib.ERR_FORMAT
+
+
+def test_set_ic_factor_zero_diagonal_raises_like_spsolve_triangular(gpu_ctx):
+    """a given factor with a zero diagonal entry is refused at installation with the
+    error the reference's apply raises (scipy spsolve_triangular: LinAlgError "A is singular"),
+    not a solve that stops as non-finite."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    A = sp.csr_matrix(P.kuhn_laplacian(4))
+    L = sp.csr_matrix(sp.tril(A))
+    L.sort_indices()
+    L.data[L.indptr[6] - 1] = 0.0  # row 5's diagonal (stored last), kept as an explicit zero
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ic")
+    with pytest.raises(np.linalg.LinAlgError, match="singular"):
+        s.set_ic_factor(L)
+    with pytest.raises(np.linalg.LinAlgError):  # the reference's own apply on the same factor
+        from scipy.sparse.linalg import spsolve_triangular
+
+        spsolve_triangular(L, np.ones(A.shape[0]), lower=True)

@@ -41,7 +41,7 @@ PY
 fi
 mkdir -p gpurun_out/matrix
 # WORKLOADS (env, optional): another list, e.g. WORKLOADS="kuhn61 kuhn81" EXTRA="--no-variants"
-for W in ${WORKLOADS:-kuhn101 kuhn151 kuhn201 elast poisson256 kuhn41 synthetic}; do
+for W in ${WORKLOADS:-kuhn101 kuhn101rcm kuhn101rand kuhn151 kuhn201 elast poisson256 kuhn41 synthetic}; do
   timeout -k 10 240 python bench.py --workload $W --no-cpu --steps 3 --warmup 1 $EXTRA > gpurun_out/matrix/$W.json 2> gpurun_out/matrix/$W.err || exit 1
   echo "$W done"
 done
