@@ -49,6 +49,7 @@ struct PcgState {
   int64_t max_iter;
   int32_t done;     // 0 running, 1 converged, 2 max_iter reached, 3 non-finite residual
   int32_t pad;
+  double rho_k;     // split schedule: ρ_k as UP summed it from KB's groups, read by UR (same bits)
 };
 
 template <typename T>
@@ -409,8 +410,11 @@ struct EpiQG {
 };
 
 // UP.  The first chunk's vector loads are issued before the group sums, so their latency overlaps
-// the scalar reduction instead of following it.
-template <typename T, bool NTX = false>
+// the scalar reduction instead of following it.  x is read and written with non-temporal accesses:
+// nothing else in the iteration touches it, and streaming it past the caches keeps its 8 B per row
+// out of the loop's Infinity-Cache working set (kuhn101: 69.2 vs 71.0 us per iteration,
+// tools/loop_ab.py, profiles/r4_loop_ab_v1.jsonl).
+template <typename T>
 __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S, const double* __restrict__ gz, int ngz,
                                                          const T* __restrict__ z, T* __restrict__ p,
                                                          T* __restrict__ x) {
@@ -427,8 +431,7 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
       if (j < nv) {
         zz[u] = reinterpret_cast<const V*>(z)[j];
         pp[u] = reinterpret_cast<const V*>(p)[j];
-        if constexpr (NTX) xx[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(x) + j);
-        else xx[u] = reinterpret_cast<const V*>(x)[j];
+        xx[u] = __builtin_nontemporal_load(reinterpret_cast<const V*>(x) + j);
       }
     }
   };
@@ -461,6 +464,7 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
       if (hist) hist[k] = double(tsqrt<T>(T(rr)));
     }
     if (code) S->done = code;
+    else S->rho_k = rho;
   }
   if (code) return;
   const bool first = k == 0;
@@ -472,10 +476,7 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
     for (int u = 0; u < kElemUnroll; ++u) {
       const int64_t j = j0 + u * ts;
       if (j < nv) {
-        if (!first) {
-          if constexpr (NTX) __builtin_nontemporal_store(xx[u] + alpha * pp[u], reinterpret_cast<V*>(x) + j);
-          else reinterpret_cast<V*>(x)[j] = xx[u] + alpha * pp[u];
-        }
+        if (!first) __builtin_nontemporal_store(xx[u] + alpha * pp[u], reinterpret_cast<V*>(x) + j);
         reinterpret_cast<V*>(p)[j] = first ? zz[u] : (pp[u] * beta) + zz[u];
       }
     }
@@ -487,11 +488,12 @@ __global__ void __launch_bounds__(kThreads) k_update_p_g(int64_t n, PcgState* S,
   }
 }
 
-// UR (first chunk loaded before the group sums, as in UP)
+// UR (first chunk loaded before the group sum, as in UP).  ρ_k is read from the state, where UP's
+// workgroup 0 stored the value every UP workgroup summed from KB's groups (one scalar load instead
+// of a second group sum here; the same bits).
 template <typename T>
-__global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S, const double* __restrict__ gz, int ngz,
-                                                         const double* __restrict__ gq, int ngq,
-                                                         const T* __restrict__ q, T* __restrict__ r) {
+__global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S, const double* __restrict__ gq,
+                                                         int ngq, const T* __restrict__ q, T* __restrict__ r) {
   using V = typename VecT<T>::type;
   constexpr int W = VecT<T>::W;
   const int64_t nv = n / W;
@@ -512,11 +514,10 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
   const int32_t done = S->done;
   const int64_t k = S->iter;
   const double rho_prev = S->rho;
-  double vz[2], vq[1];
-  group_sum_dd<2>(gz, ngz, vz);
+  const double rho = S->rho_k;
+  double vq[1];
   group_sum_dd<1>(gq, ngq, vq);
   if (done) return;
-  const double rho = round_to<T>(vz[0]);
   const double pq = round_to<T>(vq[0]);
   const T alpha = T(rho) / T(pq);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1106,7 +1107,6 @@ struct lspcg_solver {
   void *x = nullptr, *b = nullptr, *r = nullptr, *z = nullptr, *t = nullptr, *p = nullptr, *q = nullptr,
        *d = nullptr;
   bool split = false;   // current ext_spai schedule uses the split reductions (set_spai decides)
-  int exp = 0;          // LSPCG_EXP: bit mask of measurement-only kernel variants
   bool allow_split = true;  // LSPCG_SPLIT_REDUCE=0 keeps the last-arriver reductions
   int split_mode = -1;  // -1 auto (by grid size), 1 groups, 2 no groups (LSPCG_SPLIT_REDUCE)
   double* groups = nullptr;  // [GZ: <= 4096 x 2 dots x DD | GQ: <= 4096 x DD]
@@ -1342,19 +1342,15 @@ static int enqueue_iteration_split(lspcg_solver* s, hipStream_t st) {
                     EpiZG<T, SC>{z, r, d, T(s->eps), s->partials, s->ticket, gz, s->gsz_l}, st);
   if (rc) return rc;
   mark(s, st);
-  if (s->exp & 1)  // experiment switch (LSPCG_EXP bit 0): x streamed with non-temporal loads / stores
-    hipLaunchKernelGGL((k_update_p_g<T, true>), dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz),
-                       s->ng_l, static_cast<const T*>(z), p, x);
-  else
-    hipLaunchKernelGGL(k_update_p_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
-                       static_cast<const T*>(z), p, x);
+  hipLaunchKernelGGL(k_update_p_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
+                     static_cast<const T*>(z), p, x);
   mark(s, st);
   rc = launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQG<T>{q, p, s->partials, s->ticket, gq, s->gsz_a},
                     st);
   if (rc) return rc;
   mark(s, st);
-  hipLaunchKernelGGL(k_update_r_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
-                     static_cast<const double*>(gq), s->ng_a, static_cast<const T*>(q), r);
+  hipLaunchKernelGGL(k_update_r_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gq), s->ng_a,
+                     static_cast<const T*>(q), r);
   mark(s, st);
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
@@ -1626,7 +1622,6 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
   if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SMALL_N")) s->small_n = std::max<int64_t>(0, std::atoll(e));
   if (const char* e = std::getenv("LSPCG_SMALL_SELL")) s->small_sell = e[0] != '0';
-  if (const char* e = std::getenv("LSPCG_EXP")) s->exp = std::atoi(e);
   if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
     s->allow_split = e[0] != '0';
     s->split_mode = std::atoi(e);

@@ -223,13 +223,32 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
 
 // SELL-DIA SpMV (layout: see kSdiaMax): one wave = one 64-row slice of a 256-row tile, SB slots
 // per batch, every load of a batch issued before the first add (value loads and vector loads are
-// independent: the slot's offset is a scalar).
+// independent: the slot's offset is a scalar).  A slice's metadata -- its slot range (gp), its
+// whole 16-entry offset dictionary (one scalar block load: entries past the slice's count are
+// never used, masked lanes read x[base]) and its row masks -- is loaded in one batch, and the
+// first tile's batch before the prologue's state read: one memory latency before the value /
+// vector loads instead of three in a row (state, gp, dictionary).
 template <typename T, typename VT, int SB, int TH, int MINW, class Pro, class Gx, class Epi>
 __global__ void __launch_bounds__(TH, MINW) k_spmv_sdia(SdiaArgs<VT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int64_t ntiles = (a.n + TH - 1) / TH;
+  int32_t g0 = 0, g1 = 0;
+  unsigned msk = 0;
+  int32_t dct[kSdiaMax];
+  auto meta = [&](int64_t sl) {
+    g0 = a.gp[sl];
+    g1 = a.gp[sl + 1];
+    msk = gld(a.mask + kSellC * sl + lane);
+    const int32_t* dp = a.dict + kSdiaMax * sl;
+#pragma unroll
+    for (int j = 0; j < kSdiaMax; ++j) dct[j] = dp[j];
+  };
+  {
+    const int64_t s = int64_t(blockIdx.x) * (TH / 64) + w;
+    if (int64_t(blockIdx.x) < ntiles && s < a.ns) meta(s);
+  }
   if (pro.exit()) return;
   gx.prepare();
   epi.prepare();
@@ -240,10 +259,8 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sdia(SdiaArgs<VT> a, Pro pro,
     const int64_t s = tile * (TH / 64) + w;
     const int64_t i = tile * TH + threadIdx.x;
     if (s < a.ns) {  // wave-uniform
-      const int32_t g0 = a.gp[s];
-      const int nd = a.gp[s + 1] - g0;
-      const int32_t* dp = a.dict + kSdiaMax * s;
-      const unsigned msk = gld(a.mask + kSellC * s + lane);
+      if (tile != int64_t(blockIdx.x)) meta(s);
+      const int nd = g1 - g0;
       const int32_t base = int32_t(s * kSellC);
       const int32_t row = base + lane;
       T acc = T(0);
@@ -259,11 +276,10 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sdia(SdiaArgs<VT> a, Pro pro,
         bool m[SB];
 #pragma unroll
         for (int u = 0; u < SB; ++u) {
-          const int j = min(j0 + u, nd - 1);
-          const int off = dp[j];  // scalar
-          m[u] = (j0 + u < nd) && ((msk >> (j0 + u)) & 1u);
-          const int32_t c = m[u] ? row + off : base;
-          v[u] = gld(a.vals + kSellC * int64_t(g0 + j) + lane);
+          const int j = j0 + u;
+          m[u] = (j < nd) && ((msk >> j) & 1u);
+          const int32_t c = m[u] ? row + dct[j] : base;
+          v[u] = gld(a.vals + kSellC * int64_t(g0 + min(j, nd - 1)) + lane);
           xv[u] = gx(c);
         }
 #pragma unroll

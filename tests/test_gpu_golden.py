@@ -181,6 +181,26 @@ def test_infer_main_parity_mode_reference_counts(gpu_ctx, tmp_path):
         assert got == [float(z[f"{i}__{col}"]) for i in range(k)], key
 
 
+def test_infer_main_cpu_rows_reference_counts(gpu_ctx, tmp_path):
+    """--cpu-rows: the reference's host rows (Neural, PCG-none-cpu, PCG-diagonal-cpu; scipy
+    restatement on the host copies of the device-assembled A and L) beside the GPU rows, with the
+    counts the reference's own infer rows recorded on folder_free (infer_folder_free.npz)."""
+    import pandas as pd
+
+    from learningsparsepreconditioner4gpu_amd.infer import main
+
+    z = np.load(GOLDEN / "infer_folder_free.npz")
+    k = int(z["len"])
+    main(["--folder", str(GOLDEN / "folder_free"), "--rtol", "1e-8", "--warmup", "1", "--out-dir", str(tmp_path),
+          "--baselines", "none,diagonal", "--cpu-rows"])
+    alls = pd.read_csv(tmp_path / "all_infer_folder_free_8.csv")
+    for key, col in (("Neural", "ext_spai"), ("PCG-none-cpu", "none"), ("PCG-diagonal-cpu", "diagonal")):
+        got = alls[alls["Key"] == key]["#Iteration"].tolist()
+        assert got == [float(z[f"{i}__{col}"]) for i in range(k)], key
+    keys = set(pd.read_csv(tmp_path / "infer_folder_free_8.csv")["Key"])
+    assert {"Neural", "Neural+CUDA", "PCG-none-cpu", "PCG-diagonal-cpu", "PCG-none-cuda", "PCG-diagonal-cuda"} <= keys
+
+
 @pytest.mark.parametrize("batch", ["1", "4"])
 def test_infer_main_writes_baseline_rows(gpu_ctx, tmp_path, batch):
     """infer CLI on an on-disk dataset: Neural+CUDA and PCG-{none,diagonal,ainv,ic}-cuda rows (the

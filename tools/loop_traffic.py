@@ -15,9 +15,9 @@ import sys
 
 KERNELS = {"KA t=L^T r": r"k_spmv_s(?:ell|dia)<double, float.*EpiT<double, false>",
            "KB z=L t+eps r, rho": r"k_spmv_s(?:ell|dia)<double, float.*EpiZG<double, false>",
-           "UP p, x": r"k_update_p_g<double>",
+           "UP p, x": r"k_update_p_g<double",
            "KC q=A p, pi": r"k_spmv_s(?:ell|dia)<double, float.*EpiQG<double>",
-           "UR r": r"k_update_r_g<double>"}
+           "UR r": r"k_update_r_g<double"}
 
 
 def per_dispatch(tag, counter):

@@ -32,8 +32,8 @@ def main(path):
     import re
     loop = {"KA t=L^T r": r"k_spmv_s(?:ell|dia)<double, float.*EpiT<double, false>",
             "KB z=L t+eps r, rho": r"k_spmv_s(?:ell|dia)<double, float.*EpiZG<double, false>",
-            "UP p, x": r"k_update_p_g<double>", "KC q=A p, pi": r"k_spmv_s(?:ell|dia)<double, float.*EpiQG<double>",
-            "UR r": r"k_update_r_g<double>"}
+            "UP p, x": r"k_update_p_g<double", "KC q=A p, pi": r"k_spmv_s(?:ell|dia)<double, float.*EpiQG<double>",
+            "UR r": r"k_update_r_g<double"}
     # the bench system's launches only: the largest grid of each kind (smaller systems -- C1, C5 --
     # launch smaller grids), without the predicated launches that exit at once after convergence
     # (chunk tails: < 1/3 of that grid's median)
@@ -46,11 +46,19 @@ def main(path):
     for r in rows:
         for k, pat in loop.items():
             if re.search(pat, r["Kernel_Name"]):
-                lk.setdefault(k, []).append((grid(r), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3))
+                lk.setdefault(k, []).append((grid(r), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3,
+                                             r["Kernel_Name"]))
     out = {}
     for k, v in lk.items():
         g = max(x[0] for x in v)
-        d = [x[1] for x in v if x[0] == g]
+        # the bench system's own kernel: the most frequent name at that grid (the irregular leg's
+        # system has the same n but runs the SELL-64 kernels, and far fewer launches)
+        names = {}
+        for x in v:
+            if x[0] == g:
+                names[x[2]] = names.get(x[2], 0) + 1
+        top = max(names, key=names.get)
+        d = [x[1] for x in v if x[0] == g and x[2] == top]
         m = med(d)
         d = [x for x in d if x >= m / 3]
         out[k] = {"grid": g, "n": len(d), "avg": avg(d), "median": med(d)}
