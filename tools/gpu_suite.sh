@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU evidence run: full GPU suite, smoke, default bench (optionally rocprofv3 kernel stats and
 # the roofline SpMV's PMC traffic).  Usage (on the box, via gpurun):
-#   bash tools/gpu_suite.sh TAG [tests] [bench] [prof] [traffic]
+#   bash tools/gpu_suite.sh TAG [tests] [bench] [prof] [traffic] [looptraffic] [gnn] [t=FILES] [ab=JSON]
 # Every GPU step runs under its own time limit; the script stops at the first failing step.
 set -o pipefail
 tag=$1; shift
@@ -25,10 +25,18 @@ import json; d=json.load(open('$out/bench.json')); print(d['value'], d['pcg_iter
       f=$(find "gpurun_out/prof_$tag" -name "*kernel_stats.csv" | head -1); cp "$f" "$out/kernel_stats.csv"
       # the per-dispatch trace is tens of MB: keep the roofline SpMV's launches and the loop's
       python3 tools/trace_split.py "$(find "gpurun_out/prof_$tag" -name "*kernel_trace.csv" | head -1)" > "$out/trace_split.json" 2>&1 || true
-      find "gpurun_out/prof_$tag" -name "*kernel_trace.csv" -delete ;;
+      find "gpurun_out/prof_$tag" -name "*kernel_trace.csv" -delete
+      python3 -c "import json; d = json.load(open('$out/trace_split.json')); print(json.dumps(d.get('pcg_loop_kernels_us')))" || true ;;
     traffic)
       bash tools/spmv_traffic.sh "$tag" || exit $?
       cat "gpurun_out/traffic_$tag/summary.json" ;;
+    looptraffic)  # the PCG loop's five launches: FETCH_SIZE / WRITE_SIZE passes over a short bench
+      bash tools/pmc_run.sh "$tag" bench.py --steps 1 --warmup 1 --no-cpu --no-variants -- FETCH_SIZE WRITE_SIZE || exit $?
+      python3 tools/loop_traffic.py "$tag" 1 > "$out/pcg_loop_traffic.json" && cat "$out/pcg_loop_traffic.json"
+      find "gpurun_out/pmc_$tag" -name "*.csv" -size +2M -delete ;;
+    ab=*)  # interleaved loop A/B: ab='{"base": {}, "x": {"ENV": "1"}}'
+      timeout -k 10 400 python -u tools/loop_ab.py "${s#ab=}" kuhn101 11 "$out/loop_ab.jsonl" > "$out/loop_ab.txt" 2>&1 || exit $?
+      cat "$out/loop_ab.txt" ;;
     gnn)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_gnn.py -x -q --timeout 200 --timeout-method thread > "$out/gnn_tests.txt" 2>&1
       rc=$?; tail -2 "$out/gnn_tests.txt"; [ $rc -eq 0 ] || exit $rc
