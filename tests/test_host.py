@@ -180,3 +180,27 @@ def test_heat_bunny_c3_stand_in():
     # same seed, same system
     A2, _, f2 = P.heat_bunny()
     assert (A != A2).nnz == 0 and np.array_equal(feats, f2)
+
+
+@pytest.mark.parametrize("order", ["rcm", "rand"])
+def test_renumbered_workloads_are_the_same_system(order):
+    """problems.workload('kuhn<N>rcm' / 'kuhn<N>rand'): P A Pᵀ and P mask of the structured system
+    (same nnz, same spectrum-defining entries), seeded, and -- for rcm -- banded with many more
+    distinct row-relative offsets per 64-row slice than the structured ordering (SELL-DIA's 16)."""
+    import bench
+
+    A0, m0, _, _, _ = P.workload("kuhn17")
+    A1, m1, f, bs, e2n = P.workload(f"kuhn17{order}")
+    A2, _, _, _, _ = P.workload(f"kuhn17{order}")
+    assert (A1 != A2).nnz == 0 and bs == 1 and f is None
+    assert A1.nnz == A0.nnz and A1.shape == A0.shape and m1.sum() == m0.sum()
+    assert np.allclose(np.sort(A1.diagonal()), np.sort(A0.diagonal()))
+    assert np.array_equal(np.sort(A1.data), np.sort(A0.data))
+    assert np.array_equal(np.sort(np.diff(A1.indptr)), np.sort(np.diff(A0.indptr)))
+    d0 = bench.dia_counts(A0.indptr, A0.indices)
+    d1 = bench.dia_counts(A1.indptr, A1.indices)
+    assert d0.max() <= 16 and d1.mean() > d0.mean()
+    rows = np.repeat(np.arange(A1.shape[0]), np.diff(A1.indptr))
+    bw1 = np.abs(A1.indices - rows).max()
+    if order == "rcm":
+        assert bw1 < A1.shape[0] // 4
