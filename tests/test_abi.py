@@ -58,3 +58,24 @@ def test_product_never_imports_oracle():
     for f in pkg.rglob("*.py"):
         src = f.read_text()
         assert not re.search(r"^\s*(from|import)\s+oracle\b", src, flags=re.M), f
+
+
+def test_host_solver_only_in_cpu_rows():
+    """The only host (scipy) CG in the package is cpu_rows.py -- the reference's own scipy
+    restatement behind infer's opt-in --cpu-rows comparison rows and the *_scipy names of
+    validate.py; no device-path module calls it or falls back to it."""
+    pkg = ROOT / "learningsparsepreconditioner4gpu_amd"
+    users = []
+    for f in sorted(pkg.rglob("*.py")):
+        src = f.read_text()
+        # a host CG solve (scipy's cg) or a route to one (cpu_rows); dataset.FolderWriter's splu is the
+        # offline dataset writer's reference solution (datagen_helper.py), not a solver path
+        if re.search(r"import[^\n]*\bcg\b|\bcg\(|\bcpu_rows\b", src):
+            users.append(f.name)
+    assert set(users) <= {"cpu_rows.py", "validate.py", "infer.py"}, users
+    vsrc = (pkg / "validate.py").read_text()
+    # validate only re-exports the host names; its device functions never reach them
+    body = vsrc.split("from .cpu_rows import")[1]
+    assert "get_pcg_iter_time_scipy" not in body.split(")", 1)[1]
+    isrc = (pkg / "infer.py").read_text()
+    assert len(re.findall(r"cpu_rows\.\w+\(", isrc)) == 2 and "if args.cpu_rows" in isrc
