@@ -151,9 +151,17 @@ def rhs_for(rhs: str, mask: np.ndarray, sample: Optional[GraphSample] = None) ->
     raise ValueError(f"Unknown rhs type: {rhs}")
 
 
+def _rhs(rhs: str, i: int, s: GraphSample, rhs_vectors: Optional[Dict[int, np.ndarray]]) -> np.ndarray:
+    """Sample i's right-hand side: the shared one when given (infer.py:296-307 builds r once per
+    sample and solves every row with it), else rhs_for."""
+    if rhs_vectors is not None:
+        return rhs_vectors[i]
+    return rhs_for(rhs, s.mask.cpu().numpy(), s)
+
+
 def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: float = 1e-6, repeat: int = 1,
         rhs: str = "mask", warmup: int = 20, concurrency: int = 1, batch: int = 1, dot_order: str = "compensated",
-        dot_threads: int = 1) -> List[SolveRecord]:
+        dot_threads: int = 1, rhs_vectors: Optional[Dict[int, np.ndarray]] = None) -> List[SolveRecord]:
     """The ``Neural+CUDA`` row of infer.py:278-331 (GNN -> L, A; ext_spai PCG).  ``concurrency``
     > 1 keeps that many solves of this rank in flight at once (run_sharded_concurrent): the same
     iterates and counts, a higher batch throughput on the reference's mid-size systems.  ``batch``
@@ -182,7 +190,7 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
         prec /= repeat
         L, _ = ws.inference_step(s)
         A = ws.system_matrix(s)
-        r = rhs_for(rhs, s.mask.cpu().numpy(), s)
+        r = _rhs(rhs, i, s, rhs_vectors)
         return i, A, L, r, prec
 
     def finish(job) -> SolveRecord:
@@ -215,7 +223,7 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
             prec += dt
         prec /= repeat * len(items)
         Ls, _ = ws.inference_step_batch(ss)
-        return [(i, ws.system_matrix(s), L, rhs_for(rhs, s.mask.cpu().numpy(), s), prec)
+        return [(i, ws.system_matrix(s), L, _rhs(rhs, i, s, rhs_vectors), prec)
                 for i, s, L in zip(items, ss, Ls)]
 
     weights = [float(s.edge_index.shape[1]) for s in samples]
@@ -228,7 +236,7 @@ def run(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: floa
 
 def run_baseline(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, method: str, rtol: float = 1e-6,
                  repeat: int = 1, rhs: str = "mask", dot_order: str = "compensated",
-                 dot_threads: int = 1) -> List[SolveRecord]:
+                 dot_threads: int = 1, rhs_vectors: Optional[Dict[int, np.ndarray]] = None) -> List[SolveRecord]:
     """The ``PCG-{method}-cuda`` rows (infer.py:310-321: get_cg_iter_time with method none /
     diagonal / ainv / ic on the same A and rhs).  A non-converged solve raises RuntimeError in
     the reference (caught at :363); here its row is NaN and left out of the statistics."""
@@ -237,7 +245,7 @@ def run_baseline(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, m
     def solve(i: int) -> SolveRecord:
         s = samples[i].to(dev)
         A = ws.system_matrix(s)
-        r = rhs_for(rhs, s.mask.cpu().numpy(), s)
+        r = _rhs(rhs, i, s, rhs_vectors)
         info = {}
         try:
             it, prec, sol = get_cg_iter_time(A, r, rtol=rtol, repeat=repeat, method=method, info=info,
@@ -254,7 +262,8 @@ def run_baseline(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, m
 
 def run_cpu_rows(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, rtol: float = 1e-6, repeat: int = 1,
                  rhs: str = "mask", methods: Sequence[str] = ("none", "diagonal"),
-                 threads: Optional[int] = None) -> Dict[str, List[SolveRecord]]:
+                 threads: Optional[int] = None,
+                 rhs_vectors: Optional[Dict[int, np.ndarray]] = None) -> Dict[str, List[SolveRecord]]:
     """The reference's host rows (infer.py:310-330 with device="cpu"): ``Neural`` (ext_spai or its
     scaled variant on the host copies of A and of the GNN's L) and ``PCG-{method}-cpu`` for
     ``methods`` (none / diagonal), each from cpu_rows (the reference's scipy restatement; its
@@ -276,7 +285,7 @@ def run_cpu_rows(samples: Sequence[GraphSample], ws: SimpleInferenceWorkspace, r
         L, _ = ws.inference_step(s)
         A = ws.system_matrix(s)
         Ah, Lh = A.to_scipy().tocsr(), L.to_scipy().tocsr()
-        r = rhs_for(rhs, s.mask.cpu().numpy(), s)
+        r = _rhs(rhs, i, s, rhs_vectors)
         it, sol = cpu_rows.neural_row(Ah, r, Lh, ws.epsilon, rtol, scaled=scaled, repeat=repeat, threads=threads)
         recs = [SolveRecord(index=i, iters=it, rel_res=float("nan"), t_prec=prec, t_solve=sol, n=A.n, nnz=A.nnz,
                             converged=it < A.n)]
@@ -360,15 +369,19 @@ def main(argv=None):
                  epsilon=args.epsilon, seed=0)
     rows = {}
     dots = dict(dot_order=args.dot_order, dot_threads=args.dot_threads)
+    # one right-hand side per sample, shared by every row (infer.py:296-307); only "random" draws
+    rhs_vectors = ({i: rhs_for(args.rhs, s.mask.numpy(), s) for i, s in enumerate(samples)}
+                   if args.rhs == "random" else None)
     for m in [b for b in args.baselines.split(",") if b]:
-        rows[f"PCG-{m}-cuda"] = run_baseline(samples, ws, m, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, **dots)
+        rows[f"PCG-{m}-cuda"] = run_baseline(samples, ws, m, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs,
+                                             rhs_vectors=rhs_vectors, **dots)
     key = "Neural+HIP" if args.hip_key else "Neural+CUDA"
     rows[key] = run(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs, warmup=args.warmup,
-                    concurrency=args.concurrency, batch=args.batch, **dots)
+                    concurrency=args.concurrency, batch=args.batch, rhs_vectors=rhs_vectors, **dots)
     recs = rows[key]
     if args.cpu_rows and (not dist.is_initialized() or dist.get_rank() == 0):
         rows.update(run_cpu_rows(samples, ws, rtol=args.rtol, repeat=args.repeat, rhs=args.rhs,
-                                 threads=args.cpu_threads))
+                                 threads=args.cpu_threads, rhs_vectors=rhs_vectors))
     if not dist.is_initialized() or dist.get_rank() == 0:
         stats = Timestat()
         for key, rs in rows.items():
