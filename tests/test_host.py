@@ -204,3 +204,22 @@ def test_renumbered_workloads_are_the_same_system(order):
     bw1 = np.abs(A1.indices - rows).max()
     if order == "rcm":
         assert bw1 < A1.shape[0] // 4
+
+
+def test_sell_format_model_matches_layouts():
+    """bench.sell_kind / sell_format_bytes restate the SELL-64 build's choice and bytes
+    (csrc/lspcg_sell.hpp): the Kuhn grid takes SELL-DIA (<= 16 offsets per slice; 64 value slots
+    per distinct offset + 128 B of row masks + a 64-B dictionary per slice), its RCM renumbering
+    16-bit offsets (4-entry groups, value + 2-B column per slot), a random renumbering int32."""
+    import bench
+
+    A, _, _, _, _ = P.workload("kuhn17")
+    ns = (A.shape[0] + 63) // 64
+    assert bench.sell_kind(A.indptr, A.indices) == 1
+    d = bench.dia_counts(A.indptr, A.indices)
+    assert bench.sell_format_bytes(A.indptr, A.indices, 1, 4) == 64 * int(d.sum()) * 4 + ns * (128 + 64)
+    R, _, _, _, _ = P.workload("kuhn17rcm")
+    assert bench.sell_kind(R.indptr, R.indices) == 16
+    assert bench.sell_format_bytes(R.indptr, R.indices, 16, 4) == bench.sell_slots(R.indptr) * 6
+    X, _, _, _, _ = P.workload("kuhn41rand")
+    assert bench.sell_kind(X.indptr, X.indices) == 32
