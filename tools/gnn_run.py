@@ -13,6 +13,7 @@ def main():
     ap.add_argument("--workload", default="kuhn101")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--idle-ms", type=float, default=0.0, help="host sleep before each wall-clock call")
+    ap.add_argument("--dump", default="", help="save the forward's output here (.npy)")
     args = ap.parse_args()
     sys.path.insert(0, ".")
     from learningsparsepreconditioner4gpu_amd import problems as P
@@ -44,6 +45,9 @@ def main():
         torch.cuda.synchronize()
         walls.append((time.perf_counter() - t0) * 1e3)
         pre.append((t1 - t0) * 1e3)
+    if args.dump:
+        import numpy as np
+        np.save(args.dump, ws.forward(d.x, d.edge_index, d.edge_attr).float().cpu().numpy())
     print(json.dumps({"workload": args.workload, "edges": int(d.edge_index.shape[1]), "forward_ms": fwd_ms,
                       "wall_ms": sorted(walls)[len(walls) // 2], "host_return_ms": sorted(pre)[len(pre) // 2]}))
 
