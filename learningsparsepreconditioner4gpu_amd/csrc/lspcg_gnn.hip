@@ -55,14 +55,9 @@ __host__ __device__ constexpr int frag_size(int s1) { return s1 * 64 + 5 * 256; 
 // reference's (tests/test_gpu_gnn.py, 1e-5).  Two values at a time in packed fp32
 // (v_pk_fma_f32); |v| and the clamp are one v_med3_f32 with the abs modifier.
 using f2 = float __attribute__((ext_vector_type(2)));
-#ifdef LSPCG_GELU_SCALAR
-__device__ __forceinline__ f2 pfma(f2 a, f2 b, float c) {
-  return (f2){__builtin_fmaf(a.x, b.x, c), __builtin_fmaf(a.y, b.y, c)};
-}
-#else
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, float c) { return __builtin_elementwise_fma(a, b, (f2)(c)); }
-#endif
 constexpr float kGeluClamp = 5.75f;
+constexpr int kGeluDeg = 8;
 constexpr float kGeluC[9] = {-9.999883175e-01f, -1.151304364e+00f, -4.583674073e-01f, -5.401911587e-02f,
                              8.511481807e-03f,  -9.210868739e-04f, 5.780859647e-05f,  -1.258388238e-06f,
                              -3.159780704e-08f};
@@ -81,10 +76,10 @@ __device__ __forceinline__ void gelu_n(f2 (&v)[K]) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     a[k] = (f2){abs_clamp(v[k].x), abs_clamp(v[k].y)};
-    p[k] = pfma(a[k], (f2)(kGeluC[8]), kGeluC[7]);
+    p[k] = pfma(a[k], (f2)(kGeluC[kGeluDeg]), kGeluC[kGeluDeg - 1]);
   }
 #pragma unroll
-  for (int c = 6; c >= 0; --c)
+  for (int c = kGeluDeg - 2; c >= 0; --c)
 #pragma unroll
     for (int k = 0; k < K; ++k) p[k] = pfma(a[k], p[k], kGeluC[c]);
 #pragma unroll
@@ -474,24 +469,6 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
         if constexpr (S1E > 0) qe = perm[kn];
       }
       // LayerNorm(48) statistics: 12 values per lane, 4 lanes per edge, packed fp32 pairs
-#ifdef LSPCG_LN_SCALAR
-      float v[12] = {xd.x, xd.y, xd.z, xd.w, xs.x, xs.y, xs.z, xs.w, ea.x, ea.y, ea.z, ea.w};
-      float sp[2], qp[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-        sp[c] = ((v[c] + v[2 + c]) + (v[4 + c] + v[6 + c])) + (v[8 + c] + v[10 + c]);
-      const float mean = quad_sum(sp[0] + sp[1]) * (1.0f / 48.0f);
-      qp[0] = 0.f;
-      qp[1] = 0.f;
-#pragma unroll
-      for (int j = 0; j < 12; ++j) {
-        v[j] -= mean;
-        qp[j & 1] = __builtin_fmaf(v[j], v[j], qp[j & 1]);
-      }
-      const float rstd = __builtin_amdgcn_rsqf(quad_sum(qp[0] + qp[1]) * (1.0f / 48.0f) + 1e-5f);
-#pragma unroll
-      for (int j = 0; j < 12; ++j) v[j] *= rstd;
-#else
       f2 w[6] = {(f2){xd.x, xd.y}, (f2){xd.z, xd.w}, (f2){xs.x, xs.y},
                  (f2){xs.z, xs.w}, (f2){ea.x, ea.y}, (f2){ea.z, ea.w}};
       const f2 s2 = ((w[0] + w[1]) + (w[2] + w[3])) + (w[4] + w[5]);
@@ -510,7 +487,6 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
         v[2 * j] = w[j].x;
         v[2 * j + 1] = w[j].y;
       }
-#endif
       f4 m, u;
       ff2_48(fmsg, fedge, v, lane, m, u);
       if (edge_res) u += ea;

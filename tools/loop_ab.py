@@ -8,7 +8,8 @@ switches are read at solver creation), then runs `rounds` rounds of one solve pe
 turn (A B A B ...: box drift hits every variant alike) and reports, per variant, the median
 microseconds per iteration, the iteration count and whether x and the residual history are
 bit-identical to the first variant's.  With LOOP_AB_KERNELS=1 it also reports the per-launch
-times of the loop (lspcg_solver_time_kernels, direct launches).
+times of the loop (lspcg_solver_time_kernels, direct launches); LOOP_AB_MAXIT caps the iterations
+of every solve (timing-only variants whose arithmetic is not the solver's).
 """
 import json
 import os
@@ -54,7 +55,8 @@ def main():
     for r in range(rounds + 1):
         for name, sv in solvers.items():
             x = torch.zeros_like(b)
-            it, conv, sec, hist = sv.solve(b, x, rtol=1e-8, return_history=True)
+            it, conv, sec, hist = sv.solve(b, x, rtol=1e-8, max_iter=int(os.environ.get("LOOP_AB_MAXIT", "0")),
+                                           return_history=True)
             if r > 0:
                 times[name].append(sec / it * 1e6)
             res[name] = (it, x, hist)
