@@ -1109,10 +1109,6 @@ struct lspcg_solver {
   void *x = nullptr, *b = nullptr, *r = nullptr, *z = nullptr, *t = nullptr, *p = nullptr, *q = nullptr,
        *d = nullptr;
   bool split = false;   // current ext_spai schedule uses the split reductions (set_spai decides)
-  // SELL-DIA value streams loaded non-temporally, bit w = view w (0 A in KC, 1 L in KB, 2 Lt in KA):
-  // L and Lt by default -- they are read once per iteration, and keeping them out of the caches
-  // leaves the 256 MiB MALL to A and the vectors (LSPCG_SELL_NT overrides)
-  int nt_vals = 6;
   bool allow_split = true;  // LSPCG_SPLIT_REDUCE=0 keeps the last-arriver reductions
   int split_mode = -1;  // -1 auto (by grid size), 1 groups, 2 no groups (LSPCG_SPLIT_REDUCE)
   double* groups = nullptr;  // [GZ: <= 4096 x 2 dots x DD | GQ: <= 4096 x DD]
@@ -1241,14 +1237,13 @@ static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view) {
 template <typename T, class Gx, class Pro, class Epi>
 static int launch_it_gx(lspcg_solver* s, int w, Gx gx, Pro pro, Epi epi, hipStream_t st) {
   if (const SellPattern* P = s->sp[w]) {
-    const int nt = (s->nt_vals >> w) & 1;
     if constexpr (sizeof(T) == 8) {
       if (s->svd[w] == LSPCG_F32) {
-        launch_spmv_sell_cfg<T, float>(*P, s->sv[w], gx, pro, epi, st, false, nt);
+        launch_spmv_sell_cfg<T, float>(*P, s->sv[w], gx, pro, epi, st);
         return LSPCG_OK;
       }
     }
-    launch_spmv_sell_cfg<T, T>(*P, s->sv[w], gx, pro, epi, st, false, nt);
+    launch_spmv_sell_cfg<T, T>(*P, s->sv[w], gx, pro, epi, st);
     return LSPCG_OK;
   }
   const lspcg_mat* V = w == 0 ? &s->Av : (w == 1 ? &s->Lv : &s->LTv);
@@ -1629,7 +1624,6 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
   if (const char* e = std::getenv("LSPCG_NO_SELL")) s->use_sell = e[0] == '0';
   if (const char* e = std::getenv("LSPCG_SMALL_N")) s->small_n = std::max<int64_t>(0, std::atoll(e));
   if (const char* e = std::getenv("LSPCG_SMALL_SELL")) s->small_sell = e[0] != '0';
-  if (const char* e = std::getenv("LSPCG_SELL_NT")) s->nt_vals = std::atoi(e) & 7;
   if (const char* e = std::getenv("LSPCG_SPLIT_REDUCE")) {
     s->allow_split = e[0] != '0';
     s->split_mode = std::atoi(e);

@@ -98,7 +98,6 @@ struct SdiaArgs {
   const uint16_t* mask;
   const int32_t* dict;
   const VT* vals;
-  int nt = 0;  // values loaded non-temporally (a stream read once per PCG iteration)
 };
 
 // ---- the SpMV ----------------------------------------------------------------
@@ -280,8 +279,7 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sdia(SdiaArgs<VT> a, Pro pro,
           const int j = j0 + u;
           m[u] = (j < nd) && ((msk >> j) & 1u);
           const int32_t c = m[u] ? row + dct[j] : base;
-          const VT* vp = a.vals + kSellC * int64_t(g0 + min(j, nd - 1)) + lane;
-          v[u] = a.nt ? __builtin_nontemporal_load((const __attribute__((address_space(1))) VT*)vp) : gld(vp);
+          v[u] = gld(a.vals + kSellC * int64_t(g0 + min(j, nd - 1)) + lane);
           xv[u] = gx(c);
         }
 #pragma unroll
@@ -466,11 +464,11 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
 // SELL-DIA launch
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sdia(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
-                             bool one_tile_per_wg = false, int nt = 0) {
+                             bool one_tile_per_wg = false) {
   int64_t grid = (P.nb + kSellWG - 1) / kSellWG;
   if (!one_tile_per_wg) grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
-  SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals), nt};
+  SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals)};
   constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? 1536 / kSellWG : 1;
   hipLaunchKernelGGL((k_spmv_sdia<T, VT, kSdiaSB, kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
                      0, st, a, pro, gx, epi);
@@ -478,8 +476,8 @@ inline void launch_spmv_sdia(const SellPattern& P, const void* vals, Gx gx, Pro 
 
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
-                                 bool one_tile_per_wg = false, int nt = 0) {
-  if (P.col_bits == 1) launch_spmv_sdia<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg, nt);
+                                 bool one_tile_per_wg = false) {
+  if (P.col_bits == 1) launch_spmv_sdia<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else launch_spmv_sell_th<T, VT, int32_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
 }

@@ -136,3 +136,45 @@ def test_multi_rank_matches_oracle(gpu_ctx, world, blocks):
         np.testing.assert_allclose(hist, h_o[: it + 1], rtol=1e-12, atol=0)
         assert np.linalg.norm(xg - x_o) <= 1e-12 * np.linalg.norm(x_o)
     assert all(np.array_equal(outs[0][3], o[3]) for o in outs)  # every rank holds the same solution
+
+
+def _rank_rccl(port, q):
+    """World 1 over nccl (RCCL): the collectives the multi-GPU paths issue, on device tensors."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    import bench
+    from learningsparsepreconditioner4gpu_amd import distributed as D
+    from learningsparsepreconditioner4gpu_amd.dist_pcg import DistributedPCG
+
+    A, L, b = _system("kuhn")
+    d = DistributedPCG(A, L, EPS)
+    it, conv, x = d.solve(b, rtol=1e-8)
+    xg = d.gather_solution(x)
+    recs = [D.SolveRecord(index=i, iters=10 + i, rel_res=0.5, t_prec=2e-3, t_solve=1e-3, n=100, nnz=500)
+            for i in (2, 0)]
+    got = D.gather_records(recs, 3)
+    mx, sm = bench.reduce_timing(1.25, 7.0, torch.device("cuda", 0))
+    dist.barrier()
+    q.put((dist.get_backend(), it, bool(conv), xg, [(int(r.index), int(r.iters)) for r in got], mx, sm))
+    dist.destroy_process_group()
+
+
+def test_rccl_world1_collectives(gpu_ctx):
+    """The nccl backend (RCCL) initialises on the box's GPU and carries the collectives of
+    bench.py's max-over-ranks timing, distributed.gather_records and dist_pcg at world 1 (more
+    ranks need more GPUs: the driver's scaling run; the multi-rank logic is covered over gloo above)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rank_rccl, args=(_free_port(), q))
+    p.start()
+    be, it, conv, xg, recs, mx, sm = q.get(timeout=100)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and be == "nccl"
+    A, L, b = _system("kuhn")
+    it_o, x_o, _ = _oracle(A, L, b, 1e-8)
+    assert conv and it == it_o
+    assert np.linalg.norm(xg - x_o) <= 1e-12 * np.linalg.norm(x_o)
+    assert recs == [(0, 10), (2, 12)] and (mx, sm) == (1.25, 7.0)

@@ -35,7 +35,7 @@ import json; d=json.load(open('$out/bench.json')); print(d['value'], d['pcg_iter
       python3 tools/loop_traffic.py "$tag" 1 > "$out/pcg_loop_traffic.json" && cat "$out/pcg_loop_traffic.json"
       find "gpurun_out/pmc_$tag" -name "*.csv" -size +2M -delete ;;
     ab=*)  # interleaved loop A/B: ab='{"base": {}, "x": {"ENV": "1"}}'
-      timeout -k 10 400 python -u tools/loop_ab.py "${s#ab=}" kuhn101 11 "$out/loop_ab.jsonl" > "$out/loop_ab.txt" 2>&1 || exit $?
+      LOOP_AB_REPLICAS=${LOOP_AB_REPLICAS:-1} timeout -k 10 600 python -u tools/loop_ab.py "${s#ab=}" kuhn101 ${LOOP_AB_ROUNDS:-11} "$out/loop_ab.jsonl" > "$out/loop_ab.txt" 2>&1 || exit $?
       cat "$out/loop_ab.txt" ;;
     gnn)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_gnn.py -x -q --timeout 200 --timeout-method thread > "$out/gnn_tests.txt" 2>&1
