@@ -48,19 +48,19 @@ __host__ __device__ constexpr int ff_size(int in, int out) { return H * in + H +
 __host__ __device__ constexpr int frag_size(int s1) { return s1 * 64 + 5 * 256; }
 
 // GELU(v) = v Phi(v) = max(v, 0) - |v| m(|v|),  m(a) = Phi(-a) = erfc(a / sqrt2) / 2 (either sign
-// of v; nn.GELU's exact-erf form).  log2 m(a) on [0, 5.75] is a degree-8 polynomial (Chebyshev
-// fit, fp32 coefficients; a clamps at 5.75, where m < 5e-9), so a value costs one exp2 and 8
-// FMAs -- no reciprocal (round 2's erfcc took rcp + exp2 + 10 FMAs): |GELU error| <= 4.5e-7
-// absolute over every fp32 v against torch's erf GELU, and the forward stays within ~1e-7 of the
-// reference's (tests/test_gpu_gnn.py, 1e-5).  Two values at a time in packed fp32
+// of v; nn.GELU's exact-erf form).  log2 m(a) on [0, 5.75] is a degree-7 polynomial (Chebyshev
+// fit, fp32 coefficients; a clamps at 5.75, where m < 5e-9), so a value costs one exp2 and 7
+// FMAs -- no reciprocal (round 2's erfcc took rcp + exp2 + 10 FMAs): |GELU error| <= 4.8e-7
+// absolute over every fp32 v against the exact erf GELU (degree 8: 4.1e-7), and the forward stays
+// within ~1e-7 of the reference's (tests/test_gpu_gnn.py, 1e-5).  Two values at a time in packed fp32
 // (v_pk_fma_f32); |v| and the clamp are one v_med3_f32 with the abs modifier.
 using f2 = float __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, float c) { return __builtin_elementwise_fma(a, b, (f2)(c)); }
 constexpr float kGeluClamp = 5.75f;
-constexpr int kGeluDeg = 8;
-constexpr float kGeluC[9] = {-9.999883175e-01f, -1.151304364e+00f, -4.583674073e-01f, -5.401911587e-02f,
-                             8.511481807e-03f,  -9.210868739e-04f, 5.780859647e-05f,  -1.258388238e-06f,
-                             -3.159780704e-08f};
+constexpr int kGeluDeg = 7;
+constexpr float kGeluC[8] = {-0.99998539686203f,    -1.1513410806655884f,    -0.4582555294036865f,
+                             -0.054161783307790756f, 0.008604509755969048f,  -0.0009547343943268061f,
+                             6.46349653834477e-05f,  -1.9851854631269816e-06f};
 // max(v, 0) as one v_max_i32 on the bit pattern (negative floats, -0 included, are negative
 // integers); fmaxf would add a canonicalising v_max
 __device__ __forceinline__ float relu(float v) {
@@ -82,10 +82,14 @@ __device__ __forceinline__ void gelu_n(f2 (&v)[K]) {
   for (int c = kGeluDeg - 2; c >= 0; --c)
 #pragma unroll
     for (int k = 0; k < K; ++k) p[k] = pfma(a[k], p[k], kGeluC[c]);
+  // the clamped |v| (a) multiplies m: for |v| > 5.75 that changes |v| m(|v|) < 2.6e-8 |v| / 5.75 by less
+  // than its own size -- below fp32's half ulp of GELU(v) for v > 0 and 2.6e-8 absolute for v < 0 --
+  // and the pair's last step is one v_pk_fma_f32 with a neg modifier (|v| would need two v_and)
 #pragma unroll
-  for (int k = 0; k < K; ++k)
-    v[k] = (f2){__builtin_fmaf(-__builtin_fabsf(v[k].x), __builtin_amdgcn_exp2f(p[k].x), relu(v[k].x)),
-                __builtin_fmaf(-__builtin_fabsf(v[k].y), __builtin_amdgcn_exp2f(p[k].y), relu(v[k].y))};
+  for (int k = 0; k < K; ++k) {
+    const f2 e = (f2){__builtin_amdgcn_exp2f(p[k].x), __builtin_amdgcn_exp2f(p[k].y)};
+    v[k] = __builtin_elementwise_fma(-a[k], e, (f2){relu(v[k].x), relu(v[k].y)});
+  }
 }
 __device__ __forceinline__ f4 gelu4(f4 a) {
   f2 v[2] = {(f2){a.x, a.y}, (f2){a.z, a.w}};
@@ -103,6 +107,7 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ float comp(f4 v, int i) { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; }
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
 // One FeedForward's fragment block held in this lane's registers (the fused edge encoder of the
 // first MP layer: its ~21 floats per lane fit beside the layer, whose occupancy is LDS-bound, so
@@ -142,8 +147,10 @@ __device__ __forceinline__ f4 ff_tail(const float* fr, int s1, f4 h, int lane) {
   return o;
 }
 
+#ifdef LSPCG_GNN_F32
 // Two FFs with 48 inputs sharing the same B operand (message + edge MLP of an MPLayer): the
-// two dependent MFMA chains and the two GELU blocks are interleaved so they overlap.
+// two dependent MFMA chains and the two GELU blocks are interleaved so they overlap (f32 MFMA;
+// the default build runs the split-f16 version below).
 __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const float (&in)[12], int lane, f4& oa,
                                        f4& ob) {
   f4 ha = *reinterpret_cast<const f4*>(fa + 12 * 64 + lane * 4);
@@ -175,6 +182,157 @@ __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const f
   }
 }
 
+#endif
+
+#ifndef LSPCG_GNN_F32
+// ---- The message + edge MLPs of an MPLayer on f16 MFMAs with split operands -----------------
+// On gfx950 an f32 MFMA and a vector instruction never execute together on a SIMD (the layer's PMC:
+// SQ_VALU_MFMA_COEXEC_CYCLES = 0, MFMA 47 % + VALU 44 % of the cycles; tools/coexec_probe.hip: one
+// f32 MFMA plus 8 FMAs take the sum of both), while an f16 MFMA runs beside the VALU.  So the two
+// MLPs' products go to v_mfma_f32_16x16x32_f16 / 16x16x16f16 with every fp32 operand split into an
+// f16 pair, x = xh + xl (RNE; x - xh is exact in fp32): W x ~ Wl xh + Wh xl + Wh xh (the dropped
+// Wl xl is ~2^-22 relative), products exact and summed in fp32.  Each weight matrix is scaled by a
+// power of two 2^s (max |W| 2^s in [2^10, 2^11): its low halves stay normal f16) and the
+// accumulator by 2^-s after the chain.  Error vs an fp64 forward ~5e-8 at kuhn / Poisson sizes,
+// the same order as the fp32 forward's own (2e-8; tests/test_gpu_gnn.py holds it to 1e-5).
+// Activations must stay below f16's 65504 (LayerNorm outputs are |v| <= 6.9; hidden layers are
+// GELU outputs of O(1..10) pre-activations).
+using h4 = _Float16 __attribute__((ext_vector_type(4)));
+using hf2 = _Float16 __attribute__((ext_vector_type(2)));
+
+// f16 block of one FeedForward(48 -> 16 -> 16 -> out) (dwords, 64 lanes): [W1 hi, K block 0 / 1 / 2
+// (2 dwords = 4 halves per lane each) | W1 lo, blocks 0 / 1 / 2 | C1 (4 floats / lane) | W2 hi | W2 lo |
+// C2 | W3 hi | W3 lo | C3 | 2^-s1, 2^-s2, 2^-s3, pad].  Every product is a v_mfma_f32_16x16x16f16:
+// K slot (q, j) of block i is the lane's in[4i + j] (feature 16i + 4q + j, as feat48); C = 2^s b in
+// accumulator layout.  (v_mfma_f32_16x16x32_f16 -- one instruction for blocks 0 and 1 -- lost its
+// operands: hipcc reused its A / B registers for VALU results right after issue, and the products
+// went missing in the edge decoder; 16x16x16 has no such hazard gap.)
+constexpr int kH48 = 2052;
+constexpr int kH48W1h = 0, kH48W1l = 384, kH48C1 = 768;
+constexpr int kH48W2h = 1024, kH48W2l = 1152, kH48C2 = 1280, kH48W3h = 1536, kH48W3l = 1664, kH48C3 = 1792;
+constexpr int kH48S = 2048;
+
+// (a, b) -> packed f16 pairs hi = RNE(a, b), lo = RNE(a - hi, b - hi) (x - hi is exact in fp32).
+// Plain conversions, so the compiler sees every write: a three-instruction inline-asm form
+// (v_fma_mix{lo,hi}_f16 for the residuals) produced wrong layers -- the compiler pads no wait states
+// around inline asm, and its outputs landed in the operand registers of an in-flight MFMA.
+__device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned& lo) {
+  const hf2 h = __builtin_convertvector((f2){a, b}, hf2);
+  const f2 r = (f2){a, b} - __builtin_convertvector(h, f2);
+  hi = __builtin_bit_cast(unsigned, h);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector(r, hf2));
+}
+__device__ __forceinline__ void split4(const float* v, h4& hi, h4& lo) {
+  unsigned h[2], l[2];
+  split2(v[0], v[1], h[0], l[0]);
+  split2(v[2], v[3], h[1], l[1]);
+  hi = __builtin_bit_cast(h4, (unsigned __attribute__((ext_vector_type(2)))){h[0], h[1]});
+  lo = __builtin_bit_cast(h4, (unsigned __attribute__((ext_vector_type(2)))){l[0], l[1]});
+}
+__device__ __forceinline__ h4 ldh4(const float* p) { return *reinterpret_cast<const h4*>(p); }
+__device__ __forceinline__ f4 mfma16h(h4 a, h4 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0); }
+
+// layer 1 of a 48-input FeedForward: acc = C + sum over the 3 K blocks of Wl xh, then Wh xl, then Wh xh
+__device__ __forceinline__ f4 layer48h(const float* w, const h4 (&xh)[3], const h4 (&xl)[3], int lane) {
+  h4 wh[3], wlo[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    wh[i] = ldh4(w + kH48W1h + 128 * i + 2 * lane);
+    wlo[i] = ldh4(w + kH48W1l + 128 * i + 2 * lane);
+  }
+  f4 acc = ld4(w + kH48C1 + 4 * lane);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) acc = mfma16h(wlo[i], xh[i], acc);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) acc = mfma16h(wh[i], xl[i], acc);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) acc = mfma16h(wh[i], xh[i], acc);
+  return acc;
+}
+
+// one 16x16 layer on split operands: acc = C + Wl xh + Wh xl + Wh xh (small terms first)
+__device__ __forceinline__ f4 layer16h(const float* w, int oh, int ol, int oc, float unscale, h4 xh, h4 xl,
+                                       int lane) {
+  const h4 wh = ldh4(w + oh + 2 * lane), wlo = ldh4(w + ol + 2 * lane);
+  f4 acc = ld4(w + oc + 4 * lane);
+  acc = mfma16h(wlo, xh, acc);
+  acc = mfma16h(wh, xl, acc);
+  acc = mfma16h(wh, xh, acc);
+  return acc * unscale;
+}
+
+// us[0..2] / us[3..5]: the unscale factors 2^-s of the message / edge MLP's three layers (uniform:
+// read once per kernel from the global blob, so they live in SGPRs)
+__device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const float (&in)[12], int lane, f4& oa,
+                                       f4& ob, const float (&us)[6]) {
+  h4 xh[3], xl[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) split4(in + 4 * i, xh[i], xl[i]);
+  f4 ha = layer48h(fa, xh, xl, lane);
+  f4 hb = layer48h(fb, xh, xl, lane);
+  ha *= us[0];
+  hb *= us[3];
+  gelu4x2(ha, hb);
+  h4 xah, xal, xbh, xbl;
+  {
+    const float va[4] = {ha.x, ha.y, ha.z, ha.w}, vb[4] = {hb.x, hb.y, hb.z, hb.w};
+    split4(va, xah, xal);
+    split4(vb, xbh, xbl);
+  }
+  f4 h2a = layer16h(fa, kH48W2h, kH48W2l, kH48C2, us[1], xah, xal, lane);
+  f4 h2b = layer16h(fb, kH48W2h, kH48W2l, kH48C2, us[4], xbh, xbl, lane);
+  gelu4x2(h2a, h2b);
+  {
+    const float va[4] = {h2a.x, h2a.y, h2a.z, h2a.w}, vb[4] = {h2b.x, h2b.y, h2b.z, h2b.w};
+    split4(va, xah, xal);
+    split4(vb, xbh, xbl);
+  }
+  oa = layer16h(fa, kH48W3h, kH48W3l, kH48C3, us[2], xah, xal, lane);
+  ob = layer16h(fb, kH48W3h, kH48W3l, kH48C3, us[5], xbh, xbl, lane);
+}
+
+// one FeedForward(48 -> 16 -> 16 -> out) on split operands (the edge decoder); us = its 2^-s factors
+__device__ __forceinline__ f4 ff1_48(const float* fa, const float (&in)[12], int lane, const float (&us)[3]) {
+  h4 xh[3], xl[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) split4(in + 4 * i, xh[i], xl[i]);
+  f4 ha = layer48h(fa, xh, xl, lane);
+  ha = gelu4(ha * us[0]);
+  h4 xah, xal;
+  {
+    const float va[4] = {ha.x, ha.y, ha.z, ha.w};
+    split4(va, xah, xal);
+  }
+  f4 h2 = gelu4(layer16h(fa, kH48W2h, kH48W2l, kH48C2, us[1], xah, xal, lane));
+  {
+    const float va[4] = {h2.x, h2.y, h2.z, h2.w};
+    split4(va, xah, xal);
+  }
+  return layer16h(fa, kH48W3h, kH48W3l, kH48C3, us[2], xah, xal, lane);
+}
+
+// FeedForward(16 -> 16 -> 16 -> 16) (the node MLP) on split operands: block [W1 hi | W1 lo | C1 | W2 hi |
+// W2 lo | C2 | W3 hi | W3 lo | C3 | 2^-s1..3, pad] (kH16 dwords; K slot (q, j) = the lane's in[j], i.e.
+// feature 4q + j, as feat16); us = its 2^-s factors
+constexpr int kH16 = 1540;
+constexpr int kH16S = 1536;
+__device__ __forceinline__ f4 ff1_16(const float* fa, const float (&in)[4], int lane, const float (&us)[3]) {
+  h4 xh, xl;
+  split4(in, xh, xl);
+  f4 h = gelu4(layer16h(fa, 0, 128, 256, us[0], xh, xl, lane));
+  {
+    const float va[4] = {h.x, h.y, h.z, h.w};
+    split4(va, xh, xl);
+  }
+  h = gelu4(layer16h(fa, 512, 640, 768, us[1], xh, xl, lane));
+  {
+    const float va[4] = {h.x, h.y, h.z, h.w};
+    split4(va, xh, xl);
+  }
+  return layer16h(fa, 1024, 1152, 1280, us[2], xh, xl, lane);
+}
+#endif
+
 template <int S1>
 __device__ __forceinline__ f4 ff_tile_regs(const FragRegs<S1>& w, const float (&in)[S1]) {
   f4 h = w.c1;
@@ -199,7 +357,6 @@ __device__ __forceinline__ f4 ff_tile(const float* fr, const float (&in)[S1], in
   return ff_tail(fr, S1, h, lane);
 }
 
-__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
 
 __device__ __forceinline__ void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
@@ -352,8 +509,14 @@ __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __rest
                                                  float* __restrict__ out) {
   // the decoder's fragment block in LDS (8 KiB): the per-tile weight reads stay off the gathers'
   // memory queue
-  __shared__ __attribute__((aligned(16))) float wd[frag_size(12)];
-  for (int i = threadIdx.x; i < frag_size(12) / 4; i += 256) reinterpret_cast<f4*>(wd)[i] = ld4(fr + 4 * i);
+#ifdef LSPCG_GNN_F32
+  constexpr int kDec = frag_size(12);
+#else
+  constexpr int kDec = kH48;  // split-f16 block (ff1_48)
+  const float us[3] = {fr[kH48S], fr[kH48S + 1], fr[kH48S + 2]};
+#endif
+  __shared__ __attribute__((aligned(16))) float wd[kDec];
+  for (int i = threadIdx.x; i < kDec / 4; i += 256) reinterpret_cast<f4*>(wd)[i] = ld4(fr + 4 * i);
   __syncthreads();
   const int lane = threadIdx.x & 63, it = lane & 15, q = lane >> 4;
   const int64_t ntiles = (E + 15) / 16;
@@ -363,7 +526,11 @@ __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __rest
     const int64_t ee = valid ? e : E - 1;
     float in[12];
     pack12(ld4(ecsc + int64_t(inv[ee]) * H + 4 * q), ld4(x + ei[ee] * H + 4 * q), ld4(x + ei[E + ee] * H + 4 * q), in);
+#ifdef LSPCG_GNN_F32
     const f4 o = ff_tile<12>(wd, in, lane);
+#else
+    const f4 o = ff1_48(wd, in, lane, us);
+#endif
     if (valid) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -375,8 +542,16 @@ __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __rest
 // ---------------------------------------------------------------------------
 // One MPLayer (basic_layers.py:193-225) as one kernel
 // ---------------------------------------------------------------------------
+#ifdef LSPCG_GNN_F32
 constexpr int kFrag48 = frag_size(12);
+#else
+constexpr int kFrag48 = kH48;  // split-f16 blocks (ff2_48, ff1_16)
+#endif
+#ifdef LSPCG_GNN_F32
 constexpr int kFrag16 = frag_size(4);
+#else
+constexpr int kFrag16 = kH16;
+#endif
 constexpr int kLayerFrag = 2 * kFrag48 + kFrag16;  // [msg | edge | node]
 
 // S1E > 0 (first layer): the edge encoder is fused in -- the layer's input edge state is computed
@@ -395,9 +570,16 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, it = lane & 15, q = lane >> 4;
   for (int i = tid; i < kLayerFrag / 4; i += 256) reinterpret_cast<f4*>(wl)[i] = ld4(frag + 4 * i);
   __syncthreads();
+#ifdef LSPCG_GNN_F32
   FragRegs<SE> wenc;
   if constexpr (S1E > 0) wenc.load(fenc, lane);
+#endif
   const float* fmsg = wl;
+#ifndef LSPCG_GNN_F32
+  const float us[6] = {frag[kH48S], frag[kH48S + 1], frag[kH48S + 2], frag[kH48 + kH48S], frag[kH48 + kH48S + 1],
+                       frag[kH48 + kH48S + 2]};
+  const float usn[3] = {frag[2 * kH48 + kH16S], frag[2 * kH48 + kH16S + 1], frag[2 * kH48 + kH16S + 2]};
+#endif
   const float* fedge = wl + kFrag48;
   const float* fnode = wl + 2 * kFrag48;
   const int n0 = blockIdx.x * 256;
@@ -417,6 +599,7 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
   auto edge_of = [&](int T) { const int k = k0 + T * 16 + it; return k < k1 ? k : klast; };
   int qd = 0, qs = 0, qe = 0;
   f4 pxd{}, pxs{}, pea{};
+#ifdef LSPCG_GNN_F32
   float pin[SE];  // fused encoder: this lane's raw input features of the prefetched edge
   auto load_in = [&](int row) {
 #pragma unroll
@@ -425,6 +608,22 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
       pin[s] = f < fin ? eattr[row * fin + f] : 0.f;
     }
   };
+#else
+  float pin[4];  // fused encoder (split-f16 block, fenc): features 4q .. 4q+3 of the prefetched edge
+  auto load_in = [&](int row) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = 4 * q + j;
+      pin[j] = f < fin ? eattr[row * fin + f] : 0.f;
+    }
+  };
+  float use[3] = {0.f, 0.f, 0.f};
+  if constexpr (S1E > 0) {
+    use[0] = fenc[kH16S];
+    use[1] = fenc[kH16S + 1];
+    use[2] = fenc[kH16S + 2];
+  }
+#endif
   if (wave < NT) {
     const int kk = edge_of(wave);
     qd = dst[kk];
@@ -451,10 +650,16 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
       const f4 xd = pxd, xs = pxs;  // x_i (target), x_j (source)
       f4 ea;                         // edge attr
       if constexpr (S1E > 0) {
+#ifdef LSPCG_GNN_F32
         float iv[SE];
 #pragma unroll
         for (int s = 0; s < SE; ++s) iv[s] = pin[s];
         ea = ff_tile_regs<SE>(wenc, iv);  // k_encode<true>'s MLP on this edge
+#else
+        const float iv[4] = {pin[0], pin[1], pin[2], pin[3]};
+        ea = ff1_16(fenc, iv, lane, use);  // k_encode<true>'s MLP on this edge (split-f16 block, read
+                                           // through the cache)
+#endif
       } else {
         ea = pea;
       }
@@ -488,7 +693,11 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
         v[2 * j + 1] = w[j].y;
       }
       f4 m, u;
+#ifdef LSPCG_GNN_F32
       ff2_48(fmsg, fedge, v, lane, m, u);
+#else
+      ff2_48(fmsg, fedge, v, lane, m, u, us);
+#endif
       if (edge_res) u += ea;
       if (valid) {
         st4(e + int64_t(k) * H + 4 * q, u);
@@ -518,7 +727,11 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
     const float rstd = __builtin_amdgcn_rsqf(quad_sum(sq) * (1.0f / 16.0f) + 1e-5f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] *= rstd;
+#ifdef LSPCG_GNN_F32
     f4 o = ff_tile<4>(fnode, v, lane);
+#else
+    f4 o = ff1_16(fnode, v, lane, usn);
+#endif
     if (i < n1) {
       if (node_res) o += ld4(x + int64_t(i) * H + 4 * q);
       st4(xout + int64_t(i) * H + 4 * q, o);
@@ -606,6 +819,77 @@ void emit_frag(std::vector<float>& o, const FF& f, int s1, Feat feat, const floa
 }
 
 auto feat48 = [](int s, int q) { return (s >> 2) * 16 + 4 * q + (s & 3); };
+
+#ifndef LSPCG_GNN_F32
+// The split-f16 block of a FeedForward(48 -> 16 -> 16 -> out) (ff2_48; layout at kH48): weights
+// scaled by 2^s per matrix (max |W| 2^s in [2^10, 2^11)), split into RNE f16 pairs.
+void emit_frag_h_any(std::vector<float>& o, const FF& f, const float* gamma, const float* beta, bool in48) {
+  std::vector<float> W1(H * f.in), b1(H);
+  for (int i = 0; i < H; ++i) {
+    double bb = f.b1[i];
+    for (int k = 0; k < f.in; ++k) {
+      const double w = f.W1[i * f.in + k];
+      W1[i * f.in + k] = float(gamma ? w * gamma[k] : w);
+      if (beta) bb += w * beta[k];
+    }
+    b1[i] = float(bb);
+  }
+  auto scale_exp = [](auto get, int rows, int cols) {
+    double mx = 0;
+    for (int i = 0; i < rows; ++i)
+      for (int k = 0; k < cols; ++k) mx = std::max(mx, std::fabs(double(get(i, k))));
+    if (mx == 0) return 0;
+    int e;
+    std::frexp(mx, &e);  // mx in [2^(e-1), 2^e)
+    return 11 - e;       // max |W| 2^s in [2^10, 2^11)
+  };
+  auto w1 = [&](int i, int k) { return k < f.in ? W1[i * f.in + k] : 0.f; };  // 16-slot blocks pad fin < 16
+  auto w2 = [&](int i, int k) { return f.W2[i * H + k]; };
+  auto w3 = [&](int i, int k) { return i < f.out ? f.W3[i * H + k] : 0.f; };
+  const int s1 = scale_exp(w1, H, f.in), s2 = scale_exp(w2, H, H), s3 = scale_exp(w3, H, H);
+  auto push_pairs = [&](auto get, int s, int per_lane, auto kidx, bool lo) {  // per lane: per_lane halves
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < per_lane; j += 2) {
+        unsigned u = 0;
+        for (int t = 0; t < 2; ++t) {
+          const int k = kidx(l >> 4, j + t);
+          const float x = k >= 0 ? std::ldexp(get(l & 15, k), s) : 0.f;
+          const _Float16 h = static_cast<_Float16>(x);
+          const _Float16 v = lo ? static_cast<_Float16>(x - static_cast<float>(h)) : h;
+          u |= unsigned(__builtin_bit_cast(unsigned short, v)) << (16 * t);
+        }
+        o.push_back(__builtin_bit_cast(float, u));
+      }
+  };
+  auto push_bias = [&](auto get, int s) {
+    for (int l = 0; l < 64; ++l)
+      for (int r = 0; r < 4; ++r) o.push_back(std::ldexp(get(4 * (l >> 4) + r), s));
+  };
+  auto kh = [](int q, int j) { return 4 * q + j; };  // 16-wide inputs / hidden layers
+  if (in48) {  // three K blocks of 16: block i, slot (q, j) = feature 16 i + 4 q + j = feat48(4 i + j, q)
+    for (bool lo : {false, true})
+      for (int i = 0; i < 3; ++i) push_pairs(w1, s1, 4, [i](int q, int j) { return feat48(4 * i + j, q); }, lo);
+  } else {  // 16 inputs: one 16x16x16 product, K slot (q, j) = feature 4q + j
+    push_pairs(w1, s1, 4, kh, false);
+    push_pairs(w1, s1, 4, kh, true);
+  }
+  push_bias([&](int i) { return b1[i]; }, s1);
+  push_pairs(w2, s2, 4, kh, false);
+  push_pairs(w2, s2, 4, kh, true);
+  push_bias([&](int i) { return f.b2[i]; }, s2);
+  push_pairs(w3, s3, 4, kh, false);
+  push_pairs(w3, s3, 4, kh, true);
+  push_bias([&](int i) { return i < f.out ? f.b3[i] : 0.f; }, s3);
+  for (int s : {s1, s2, s3}) o.push_back(std::ldexp(1.0f, -s));
+  o.push_back(0.f);
+}
+void emit_frag_h(std::vector<float>& o, const FF& f, const float* gamma, const float* beta) {
+  emit_frag_h_any(o, f, gamma, beta, true);  // kH48 dwords
+}
+void emit_frag_h16(std::vector<float>& o, const FF& f, const float* gamma, const float* beta) {
+  emit_frag_h_any(o, f, gamma, beta, false);  // kH16 dwords
+}
+#endif
 auto feat16 = [](int s, int q) { return 4 * q + s; };
 auto featenc = [](int s, int q) { return 4 * s + q; };
 
@@ -616,6 +900,7 @@ struct lspcg_gnn {
   lspcg_gnn_desc d{};
   float* frag = nullptr;  // device fragment blob
   int64_t o_node_enc = 0, o_edge_enc = 0, o_dec = 0;
+  int64_t o_edge_enc_h = 0;  // split-f16 block of the edge encoder (the first layer's fused copy)
   std::vector<int64_t> o_layer;  // per layer: [msg | edge | node] fragment block
   // workspace
   int64_t capN = -1, capE = -1;
@@ -703,6 +988,7 @@ int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* we
   o += ff_size(d.node_in, H);
   g->o_edge_enc = int64_t(fr.size());
   emit_frag(fr, ff_at(w.data() + o, d.edge_in, H), (d.edge_in + 3) / 4, featenc, nullptr, nullptr);
+  const float* enc_w = w.data() + o;
   o += ff_size(d.edge_in, H);
   for (int l = 0; l < d.num_mp_layers; ++l) {
     const float* node = w.data() + o;  // [ln_g 16 | ln_b 16 | FF(16->16)]
@@ -712,12 +998,31 @@ int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* we
     const float* msgp = w.data() + o;
     o += 6 * H + ff_size(3 * H, H);
     g->o_layer.push_back(int64_t(fr.size()));
+#ifdef LSPCG_GNN_F32
     emit_frag(fr, ff_at(msgp + 6 * H, 3 * H, H), 12, feat48, msgp, msgp + 3 * H);
     emit_frag(fr, ff_at(edge + 6 * H, 3 * H, H), 12, feat48, edge, edge + 3 * H);
+#else
+    emit_frag_h(fr, ff_at(msgp + 6 * H, 3 * H, H), msgp, msgp + 3 * H);
+    emit_frag_h(fr, ff_at(edge + 6 * H, 3 * H, H), edge, edge + 3 * H);
+#endif
+#ifdef LSPCG_GNN_F32
     emit_frag(fr, ff_at(node + 2 * H, H, H), 4, feat16, node, node + H);
+#else
+    emit_frag_h16(fr, ff_at(node + 2 * H, H, H), node, node + H);
+#endif
   }
   g->o_dec = int64_t(fr.size());
+#ifdef LSPCG_GNN_F32
   emit_frag(fr, ff_at(w.data() + o, 3 * H, d.edge_out), 12, feat48, nullptr, nullptr);
+#else
+  emit_frag_h(fr, ff_at(w.data() + o, 3 * H, d.edge_out), nullptr, nullptr);
+#endif
+#ifndef LSPCG_GNN_F32
+  g->o_edge_enc_h = int64_t(fr.size());
+  if (d.edge_in <= 16) emit_frag_h16(fr, ff_at(enc_w, d.edge_in, H), nullptr, nullptr);
+#else
+  (void)enc_w;
+#endif
   LSPCG_HIP(hipMalloc(&g->frag, sizeof(float) * fr.size()));
   LSPCG_HIP(hipMemcpy(g->frag, fr.data(), sizeof(float) * fr.size(), hipMemcpyHostToDevice));
   *out = g.release();
@@ -800,7 +1105,11 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
   float* xc = g->xa;
   float* xn = g->xb;
   const unsigned lg = unsigned((N + 255) / 256);
+#ifdef LSPCG_GNN_F32
   const float* fenc = g->frag + g->o_edge_enc;
+#else
+  const float* fenc = g->frag + g->o_edge_enc_h;  // the fused copy reads the split-f16 block
+#endif
   for (int l = 0; l < d.num_mp_layers; ++l) {
     const int se = (l == 0 && fuse_enc) ? s1e : 0;
     auto kern = se == 1 ? k_mp_layer<1> : se == 2 ? k_mp_layer<2> : se == 3 ? k_mp_layer<3> : k_mp_layer<0>;
