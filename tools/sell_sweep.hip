@@ -50,6 +50,92 @@ void launch_fused(const SellPattern& P, const void* vals, const double* x, doubl
                      EpiStore<double>{y});
 }
 
+// bound experiment: every slot's vector entry a constant (no x load): the values-only stream
+struct GatherConst {
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ double operator()(int64_t) const { return 1.0; }
+};
+
+template <typename VT, int SB, int MINW>
+void launch_xconst(const SellPattern& P, const void* vals, const double*, double* y, hipStream_t st) {
+  const int64_t grid = (P.nb + kSellWG - 1) / kSellWG;
+  SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals)};
+  hipLaunchKernelGGL((k_spmv_sdia<double, VT, SB, kSellWG, MINW, ProNone, GatherConst, EpiStore<double>>),
+                     dim3(unsigned(grid)), dim3(kSellWG), 0, st, a, ProNone{}, GatherConst{}, EpiStore<double>{y});
+}
+
+// Experiment (round 4): slots whose offset is the previous slot's + 1 (the stencil's offset clusters,
+// e.g. {-1, 0, 1}, {101, 102}) take their vector entries from the previous slot's by a one-lane DPP
+// wave shift instead of a load; lane 63's entry comes from one extra per-slice gather (lane k <
+// D_s: x[base + 63 + dict[k]]).  MODE 2: the same kernel with every slot loaded (the baseline of
+// this structure); MODE 0: shifted slots reuse the previous vector unshifted (wrong, timing bound);
+// MODE 1: the DPP shift (bit-identical).  All 16 slots in one batch; cluster heads loaded at clamped
+// addresses on every lane so the shifted entries are right wherever the row has the entry.
+__device__ __forceinline__ double wave_shl1(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b), 0x130, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), 0x130, 0xf, 0xf, true);
+  return __builtin_bit_cast(double, (long long)(unsigned)lo | ((long long)hi << 32));
+}
+
+template <typename VT, int MODE, int MINW>
+__global__ void __launch_bounds__(256, MINW) k_sdia_clu(int64_t n, int64_t ns, const int32_t* __restrict__ gp,
+                                                        const uint16_t* __restrict__ mask,
+                                                        const int32_t* __restrict__ dict, const VT* __restrict__ vals,
+                                                        const double* __restrict__ x, double* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int64_t s = int64_t(blockIdx.x) * 4 + w;
+  if (s >= ns) return;
+  const int g0 = gp[s], nd = gp[s + 1] - g0;
+  const unsigned msk = mask[kSellC * s + lane];
+  const int32_t* dp = dict + kSdiaMax * s;
+  int32_t dct[kSdiaMax];
+#pragma unroll
+  for (int j = 0; j < kSdiaMax; ++j) dct[j] = dp[j];
+  const int32_t base = int32_t(s * kSellC), row = base + lane;
+  const int32_t nm1 = int32_t(n - 1);
+  double ext = 0.0;
+  if constexpr (MODE == 1) {
+    const int32_t e = base + 63 + dp[lane & 15];
+    ext = gld(x + min(max(e, 0), nm1));
+  }
+  VT v[kSdiaMax];
+  double xv[kSdiaMax];
+#pragma unroll
+  for (int j = 0; j < kSdiaMax; ++j) v[j] = gld(vals + kSellC * int64_t(g0 + min(j, nd - 1)) + lane);
+#pragma unroll
+  for (int j = 0; j < kSdiaMax; ++j) {
+    if (j >= nd) continue;
+    const bool sh = MODE != 2 && j > 0 && dct[j] == dct[j - 1] + 1;
+    if (sh) {
+      if constexpr (MODE == 0) {
+        xv[j] = xv[j - 1];
+      } else {
+        const double t = wave_shl1(xv[j - 1]);
+        const double e = __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(
+                             int(__builtin_bit_cast(long long, ext) >> 32), j)) << 32 |
+                             (unsigned)__builtin_amdgcn_readlane(int(__builtin_bit_cast(long long, ext)), j)));
+        xv[j] = lane == 63 ? e : t;
+      }
+    } else {
+      xv[j] = gld(x + min(max(row + dct[j], 0), nm1));
+    }
+  }
+  double acc = 0.0;
+#pragma unroll
+  for (int j = 0; j < kSdiaMax; ++j) {
+    if (j < nd && ((msk >> j) & 1u)) acc = acc + double(v[j]) * xv[j];
+  }
+  if (row < n) y[row] = acc;
+}
+
+template <typename VT, int MODE, int MINW>
+void launch_clu(const SellPattern& P, const void* vals, const double* x, double* y, hipStream_t st) {
+  hipLaunchKernelGGL((k_sdia_clu<VT, MODE, MINW>), dim3(unsigned((P.ns + 3) / 4)), dim3(256), 0, st, P.n, P.ns, P.gp,
+                     static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals), x, y);
+}
+
 using Fn = void (*)(const SellPattern&, const void*, const double*, double*, hipStream_t);
 
 // config id -> (value bytes, slots per batch SB, MINW, transposed)
@@ -62,6 +148,9 @@ const Cfg kCfgs[] = {
     {8, 8, 4, 0, launch<double, 8, 4>},  {4, 4, 6, 0, launch<float, 4, 6>},  {4, 8, 6, 0, launch<float, 8, 6>},
     {4, 16, 6, 0, launch<float, 16, 6>}, {4, 8, 8, 0, launch<float, 8, 8>},  {4, 8, 1, 0, launch<float, 8, 1>},
     {4, 8, 6, 1, launch_fused<float, 8, 6>}, {4, 16, 6, 1, launch_fused<float, 16, 6>},
+    {8, 8, 1, 3, launch_xconst<double, 8, 1>}, {4, 8, 6, 3, launch_xconst<float, 8, 6>},
+    {8, 16, 1, 4, launch_clu<double, 2, 1>}, {8, 16, 1, 5, launch_clu<double, 0, 1>}, {8, 16, 1, 6, launch_clu<double, 1, 1>},
+    {4, 16, 6, 4, launch_clu<float, 2, 6>},  {4, 16, 6, 5, launch_clu<float, 0, 6>},  {4, 16, 6, 6, launch_clu<float, 1, 6>},
 };
 
 template <typename VT, int QB, int MINW>

@@ -132,7 +132,8 @@ def main(wl):
         rc = lib.sweep_run(cid, C.c_int64(A.shape[0]), C.c_int64(A.nnz), p(rp), p(ci), p(va), p(x), p(y), 20,
                            C.c_int64(FLUSH_BYTES), C.byref(cold), C.byref(warm))
         print(json.dumps({"workload": wl, "values": "fp64" if vb.value == 8 else "fp32", "SB": qb.value,
-                          "MINW": mw.value, "fused_gather": tr.value == 1, "nt_values": tr.value == 2, "rc": rc,
+                          "MINW": mw.value, "fused_gather": tr.value == 1, "x_const": tr.value == 3,
+                          "cluster": {4: "all loads", 5: "reuse (bound)", 6: "dpp shift"}.get(tr.value), "rc": rc,
                           "cold_us": cold.value * 1e3, "warm_us": warm.value * 1e3,
                           "frac_alg_cold": alg / (cold.value * 1e-3) / 8e12,
                           "bitexact": bool(torch.equal(y, reff if tr.value == 1 else ref))}),
