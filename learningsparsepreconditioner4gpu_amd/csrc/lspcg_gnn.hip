@@ -233,14 +233,15 @@ __device__ __forceinline__ h4 ldh4(const float* p) { return *reinterpret_cast<co
 __device__ __forceinline__ f4 mfma16h(h4 a, h4 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0); }
 
 // layer 1 of a 48-input FeedForward: acc = C + sum over the 3 K blocks of Wl xh, then Wh xl, then Wh xh
-__device__ __forceinline__ f4 layer48h(const float* w, const h4 (&xh)[3], const h4 (&xl)[3], int lane) {
+__device__ __forceinline__ f4 layer48h(const float* w, const h4 (&xh)[3], const h4 (&xl)[3], int lane,
+                                      float cmul = 1.0f) {
   h4 wh[3], wlo[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     wh[i] = ldh4(w + kH48W1h + 128 * i + 2 * lane);
     wlo[i] = ldh4(w + kH48W1l + 128 * i + 2 * lane);
   }
-  f4 acc = ld4(w + kH48C1 + 4 * lane);
+  f4 acc = ld4(w + kH48C1 + 4 * lane) * cmul;  // cmul: a power of two (1 but for ff1_48's guard)
 #pragma unroll
   for (int i = 0; i < 3; ++i) acc = mfma16h(wlo[i], xh[i], acc);
 #pragma unroll
@@ -291,30 +292,11 @@ __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const f
   ob = layer16h(fb, kH48W3h, kH48W3l, kH48C3, us[5], xbh, xbl, lane);
 }
 
-// one FeedForward(48 -> 16 -> 16 -> out) on split operands (the edge decoder); us = its 2^-s factors
-__device__ __forceinline__ f4 ff1_48(const float* fa, const float (&in)[12], int lane, const float (&us)[3]) {
-  h4 xh[3], xl[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) split4(in + 4 * i, xh[i], xl[i]);
-  f4 ha = layer48h(fa, xh, xl, lane);
-  ha = gelu4(ha * us[0]);
-  h4 xah, xal;
-  {
-    const float va[4] = {ha.x, ha.y, ha.z, ha.w};
-    split4(va, xah, xal);
-  }
-  f4 h2 = gelu4(layer16h(fa, kH48W2h, kH48W2l, kH48C2, us[1], xah, xal, lane));
-  {
-    const float va[4] = {h2.x, h2.y, h2.z, h2.w};
-    split4(va, xah, xal);
-  }
-  return layer16h(fa, kH48W3h, kH48W3l, kH48C3, us[2], xah, xal, lane);
-}
-
 // FeedForward(16 -> 16 -> 16 -> 16) (the node MLP) on split operands: block [W1 hi | W1 lo | C1 | W2 hi |
-// W2 lo | C2 | W3 hi | W3 lo | C3 | 2^-s1..3, pad] (kH16 dwords; K slot (q, j) = the lane's in[j], i.e.
+// W2 lo | C2 | W3 hi | W3 lo | C3 | 2^-s1..3, pad | the encoder's magnitude bounds B1, c1, B2, c2
+// (ff1_16_enc)] (kH16 dwords; K slot (q, j) = the lane's in[j], i.e.
 // feature 4q + j, as feat16); us = its 2^-s factors
-constexpr int kH16 = 1540;
+constexpr int kH16 = 1544;
 constexpr int kH16S = 1536;
 __device__ __forceinline__ f4 ff1_16(const float* fa, const float (&in)[4], int lane, const float (&us)[3]) {
   h4 xh, xl;
@@ -330,6 +312,147 @@ __device__ __forceinline__ f4 ff1_16(const float* fa, const float (&in)[4], int 
     split4(va, xh, xl);
   }
   return layer16h(fa, 1024, 1152, 1280, us[2], xh, xl, lane);
+}
+
+// 2^t as a float (t in [-126, 127])
+__device__ __forceinline__ float exp2i(int t) { return __builtin_bit_cast(float, unsigned(t + 127) << 23); }
+
+// max over the 4 lanes of an item (l, l^16, l^32, l^48): row-swap permutes, as swap_sum16 / 32 below
+__device__ __forceinline__ float swap_max16(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const unsigned long long r = __builtin_bit_cast(unsigned long long, __builtin_amdgcn_permlane16_swap(u, u, false, false));
+  return fmaxf(__builtin_bit_cast(float, unsigned(r)), __builtin_bit_cast(float, unsigned(r >> 32)));
+}
+__device__ __forceinline__ float swap_max32(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const unsigned long long r = __builtin_bit_cast(unsigned long long, __builtin_amdgcn_permlane32_swap(u, u, false, false));
+  return fmaxf(__builtin_bit_cast(float, unsigned(r)), __builtin_bit_cast(float, unsigned(r >> 32)));
+}
+
+// Per-edge power-of-two input scale of the fused edge encoder.  Raw edge features (the matrix
+// values, any magnitude: data.py:247-267 allows normalize_matrix="none") are multiplied by 2^t,
+// t chosen per edge so the largest |feature| of the edge lands in [2^10, 2^11); the bias of that
+// edge's output column is scaled alike and the column unscaled after the chain (an MFMA column is
+// one edge, and lane l holds edge l & 15's inputs and outputs, so no lane exchange beyond the
+// edge's own 4 lanes).  Without it an input >= 65520 splits into an infinite f16 and inputs below
+// 2^-14 lose their low bits in f16 subnormals; with it the split's error is relative to the edge's
+// largest feature, like an fp32 dot product's.  Exact (powers of two): inputs already in f16's
+// normal range give the same bits as unscaled, and the scale depends on the edge alone.
+__device__ __forceinline__ int enc_scale_exp(float m) {
+  // m in [2^(e-127), 2^(e-126)) -> [2^10, 2^11); clamped to [-60, 60]: a zero edge (e = 0) keeps its
+  // bias finite (|C| 2^60 < 2^128), an inf / NaN one (e = 255) stays inf / NaN
+  const int e = int(__builtin_bit_cast(unsigned, m) >> 23);  // m >= 0: no sign bit
+  return min(max(137 - e, -60), 60);  // v_med3_i32
+}
+
+// hidden activations of the edge decoder follow the raw edge features' magnitude (through the edge
+// residuals): a wave whose largest |h| reaches 2^15 scales them by 2^t (t < 0, so the largest lands in [2^14, 2^15)) and the next
+// layer undoes it (its bias times 2^t, its product times 2^-t), so no split overflows f16.  The
+// check is 3 VALU + a wave-uniform branch that normal magnitudes never take; returns t (0: none).
+__device__ __forceinline__ int enc_guard(f4& h) {
+  const float m = fmaxf(fmaxf(fabsf(h.x), fabsf(h.y)), fmaxf(fabsf(h.z), fabsf(h.w)));
+  if (!__builtin_amdgcn_ballot_w64(!(m < 32768.0f))) return 0;  // NaN takes the slow path too
+  float w = m;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) w = fmaxf(w, __shfl_xor(w, o));
+  const int e = int(__builtin_bit_cast(unsigned, w) >> 23) & 0xff;
+  if (e == 0xff) return 0;  // inf / NaN: propagates either way
+  const int t = 141 - e;    // e >= 142 here, so -113 <= t <= -1
+  h *= exp2i(t);
+  return t;
+}
+
+// one 16x16 layer on split operands: acc = C cmul + Wl xh + Wh xl + Wh xh, times omul (cmul / omul
+// powers of two: the input's scale and the weights' unscale with the input's scale undone)
+__device__ __forceinline__ f4 layer16h_sc(const float* w, int oh, int ol, int oc, float cmul, float omul, h4 xh,
+                                          h4 xl, int lane) {
+  const h4 wh = ldh4(w + oh + 2 * lane), wlo = ldh4(w + ol + 2 * lane);
+  f4 acc = ld4(w + oc + 4 * lane) * cmul;
+  acc = mfma16h(wlo, xh, acc);
+  acc = mfma16h(wh, xl, acc);
+  acc = mfma16h(wh, xh, acc);
+  return acc * omul;
+}
+__device__ __forceinline__ f4 layer16h_guarded(const float* w, int oh, int ol, int oc, float unscale, int t, h4 xh,
+                                               h4 xl, int lane) {
+  if (t == 0) return layer16h(w, oh, ol, oc, unscale, xh, xl, lane);
+  return layer16h_sc(w, oh, ol, oc, exp2i(t), unscale * exp2i(-t), xh, xl, lane);
+}
+
+// the fused edge encoder FeedForward(fin -> 16 -> 16 -> 16) (kH16 block) on raw features `in`
+// (this lane's features 4q .. 4q+3 of edge lane & 15), scaled per edge (enc_scale_exp)
+__device__ __forceinline__ f4 ff1_16_enc(const float* fa, const float (&in)[4], int lane, const float (&us)[3]) {
+  const float m = swap_max32(swap_max16(fmaxf(fmaxf(fabsf(in[0]), fabsf(in[1])), fmaxf(fabsf(in[2]), fabsf(in[3])))));
+  const unsigned scb = unsigned(enc_scale_exp(m) + 127) << 23;
+  const float sc = __builtin_bit_cast(float, scb), isc = __builtin_bit_cast(float, 0x7f000000u - scb);  // 2^t, 2^-t
+  // the hidden layers' scale, branch-free: |h1| <= B1 m + c1 and |h2| <= B2 |h1| + c2 (B = max row
+  // sum of |W|, c = max |bias| + 0.17 for GELU's negative lobe; host constants), so 2^k with
+  // k = min(0, 14 - exponent of the larger bound) keeps every split below 2^15 (1 on normal data)
+  const float h1b = fmaf(fa[kH16S + 4], m, fa[kH16S + 5]);
+  const float hb = fmaxf(h1b, fmaf(fa[kH16S + 6], h1b, fa[kH16S + 7]));
+  const int ke = int(__builtin_bit_cast(unsigned, hb) >> 23);
+  const unsigned hsb = unsigned(min(max(141 - ke, -100), 0) + 127) << 23;
+  const float hs = __builtin_bit_cast(float, hsb), ihs = __builtin_bit_cast(float, 0x7f000000u - hsb);
+  h4 xh, xl;
+  {
+    const float v[4] = {in[0] * sc, in[1] * sc, in[2] * sc, in[3] * sc};
+    split4(v, xh, xl);
+  }
+  f4 h = gelu4(layer16h_sc(fa, 0, 128, 256, sc, us[0] * isc, xh, xl, lane)) * hs;
+  {
+    const float va[4] = {h.x, h.y, h.z, h.w};
+    split4(va, xh, xl);
+  }
+  h = gelu4(layer16h_sc(fa, 512, 640, 768, hs, us[1] * ihs, xh, xl, lane)) * hs;
+  {
+    const float va[4] = {h.x, h.y, h.z, h.w};
+    split4(va, xh, xl);
+  }
+  return layer16h_sc(fa, 1024, 1152, 1280, hs, us[2] * ihs, xh, xl, lane);
+}
+
+// one FeedForward(48 -> 16 -> 16 -> out) on split operands (the edge decoder); us = its 2^-s
+// factors.  Its input -- the edge state and both endpoints' node states -- has no LayerNorm in
+// front (gnns.py:88-95), so it carries the magnitude of the raw edge features through the edge
+// residuals: an edge whose largest |input| reaches 2^15 is scaled down by a power of two (its bias
+// column alike, its output column back; exact), and each hidden layer by enc_guard.  Normal
+// magnitudes never leave the fast path (a max and a compare per value pair).
+__device__ __forceinline__ f4 ff1_48(const float* fa, const float (&in)[12], int lane, const float (&us)[3]) {
+  float v[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) v[i] = in[i];
+  float cmul = 1.0f, omul = us[0];
+  {
+    float m = fmaxf(fabsf(v[0]), fabsf(v[1]));
+#pragma unroll
+    for (int i = 2; i < 12; ++i) m = fmaxf(m, fabsf(v[i]));
+    if (__builtin_amdgcn_ballot_w64(!(m < 32768.0f))) {  // wave-uniform; rare
+      m = swap_max32(swap_max16(m));
+      const int e = int(__builtin_bit_cast(unsigned, m) >> 23) & 0xff;
+      const int t = (m >= 32768.0f && e != 0xff) ? 141 - e : 0;  // this edge's largest -> [2^14, 2^15)
+      cmul = exp2i(t);
+      omul = us[0] * exp2i(-t);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) v[i] *= cmul;
+    }
+  }
+  h4 xh[3], xl[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) split4(v + 4 * i, xh[i], xl[i]);
+  f4 ha = gelu4(layer48h(fa, xh, xl, lane, cmul) * omul);
+  int tg = enc_guard(ha);
+  h4 xah, xal;
+  {
+    const float va[4] = {ha.x, ha.y, ha.z, ha.w};
+    split4(va, xah, xal);
+  }
+  f4 h2 = gelu4(layer16h_guarded(fa, kH48W2h, kH48W2l, kH48C2, us[1], tg, xah, xal, lane));
+  tg = enc_guard(h2);
+  {
+    const float va[4] = {h2.x, h2.y, h2.z, h2.w};
+    split4(va, xah, xal);
+  }
+  return layer16h_guarded(fa, kH48W3h, kH48W3l, kH48C3, us[2], tg, xah, xal, lane);
 }
 #endif
 
@@ -564,7 +687,7 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
                                                  const float* __restrict__ x, float* __restrict__ e,
                                                  float* __restrict__ xout, const float* __restrict__ fenc, int fin,
                                                  const float* __restrict__ eattr, const int32_t* __restrict__ perm) {
-  constexpr int SE = S1E > 0 ? S1E : 1;
+  [[maybe_unused]] constexpr int SE = S1E > 0 ? S1E : 1;
   __shared__ __attribute__((aligned(16))) float wl[kLayerFrag];
   __shared__ __attribute__((aligned(16))) float msg[CE * H];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, it = lane & 15, q = lane >> 4;
@@ -657,8 +780,8 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
         ea = ff_tile_regs<SE>(wenc, iv);  // k_encode<true>'s MLP on this edge
 #else
         const float iv[4] = {pin[0], pin[1], pin[2], pin[3]};
-        ea = ff1_16(fenc, iv, lane, use);  // k_encode<true>'s MLP on this edge (split-f16 block, read
-                                           // through the cache)
+        ea = ff1_16_enc(fenc, iv, lane, use);  // k_encode<true>'s MLP on this edge (split-f16 block, read
+                                               // through the cache)
 #endif
       } else {
         ea = pea;
@@ -882,6 +1005,26 @@ void emit_frag_h_any(std::vector<float>& o, const FF& f, const float* gamma, con
   push_bias([&](int i) { return i < f.out ? f.b3[i] : 0.f; }, s3);
   for (int s : {s1, s2, s3}) o.push_back(std::ldexp(1.0f, -s));
   o.push_back(0.f);
+  if (!in48) {  // magnitude bounds for ff1_16_enc: max row sum of |W|, max |bias| + GELU's 0.17
+    auto rowsum = [](auto get, int rows, int cols) {
+      double mx = 0;
+      for (int i = 0; i < rows; ++i) {
+        double r = 0;
+        for (int k = 0; k < cols; ++k) r += std::fabs(double(get(i, k)));
+        mx = std::max(mx, r);
+      }
+      return float(mx);
+    };
+    auto absmax = [](auto get, int n) {
+      double mx = 0;
+      for (int i = 0; i < n; ++i) mx = std::max(mx, std::fabs(double(get(i))));
+      return float(mx + 0.17);
+    };
+    o.push_back(rowsum(w1, H, f.in));
+    o.push_back(absmax([&](int i) { return b1[i]; }, H));
+    o.push_back(rowsum(w2, H, H));
+    o.push_back(absmax([&](int i) { return f.b2[i]; }, H));
+  }
 }
 void emit_frag_h(std::vector<float>& o, const FF& f, const float* gamma, const float* beta) {
   emit_frag_h_any(o, f, gamma, beta, true);  // kH48 dwords
@@ -890,7 +1033,7 @@ void emit_frag_h16(std::vector<float>& o, const FF& f, const float* gamma, const
   emit_frag_h_any(o, f, gamma, beta, false);  // kH16 dwords
 }
 #endif
-auto feat16 = [](int s, int q) { return 4 * q + s; };
+[[maybe_unused]] auto feat16 = [](int s, int q) { return 4 * q + s; };
 auto featenc = [](int s, int q) { return 4 * s + q; };
 
 }  // namespace
