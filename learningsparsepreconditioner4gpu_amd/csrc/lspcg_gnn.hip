@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <memory>
@@ -1026,6 +1027,28 @@ void emit_frag_h_any(std::vector<float>& o, const FF& f, const float* gamma, con
     o.push_back(absmax([&](int i) { return f.b2[i]; }, H));
   }
 }
+// Largest |hidden activation| a LayerNorm-fed FeedForward can produce: LayerNorm outputs are at most
+// sqrt(n - 1) in magnitude (gamma / beta folded into layer 1), |GELU(z)| <= max(|z|, 0.17), so
+// |h1| <= ||W1'||_inf sqrt(n - 1) + max |b1'| + 0.17 and |h2| <= ||W2||_inf |h1| + max |b2| + 0.17.
+// The split-f16 products need it below 2^15 (f16 holds 65504): gnn_create refuses weights past it.
+double ln_ff_hidden_bound(const FF& f, const float* gamma, const float* beta) {
+  double h1 = 0, h2 = 0, b2 = 0;
+  for (int i = 0; i < H; ++i) {
+    double r = 0, bb = f.b1[i];
+    for (int k = 0; k < f.in; ++k) {
+      r += std::fabs(double(f.W1[i * f.in + k]) * gamma[k]);
+      bb += double(f.W1[i * f.in + k]) * beta[k];
+    }
+    h1 = std::max(h1, r * std::sqrt(double(f.in - 1)) + std::fabs(bb) + 0.17);
+  }
+  for (int i = 0; i < H; ++i) {
+    double r = 0;
+    for (int k = 0; k < H; ++k) r += std::fabs(double(f.W2[i * H + k]));
+    h2 = std::max(h2, r);
+    b2 = std::max(b2, std::fabs(double(f.b2[i])));
+  }
+  return std::max(h1, h2 * h1 + b2 + 0.17);
+}
 void emit_frag_h(std::vector<float>& o, const FF& f, const float* gamma, const float* beta) {
   emit_frag_h_any(o, f, gamma, beta, true);  // kH48 dwords
 }
@@ -1141,6 +1164,16 @@ int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* we
     const float* msgp = w.data() + o;
     o += 6 * H + ff_size(3 * H, H);
     g->o_layer.push_back(int64_t(fr.size()));
+#ifndef LSPCG_GNN_F32
+    {
+      const double hb = std::max({ln_ff_hidden_bound(ff_at(msgp + 6 * H, 3 * H, H), msgp, msgp + 3 * H),
+                                  ln_ff_hidden_bound(ff_at(edge + 6 * H, 3 * H, H), edge, edge + 3 * H),
+                                  ln_ff_hidden_bound(ff_at(node + 2 * H, H, H), node, node + H)});
+      LSPCG_CHECK(hb < 32768.0, LSPCG_ERR_UNSUPPORTED,
+                  "gnn_create: layer " + std::to_string(l) + "'s MLP weights allow hidden activations up to " +
+                      std::to_string(hb) + ", past the split-f16 GEMMs' 2^15");
+    }
+#endif
 #ifdef LSPCG_GNN_F32
     emit_frag(fr, ff_at(msgp + 6 * H, 3 * H, H), 12, feat48, msgp, msgp + 3 * H);
     emit_frag(fr, ff_at(edge + 6 * H, 3 * H, H), 12, feat48, edge, edge + 3 * H);

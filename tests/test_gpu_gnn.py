@@ -74,6 +74,22 @@ def test_gnn_edge_feature_magnitudes(gpu_ctx, case, scale):
     _close(got, want.numpy())
 
 
+def test_gnn_refuses_weights_past_f16_range(gpu_ctx):
+    """MLP weights whose LayerNorm-fed hidden activations could reach 2^15 (the split-f16 GEMMs'
+    limit; f16 holds 65504) are refused at creation with an error naming the bound, not run."""
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+
+    A, mask, _ = P.poisson2d_grid(10, 10)
+    s = make_sample(A, mask).to("cuda")
+    _, gpu = _pair(s.x.shape[1], s.edge_attr.shape[1], 1, seed=2)
+    gpu(s.x, s.edge_index, s.edge_attr)  # fine as initialised
+    with torch.no_grad():
+        for p in gpu.parameters():
+            p.mul_(1e3)
+    with pytest.raises(Exception, match="2\\^15"):
+        gpu(s.x, s.edge_index, s.edge_attr)
+
+
 def test_gnn_deterministic(gpu_ctx):
     from learningsparsepreconditioner4gpu_amd.data import make_sample
 
