@@ -228,7 +228,9 @@ typedef struct lspcg_gnn_desc {
 } lspcg_gnn_desc;
 
 /* weights: packed fp32 blob in the order documented in learningsparsepreconditioner4gpu_amd/nn.py
- * (pack_weights); host or device pointer */
+ * (pack_weights); host or device pointer.  The MLP products run as fp32-accurate split-f16 GEMMs:
+ * LSPCG_ERR_UNSUPPORTED when a LayerNorm-fed MLP's weights bound its hidden activations at 2^15 or
+ * more (the error message gives the bound); raw edge features of any magnitude are scaled inside. */
 int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* weights,
                      int64_t nweights, lspcg_gnn** out);
 /* Structure analysis of a graph (its CSC by destination), like a sparse library's analysis step:
