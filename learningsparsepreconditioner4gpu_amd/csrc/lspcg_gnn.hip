@@ -382,15 +382,16 @@ __device__ __forceinline__ f4 layer16h_guarded(const float* w, int oh, int ol, i
 
 // the fused edge encoder FeedForward(fin -> 16 -> 16 -> 16) (kH16 block) on raw features `in`
 // (this lane's features 4q .. 4q+3 of edge lane & 15), scaled per edge (enc_scale_exp)
-__device__ __forceinline__ f4 ff1_16_enc(const float* fa, const float (&in)[4], int lane, const float (&us)[3]) {
+__device__ __forceinline__ f4 ff1_16_enc(const float* fa, const float (&in)[4], int lane, const float (&us)[3],
+                                         const float (&bd)[4]) {
   const float m = swap_max32(swap_max16(fmaxf(fmaxf(fabsf(in[0]), fabsf(in[1])), fmaxf(fabsf(in[2]), fabsf(in[3])))));
   const unsigned scb = unsigned(enc_scale_exp(m) + 127) << 23;
   const float sc = __builtin_bit_cast(float, scb), isc = __builtin_bit_cast(float, 0x7f000000u - scb);  // 2^t, 2^-t
   // the hidden layers' scale, branch-free: |h1| <= B1 m + c1 and |h2| <= B2 |h1| + c2 (B = max row
   // sum of |W|, c = max |bias| + 0.17 for GELU's negative lobe; host constants), so 2^k with
   // k = min(0, 14 - exponent of the larger bound) keeps every split below 2^15 (1 on normal data)
-  const float h1b = fmaf(fa[kH16S + 4], m, fa[kH16S + 5]);
-  const float hb = fmaxf(h1b, fmaf(fa[kH16S + 6], h1b, fa[kH16S + 7]));
+  const float h1b = fmaf(bd[0], m, bd[1]);  // bd: fa[kH16S + 4 .. 7], read once per kernel
+  const float hb = fmaxf(h1b, fmaf(bd[2], h1b, bd[3]));
   const int ke = int(__builtin_bit_cast(unsigned, hb) >> 23);
   const unsigned hsb = unsigned(min(max(141 - ke, -100), 0) + 127) << 23;
   const float hs = __builtin_bit_cast(float, hsb), ihs = __builtin_bit_cast(float, 0x7f000000u - hsb);
@@ -741,11 +742,13 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
       pin[j] = f < fin ? eattr[row * fin + f] : 0.f;
     }
   };
-  float use[3] = {0.f, 0.f, 0.f};
+  float use[3] = {0.f, 0.f, 0.f}, ebd[4] = {0.f, 0.f, 0.f, 0.f};
   if constexpr (S1E > 0) {
     use[0] = fenc[kH16S];
     use[1] = fenc[kH16S + 1];
     use[2] = fenc[kH16S + 2];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ebd[j] = fenc[kH16S + 4 + j];
   }
 #endif
   if (wave < NT) {
@@ -781,7 +784,7 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
         ea = ff_tile_regs<SE>(wenc, iv);  // k_encode<true>'s MLP on this edge
 #else
         const float iv[4] = {pin[0], pin[1], pin[2], pin[3]};
-        ea = ff1_16_enc(fenc, iv, lane, use);  // k_encode<true>'s MLP on this edge (split-f16 block, read
+        ea = ff1_16_enc(fenc, iv, lane, use, ebd);  // k_encode<true>'s MLP on this edge (split-f16 block, read
                                                // through the cache)
 #endif
       } else {
