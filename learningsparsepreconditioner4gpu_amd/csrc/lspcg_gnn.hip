@@ -297,7 +297,7 @@ __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const f
 // W2 lo | C2 | W3 hi | W3 lo | C3 | 2^-s1..3, pad | the encoder's magnitude bounds B1, c1, B2, c2
 // (ff1_16_enc)] (kH16 dwords; K slot (q, j) = the lane's in[j], i.e.
 // feature 4q + j, as feat16); us = its 2^-s factors
-constexpr int kH16 = 1544;
+constexpr int kH16 = 1548;
 constexpr int kH16S = 1536;
 __device__ __forceinline__ f4 ff1_16(const float* fa, const float (&in)[4], int lane, const float (&us)[3]) {
   h4 xh, xl;
@@ -383,24 +383,41 @@ __device__ __forceinline__ f4 layer16h_guarded(const float* w, int oh, int ol, i
 // the fused edge encoder FeedForward(fin -> 16 -> 16 -> 16) (kH16 block) on raw features `in`
 // (this lane's features 4q .. 4q+3 of edge lane & 15), scaled per edge (enc_scale_exp)
 __device__ __forceinline__ f4 ff1_16_enc(const float* fa, const float (&in)[4], int lane, const float (&us)[3],
-                                         const float (&bd)[4]) {
+                                         const float (&bd)[5]) {
   const float m = swap_max32(swap_max16(fmaxf(fmaxf(fabsf(in[0]), fabsf(in[1])), fmaxf(fabsf(in[2]), fabsf(in[3])))));
   const unsigned scb = unsigned(enc_scale_exp(m) + 127) << 23;
   const float sc = __builtin_bit_cast(float, scb), isc = __builtin_bit_cast(float, 0x7f000000u - scb);  // 2^t, 2^-t
-  // the hidden layers' scale, branch-free: |h1| <= B1 m + c1 and |h2| <= B2 |h1| + c2 (B = max row
-  // sum of |W|, c = max |bias| + 0.17 for GELU's negative lobe; host constants), so 2^k with
-  // k = min(0, 14 - exponent of the larger bound) keeps every split below 2^15 (1 on normal data)
-  const float h1b = fmaf(bd[0], m, bd[1]);  // bd: fa[kH16S + 4 .. 7], read once per kernel
-  const float hb = fmaxf(h1b, fmaf(bd[2], h1b, bd[3]));
-  const int ke = int(__builtin_bit_cast(unsigned, hb) >> 23);
-  const unsigned hsb = unsigned(min(max(141 - ke, -100), 0) + 127) << 23;
-  const float hs = __builtin_bit_cast(float, hsb), ihs = __builtin_bit_cast(float, 0x7f000000u - hsb);
   h4 xh, xl;
   {
     const float v[4] = {in[0] * sc, in[1] * sc, in[2] * sc, in[3] * sc};
     split4(v, xh, xl);
   }
-  f4 h = gelu4(layer16h_sc(fa, 0, 128, 256, sc, us[0] * isc, xh, xl, lane)) * hs;
+  const f4 z1 = layer16h_sc(fa, 0, 128, 256, sc, us[0] * isc, xh, xl, lane);
+  // the hidden layers' scale: |h1| <= B1 m + c1 and |h2| <= B2 |h1| + c2 (B = max row sum of |W|,
+  // c = max |bias| + 0.17 for GELU's negative lobe; host constants bd), so 2^k with k = min(0, 14 -
+  // exponent of the larger bound) keeps every split below 2^15.  bd[4 .. 5] hold the largest m
+  // for which k = 0: a wave with no larger edge maximum (every wave on normal data) skips it.
+#ifdef LSPCG_ENC_HSBRANCH
+  if (!__builtin_amdgcn_ballot_w64(!(m <= bd[4]))) {
+    f4 h = gelu4(z1);
+    {
+      const float va[4] = {h.x, h.y, h.z, h.w};
+      split4(va, xh, xl);
+    }
+    h = gelu4(layer16h(fa, 512, 640, 768, us[1], xh, xl, lane));
+    {
+      const float va[4] = {h.x, h.y, h.z, h.w};
+      split4(va, xh, xl);
+    }
+    return layer16h(fa, 1024, 1152, 1280, us[2], xh, xl, lane);
+  }
+#endif
+  const float h1b = fmaf(bd[0], m, bd[1]);
+  const float hb = fmaxf(h1b, fmaf(bd[2], h1b, bd[3]));
+  const int ke = int(__builtin_bit_cast(unsigned, hb) >> 23);
+  const unsigned hsb = unsigned(min(max(141 - ke, -100), 0) + 127) << 23;
+  const float hs = __builtin_bit_cast(float, hsb), ihs = __builtin_bit_cast(float, 0x7f000000u - hsb);
+  f4 h = gelu4(z1) * hs;
   {
     const float va[4] = {h.x, h.y, h.z, h.w};
     split4(va, xh, xl);
@@ -742,13 +759,13 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
       pin[j] = f < fin ? eattr[row * fin + f] : 0.f;
     }
   };
-  float use[3] = {0.f, 0.f, 0.f}, ebd[4] = {0.f, 0.f, 0.f, 0.f};
+  float use[3] = {0.f, 0.f, 0.f}, ebd[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   if constexpr (S1E > 0) {
     use[0] = fenc[kH16S];
     use[1] = fenc[kH16S + 1];
     use[2] = fenc[kH16S + 2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) ebd[j] = fenc[kH16S + 4 + j];
+    for (int j = 0; j < 5; ++j) ebd[j] = fenc[kH16S + 4 + j];
   }
 #endif
   if (wave < NT) {
@@ -1024,10 +1041,20 @@ void emit_frag_h_any(std::vector<float>& o, const FF& f, const float* gamma, con
       for (int i = 0; i < n; ++i) mx = std::max(mx, std::fabs(double(get(i))));
       return float(mx + 0.17);
     };
-    o.push_back(rowsum(w1, H, f.in));
-    o.push_back(absmax([&](int i) { return b1[i]; }, H));
-    o.push_back(rowsum(w2, H, H));
-    o.push_back(absmax([&](int i) { return f.b2[i]; }, H));
+    const float B1 = rowsum(w1, H, f.in), c1 = absmax([&](int i) { return b1[i]; }, H);
+    const float B2 = rowsum(w2, H, H), c2 = absmax([&](int i) { return f.b2[i]; }, H);
+    o.push_back(B1);
+    o.push_back(c1);
+    o.push_back(B2);
+    o.push_back(c2);
+    // the largest edge maximum m with max(B1 m + c1, B2 (B1 m + c1) + c2) < 2^14 (no hidden scale);
+    // half the device threshold, so the float rounding of the bounds cannot matter
+    const double lim = 16384.0, h1 = std::min(lim, (lim - c2) / std::max(double(B2), 1e-30));
+    const double ms = (h1 - c1) / std::max(double(B1), 1e-30);
+    o.push_back(float(std::max(0.0, ms)));
+    o.push_back(0.f);
+    o.push_back(0.f);
+    o.push_back(0.f);
   }
 }
 // Largest |hidden activation| a LayerNorm-fed FeedForward can produce: LayerNorm outputs are at most
