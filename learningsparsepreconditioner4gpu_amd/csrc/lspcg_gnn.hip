@@ -395,9 +395,8 @@ __device__ __forceinline__ f4 ff1_16_enc(const float* fa, const float (&in)[4], 
   const f4 z1 = layer16h_sc(fa, 0, 128, 256, sc, us[0] * isc, xh, xl, lane);
   // the hidden layers' scale: |h1| <= B1 m + c1 and |h2| <= B2 |h1| + c2 (B = max row sum of |W|,
   // c = max |bias| + 0.17 for GELU's negative lobe; host constants bd), so 2^k with k = min(0, 14 -
-  // exponent of the larger bound) keeps every split below 2^15.  bd[4 .. 5] hold the largest m
+  // exponent of the larger bound) keeps every split below 2^15.  bd[4] holds the largest m
   // for which k = 0: a wave with no larger edge maximum (every wave on normal data) skips it.
-#ifdef LSPCG_ENC_HSBRANCH
   if (!__builtin_amdgcn_ballot_w64(!(m <= bd[4]))) {
     f4 h = gelu4(z1);
     {
@@ -411,7 +410,6 @@ __device__ __forceinline__ f4 ff1_16_enc(const float* fa, const float (&in)[4], 
     }
     return layer16h(fa, 1024, 1152, 1280, us[2], xh, xl, lane);
   }
-#endif
   const float h1b = fmaf(bd[0], m, bd[1]);
   const float hb = fmaxf(h1b, fmaf(bd[2], h1b, bd[3]));
   const int ke = int(__builtin_bit_cast(unsigned, hb) >> 23);
