@@ -218,9 +218,9 @@ constexpr int kH48W2h = 1024, kH48W2l = 1152, kH48C2 = 1280, kH48W3h = 1536, kH4
 constexpr int kH48S = 2048;
 
 // (a, b) -> packed f16 pairs hi = RNE(a, b), lo = RNE(a - hi, b - hi) (x - hi is exact in fp32).
-// Plain conversions, so the compiler sees every write: a three-instruction inline-asm form
-// (v_fma_mix{lo,hi}_f16 for the residuals) produced wrong layers -- the compiler pads no wait states
-// around inline asm, and its outputs landed in the operand registers of an in-flight MFMA.
+// Plain conversions: a three-instruction inline-asm form (v_fma_mix{lo,hi}_f16 for the residuals)
+// gives the same bits but, with the 2 wait states its MFMA consumers need inside the string (hipcc
+// pads nothing inside inline asm), measured no faster.
 __device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned& lo) {
   const hf2 h = __builtin_convertvector((f2){a, b}, hf2);
   const f2 r = (f2){a, b} - __builtin_convertvector(h, f2);
