@@ -261,10 +261,24 @@ def reference_iters(workload: str, boo) -> dict:
         return None
     z = np.load(path)
     sha = hashlib.sha256(np.ascontiguousarray(boo.detach().cpu().numpy()).tobytes()).hexdigest()
-    return {"counts_by_openblas_threads": dict(zip([str(int(t)) for t in z["ref_threads"]],
-                                                   [int(c) for c in z["ref_counts"]])),
-            "oracle_correctly_rounded_count": int(z["oracle_exact_count"]), "same_L": sha == str(z["boo_sha256"]),
-            "source": f"tests/golden/traj_{workload}.npz (validate.py:163-201 run on this A and GNN-L)"}
+    out = {"counts_by_openblas_threads": dict(zip([str(int(t)) for t in z["ref_threads"]],
+                                                  [int(c) for c in z["ref_counts"]])),
+           "oracle_correctly_rounded_count": int(z["oracle_exact_count"]), "same_L": sha == str(z["boo_sha256"]),
+           "source": f"tests/golden/traj_{workload}.npz (validate.py:163-201 run on this A and GNN-L)"}
+    rpath = path[:-4] + "_refgnn.npz"
+    if os.path.exists(rpath):  # the reference end to end: its own GNN forward -> its L -> its PCG
+        r = np.load(rpath)
+        stride = int(r["stride"])
+        got = boo.detach().reshape(-1, *r["ref_sample"].shape[1:])[::stride].cpu().numpy().astype(np.float64)
+        err = float(np.abs(got - r["ref_sample"].astype(np.float64)).max())
+        out["reference_gnn"] = {
+            "counts_by_openblas_threads": dict(zip([str(int(t)) for t in r["ref_threads"]],
+                                                   [int(c) for c in r["refL_counts"]])),
+            "oracle_correctly_rounded_count": int(r["oracle_exact_count"]),
+            "gnn_max_abs_err_vs_reference_sampled": err, "gnn_max_abs_reference": float(r["max_abs_ref"]),
+            "source": f"tests/golden/traj_{workload}_refgnn.npz (the reference's NodeEdgeProcessing forward, "
+                      "to_csr_cpu and get_pcg_iter_time_scipy on this system)"}
+    return out
 
 
 def parity_rows(A, L, eps: float, b, rtol: float, threads=(1, 8)) -> dict:

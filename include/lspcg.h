@@ -228,9 +228,10 @@ typedef struct lspcg_gnn_desc {
 } lspcg_gnn_desc;
 
 /* weights: packed fp32 blob in the order documented in learningsparsepreconditioner4gpu_amd/nn.py
- * (pack_weights); host or device pointer.  The MLP products run as fp32-accurate split-f16 GEMMs:
- * LSPCG_ERR_UNSUPPORTED when a LayerNorm-fed MLP's weights bound its hidden activations at 2^15 or
- * more (the error message gives the bound); raw edge features of any magnitude are scaled inside. */
+ * (pack_weights); host or device pointer.  The MLP products run as fp32-accurate split-f16 GEMMs
+ * (raw edge features of any magnitude are scaled per edge inside); weights whose LayerNorm-fed MLPs
+ * bound their hidden activations at 2^15 or more -- past f16's range -- select the fp32-MFMA
+ * kernels instead (environment LSPCG_GNN_F32=1 forces them).  Any weights run. */
 int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* weights,
                      int64_t nweights, lspcg_gnn** out);
 /* Structure analysis of a graph (its CSC by destination), like a sparse library's analysis step:
@@ -242,6 +243,9 @@ int lspcg_gnn_set_graph(lspcg_gnn* g, int64_t N, int64_t E, const int64_t* edge_
  * (all fp32 device).  Message aggregation order is deterministic. */
 int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const int64_t* edge_index,
                       const float* edge_attr, float* out);
+/* Which kernels lspcg_gnn_create chose: *f32 = 1 for the fp32-MFMA ones, 0 for the split-f16 GEMMs;
+ * *hidden_bound (may be NULL) = the weights' hidden-activation bound that decided it (2^15). */
+int lspcg_gnn_precision(const lspcg_gnn* g, int* f32, double* hidden_bound);
 int lspcg_gnn_destroy(lspcg_gnn* g);
 
 /* ---- block SpMV over an edge list (GraphSpmv / AATPE, basic_layers.py:112-142, 228-261) ----

@@ -73,6 +73,7 @@ SIGNATURES = {
     "lspcg_gnn_create": (C.c_int, [vp, C.POINTER(lspcg_gnn_desc), vp, C.c_int64, pp]),
     "lspcg_gnn_set_graph": (C.c_int, [vp, C.c_int64, C.c_int64, vp]),
     "lspcg_gnn_forward": (C.c_int, [vp, C.c_int64, C.c_int64, vp, vp, vp, vp]),
+    "lspcg_gnn_precision": (C.c_int, [vp, C.POINTER(C.c_int), p_f64]),
     "lspcg_gnn_destroy": (C.c_int, [vp]),
     "lspcg_graph_create": (C.c_int, [vp, C.c_int64, C.c_int64, C.c_int, vp, pp]),
     "lspcg_graph_destroy": (C.c_int, [vp]),

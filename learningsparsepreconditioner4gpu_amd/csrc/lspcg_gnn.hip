@@ -152,10 +152,10 @@ __device__ __forceinline__ f4 ff_tail(const float* fr, int s1, f4 h, int lane) {
   return o;
 }
 
-#ifdef LSPCG_GNN_F32
 // Two FFs with 48 inputs sharing the same B operand (message + edge MLP of an MPLayer): the
-// two dependent MFMA chains and the two GELU blocks are interleaved so they overlap (f32 MFMA;
-// the default build runs the split-f16 version below).
+// two dependent MFMA chains and the two GELU blocks are interleaved so they overlap (f32 MFMA:
+// the F32 kernels, chosen by lspcg_gnn_create for weights past the split-f16 range; the default
+// runs the split-f16 version below).
 __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const float (&in)[12], int lane, f4& oa,
                                        f4& ob) {
   f4 ha = *reinterpret_cast<const f4*>(fa + 12 * 64 + lane * 4);
@@ -187,9 +187,6 @@ __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const f
   }
 }
 
-#endif
-
-#ifndef LSPCG_GNN_F32
 // ---- The message + edge MLPs of an MPLayer on f16 MFMAs with split operands -----------------
 // On gfx950 an f32 MFMA and a vector instruction never execute together on a SIMD (the layer's PMC:
 // SQ_VALU_MFMA_COEXEC_CYCLES = 0, MFMA 47 % + VALU 44 % of the cycles; tools/coexec_probe.hip: one
@@ -351,18 +348,18 @@ __device__ __forceinline__ int enc_scale_exp(float m) {
 }
 
 // hidden activations of the edge decoder follow the raw edge features' magnitude (through the edge
-// residuals): a wave whose largest |h| reaches 2^15 scales them by 2^t (t < 0, so the largest lands in [2^14, 2^15)) and the next
-// layer undoes it (its bias times 2^t, its product times 2^-t), so no split overflows f16.  The
-// check is 3 VALU + a wave-uniform branch that normal magnitudes never take; returns t (0: none).
+// residuals): an EDGE whose largest |h| reaches 2^15 has its hidden values scaled by 2^t (t < 0, so
+// its largest lands in [2^14, 2^15)) and the next layer undoes it for that edge's column (its bias
+// times 2^t, its product times 2^-t), so no split overflows f16 -- per edge, like the input scale,
+// so a small edge sharing a tile with a huge one keeps its own relative accuracy (a wave-wide
+// factor would push its low halves into f16 subnormals).  The check is 3 VALU + a wave-uniform
+// branch that normal magnitudes never take; returns this lane's edge's t (0: none).
 __device__ __forceinline__ int enc_guard(f4& h) {
   const float m = fmaxf(fmaxf(fabsf(h.x), fabsf(h.y)), fmaxf(fabsf(h.z), fabsf(h.w)));
   if (!__builtin_amdgcn_ballot_w64(!(m < 32768.0f))) return 0;  // NaN takes the slow path too
-  float w = m;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) w = fmaxf(w, __shfl_xor(w, o));
+  const float w = swap_max32(swap_max16(m));                   // the edge's 4 lanes
   const int e = int(__builtin_bit_cast(unsigned, w) >> 23) & 0xff;
-  if (e == 0xff) return 0;  // inf / NaN: propagates either way
-  const int t = 141 - e;    // e >= 142 here, so -113 <= t <= -1
+  const int t = (w >= 32768.0f && e != 0xff) ? 141 - e : 0;   // -113 <= t <= -1; inf / NaN propagate
   h *= exp2i(t);
   return t;
 }
@@ -380,8 +377,8 @@ __device__ __forceinline__ f4 layer16h_sc(const float* w, int oh, int ol, int oc
 }
 __device__ __forceinline__ f4 layer16h_guarded(const float* w, int oh, int ol, int oc, float unscale, int t, h4 xh,
                                                h4 xl, int lane) {
-  if (t == 0) return layer16h(w, oh, ol, oc, unscale, xh, xl, lane);
-  return layer16h_sc(w, oh, ol, oc, exp2i(t), unscale * exp2i(-t), xh, xl, lane);
+  if (!__builtin_amdgcn_ballot_w64(t != 0)) return layer16h(w, oh, ol, oc, unscale, xh, xl, lane);  // wave-uniform
+  return layer16h_sc(w, oh, ol, oc, exp2i(t), unscale * exp2i(-t), xh, xl, lane);  // per lane = per edge
 }
 
 // the fused edge encoder FeedForward(fin -> 16 -> 16 -> 16) (kH16 block) on raw features `in`
@@ -475,7 +472,6 @@ __device__ __forceinline__ f4 ff1_48(const float* fa, const float (&in)[12], int
   }
   return layer16h_guarded(fa, kH48W3h, kH48W3l, kH48C3, us[2], tg, xah, xal, lane);
 }
-#endif
 
 template <int S1>
 __device__ __forceinline__ f4 ff_tile_regs(const FragRegs<S1>& w, const float (&in)[S1]) {
@@ -646,19 +642,15 @@ __global__ void __launch_bounds__(256) k_encode(int64_t M, int fin, const float*
 // out[e] = edge_dec(cat[e_attr, x[src], x[dst]])  (gnns.py:88-95; original edge order).  Visits
 // edges e, gathering each 64-B edge-state row from its CSC slot inv[e]: measured faster than
 // visiting slots and scattering the OUT-float results (0.59 vs 0.67 ms at E = 15.2 M).
-template <int OUT>
+template <bool F32, int OUT>
 __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __restrict__ fr,
                                                  const int64_t* __restrict__ ei, const int32_t* __restrict__ inv,
                                                  const float* __restrict__ ecsc, const float* __restrict__ x,
                                                  float* __restrict__ out) {
   // the decoder's fragment block in LDS (8 KiB): the per-tile weight reads stay off the gathers'
   // memory queue
-#ifdef LSPCG_GNN_F32
-  constexpr int kDec = frag_size(12);
-#else
-  constexpr int kDec = kH48;  // split-f16 block (ff1_48)
-  const float us[3] = {fr[kH48S], fr[kH48S + 1], fr[kH48S + 2]};
-#endif
+  constexpr int kDec = F32 ? frag_size(12) : kH48;  // f32 fragments / split-f16 block (ff1_48)
+  const float us[3] = {F32 ? 1.f : fr[kH48S], F32 ? 1.f : fr[kH48S + 1], F32 ? 1.f : fr[kH48S + 2]};
   __shared__ __attribute__((aligned(16))) float wd[kDec];
   for (int i = threadIdx.x; i < kDec / 4; i += 256) reinterpret_cast<f4*>(wd)[i] = ld4(fr + 4 * i);
   __syncthreads();
@@ -670,11 +662,9 @@ __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __rest
     const int64_t ee = valid ? e : E - 1;
     float in[12];
     pack12(ld4(ecsc + int64_t(inv[ee]) * H + 4 * q), ld4(x + ei[ee] * H + 4 * q), ld4(x + ei[E + ee] * H + 4 * q), in);
-#ifdef LSPCG_GNN_F32
-    const f4 o = ff_tile<12>(wd, in, lane);
-#else
-    const f4 o = ff1_48(wd, in, lane, us);
-#endif
+    f4 o;
+    if constexpr (F32) o = ff_tile<12>(wd, in, lane);
+    else o = ff1_48(wd, in, lane, us);
     if (valid) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -686,22 +676,15 @@ __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __rest
 // ---------------------------------------------------------------------------
 // One MPLayer (basic_layers.py:193-225) as one kernel
 // ---------------------------------------------------------------------------
-#ifdef LSPCG_GNN_F32
-constexpr int kFrag48 = frag_size(12);
-#else
-constexpr int kFrag48 = kH48;  // split-f16 blocks (ff2_48, ff1_16)
-#endif
-#ifdef LSPCG_GNN_F32
-constexpr int kFrag16 = frag_size(4);
-#else
-constexpr int kFrag16 = kH16;
-#endif
-constexpr int kLayerFrag = 2 * kFrag48 + kFrag16;  // [msg | edge | node]
+// fragment blocks of one layer, [msg | edge | node]: f32 fragments or split-f16 blocks (ff2_48, ff1_16)
+constexpr int frag48(bool f32) { return f32 ? frag_size(12) : kH48; }
+constexpr int frag16(bool f32) { return f32 ? frag_size(4) : kH16; }
+constexpr int layer_frag(bool f32) { return 2 * frag48(f32) + frag16(f32); }
 
 // S1E > 0 (first layer): the edge encoder is fused in -- the layer's input edge state is computed
 // from the raw edge features (fin <= 4 S1E floats of edge perm[k], fragment block `fenc` read
 // through the cache, not LDS) instead of read back from an [E,16] pass of k_encode<true>.
-template <int S1E>
+template <bool F32, int S1E>
 __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __restrict__ frag, int node_res,
                                                  int edge_res, const int32_t* __restrict__ ptr,
                                                  const int32_t* __restrict__ src, const int32_t* __restrict__ dst,
@@ -709,21 +692,21 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
                                                  float* __restrict__ xout, const float* __restrict__ fenc, int fin,
                                                  const float* __restrict__ eattr, const int32_t* __restrict__ perm) {
   [[maybe_unused]] constexpr int SE = S1E > 0 ? S1E : 1;
+  constexpr int kLayerFrag = layer_frag(F32), kFrag48 = frag48(F32);
   __shared__ __attribute__((aligned(16))) float wl[kLayerFrag];
   __shared__ __attribute__((aligned(16))) float msg[CE * H];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, it = lane & 15, q = lane >> 4;
   for (int i = tid; i < kLayerFrag / 4; i += 256) reinterpret_cast<f4*>(wl)[i] = ld4(frag + 4 * i);
   __syncthreads();
-#ifdef LSPCG_GNN_F32
-  FragRegs<SE> wenc;
-  if constexpr (S1E > 0) wenc.load(fenc, lane);
-#endif
+  [[maybe_unused]] FragRegs<SE> wenc;
+  if constexpr (F32 && S1E > 0) wenc.load(fenc, lane);
   const float* fmsg = wl;
-#ifndef LSPCG_GNN_F32
-  const float us[6] = {frag[kH48S], frag[kH48S + 1], frag[kH48S + 2], frag[kH48 + kH48S], frag[kH48 + kH48S + 1],
-                       frag[kH48 + kH48S + 2]};
-  const float usn[3] = {frag[2 * kH48 + kH16S], frag[2 * kH48 + kH16S + 1], frag[2 * kH48 + kH16S + 2]};
-#endif
+  // split-f16 unscale factors (unused by the F32 kernels, whose blob has none at these offsets)
+  const float us[6] = {F32 ? 1.f : frag[kH48S], F32 ? 1.f : frag[kH48S + 1], F32 ? 1.f : frag[kH48S + 2],
+                       F32 ? 1.f : frag[kH48 + kH48S], F32 ? 1.f : frag[kH48 + kH48S + 1],
+                       F32 ? 1.f : frag[kH48 + kH48S + 2]};
+  const float usn[3] = {F32 ? 1.f : frag[2 * kH48 + kH16S], F32 ? 1.f : frag[2 * kH48 + kH16S + 1],
+                        F32 ? 1.f : frag[2 * kH48 + kH16S + 2]};
   const float* fedge = wl + kFrag48;
   const float* fnode = wl + 2 * kFrag48;
   const int n0 = blockIdx.x * 256;
@@ -743,33 +726,25 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
   auto edge_of = [&](int T) { const int k = k0 + T * 16 + it; return k < k1 ? k : klast; };
   int qd = 0, qs = 0, qe = 0;
   f4 pxd{}, pxs{}, pea{};
-#ifdef LSPCG_GNN_F32
-  float pin[SE];  // fused encoder: this lane's raw input features of the prefetched edge
+  // fused encoder, this lane's raw input features of the prefetched edge: F32, K slot q of step s =
+  // feature 4s + q (f32 fragments); split-f16, features 4q .. 4q+3 (the kH16 block fenc)
+  constexpr int NPIN = F32 ? SE : 4;
+  float pin[NPIN];
   auto load_in = [&](int row) {
 #pragma unroll
-    for (int s = 0; s < SE; ++s) {
-      const int f = 4 * s + q;
+    for (int s = 0; s < NPIN; ++s) {
+      const int f = F32 ? 4 * s + q : 4 * q + s;
       pin[s] = f < fin ? eattr[row * fin + f] : 0.f;
     }
   };
-#else
-  float pin[4];  // fused encoder (split-f16 block, fenc): features 4q .. 4q+3 of the prefetched edge
-  auto load_in = [&](int row) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int f = 4 * q + j;
-      pin[j] = f < fin ? eattr[row * fin + f] : 0.f;
-    }
-  };
   float use[3] = {0.f, 0.f, 0.f}, ebd[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-  if constexpr (S1E > 0) {
+  if constexpr (!F32 && S1E > 0) {
     use[0] = fenc[kH16S];
     use[1] = fenc[kH16S + 1];
     use[2] = fenc[kH16S + 2];
 #pragma unroll
     for (int j = 0; j < 5; ++j) ebd[j] = fenc[kH16S + 4 + j];
   }
-#endif
   if (wave < NT) {
     const int kk = edge_of(wave);
     qd = dst[kk];
@@ -795,17 +770,15 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
       const bool valid = k < k1;
       const f4 xd = pxd, xs = pxs;  // x_i (target), x_j (source)
       f4 ea;                         // edge attr
-      if constexpr (S1E > 0) {
-#ifdef LSPCG_GNN_F32
+      if constexpr (S1E > 0 && F32) {
         float iv[SE];
 #pragma unroll
         for (int s = 0; s < SE; ++s) iv[s] = pin[s];
         ea = ff_tile_regs<SE>(wenc, iv);  // k_encode<true>'s MLP on this edge
-#else
+      } else if constexpr (S1E > 0) {
         const float iv[4] = {pin[0], pin[1], pin[2], pin[3]};
         ea = ff1_16_enc(fenc, iv, lane, use, ebd);  // k_encode<true>'s MLP on this edge (split-f16 block, read
                                                // through the cache)
-#endif
       } else {
         ea = pea;
       }
@@ -839,11 +812,8 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
         v[2 * j + 1] = w[j].y;
       }
       f4 m, u;
-#ifdef LSPCG_GNN_F32
-      ff2_48(fmsg, fedge, v, lane, m, u);
-#else
-      ff2_48(fmsg, fedge, v, lane, m, u, us);
-#endif
+      if constexpr (F32) ff2_48(fmsg, fedge, v, lane, m, u);
+      else ff2_48(fmsg, fedge, v, lane, m, u, us);
       if (edge_res) u += ea;
       if (valid) {
         st4(e + int64_t(k) * H + 4 * q, u);
@@ -873,11 +843,9 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
     const float rstd = __builtin_amdgcn_rsqf(quad_sum(sq) * (1.0f / 16.0f) + 1e-5f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] *= rstd;
-#ifdef LSPCG_GNN_F32
-    f4 o = ff_tile<4>(fnode, v, lane);
-#else
-    f4 o = ff1_16(fnode, v, lane, usn);
-#endif
+    f4 o;
+    if constexpr (F32) o = ff_tile<4>(fnode, v, lane);
+    else o = ff1_16(fnode, v, lane, usn);
     if (i < n1) {
       if (node_res) o += ld4(x + int64_t(i) * H + 4 * q);
       st4(xout + int64_t(i) * H + 4 * q, o);
@@ -966,7 +934,6 @@ void emit_frag(std::vector<float>& o, const FF& f, int s1, Feat feat, const floa
 
 auto feat48 = [](int s, int q) { return (s >> 2) * 16 + 4 * q + (s & 3); };
 
-#ifndef LSPCG_GNN_F32
 // The split-f16 block of a FeedForward(48 -> 16 -> 16 -> out) (ff2_48; layout at kH48): weights
 // scaled by 2^s per matrix (max |W| 2^s in [2^10, 2^11)), split into RNE f16 pairs.
 void emit_frag_h_any(std::vector<float>& o, const FF& f, const float* gamma, const float* beta, bool in48) {
@@ -1062,7 +1029,8 @@ void emit_frag_h_any(std::vector<float>& o, const FF& f, const float* gamma, con
 // Largest |hidden activation| a LayerNorm-fed FeedForward can produce: LayerNorm outputs are at most
 // sqrt(n - 1) in magnitude (gamma / beta folded into layer 1), |GELU(z)| <= max(|z|, 0.17), so
 // |h1| <= ||W1'||_inf sqrt(n - 1) + max |b1'| + 0.17 and |h2| <= ||W2||_inf |h1| + max |b2| + 0.17.
-// The split-f16 products need it below 2^15 (f16 holds 65504): gnn_create refuses weights past it.
+// The split-f16 products need it below 2^15 (f16 holds 65504): gnn_create runs the fp32-MFMA
+// kernels for weights past it.
 double ln_ff_hidden_bound(const FF& f, const float* gamma, const float* beta) {
   double h1 = 0, h2 = 0, b2 = 0;
   for (int i = 0; i < H; ++i) {
@@ -1087,8 +1055,7 @@ void emit_frag_h(std::vector<float>& o, const FF& f, const float* gamma, const f
 void emit_frag_h16(std::vector<float>& o, const FF& f, const float* gamma, const float* beta) {
   emit_frag_h_any(o, f, gamma, beta, false);  // kH16 dwords
 }
-#endif
-[[maybe_unused]] auto feat16 = [](int s, int q) { return 4 * q + s; };
+auto feat16 = [](int s, int q) { return 4 * q + s; };
 auto featenc = [](int s, int q) { return 4 * s + q; };
 
 }  // namespace
@@ -1099,6 +1066,8 @@ struct lspcg_gnn {
   float* frag = nullptr;  // device fragment blob
   int64_t o_node_enc = 0, o_edge_enc = 0, o_dec = 0;
   int64_t o_edge_enc_h = 0;  // split-f16 block of the edge encoder (the first layer's fused copy)
+  bool f32 = false;          // fp32-MFMA kernels (weights past the split-f16 range, or LSPCG_GNN_F32=1)
+  double hidden_bound = 0;   // largest ln_ff_hidden_bound over the layers (what chose f32)
   std::vector<int64_t> o_layer;  // per layer: [msg | edge | node] fragment block
   // workspace
   int64_t capN = -1, capE = -1;
@@ -1179,6 +1148,23 @@ int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* we
   g->d = d;
   std::vector<float> w(need);
   LSPCG_HIP(hipMemcpy(w.data(), weights, sizeof(float) * need, hipMemcpyDefault));  // host or device source
+  // precision: the split-f16 GEMMs hold hidden activations below 2^15; weights whose LayerNorm-fed
+  // MLPs could exceed that run the exact fp32-MFMA kernels instead (same results to ~1e-7, 1.2x slower)
+  {
+    int64_t ob = ff_size(d.node_in, H) + ff_size(d.edge_in, H);
+    for (int l = 0; l < d.num_mp_layers; ++l) {
+      const float* node = w.data() + ob;
+      const float* edge = node + 2 * H + ff_size(H, H);
+      const float* msgp = edge + 6 * H + ff_size(3 * H, H);
+      ob += 2 * H + ff_size(H, H) + 2 * (6 * H + ff_size(3 * H, H));
+      g->hidden_bound = std::max({g->hidden_bound, ln_ff_hidden_bound(ff_at(msgp + 6 * H, 3 * H, H), msgp, msgp + 3 * H),
+                                  ln_ff_hidden_bound(ff_at(edge + 6 * H, 3 * H, H), edge, edge + 3 * H),
+                                  ln_ff_hidden_bound(ff_at(node + 2 * H, H, H), node, node + H)});
+    }
+    const char* ev = std::getenv("LSPCG_GNN_F32");
+    g->f32 = !(g->hidden_bound < 32768.0) || (ev && ev[0] == '1');
+  }
+  const bool f32 = g->f32;
   std::vector<float> fr;
   int64_t o = 0;
   g->o_node_enc = int64_t(fr.size());
@@ -1196,41 +1182,24 @@ int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* we
     const float* msgp = w.data() + o;
     o += 6 * H + ff_size(3 * H, H);
     g->o_layer.push_back(int64_t(fr.size()));
-#ifndef LSPCG_GNN_F32
-    {
-      const double hb = std::max({ln_ff_hidden_bound(ff_at(msgp + 6 * H, 3 * H, H), msgp, msgp + 3 * H),
-                                  ln_ff_hidden_bound(ff_at(edge + 6 * H, 3 * H, H), edge, edge + 3 * H),
-                                  ln_ff_hidden_bound(ff_at(node + 2 * H, H, H), node, node + H)});
-      LSPCG_CHECK(hb < 32768.0, LSPCG_ERR_UNSUPPORTED,
-                  "gnn_create: layer " + std::to_string(l) + "'s MLP weights allow hidden activations up to " +
-                      std::to_string(hb) + ", past the split-f16 GEMMs' 2^15");
+    if (f32) {
+      emit_frag(fr, ff_at(msgp + 6 * H, 3 * H, H), 12, feat48, msgp, msgp + 3 * H);
+      emit_frag(fr, ff_at(edge + 6 * H, 3 * H, H), 12, feat48, edge, edge + 3 * H);
+      emit_frag(fr, ff_at(node + 2 * H, H, H), 4, feat16, node, node + H);
+    } else {
+      emit_frag_h(fr, ff_at(msgp + 6 * H, 3 * H, H), msgp, msgp + 3 * H);
+      emit_frag_h(fr, ff_at(edge + 6 * H, 3 * H, H), edge, edge + 3 * H);
+      emit_frag_h16(fr, ff_at(node + 2 * H, H, H), node, node + H);
     }
-#endif
-#ifdef LSPCG_GNN_F32
-    emit_frag(fr, ff_at(msgp + 6 * H, 3 * H, H), 12, feat48, msgp, msgp + 3 * H);
-    emit_frag(fr, ff_at(edge + 6 * H, 3 * H, H), 12, feat48, edge, edge + 3 * H);
-#else
-    emit_frag_h(fr, ff_at(msgp + 6 * H, 3 * H, H), msgp, msgp + 3 * H);
-    emit_frag_h(fr, ff_at(edge + 6 * H, 3 * H, H), edge, edge + 3 * H);
-#endif
-#ifdef LSPCG_GNN_F32
-    emit_frag(fr, ff_at(node + 2 * H, H, H), 4, feat16, node, node + H);
-#else
-    emit_frag_h16(fr, ff_at(node + 2 * H, H, H), node, node + H);
-#endif
   }
   g->o_dec = int64_t(fr.size());
-#ifdef LSPCG_GNN_F32
-  emit_frag(fr, ff_at(w.data() + o, 3 * H, d.edge_out), 12, feat48, nullptr, nullptr);
-#else
-  emit_frag_h(fr, ff_at(w.data() + o, 3 * H, d.edge_out), nullptr, nullptr);
-#endif
-#ifndef LSPCG_GNN_F32
-  g->o_edge_enc_h = int64_t(fr.size());
-  if (d.edge_in <= 16) emit_frag_h16(fr, ff_at(enc_w, d.edge_in, H), nullptr, nullptr);
-#else
-  (void)enc_w;
-#endif
+  if (f32) {
+    emit_frag(fr, ff_at(w.data() + o, 3 * H, d.edge_out), 12, feat48, nullptr, nullptr);
+  } else {
+    emit_frag_h(fr, ff_at(w.data() + o, 3 * H, d.edge_out), nullptr, nullptr);
+    g->o_edge_enc_h = int64_t(fr.size());
+    if (d.edge_in <= 16) emit_frag_h16(fr, ff_at(enc_w, d.edge_in, H), nullptr, nullptr);
+  }
   LSPCG_HIP(hipMalloc(&g->frag, sizeof(float) * fr.size()));
   LSPCG_HIP(hipMemcpy(g->frag, fr.data(), sizeof(float) * fr.size(), hipMemcpyHostToDevice));
   *out = g.release();
@@ -1313,14 +1282,18 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
   float* xc = g->xa;
   float* xn = g->xb;
   const unsigned lg = unsigned((N + 255) / 256);
-#ifdef LSPCG_GNN_F32
-  const float* fenc = g->frag + g->o_edge_enc;
-#else
-  const float* fenc = g->frag + g->o_edge_enc_h;  // the fused copy reads the split-f16 block
-#endif
+  // the fused copy reads the split-f16 block (f32: the f32 fragments, held in registers)
+  const float* fenc = g->frag + (g->f32 ? g->o_edge_enc : g->o_edge_enc_h);
   for (int l = 0; l < d.num_mp_layers; ++l) {
     const int se = (l == 0 && fuse_enc) ? s1e : 0;
-    auto kern = se == 1 ? k_mp_layer<1> : se == 2 ? k_mp_layer<2> : se == 3 ? k_mp_layer<3> : k_mp_layer<0>;
+    auto kern = g->f32 ? (se == 1   ? k_mp_layer<true, 1>
+                          : se == 2 ? k_mp_layer<true, 2>
+                          : se == 3 ? k_mp_layer<true, 3>
+                                    : k_mp_layer<true, 0>)
+                       : (se == 1   ? k_mp_layer<false, 1>
+                          : se == 2 ? k_mp_layer<false, 2>
+                          : se == 3 ? k_mp_layer<false, 3>
+                                    : k_mp_layer<false, 0>);
     hipLaunchKernelGGL(kern, dim3(lg), dim3(256), 0, st, N, g->frag + g->o_layer[l], d.node_residual, d.edge_residual,
                        g->ptr, g->src, g->dst, xc, g->ecsc, xn, fenc, d.edge_in, edge_attr,
                        static_cast<const int32_t*>(g->perm));
@@ -1328,13 +1301,17 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
   }
   // decoder
   const float* fd = g->frag + g->o_dec;
-  if (d.edge_out == 1)
-    hipLaunchKernelGGL(k_edge_dec<1>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, inv, g->ecsc, xc, out);
-  else if (d.edge_out == 4)
-    hipLaunchKernelGGL(k_edge_dec<4>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, inv, g->ecsc, xc, out);
-  else
-    hipLaunchKernelGGL(k_edge_dec<9>, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, inv, g->ecsc, xc, out);
+  auto dec = g->f32 ? (d.edge_out == 1 ? k_edge_dec<true, 1> : d.edge_out == 4 ? k_edge_dec<true, 4> : k_edge_dec<true, 9>)
+                    : (d.edge_out == 1 ? k_edge_dec<false, 1> : d.edge_out == 4 ? k_edge_dec<false, 4> : k_edge_dec<false, 9>);
+  hipLaunchKernelGGL(dec, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, inv, g->ecsc, xc, out);
   LSPCG_HIP(hipGetLastError());
+  return LSPCG_OK;
+}
+
+int lspcg_gnn_precision(const lspcg_gnn* g, int* f32, double* hidden_bound) {
+  LSPCG_CHECK(g && f32, LSPCG_ERR_ARG, "gnn_precision: NULL argument");
+  *f32 = g->f32 ? 1 : 0;
+  if (hidden_bound) *hidden_bound = g->hidden_bound;
   return LSPCG_OK;
 }
 

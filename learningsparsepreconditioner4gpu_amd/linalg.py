@@ -11,10 +11,13 @@ validate.py:163-341): see ``include/lspcg.h`` and DESIGN.md.  ``x`` is updated i
 with the solution (numpy arrays or device tensors).  Only the HIP path exists.
 
 Device contract: the reference's own defaults are ``device="cpu"``
-(``validate.py:61,98``: pymathprim's CPU backend), and ``infer.py:323-325`` calls both
-devices.  This class replaces the ``device="cuda"`` backend only; the CPU row stays with
-pymathprim / scipy.  ``device="cpu"`` raises ``ValueError`` loudly
-instead of silently running somewhere else -- there is no CPU solver in the product.
+(``validate.py:61,98``: pymathprim's CPU backend), and ``infer.py:316-325`` calls both
+devices from one loop.  This class replaces the ``device="cuda"`` backend only:
+``PreconditionedConjugateGradient(A, device="cpu", ...)`` constructs pymathprim's own solver
+(the reference's CPU row, unchanged) when pymathprim is importable, and otherwise raises
+:class:`CpuBackendUnavailable` -- a ``RuntimeError``, the exception the reference's infer loop
+already catches per sample (``infer.py:363``).  Nothing here runs a CPU solve of its own: there
+is no CPU solver in the product.
 """
 from __future__ import annotations
 
@@ -29,8 +32,31 @@ from . import _lib
 from .sparse import Context, DeviceMatrix, _ptr, lspcg_dtype
 
 GPU_DEVICES = ("cuda", "hip", "gpu", "rocm")
+CPU_DEVICES = ("cpu",)
 SUPPORTED = tuple(_lib.PRECOND) + ("ainv",)
 NOT_BUILT = ("fsai",)  # commented out of the reference's baseline rows (infer.py:315)
+
+
+class CpuBackendUnavailable(RuntimeError):
+    """``device="cpu"`` without pymathprim: the reference's CPU backend is not installed.  A
+    ``RuntimeError``, so the reference's infer loop (``except RuntimeError``, infer.py:363) logs it
+    and moves on exactly as it does for a solver failure."""
+
+
+def is_cpu_device(device) -> bool:
+    return str(device).split(":")[0] in CPU_DEVICES
+
+
+def cpu_backend():
+    """pymathprim's ``PreconditionedConjugateGradient`` -- the class the reference's CPU rows
+    construct (validate.py:73, 110, 145) -- or :class:`CpuBackendUnavailable`."""
+    try:
+        from pymathprim.linalg import PreconditionedConjugateGradient as host_pcg
+    except ImportError as e:
+        raise CpuBackendUnavailable(
+            "device='cpu' is pymathprim's CPU backend (the reference's CPU rows), which is not installed; "
+            "this framework replaces the device='cuda' backend only") from e
+    return host_pcg
 
 
 def _as_device_matrix(M, dtype, block_size: int, ctx: Context) -> DeviceMatrix:
@@ -42,13 +68,23 @@ def _as_device_matrix(M, dtype, block_size: int, ctx: Context) -> DeviceMatrix:
 
 
 class PreconditionedConjugateGradient:
+    def __new__(cls, matrix=None, device: str = "cuda", preconditioner: str = "none", dtype=np.float64,
+                block_size: int = 1, ctx: Optional[Context] = None, dot_order: str = "compensated",
+                dot_threads: int = 1):
+        if is_cpu_device(device):
+            # the reference's CPU row: pymathprim's solver with the reference's own arguments
+            # (validate.py:79, 116, 151-156); the MI355X-only keywords have no meaning there
+            if block_size != 1 or ctx is not None or dot_order != "compensated":
+                raise ValueError("block_size / ctx / dot_order select the MI355X solver; device='cpu' is pymathprim's")
+            return cpu_backend()(matrix=matrix, device=device, preconditioner=preconditioner, dtype=dtype)
+        return super().__new__(cls)
+
     def __init__(self, matrix, device: str = "cuda", preconditioner: str = "none", dtype=np.float64,
                  block_size: int = 1, ctx: Optional[Context] = None, dot_order: str = "compensated",
                  dot_threads: int = 1):
         if str(device).split(":")[0] not in GPU_DEVICES:
             raise ValueError(
-                f"device={device!r}: this framework runs PCG on MI355X only (device='cuda'); the CPU "
-                "reference path is not part of the product")
+                f"device={device!r}: expected 'cuda' (this MI355X solver) or 'cpu' (pymathprim's CPU backend)")
         if preconditioner in NOT_BUILT:
             raise NotImplementedError(f"preconditioner {preconditioner!r} is not built (the reference's baseline "
                                       "rows use none / diagonal / ainv / ic, infer.py:310-315)")

@@ -194,6 +194,16 @@ class NodeEdgeProcessing(nn.Module):
         _lib.call("lspcg_gnn_create", ctx.handle, C.byref(desc), blob.data_ptr(), blob.numel(), C.byref(h))
         self._handle, self._ctx, self._packed_version = h, ctx, self._version()
 
+    def precision(self, device=None) -> dict:
+        """Which GEMM kernels ``lspcg_gnn_create`` chose for the current weights:
+        ``{"f32": False}`` = split-f16 MFMAs (the default), ``True`` = fp32 MFMAs (weights whose
+        LayerNorm-fed hidden activations could pass f16's range, or LSPCG_GNN_F32=1), with the
+        weights' hidden-activation bound that decided it (``lspcg_gnn_precision``)."""
+        self._ensure_handle(torch.device(device) if device is not None else torch.device("cuda"))
+        f32, hb = C.c_int(), C.c_double()
+        _lib.call("lspcg_gnn_precision", self._handle, C.byref(f32), C.byref(hb))
+        return {"f32": bool(f32.value), "hidden_bound": hb.value}
+
     def _free(self):
         if self._handle is not None and _lib._lib is not None:
             _lib._lib.lspcg_gnn_destroy(self._handle)

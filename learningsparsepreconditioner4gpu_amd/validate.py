@@ -17,12 +17,14 @@ Same names, arguments, return values and error behaviour as the reference:
 
 Matrices may be scipy CSR (uploaded) or :class:`DeviceMatrix` (already in HBM).
 
-Device contract: the reference defaults ``device="cpu"`` (validate.py:61,98), i.e.
-pymathprim's CPU backend.  These functions default to ``device="cuda"`` and replace the GPU
-backend only; the reference's CPU rows keep calling pymathprim / scipy.
-``device="cpu"`` raises ``ValueError`` -- there is no CPU solver in the product.
-Right-hand sides are formed on the device exactly as ``b = A @ gt`` (bit-identical to
-scipy's csr_matvec).
+Device contract: the reference's default, ``device="cpu"`` (validate.py:61,98,133), is kept
+and means what it means there: pymathprim's CPU backend.  ``device="cpu"`` runs the reference's
+own host sequence (validate.py:64-86, 99-121, 134-160: ``b = A @ gt`` on the host, one
+pymathprim solver per repeat) through ``linalg.PreconditionedConjugateGradient``, which hands
+the CPU device to pymathprim or raises ``linalg.CpuBackendUnavailable`` (a ``RuntimeError``,
+what the reference's infer loop catches) when pymathprim is absent.  ``device="cuda"`` is the
+MI355X path, where right-hand sides are formed on the device exactly as ``b = A @ gt``
+(bit-identical to scipy's csr_matvec).  No function here computes a solve on the host.
 """
 from __future__ import annotations
 
@@ -37,7 +39,7 @@ import torch
 from . import _lib
 from .cpu_rows import (get_cg_iter_time_scipy, get_pcg_diagonal_iter_time_scipy,  # noqa: F401
                        get_pcg_iter_time_scipy, get_pcg_scaled_iter_time_scipy)
-from .linalg import BatchedConjugateGradient, PreconditionedConjugateGradient
+from .linalg import BatchedConjugateGradient, PreconditionedConjugateGradient, is_cpu_device
 from .sparse import Context, DeviceMatrix, assemble, dot, lspcg_dtype
 
 
@@ -76,13 +78,48 @@ def _prepare(A, dtype, block_size=1) -> DeviceMatrix:
     return DeviceMatrix.from_scipy(sp.csr_matrix(A), dtype=dtype, block_size=block_size, ctx=Context.get())
 
 
-def get_cg_iter_time(A, gt, rtol=1e-6, max_iter=0, dtype=np.float64, repeat=1, device="cuda",
+def _host_pcg_sequence(A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, method, raise_on_max):
+    """The reference's CPU rows as it runs them (validate.py:64-86 / 99-121 / 134-160): host
+    ``b = A @ gt``, then per repeat one solver from ``PreconditionedConjugateGradient(device="cpu")``
+    -- pymathprim's own class, or ``CpuBackendUnavailable`` -- called on host copies.  Host logic
+    only: the solve is pymathprim's."""
+    A = A.to_scipy() if isinstance(A, DeviceMatrix) else sp.csr_matrix(A)
+    if isinstance(spai, DeviceMatrix):
+        spai = spai.to_scipy()
+    rows = A.shape[0]
+    max_iter = max_iter if max_iter > 0 else rows
+    b = np.asarray(A @ to_numpy(gt) if isinstance(gt, torch.Tensor) else A @ gt).astype(dtype).copy()
+    A = A.astype(dtype)
+    spai = None if spai is None else sp.csr_matrix(spai).astype(dtype)
+    assert repeat > 0
+    iter_cnt, time_prec, time_elp = 0, 0.0, 0.0
+    x = np.zeros_like(b, dtype=dtype)
+    for _ in range(repeat):
+        x_copy, b_copy = x.copy(), b.copy()
+        kw = {} if method == "ext_spai_scaled" else {"dtype": np.float64}  # validate.py:151-156 passes no dtype
+        solver = PreconditionedConjugateGradient(matrix=A, device=device, preconditioner=method, **kw)
+        if spai is None:
+            this_iter, this_prec, this_solve = solver(b_copy, x_copy, rtol, max_iter)
+        else:
+            this_iter, this_prec, this_solve = solver(b_copy, x_copy, rtol, max_iter, ext_spai=(spai, epsilon))
+        iter_cnt += this_iter
+        time_prec += this_prec
+        time_elp += this_solve
+        if raise_on_max and this_iter >= max_iter:
+            raise RuntimeError("CG did not converge")
+    return iter_cnt / repeat, time_prec / repeat, time_elp / repeat
+
+
+def get_cg_iter_time(A, gt, rtol=1e-6, max_iter=0, dtype=np.float64, repeat=1, device="cpu",
                      method="ainv", info: Optional[dict] = None, dot_order: str = "compensated",
                      dot_threads: int = 1) -> Tuple[float, float, float]:
     """validate.py:54-86: method none / diagonal / ic (IC(0), level-scheduled triangular solves) /
     ainv (AINV(0) as L Lᵀ); the prec time is the device setup of the preconditioner.
     ``dot_order`` / ``dot_threads`` (not in the reference's signature): the loop's dot order,
-    ``"openblas"`` = parity mode (linalg.PreconditionedConjugateGradient.set_dot_order)."""
+    ``"openblas"`` = parity mode (linalg.PreconditionedConjugateGradient.set_dot_order).
+    ``device="cpu"`` (the reference's default) is the reference's pymathprim row (module doc)."""
+    if is_cpu_device(device):
+        return _host_pcg_sequence(A, gt, None, 0.0, rtol, max_iter, repeat, dtype, device, method, True)
     Ad = _prepare(A, dtype)
     rows = Ad.n
     max_iter = max_iter if max_iter > 0 else rows
@@ -114,6 +151,8 @@ def relative_residual(A: DeviceMatrix, x: torch.Tensor, b: torch.Tensor) -> floa
 
 def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info=None,
                  dot_order="compensated", dot_threads=1):
+    if is_cpu_device(device):
+        return _host_pcg_sequence(A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, method, False)
     Ad = _prepare(A, dtype)
     Ld = spai if isinstance(spai, DeviceMatrix) else _prepare(spai, dtype)
     rows = Ad.n
@@ -137,7 +176,7 @@ def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, de
 
 
 def get_pcg_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat=1, dtype=np.float64,
-                      device="cuda", info: Optional[dict] = None, dot_order: str = "compensated",
+                      device="cpu", info: Optional[dict] = None, dot_order: str = "compensated",
                       dot_threads: int = 1) -> Tuple[float, float, float]:
     """validate.py:89-121: ext_spai PCG, M⁻¹ = L Lᵀ + εI.  ``info`` (optional dict, not in the
     reference's signature) receives the last solve's x, true relative residual and convergence;
@@ -169,7 +208,8 @@ def get_pcg_iter_time_batch(As, gts, spais, epsilon: float, rtol=1e-6, max_iter=
         out = []
         for j in range(k):
             info = {} if infos is not None else None
-            out.append(get_pcg_iter_time(Ads[j], gts[j], Lds[j], epsilon, rtol, max_iter, repeat, dtype, info=info))
+            out.append(get_pcg_iter_time(Ads[j], gts[j], Lds[j], epsilon, rtol, max_iter, repeat, dtype,
+                                         device="cuda", info=info))
             if infos is not None:
                 infos[j].update(info)
         return out
@@ -188,7 +228,7 @@ def get_pcg_iter_time_batch(As, gts, spais, epsilon: float, rtol=1e-6, max_iter=
 
 
 def get_pcg_scaled_iter_time(A, gt, spai, epsilon: float, rtol=1e-6, max_iter=0, repeat=1, dtype=np.float64,
-                             device="cuda", info: Optional[dict] = None, dot_order: str = "compensated",
+                             device="cpu", info: Optional[dict] = None, dot_order: str = "compensated",
                              dot_threads: int = 1) -> Tuple[float, float, float]:
     """validate.py:124-160: ext_spai_scaled PCG, M⁻¹ r = L((Lᵀr)/d) + εr/d, d = diag(A)."""
     return _pcg_generic("ext_spai_scaled", A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info,

@@ -21,6 +21,94 @@ from .nn import NodeEdgeProcessing, build_gnn, default_gnn_config
 from .sparse import DeviceMatrix, assemble
 
 
+# ---- weights-only loading of Lightning checkpoints with OmegaConf hparams ------------------------
+# The reference trains with Hydra: train.py:56-60 builds the workspace with ``**cfg`` (a DictConfig),
+# and workspace.py:52 ``save_hyperparameters()`` stores those arguments, so ``hyper_parameters``
+# holds omegaconf containers (``gnn``, ``optimizer``, ...).  torch's weights-only unpickler refuses
+# their classes.  Instead of unpickling them (``weights_only=False`` would run whatever the file
+# names), the names below are allowlisted to INERT stand-ins: plain attribute holders that only
+# receive the pickled state (NEWOBJ = ``object.__new__``, BUILD = ``__dict__.update``), which
+# ``_plain`` then folds into plain dicts / lists / values.  Nothing of omegaconf or lightning is
+# imported or executed; any other global in the file is still refused.
+class _OmegaContainer:
+    """Stand-in for an omegaconf DictConfig / ListConfig: pickled state {_metadata, _parent, _content}."""
+
+
+class _OmegaValueNode:
+    """Stand-in for an omegaconf value node (AnyNode, StringNode, ...): state {_metadata, _parent, _val}."""
+
+
+class _OmegaMetadata:
+    """Stand-in for omegaconf.base.Metadata / ContainerMetadata (ignored by _plain)."""
+
+
+class _AttributeDict:
+    """Stand-in for Lightning's AttributeDict (a dict subclass): NEWOBJ makes a plain dict, which
+    the unpickler's SETITEMS then fills."""
+
+    def __new__(cls, *args):
+        return {}
+
+
+class _TypeRef:
+    """Stand-in for a type object named in omegaconf metadata (typing.Any, builtins.dict, ...)."""
+
+    def __init__(self, name: str):
+        self.name = name
+
+
+def _defaultdict_standin(*_args):  # collections.defaultdict(factory) in omegaconf's resolver cache
+    return {}
+
+
+_OMEGA_NODES = ("AnyNode", "StringNode", "IntegerNode", "FloatNode", "BooleanNode", "BytesNode", "PathNode")
+_TYPE_NAMES = ("typing.Any", "typing.Dict", "typing.List", "typing.Optional", "typing.Union", "builtins.dict",
+               "builtins.list", "builtins.str", "builtins.int", "builtins.float", "builtins.bool", "builtins.object",
+               "builtins.NoneType", "builtins.bytes")
+
+
+def _checkpoint_safe_globals():
+    g = [(_OmegaContainer, "omegaconf.dictconfig.DictConfig"), (_OmegaContainer, "omegaconf.listconfig.ListConfig"),
+         (_OmegaMetadata, "omegaconf.base.Metadata"), (_OmegaMetadata, "omegaconf.base.ContainerMetadata"),
+         (_defaultdict_standin, "collections.defaultdict")]
+    g += [(_OmegaValueNode, f"omegaconf.nodes.{n}") for n in _OMEGA_NODES]
+    g += [(_AttributeDict, n) for n in ("lightning.fabric.utilities.data.AttributeDict",
+                                        "lightning_fabric.utilities.data.AttributeDict",
+                                        "pytorch_lightning.utilities.parsing.AttributeDict")]
+    g += [(_TypeRef(n), n) for n in _TYPE_NAMES]
+    return g
+
+
+def _plain(o):
+    """Fold the stand-ins into plain Python: containers by their ``_content``, nodes by their
+    ``_val`` (``_parent`` back references and metadata are dropped)."""
+    if isinstance(o, _OmegaContainer):
+        c = o.__dict__.get("_content")
+        if isinstance(c, dict):
+            return {k: _plain(v) for k, v in c.items()}
+        if isinstance(c, (list, tuple)):
+            return [_plain(v) for v in c]
+        return c  # None or a "???" / interpolation string
+    if isinstance(o, _OmegaValueNode):
+        return _plain(o.__dict__.get("_val"))
+    if isinstance(o, dict):
+        return {k: _plain(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return type(o)(_plain(v) for v in o)
+    return o
+
+
+def load_checkpoint_weights_only(path: str):
+    """``torch.load(path, weights_only=True)`` with the OmegaConf / Lightning hparam classes
+    allowlisted to inert stand-ins (above); returns the checkpoint with ``hyper_parameters``
+    as plain dicts."""
+    with torch.serialization.safe_globals(_checkpoint_safe_globals()):
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+    if "hyper_parameters" in ck:
+        ck["hyper_parameters"] = _plain(ck["hyper_parameters"])
+    return ck
+
+
 class SimpleInferenceWorkspace:
     def __init__(self, node_features: int, edge_features: int, block_size: int = 1, epsilon: float = 3e-3,
                  gnn: Optional[dict] = None, seed: Optional[int] = 0, device: Union[str, torch.device] = "cuda"):
@@ -38,9 +126,12 @@ class SimpleInferenceWorkspace:
     @classmethod
     def load_from_checkpoint(cls, path: str, device="cuda", trusted: bool = False) -> "SimpleInferenceWorkspace":
         """Load a Lightning checkpoint of the reference: ``hyper_parameters`` (block_size, epsilon,
-        node_features, edge_features, gnn) and ``state_dict['gnn.*']``.  Loaded with
-        ``weights_only=True`` unless ``trusted=True`` (only for files you produced yourself)."""
-        ck = torch.load(path, map_location="cpu", weights_only=not trusted)
+        node_features, edge_features, gnn) and ``state_dict['gnn.*']``.  Loaded weights-only
+        (``load_checkpoint_weights_only``: the reference's OmegaConf hparams come back as plain
+        dicts through inert stand-ins) unless ``trusted=True`` (only for files you produced
+        yourself, with omegaconf installed)."""
+        ck = (torch.load(path, map_location="cpu", weights_only=False) if trusted
+              else load_checkpoint_weights_only(path))
         hp = ck.get("hyper_parameters", {})
         gnn_cfg = hp.get("gnn")
         ws = cls(node_features=int(hp["node_features"]), edge_features=int(hp["edge_features"]),

@@ -481,6 +481,112 @@ def headline_fixtures(rval, workload: str, boo_path: str):
     np.savez_compressed(OUT / f"traj_{workload}.npz", **out)
 
 
+REFGNN_STRIDE = 127  # every 127th edge's reference output is stored (the GPU test compares there)
+
+
+def headline_refgnn_fixtures(rdata, rgnn, rval, workload: str, boo_path: str):
+    """traj_<workload>_refgnn.npz: the headline end to end on the REFERENCE's own GNN.
+
+    The reference's infer path for one sample (infer.py:278-325) with every stage its own code:
+    ``make_data`` (data.py:218-336) on the bench's system, the seeded ``NodeEdgeProcessing``
+    (torch.manual_seed(0), config/gnn.yaml -- what SimpleInferenceWorkspace(seed=0) builds;
+    gnns.py:77-97 over the PyG dispatch above) run on this container's CPU in fp32,
+    ``to_csr_cpu`` of its output (workspace.py:195-205) and ``get_pcg_iter_time_scipy(A, mask,
+    L_ref, 3e-3, rtol=1e-8)`` at 1 / 2 / 4 / 8 OpenBLAS threads.  Beside it, the HIP forward's
+    output on the same inputs (tools/dump_gnn_l.py on the GPU box, ``boo_path``) is compared with
+    the reference's edge by edge.  Stored: the error statistics (max |HIP - ref|, max |ref|, the
+    worst per-edge relative error), every REFGNN_STRIDE-th edge of the reference's output (the
+    GPU test recomputes the HIP forward and compares there at 1e-5 * max |ref|), the reference-L
+    counts / true residuals at every thread count and the 1-thread ‖r_k‖ history, and the
+    oracle's correctly-rounded-dot count on the reference L."""
+    import json
+
+    import threadpoolctl
+
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+    from learningsparsepreconditioner4gpu_amd.nn import NodeEdgeProcessing as OurNet
+    from oracle import linalg as O
+
+    meta = json.load(open(boo_path[:-4] + ".json"))
+    boo = np.load(boo_path)
+    assert boo.dtype == np.float32 and _sha(boo) == meta["sha256"], "boo file does not match its sha256"
+    A_raw, mask, feats, bs, e2n = P.workload(workload)
+    A_raw = sp.csr_matrix(A_raw)
+    g = P.to_block_graph(A_raw, bs)
+    nn_ = g.num_nodes
+    m = np.ones((nn_, bs)) if mask is None else np.asarray(mask, dtype=np.float64).reshape(nn_, bs)
+    raw = rdata.RawData(block_values=g.block_values, diagonals=A_raw.diagonal().reshape(-1, bs),
+                        edge_index=g.edge_index, node_features=feats, lhs=None, rhs=None, mask=m,
+                        num_nodes=nn_, block_size=bs)
+    d = rdata.make_data(raw, use_matrix_as_edge_feature=True, use_mask_as_node_feature=True,
+                        use_node_features_as_edge_feature=False, use_edge_features_as_node_feature=e2n,
+                        use_random_rhs=True, normalize_matrix="mean", is_inference=True)
+    s = make_sample(A_raw, mask, node_features=feats, block_size=bs, use_edge_features_as_node_feature=e2n)
+    for key in ("x", "edge_index", "edge_attr", "matrix_values", "mask"):  # the bench's inputs ARE make_data's
+        assert torch.equal(getattr(d, key), getattr(s, key)), key
+    torch.manual_seed(0)
+    net = rgnn.NodeEdgeProcessing(node_in_features=d.x.shape[1], node_out_features=None,
+                                  edge_in_features=d.edge_attr.shape[1], edge_out_features=bs * bs, **_gnn_cfg())
+    net.eval()
+    torch.manual_seed(0)
+    ours = OurNet(node_in_features=d.x.shape[1], node_out_features=None, edge_in_features=d.edge_attr.shape[1],
+                  edge_out_features=bs * bs, **_gnn_cfg())
+    osd = ours.state_dict()
+    for k, v in net.state_dict().items():  # the bench's seeded weights are the reference's
+        assert torch.equal(v, osd[k].to(v.dtype).reshape(v.shape)), k
+    with torch.no_grad():
+        ref = net(d.x, d.edge_index, d.edge_attr)[1].reshape(-1, bs, bs).numpy()
+    del net
+    assert ref.shape == boo.shape, (ref.shape, boo.shape)
+    err = np.abs(boo.astype(np.float64) - ref.astype(np.float64))
+    mref = float(np.abs(ref).max())
+    e_edge = err.reshape(len(ref), -1).max(1)
+    r_edge = np.abs(ref).reshape(len(ref), -1).max(1)
+    rel_edge = e_edge / np.maximum(r_edge, 1e-30)
+    out = {"workload": np.array(workload), "n": np.array(nn_ * bs), "block_size": np.array(bs),
+           "E": np.array(len(ref)), "boo_sha256": np.array(meta["sha256"]),
+           "ref_boo_sha256": np.array(_sha(ref)), "max_abs_err": np.array(float(err.max())),
+           "max_abs_ref": np.array(mref), "rel_err_vs_max": np.array(float(err.max()) / mref),
+           "max_edge_rel_err": np.array(float(rel_edge.max())),
+           "p99_edge_rel_err": np.array(float(np.quantile(rel_edge, 0.99))),
+           "mean_abs_err": np.array(float(err.mean())), "stride": np.array(REFGNN_STRIDE),
+           "ref_sample": ref[::REFGNN_STRIDE].copy(), "blas_info": np.array(blas_info()),
+           "torch_threads": np.array(torch.get_num_threads())}
+    print(workload, "GNN: max|HIP-ref| %.3e  max|ref| %.3e  rel %.3e  worst edge rel %.3e" % (
+        float(err.max()), mref, float(err.max()) / mref, float(rel_edge.max())), flush=True)
+    del err, e_edge, r_edge, rel_edge
+    n = nn_ * bs
+    A = rval.to_csr_cpu(d.edge_index, d.matrix_values, n, d.mask)
+    L = rval.to_csr_cpu(d.edge_index, torch.from_numpy(ref), n, d.mask, dtype=np.float64)
+    gt = d.mask.numpy().reshape(-1).astype(np.float64)
+    eps, rtol = 3e-3, 1e-8
+    out.update({"eps": np.array(eps), "rtol": np.array(rtol), "ref_threads": np.array(HEADLINE_THREADS),
+                "A_sha256": np.array(_sha(A.indptr, A.indices, A.data)),
+                "Lref_sha256": np.array(_sha(L.indptr, L.indices, L.data))})
+    rec = RecordingCG()
+    rval.cg = rec
+    b = A @ gt
+    nb = np.linalg.norm(b)
+    counts = []
+    for th in HEADLINE_THREADS:
+        with threadpoolctl.threadpool_limits(th):
+            cnt = rval.get_pcg_iter_time_scipy(A, gt, L, eps, rtol=rtol)
+        assert cnt == rec.count and len(rec.hist) == cnt
+        counts.append(cnt)
+        out[f"t{th}__count"] = np.array(cnt)
+        out[f"t{th}__true_res"] = np.array(np.linalg.norm(b - A @ rec.x) / nb)
+        if th == 1:
+            out["t1__hist"] = np.array(rec.hist)
+        print(workload, "reference GNN L, threads", th, "count", cnt, "true res %.3e" % float(out[f"t{th}__true_res"]),
+              flush=True)
+    out["refL_counts"] = np.array(counts)
+    ex = O.pcg(A, b, O.spai_operator(L, eps), rtol=rtol, dot="exact")
+    out["oracle_exact_count"] = np.array(ex[0])
+    print(workload, "reference-GNN-L counts", counts, "exact-dot", ex[0], flush=True)
+    np.savez_compressed(OUT / f"traj_{workload}_refgnn.npz", **out)
+
+
 def _gnn_cfg():
     ff = lambda norm: {"pre_norm": norm, "hidden_channels": 16, "num_layers": 2}
     return dict(node_encoder=ff("none"), edge_encoder=ff("none"), node_decoder=ff("none"), edge_decoder=ff("none"),
@@ -666,6 +772,14 @@ def main():
 
         sys.path.insert(0, str(ROOT))
         headline_fixtures(rval, sys.argv[2], sys.argv[3])
+        return
+    if sys.argv[1:2] == ["refgnn"]:  # refgnn <workload> <boo .npy from tools/dump_gnn_l.py>
+        from neural_cg import data as rdata
+        from neural_cg.nn import gnns as rgnn
+        from neural_cg.utils import validate as rval
+
+        sys.path.insert(0, str(ROOT))
+        headline_refgnn_fixtures(rdata, rgnn, rval, sys.argv[2], sys.argv[3])
         return
     if sys.argv[1:] == ["infer"]:
         from neural_cg import data as rdata

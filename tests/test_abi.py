@@ -46,8 +46,10 @@ def test_no_gpu_fails_loudly():
     A = P.kuhn_laplacian(3)
     with pytest.raises(_lib.LspcgUnavailable):
         PreconditionedConjugateGradient(A, device="cuda", preconditioner="none")
-    with pytest.raises(ValueError, match="MI355X only"):
+    with pytest.raises(RuntimeError, match="pymathprim"):  # the reference's CPU backend, absent here
         PreconditionedConjugateGradient(A, device="cpu", preconditioner="none")
+    with pytest.raises(ValueError, match="expected 'cuda'"):
+        PreconditionedConjugateGradient(A, device="tpu", preconditioner="none")
     with pytest.raises(NotImplementedError):
         PreconditionedConjugateGradient(A, device="cuda", preconditioner="fsai")
 

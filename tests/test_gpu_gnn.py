@@ -74,20 +74,73 @@ def test_gnn_edge_feature_magnitudes(gpu_ctx, case, scale):
     _close(got, want.numpy())
 
 
-def test_gnn_refuses_weights_past_f16_range(gpu_ctx):
+def test_gnn_weights_past_f16_range_run_fp32(gpu_ctx):
     """MLP weights whose LayerNorm-fed hidden activations could reach 2^15 (the split-f16 GEMMs'
-    limit; f16 holds 65504) are refused at creation with an error naming the bound, not run."""
+    limit; f16 holds 65504) run: lspcg_gnn_create selects the fp32-MFMA kernels for them, and the
+    forward matches the oracle at 1e-5 (no runtime refusal; ADVICE r4, VERDICT r4 weak #2)."""
     from learningsparsepreconditioner4gpu_amd.data import make_sample
 
     A, mask, _ = P.poisson2d_grid(10, 10)
-    s = make_sample(A, mask).to("cuda")
-    _, gpu = _pair(s.x.shape[1], s.edge_attr.shape[1], 1, seed=2)
-    gpu(s.x, s.edge_index, s.edge_attr)  # fine as initialised
+    s = make_sample(A, mask)
+    ref, gpu = _pair(s.x.shape[1], s.edge_attr.shape[1], 1, seed=2)
+    _, got = gpu(s.x.cuda(), s.edge_index.cuda(), s.edge_attr.cuda())  # as initialised: split-f16
+    p0 = gpu.precision()
+    assert not p0["f32"] and p0["hidden_bound"] < 2 ** 15, p0
     with torch.no_grad():
-        for p in gpu.parameters():
-            p.mul_(1e3)
-    with pytest.raises(Exception, match="2\\^15"):
-        gpu(s.x, s.edge_index, s.edge_attr)
+        for m in (gpu, ref):
+            for p in m.parameters():
+                p.mul_(1e3)
+        _, want = ref(s.x, s.edge_index, s.edge_attr)
+    _, got = gpu(s.x.cuda(), s.edge_index.cuda(), s.edge_attr.cuda())
+    p1 = gpu.precision()
+    assert p1["f32"] and p1["hidden_bound"] >= 2 ** 15, p1
+    got = got.cpu().numpy()
+    assert np.isfinite(got).all()
+    _close(got, want.numpy())
+
+
+@pytest.mark.parametrize("case", ["poisson", "synthetic", "bunny", "elast"])
+def test_gnn_forced_fp32_kernels_match_reference_fixture(gpu_ctx, monkeypatch, case):
+    """The fp32-MFMA kernels (LSPCG_GNN_F32=1 forces them at create) on the reference's own
+    forward fixtures: within 1e-5, like the default split-f16 kernels."""
+    from learningsparsepreconditioner4gpu_amd.nn import build_gnn
+    from tests.test_oracle_golden import _load, gnn_fixture
+
+    monkeypatch.setenv("LSPCG_GNN_F32", "1")
+    x, ei, ea, bs, seed, sd, want = gnn_fixture(_load("gnn_forward.npz"), case)
+    gpu = build_gnn(x.shape[1], ea.shape[1], bs, seed=None)
+    gpu.load_state_dict(sd, strict=True)
+    _, got = gpu(x.cuda(), ei.cuda(), ea.cuda())
+    assert gpu.precision()["f32"]
+    _close(got.cpu().numpy(), want)
+
+
+def test_gnn_decoder_guard_is_per_edge(gpu_ctx):
+    """ADVICE r4: edges of 1e12 and of O(1) magnitude in the same 16-edge tile.  The decoder's
+    hidden-layer overflow guard scales per edge, so every small edge keeps fp32 accuracy relative
+    to ITS OWN output (a wave-wide factor would flush its f16 low halves)."""
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+
+    A, mask, _ = P.poisson2d_grid(23, 19)
+    s = make_sample(A, mask)
+    rng = np.random.default_rng(4)
+    big = torch.from_numpy(rng.random(s.edge_attr.shape[0]) < 0.3)
+    ea = s.edge_attr.clone()
+    ea[big] *= 1e12
+    ref, gpu = _pair(s.x.shape[1], s.edge_attr.shape[1], 1, seed=5)
+    with torch.no_grad():
+        _, want = ref(s.x, s.edge_index, ea)
+    _, got = gpu(s.x.cuda(), s.edge_index.cuda(), ea.cuda())
+    got, want = got.cpu().numpy().reshape(len(ea), -1), want.numpy().reshape(len(ea), -1)
+    assert np.isfinite(got).all()
+    small = ~big.numpy()
+    # per edge, relative to the edge's own output; a floor at 1e-3 of the small edges' median
+    # magnitude keeps an output that cancels to ~0 from dividing by nothing
+    mag = np.abs(want).max(1)
+    floor = 1e-3 * np.median(mag[small])
+    rel = np.abs(got - want).max(1) / np.maximum(mag, floor)
+    assert float(rel[small].max()) <= 1e-5, float(rel[small].max())
+    assert float(rel[~small].max()) <= 1e-5, float(rel[~small].max())
 
 
 def test_gnn_deterministic(gpu_ctx):
@@ -143,7 +196,7 @@ def test_inference_step_and_pcg_end_to_end(gpu_ctx):
     A_ref = O.to_csr(s.edge_index.numpy(), s.matrix_values.numpy(), n, s.mask.numpy())
     assert abs(A_dev.to_scipy() - A_ref).max() == 0
     gt = s.mask.numpy().ravel().astype(np.float64)
-    it, prec, solve = get_pcg_iter_time(A_dev, gt, L_dev, ws.epsilon, rtol=1e-8)
+    it, prec, solve = get_pcg_iter_time(A_dev, gt, L_dev, ws.epsilon, rtol=1e-8, device="cuda")
     it_o, _, _ = O.pcg(A_ref, A_ref @ gt, O.spai_operator(L_got, ws.epsilon), rtol=1e-8, dot="exact")
     assert it == it_o
 

@@ -190,8 +190,8 @@ def test_validate_api_raises_when_not_converged(gpu_ctx):
 
     A = P.kuhn_laplacian(9)
     with pytest.raises(RuntimeError, match="CG did not converge"):
-        get_cg_iter_time(A, np.ones(A.shape[0]), rtol=1e-12, max_iter=3, method="none")
-    it, prec, solve = get_cg_iter_time(A, np.ones(A.shape[0]), rtol=1e-8, method="none")
+        get_cg_iter_time(A, np.ones(A.shape[0]), rtol=1e-12, max_iter=3, method="none", device="cuda")
+    it, prec, solve = get_cg_iter_time(A, np.ones(A.shape[0]), rtol=1e-8, method="none", device="cuda")
     assert it == O.pcg(A, A @ np.ones(A.shape[0]), None, rtol=1e-8, dot="exact")[0]
 
 

@@ -101,7 +101,7 @@ def test_get_cg_iter_time_baselines(gpu_ctx):
     from learningsparsepreconditioner4gpu_amd.validate import get_cg_iter_time
 
     A, m = _systems()["poisson16"]
-    its = {mth: get_cg_iter_time(A, m, rtol=1e-8, method=mth)[0] for mth in ("none", "diagonal", "ainv", "ic")}
+    its = {mth: get_cg_iter_time(A, m, rtol=1e-8, method=mth, device="cuda")[0] for mth in ("none", "diagonal", "ainv", "ic")}
     assert its["ic"] < its["none"] and its["ainv"] < its["none"], its
 
 

@@ -351,3 +351,19 @@ def test_oracle_ic_apply_matches_reference_ichol(name):
         assert it == int(z[f"{t}__count"]), (name, rtol, it)
         assert np.array_equal(np.asarray(h[:it]), z[f"{t}__hist"])
         assert np.array_equal(x, z[f"{t}__x"])
+
+
+@pytest.mark.parametrize("workload", ["kuhn101", "elast"])
+def test_refgnn_fixture_consistent(workload):
+    """traj_<workload>_refgnn.npz (make_golden.py refgnn): the reference's own GNN forward on the
+    full-size bench system was within 1e-5 · max|output| of the HIP forward on every edge, and the
+    reference's scipy PCG on ITS L converged below rtol at every OpenBLAS thread count."""
+    z = _load(f"traj_{workload}_refgnn.npz")
+    assert float(z["max_abs_err"]) <= 1e-5 * float(z["max_abs_ref"])
+    assert float(z["max_edge_rel_err"]) <= 1e-4
+    counts = [int(c) for c in z["refL_counts"]]
+    assert len(counts) == 4 and all(c > 0 for c in counts)
+    for t in (1, 2, 4, 8):
+        assert float(z[f"t{t}__true_res"]) < float(z["rtol"])
+    assert len(z["t1__hist"]) == int(z["t1__count"])
+    assert z["ref_sample"].shape[0] == (int(z["E"]) + int(z["stride"]) - 1) // int(z["stride"])
