@@ -328,8 +328,11 @@ def irregular_row(workload: str, eps: float, rtol: float, reps: int) -> dict:
     L, _ = ws.inference_step(d)
     A = ws.system_matrix(d)
     b = A.matvec(d.mask.reshape(-1).to(torch.float64))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", dtype=np.float64)
     s.set_spai(L, eps, block_size=bs)
+    setup_ms = (time.perf_counter() - t0) * 1e3
     x = torch.zeros_like(b)
     ts = []
     for _ in range(4):
@@ -350,8 +353,10 @@ def irregular_row(workload: str, eps: float, rtol: float, reps: int) -> dict:
     warm = A.spmv_timed(p, q, 3 * reps)
     alg = spmv_bytes(A.n, A.nnz)
     dc = dia_counts(Ah.indptr, Ah.indices)
-    return {"workload": f"{workload}: the headline system renumbered (random symmetric permutation + RCM), "
+    how = "random symmetric permutation + RCM" if workload.endswith("rcm") else "random symmetric permutation"
+    return {"workload": f"{workload}: the headline system renumbered ({how}), "
                         f"n={A.n}, nnz={A.nnz}, ext_spai, rtol {rtol:g}",
+            "solver_reorder": s.reorder_info, "solver_setup_ms": setup_ms,
             "distinct_offsets_per_slice": {"mean": float(dc.mean()), "max": int(dc.max())},
             "bandwidth": int(np.abs(Ah.indices - np.repeat(np.arange(A.n), np.diff(Ah.indptr))).max()),
             "column_storage": KIND_TEXT[kind_loop], "iters": it, "converged": bool(conv),
@@ -726,7 +731,8 @@ def main():
             parity = {"failed": str(e)}
         if args.workload == "kuhn101":
             try:
-                irregular = irregular_row("kuhn101rcm", args.epsilon, args.rtol, args.spmv_reps)
+                irregular = {w: irregular_row(w, args.epsilon, args.rtol, args.spmv_reps)
+                             for w in ("kuhn101rcm", "kuhn101rand")}
             except Exception as e:  # pragma: no cover
                 irregular = {"failed": str(e)}
 

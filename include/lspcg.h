@@ -181,6 +181,16 @@ int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, dou
  * launch, on the last-arriver multi-kernel schedule: the solve then reproduces the reference's
  * recorded count, ||r_k|| history and x bit for bit.  Measurement: DESIGN.md §3. */
 int lspcg_solver_set_dot_order(lspcg_solver* s, int order, int threads);
+/* Bandwidth-reducing analysis step (no reference counterpart; cf. scipy's reverse_cuthill_mckee
+ * before a solve): a solver whose A is numbered far from banded (mean |col - row| > 4 n^(2/3),
+ * n above the one-workgroup bound) runs the loop on P A Pᵀ, P Lᵀ Pᵀ, P L Pᵀ with P a reverse
+ * Cuthill-McKee permutation, every row's entries kept in their original order -- the same row
+ * sums bit for bit -- with b / x permuted on the device around the loop.  Environment
+ * LSPCG_REORDER = 0 (never) / 1 (always) / auto.  Not for IC, batches or the OpenBLAS dot order
+ * (which switches a reordered solver back).  *applied = 1 if the solver runs permuted;
+ * mean |col - row| before / after (either pointer may be NULL). */
+int lspcg_solver_reorder_info(const lspcg_solver* s, int* applied, double* mean_offset_before,
+                              double* mean_offset_after);
 int lspcg_solver_destroy(lspcg_solver* s);
 
 /* ---- batched lockstep ext_spai PCG over independent systems (infer.py:278-331 solves its samples

@@ -26,7 +26,7 @@ CSRC = PKG / "csrc"
 LIB = PKG / "liblspcg_hip.so"
 OBJ = ROOT / "build" / "lspcg"
 SOURCES = ["lspcg_core.hip", "lspcg_pcg.hip", "lspcg_assemble.hip", "lspcg_gnn.hip", "lspcg_factor.hip",
-           "lspcg_sell.hip", "lspcg_graph.hip", "lspcg_part.hip"]
+           "lspcg_sell.hip", "lspcg_graph.hip", "lspcg_part.hip", "lspcg_reorder.hip"]
 HEADERS = ["lspcg_internal.hpp", "lspcg_spmv.hpp", "lspcg_factor.hpp", "lspcg_sell.hpp"]
 ARCH = os.environ.get("LSPCG_ARCH", "gfx950")
 

@@ -402,6 +402,27 @@ int mat_alloc(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, int dtype, lspcg
 // A's rowptr / colind and its values are a permutation of A's
 int mat_transpose(const lspcg_mat* A, lspcg_mat** out, bool* same_pattern);
 
+// Bandwidth-reducing row placement (lspcg_reorder.hip): perm[i'] = original (block) row of row
+// i', iperm its inverse (device arrays, nb entries); off_* = mean |col - row| of the pattern in the
+// original / the permuted numbering.
+struct Reorder {
+  int32_t* perm = nullptr;
+  int32_t* iperm = nullptr;
+  int64_t nb = 0;
+  double off_before = 0, off_after = 0;
+  void release();
+};
+// mean |col - row| over the stored (block) entries
+int mean_abs_offset(const lspcg_mat* A, double* out);
+// Reverse Cuthill-McKee of A's graph.  mode 0: never, 1: always, -1: auto (only numberings far from
+// banded, and only if RCM halves the mean offset).  *applied <- out holds a permutation.
+int rcm_reorder(const lspcg_mat* A, int mode, Reorder* out, bool* applied);
+// P M P^T with every row's entries in their original order (columns renamed): same row sums
+int mat_permute(const lspcg_mat* M, const Reorder& R, lspcg_mat** out);
+// dst[i'] = src[perm[i']] (scatter = false) or dst[perm[i']] = src[i'] (scatter = true), bs scalars per row
+int vec_permute(int dtype, int64_t nb, int bs, const int32_t* perm, const void* src, void* dst, bool scatter,
+                hipStream_t st);
+
 }  // namespace lspcg
 
 // ---------------------------------------------------------------------------

@@ -1098,9 +1098,17 @@ using namespace lspcg;
 
 struct lspcg_solver {
   lspcg_ctx* ctx = nullptr;
-  const lspcg_mat* A = nullptr;
-  const lspcg_mat* L = nullptr;
-  lspcg_mat* LT = nullptr;  // owned
+  const lspcg_mat* A = nullptr;       // the system the loop runs on: A_user, or Ap when reordered
+  const lspcg_mat* A_user = nullptr;  // the caller's A
+  const lspcg_mat* L = nullptr;       // the caller's L (ext_spai)
+  lspcg_mat* LT = nullptr;  // owned (the permuted Lᵀ when reordered)
+  // bandwidth-reducing row placement (lspcg_reorder.hip): A, L, Lᵀ permuted with each row's
+  // entries in their original order, vectors gathered in / scattered out around the loop
+  Reorder ro;
+  lspcg_mat* Ap = nullptr;   // owned P A Pᵀ
+  lspcg_mat* Lp = nullptr;   // owned P L Pᵀ
+  int reorder_mode = -1;     // LSPCG_REORDER: -1 auto, 0 off, 1 always
+  bool reorder_ok = false;   // single solves in the compensated order only (not batches, IC, parity)
   int precond = LSPCG_PRECOND_NONE;
   int dtype = LSPCG_F64;
   int64_t n = 0;
@@ -1573,13 +1581,41 @@ static size_t esize(int dtype) { return dtype == LSPCG_F32 ? 4 : 8; }
 
 extern "C" {
 
-static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool dia_ok, lspcg_solver** out);
+static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool dia_ok, bool reorder_ok,
+                         lspcg_solver** out);
 
 int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_solver** out) {
-  return solver_create(ctx, A, precond, true, out);
+  return solver_create(ctx, A, precond, true, true, out);
 }
 
-static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool dia_ok, lspcg_solver** out) {
+// The A side of the solver: (optionally) the permuted system, its iteration view and SELL copy,
+// the diagonal of the Jacobi preconditioner.
+static int setup_A(lspcg_solver* s) {
+  s->A = s->A_user;
+  if (s->Ap) {
+    lspcg_mat_destroy(s->Ap);
+    s->Ap = nullptr;
+  }
+  s->ro.release();
+  bool applied = false;
+  if (s->reorder_ok && s->n > s->small_n) {
+    if (int rc = rcm_reorder(s->A_user, s->reorder_mode, &s->ro, &applied)) return rc;
+    if (applied) {
+      if (int rc = mat_permute(s->A_user, s->ro, &s->Ap)) return rc;
+      s->A = s->Ap;
+    }
+  }
+  if (int rc = make_view(s, s->A, &s->Av, nullptr, &s->own_A)) return rc;
+  if (int rc = build_sell(s, 0, &s->Av)) return rc;
+  if (s->precond == LSPCG_PRECOND_DIAGONAL) {
+    if (int rc = lspcg_mat_diagonal(s->A, s->d)) return rc;  // issues on ctx stream
+    LSPCG_HIP(hipStreamSynchronize(s->ctx->stream));
+  }
+  return LSPCG_OK;
+}
+
+static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool dia_ok, bool reorder_ok,
+                         lspcg_solver** out) {
   LSPCG_CHECK(ctx && A && out, LSPCG_ERR_ARG, "solver_create: NULL argument");
   LSPCG_CHECK(precond >= LSPCG_PRECOND_NONE && precond <= LSPCG_PRECOND_IC, LSPCG_ERR_ARG,
               "solver_create: unknown preconditioner " + std::to_string(precond));
@@ -1587,7 +1623,9 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
   std::unique_ptr<lspcg_solver> s(new lspcg_solver());
   s->ctx = ctx;
   s->A = A;
+  s->A_user = A;
   s->dia_ok = dia_ok;
+  s->reorder_ok = reorder_ok && precond != LSPCG_PRECOND_IC;
   s->precond = precond;
   s->dtype = A->dtype;
   s->n = A->n;
@@ -1628,13 +1666,8 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
     s->allow_split = e[0] != '0';
     s->split_mode = std::atoi(e);
   }
-  if (int rc = make_view(s.get(), A, &s->Av, nullptr, &s->own_A)) return rc;
-  if (int rc = build_sell(s.get(), 0, &s->Av)) return rc;
-  if (precond == LSPCG_PRECOND_DIAGONAL) {
-    int rc = lspcg_mat_diagonal(A, s->d);  // issues on ctx stream
-    if (rc) return rc;
-    LSPCG_HIP(hipStreamSynchronize(ctx->stream));
-  }
+  if (const char* e = std::getenv("LSPCG_REORDER")) s->reorder_mode = e[0] == 'a' ? -1 : std::atoi(e) ? 1 : 0;
+  if (int rc = setup_A(s.get())) return rc;
   LSPCG_HIP(hipStreamSynchronize(s->stream));
   *out = s.release();
   return LSPCG_OK;
@@ -1652,15 +1685,30 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     lspcg_mat_destroy(s->LT);
     s->LT = nullptr;
   }
+  if (s->Lp) {
+    lspcg_mat_destroy(s->Lp);
+    s->Lp = nullptr;
+  }
   bool lt_same = false;
-  int rc = mat_transpose(L, &s->LT, &lt_same);
+  int rc = mat_transpose(L, &s->LT, &lt_same);  // in the ORIGINAL numbering: Lᵀ's rows in scipy's order
   if (rc) return rc;
+  const lspcg_mat* Lu = L;
+  if (s->ro.perm) {  // reordered solver: P L Pᵀ and P Lᵀ Pᵀ, every row's entries in their original order
+    LSPCG_CHECK(L->block_size == s->A->block_size, LSPCG_ERR_ARG, "set_spai: L and A block sizes differ");
+    if ((rc = mat_permute(L, s->ro, &s->Lp))) return rc;
+    lspcg_mat* LTp = nullptr;
+    rc = mat_permute(s->LT, s->ro, &LTp);
+    lspcg_mat_destroy(s->LT);
+    s->LT = LTp;
+    if (rc) return rc;
+    Lu = s->Lp;
+  }
   if (s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) {
     rc = lspcg_mat_diagonal(s->A, s->d);
     if (rc) return rc;
   }
   int lflag = 3;
-  if ((rc = make_view(s, L, &s->Lv, &s->Av, &s->own_L, nullptr, &lflag))) return rc;
+  if ((rc = make_view(s, Lu, &s->Lv, &s->Av, &s->own_L, nullptr, &lflag))) return rc;
   if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT, lt_same ? &lflag : nullptr))) return rc;
   if ((rc = build_sell(s, 1, &s->Lv))) return rc;
   if ((rc = build_sell(s, 2, &s->LTv))) return rc;
@@ -1800,7 +1848,11 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   LSPCG_HIP(hipEventRecord(s->ev_in, s->ctx->stream));
   LSPCG_HIP(hipStreamWaitEvent(st, s->ev_in, 0));
   LSPCG_HIP(hipEventRecord(s->ev_t0, st));
-  if (n) {
+  if (n && s->ro.perm) {  // into the permuted numbering
+    const int bs = s->A->block_size;
+    if (int r2 = vec_permute(s->dtype, n / bs, bs, s->ro.perm, b, s->b, false, st)) return r2;
+    if (int r2 = vec_permute(s->dtype, n / bs, bs, s->ro.perm, x, s->x, false, st)) return r2;
+  } else if (n) {
     LSPCG_HIP(hipMemcpyAsync(s->b, b, vb, hipMemcpyDeviceToDevice, st));
     LSPCG_HIP(hipMemcpyAsync(s->x, x, vb, hipMemcpyDeviceToDevice, st));
   }
@@ -1895,7 +1947,11 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   rc = s->dtype == LSPCG_F64 ? enqueue_fixup<double>(s, st) : enqueue_fixup<float>(s, st);
   if (rc) return rc;
   const void* src = (fin.bb == 0.0) ? s->b : s->x;  // scipy returns b when ‖b‖ = 0
-  if (n) LSPCG_HIP(hipMemcpyAsync(x, src, vb, hipMemcpyDeviceToDevice, st));
+  if (n && s->ro.perm) {  // back to the caller's numbering
+    if (int r2 = vec_permute(s->dtype, n / s->A->block_size, s->A->block_size, s->ro.perm, src, x, true, st)) return r2;
+  } else if (n) {
+    LSPCG_HIP(hipMemcpyAsync(x, src, vb, hipMemcpyDeviceToDevice, st));
+  }
   LSPCG_HIP(hipEventRecord(s->ev_t1, st));
   LSPCG_HIP(hipEventRecord(s->ev_out, st));
   LSPCG_HIP(hipStreamWaitEvent(s->ctx->stream, s->ev_out, 0));
@@ -1930,6 +1986,16 @@ int lspcg_solver_set_dot_order(lspcg_solver* s, int order, int threads) {
   LSPCG_HIP(hipStreamSynchronize(s->stream));
   s->dot_order = order;
   s->dot_threads = order == LSPCG_DOT_OPENBLAS ? threads : 1;
+  if (order == LSPCG_DOT_OPENBLAS && s->reorder_ok) {
+    // numpy's ddot order runs over the ORIGINAL numbering: back to the unpermuted system for good
+    s->reorder_ok = false;
+    if (s->ro.perm) {
+      if (int rc = setup_A(s)) return rc;
+      if (s->L) {
+        if (int rc = lspcg_solver_set_spai(s, s->L, s->eps, nullptr)) return rc;
+      }
+    }
+  }
   s->split = s->split_ok && order == LSPCG_DOT_COMPENSATED;
   for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
@@ -1948,7 +2014,11 @@ int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, dou
   const size_t vb = esize(s->dtype) * n;
   LSPCG_HIP(hipEventRecord(s->ev_in, s->ctx->stream));
   LSPCG_HIP(hipStreamWaitEvent(st, s->ev_in, 0));
-  LSPCG_HIP(hipMemcpyAsync(s->b, b, vb, hipMemcpyDeviceToDevice, st));
+  if (s->ro.perm) {
+    if (int r2 = vec_permute(s->dtype, n / s->A->block_size, s->A->block_size, s->ro.perm, b, s->b, false, st)) return r2;
+  } else {
+    LSPCG_HIP(hipMemcpyAsync(s->b, b, vb, hipMemcpyDeviceToDevice, st));
+  }
   LSPCG_HIP(hipMemsetAsync(s->x, 0, vb, st));
   PcgState init{};
   init.rtol = 0.0;  // atol 0: no convergence stop, `iters` full iterations
@@ -1985,6 +2055,15 @@ int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, dou
   return LSPCG_OK;
 }
 
+int lspcg_solver_reorder_info(const lspcg_solver* s, int* applied, double* mean_offset_before,
+                              double* mean_offset_after) {
+  LSPCG_CHECK(s && applied, LSPCG_ERR_ARG, "reorder_info: NULL argument");
+  *applied = s->ro.perm ? 1 : 0;
+  if (mean_offset_before) *mean_offset_before = s->ro.off_before;
+  if (mean_offset_after) *mean_offset_after = s->ro.off_after;
+  return LSPCG_OK;
+}
+
 int lspcg_solver_destroy(lspcg_solver* s) {
   if (!s) return LSPCG_OK;
   (void)hipSetDevice(s->ctx->device);
@@ -2000,6 +2079,9 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipFree(s->groups);
   for (hipEvent_t e : {s->ev_in, s->ev_out, s->ev_poll, s->ev_poll2, s->ev_t0, s->ev_t1}) (void)hipEventDestroy(e);
   if (s->LT) lspcg_mat_destroy(s->LT);
+  if (s->Lp) lspcg_mat_destroy(s->Lp);
+  if (s->Ap) lspcg_mat_destroy(s->Ap);
+  s->ro.release();
   if (s->icL) lspcg_mat_destroy(s->icL);
   if (s->icU) lspcg_mat_destroy(s->icU);
   s->levL.release();
@@ -2639,7 +2721,7 @@ int lspcg_batch_create(lspcg_ctx* ctx, int nsys, const lspcg_mat* const* A, cons
     bt->small = !(e && e[0] == '0') && bt->bs == 1 && bt->max_n <= std::min<int64_t>(row_cap, small_n) &&
                 3 * bt->max_n * int64_t(esize(bt->dtype)) <= kSmallLds;
   }
-  if (int rc = solver_create(ctx, bt->Acat, LSPCG_PRECOND_EXT_SPAI, !bt->small, &bt->s)) return rc;
+  if (int rc = solver_create(ctx, bt->Acat, LSPCG_PRECOND_EXT_SPAI, !bt->small, false, &bt->s)) return rc;
   if (int rc = lspcg_solver_set_spai(bt->s, bt->Lcat, epsilon, nullptr)) return rc;
   LSPCG_CHECK(bt->s->sp[0] && bt->s->sp[1] && bt->s->sp[2], LSPCG_ERR_UNSUPPORTED,
               "batch_create: no SELL view of the block-diagonal system (irregular rows): solve one by one");

@@ -150,6 +150,14 @@ class PreconditionedConjugateGradient:
             _lib._lib.lspcg_solver_destroy(h)
             self.handle = None
 
+    @property
+    def reorder_info(self) -> dict:
+        """The analysis step's verdict (``lspcg_solver_reorder_info``): whether the loop runs on the
+        reverse-Cuthill-McKee-permuted system, and mean |col - row| before / after."""
+        a, b0, b1 = C.c_int(), C.c_double(), C.c_double()
+        _lib.call("lspcg_solver_reorder_info", self.handle, C.byref(a), C.byref(b0), C.byref(b1))
+        return {"applied": bool(a.value), "mean_offset_before": b0.value, "mean_offset_after": b1.value}
+
     def set_spai(self, L, epsilon: float, block_size: int = 1) -> float:
         """Install M⁻¹ = L Lᵀ + εI (ext_spai); returns the device setup time in seconds."""
         Ld = _as_device_matrix(L, self.dtype, block_size, self.ctx)

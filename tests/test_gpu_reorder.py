@@ -1,0 +1,163 @@
+"""GPU: the reverse-Cuthill-McKee analysis step of the solver (lspcg_reorder.hip).
+
+A solver whose A is numbered far from banded runs its loop on P A Pᵀ (and P L Pᵀ, P Lᵀ Pᵀ) with
+every row's entries in their original order, so each SpMV row sum keeps scipy's bits; b and x are
+permuted on the device around the loop.  Checked here:
+  * auto mode picks it for a randomly renumbered grid and leaves structured / banded ones alone;
+  * the permuted solve equals the oracle's correctly-rounded-dot trajectory (count exact, history
+    and x to 1e-12) and the unpermuted solver's result, for none / diagonal / ext_spai /
+    ext_spai_scaled, fp64 and fp32;
+  * parity mode (numpy's ddot order over the ORIGINAL numbering) switches a reordered solver back
+    and then equals an unpermuted parity solver bit for bit.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from oracle import linalg as O
+from tests import _cases
+from learningsparsepreconditioner4gpu_amd import problems as P
+
+pytestmark = pytest.mark.gpu
+
+
+def _system(kind):
+    if kind == "kuhn27rand":
+        A, m = P.renumber(*P.kuhn_dirichlet(27), "rand")
+    elif kind == "poisson160rand":
+        A0, m0, _ = P.poisson2d_grid(160, 160)
+        A, m = P.renumber(sp.csr_matrix(A0), m0.ravel(), "rand")
+    else:
+        raise KeyError(kind)
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    A.data = A.data.astype(np.float32).astype(np.float64)
+    L = _cases.spai_like(A, seed=3)
+    L.data = L.data.astype(np.float32).astype(np.float64)
+    b = A @ np.asarray(m, dtype=np.float64).ravel()
+    return A, L, b
+
+
+def _solver(A, L, pre, dtype=np.float64, **kw):
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=pre, dtype=dtype, **kw)
+    if pre.startswith("ext_spai"):
+        s.set_spai(L, 3e-3)
+    return s
+
+
+def _run(s, b, rtol=1e-8, dtype=np.float64):
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    bt = torch.as_tensor(b, dtype=tdt, device="cuda")
+    x = torch.zeros_like(bt)
+    it, conv, _t, h = s.solve(bt, x, rtol=rtol, return_history=True)
+    return it, conv, x.cpu().numpy().astype(np.float64), h
+
+
+def test_auto_mode_decisions(gpu_ctx, monkeypatch):
+    monkeypatch.delenv("LSPCG_REORDER", raising=False)
+    A, L, _ = _system("kuhn27rand")
+    s = _solver(A, L, "none")
+    info = s.reorder_info
+    assert info["applied"] and info["mean_offset_after"] < 0.1 * info["mean_offset_before"], info
+    K = sp.csr_matrix(P.kuhn_dirichlet(27)[0])  # structured: already banded
+    assert not _solver(K, None, "none").reorder_info["applied"]
+    R = sp.csr_matrix(P.renumber(*P.kuhn_dirichlet(27), "rcm")[0])  # RCM-banded irregular
+    assert not _solver(R, None, "none").reorder_info["applied"]
+
+
+@pytest.mark.parametrize("pre", ["none", "diagonal", "ext_spai", "ext_spai_scaled"])
+@pytest.mark.parametrize("kind", ["kuhn27rand", "poisson160rand"])
+def test_reordered_solve_equals_oracle_and_unpermuted(gpu_ctx, monkeypatch, kind, pre):
+    A, L, b = _system(kind)
+    monkeypatch.setenv("LSPCG_REORDER", "1")
+    sr = _solver(A, L, pre)
+    assert sr.reorder_info["applied"]
+    monkeypatch.setenv("LSPCG_REORDER", "0")
+    su = _solver(A, L, pre)
+    assert not su.reorder_info["applied"]
+    it_r, conv_r, x_r, h_r = _run(sr, b)
+    it_u, conv_u, x_u, h_u = _run(su, b)
+    ps = {"none": None, "diagonal": O.diagonal_operator(A), "ext_spai": O.spai_operator(L, 3e-3),
+          "ext_spai_scaled": O.spai_scaled_operator(A, L, 3e-3)}[pre]
+    it_o, x_o, h_o = O.pcg(A, b, ps, rtol=1e-8, dot="exact")
+    rec = {"kind": kind, "pre": pre, "reordered": it_r, "unpermuted": it_u, "oracle": it_o}
+    assert conv_r and it_r == it_o == it_u, rec
+    assert np.allclose(h_r[: it_o + 1], np.asarray(h_o)[: it_o + 1], rtol=1e-12, atol=0), rec
+    assert np.linalg.norm(x_r - x_o) <= 1e-12 * np.linalg.norm(x_o), rec
+    assert np.linalg.norm(x_r - x_u) <= 1e-12 * np.linalg.norm(x_u), rec
+
+
+def test_reordered_fp32(gpu_ctx, monkeypatch):
+    A, L, b = _system("kuhn27rand")
+    monkeypatch.setenv("LSPCG_REORDER", "1")
+    sr = _solver(A, L, "ext_spai", dtype=np.float32)
+    assert sr.reorder_info["applied"]
+    monkeypatch.setenv("LSPCG_REORDER", "0")
+    su = _solver(A, L, "ext_spai", dtype=np.float32)
+    it_r, conv_r, x_r, _ = _run(sr, b, rtol=1e-5, dtype=np.float32)
+    it_u, conv_u, x_u, _ = _run(su, b, rtol=1e-5, dtype=np.float32)
+    assert conv_r and conv_u and abs(it_r - it_u) <= 1, (it_r, it_u)
+    assert np.linalg.norm(x_r - x_u) <= 1e-4 * np.linalg.norm(x_u)
+
+
+def test_parity_mode_switches_reordering_off(gpu_ctx, monkeypatch):
+    A, L, b = _system("kuhn27rand")
+    monkeypatch.setenv("LSPCG_REORDER", "1")
+    s1 = _solver(A, L, "ext_spai")
+    assert s1.reorder_info["applied"]
+    s1.set_dot_order("openblas", 1)
+    assert not s1.reorder_info["applied"]
+    monkeypatch.setenv("LSPCG_REORDER", "0")
+    s2 = _solver(A, L, "ext_spai", dot_order="openblas", dot_threads=1)
+    it1, c1, x1, h1 = _run(s1, b)
+    it2, c2, x2, h2 = _run(s2, b)
+    assert c1 and it1 == it2 and np.array_equal(h1, h2) and np.array_equal(x1, x2)
+    it_b, x_b, h_b = O.pcg(A, b, O.spai_operator(L, 3e-3), rtol=1e-8, dot="blas1")
+    assert it1 == it_b and np.array_equal(x1, x_b)
+
+
+def test_reordered_solver_reuse_and_new_spai(gpu_ctx, monkeypatch):
+    """A reordered solver solves twice (same bits) and takes a second L (set_spai again)."""
+    A, L, b = _system("poisson160rand")
+    monkeypatch.setenv("LSPCG_REORDER", "1")
+    s = _solver(A, L, "ext_spai")
+    r1 = _run(s, b)
+    r2 = _run(s, b)
+    assert r1[0] == r2[0] and np.array_equal(r1[2], r2[2])
+    L2 = _cases.spai_like(A, seed=9)
+    L2.data = L2.data.astype(np.float32).astype(np.float64)
+    s.set_spai(L2, 3e-3)
+    it, conv, x, _ = _run(s, b)
+    it_o, x_o, _ = O.pcg(A, b, O.spai_operator(L2, 3e-3), rtol=1e-8, dot="exact")
+    assert conv and it == it_o and np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
+
+
+def test_reordered_bsr3_equals_oracle(gpu_ctx, monkeypatch):
+    """BSR 3×3 (the elasticity layout): block rows renumbered at random, then the solver's RCM on
+    the block graph (block rows permuted, every block row's blocks in their original order)."""
+    A0, m0, _ = P.elasticity_box(20, 12, 12)  # n = 8,640: above the one-workgroup bound
+    nb = A0.shape[0] // 3
+    pb = np.random.default_rng(2).permutation(nb)
+    perm = (3 * pb[:, None] + np.arange(3)[None, :]).ravel()
+    A = sp.csr_matrix(sp.csr_matrix(A0)[perm][:, perm])
+    A.sort_indices()
+    A.data = A.data.astype(np.float32).astype(np.float64)
+    L = _cases.spai_like(A, seed=4)
+    L.data = L.data.astype(np.float32).astype(np.float64)
+    b = A @ np.asarray(m0, dtype=np.float64).ravel()[perm]
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("LSPCG_REORDER", mode)
+        s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", block_size=3)
+        s.set_spai(L, 3e-3, block_size=3)
+        assert s.reorder_info["applied"] == (mode == "1")
+        res[mode] = _run(s, b)
+    it_o, x_o, h_o = O.pcg(A, b, O.spai_operator(L, 3e-3), rtol=1e-8, dot="exact")
+    for mode, (it, conv, x, h) in res.items():
+        assert conv and it == it_o, (mode, it, it_o)
+        assert np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o), mode

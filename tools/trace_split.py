@@ -1,24 +1,43 @@
 """Split the roofline SpMV's rocprofv3 kernel-trace durations into cold (dispatch right after the
 L3-evicting k_flush_read) and warm (right after another SpMV) launches, so the profile's average
-can be compared with bench.py's HIP-event cold / warm figures.
+can be compared with bench.py's HIP-event cold / warm figures.  One bucket per KERNEL (staged CSR
+``k_spmv``, SELL-DIA ``k_spmv_sdia``, SELL-64 with 16-bit / int32 columns ``k_spmv_sell``): the
+bench's irregular-ordering leg launches the SELL-64 kernel on a system of the same size, so a
+shared bucket would mix two kernels.  With ``--alg-bytes B`` (default: the headline kuhn101
+system's §8(d) bytes, 12 nnz + 20 n + 4 = 201,442,412) each bucket also gets the cold average's
+TB/s and its fraction of 8 TB/s -- what bench.py reports as ``roofline.frac``.
 
-    python tools/trace_split.py gpurun_out/prof_<tag>/bench_kernel_trace.csv
+    python tools/trace_split.py gpurun_out/prof_<tag>/bench_kernel_trace.csv [--alg-bytes B]
 """
 import csv
 import json
 import sys
 
 KEY = "EpiStore<double>"  # standalone SpMV of A (bench.py roofline launches: staged CSR, then SELL)
+PEAK_TBS = 8.0
+ALG_BYTES = 12 * 15069699 + 20 * 1030301 + 4
 
 
-def main(path):
+def _kernel_bucket(name):
+    if "k_spmv_sdia<double, double," in name:
+        return "sdia"
+    if "k_spmv_sell<double, double, short" in name:
+        return "sell_int16"
+    if "k_spmv_sell<double, double, int" in name:
+        return "sell_int32"
+    if "k_spmv<double, double, 1," in name:
+        return "csr"
+    return None
+
+
+def main(path, alg_bytes=ALG_BYTES):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     out = {}
     prev = ""
     for r in rows:
         name = r["Kernel_Name"]
-        if KEY in name and ("k_spmv<double, double, 1," in name or "k_spmv_sell<double, double," in name or "k_spmv_sdia<double, double," in name):
-            kern = "sell" if "k_spmv_s" in name else "csr"
+        kern = _kernel_bucket(name) if KEY in name else None
+        if kern:
             dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
             out.setdefault(kern, ([], []))[0 if "k_flush_read" in prev else 1].append(dur)
         prev = name
@@ -28,6 +47,9 @@ def main(path):
     for kern, (cold, warm) in out.items():
         res[kern] = {"cold_n": len(cold), "cold_avg_us": avg(cold), "cold_median_us": med(cold), "warm_n": len(warm),
                      "warm_avg_us": avg(warm), "warm_median_us": med(warm)}
+        if cold:
+            tbs = alg_bytes / (avg(cold) * 1e-6) / 1e12
+            res[kern].update(alg_bytes=alg_bytes, cold_TBps=tbs, cold_frac_of_8TBps=tbs / PEAK_TBS)
     # the PCG loop's five launches (graph-replayed and direct), average duration per kind
     import re
     loop = {"KA t=L^T r": r"k_spmv_s(?:ell|dia)<double, float.*EpiT<double, false>",
@@ -65,8 +87,8 @@ def main(path):
     res["pcg_loop_kernels_us"] = out
     # the bench system's GNN forwards (largest grid of each GNN kernel): per-kernel average and the
     # forward's kernel sum (num_mp_layers - 1 plain layers + the first layer + decoder + node encoder)
-    gnn = {"k_encode<false>": r"k_encode<false>", "k_mp_layer<0>": r"k_mp_layer<0>",
-           "k_mp_layer<S1E>": r"k_mp_layer<[123]>", "k_edge_dec": r"k_edge_dec<"}
+    gnn = {"k_encode<false>": r"k_encode<false>", "k_mp_layer<0>": r"k_mp_layer<(?:(?:false|true), )?0>",
+           "k_mp_layer<S1E>": r"k_mp_layer<(?:(?:false|true), )?[123]>", "k_edge_dec": r"k_edge_dec<"}
     gk = {}
     for r in rows:
         for k, pat in gnn.items():
@@ -88,4 +110,10 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    args = sys.argv[1:]
+    ab = ALG_BYTES
+    if "--alg-bytes" in args:
+        i = args.index("--alg-bytes")
+        ab = int(args[i + 1])
+        del args[i:i + 2]
+    main(args[0], ab)
