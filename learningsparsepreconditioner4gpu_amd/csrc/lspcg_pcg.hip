@@ -1588,6 +1588,16 @@ int lspcg_solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, lspcg_s
   return solver_create(ctx, A, precond, true, true, out);
 }
 
+// diag(A) into s->d in the loop's numbering.  lspcg_mat_diagonal binary-searches sorted rows, so
+// a permuted solver takes the caller's (sorted) A's diagonal and permutes it (s->z is scratch here:
+// no solve is in flight while the preconditioner is installed).
+static int solver_diagonal(lspcg_solver* s) {
+  if (!s->ro.perm) return lspcg_mat_diagonal(s->A, s->d);  // issues on ctx stream
+  if (int rc = lspcg_mat_diagonal(s->A_user, s->z)) return rc;
+  const int bs = s->A->block_size;
+  return vec_permute(s->dtype, s->n / bs, bs, s->ro.perm, s->z, s->d, false, s->ctx->stream);
+}
+
 // The A side of the solver: (optionally) the permuted system, its iteration view and SELL copy,
 // the diagonal of the Jacobi preconditioner.
 static int setup_A(lspcg_solver* s) {
@@ -1608,7 +1618,7 @@ static int setup_A(lspcg_solver* s) {
   if (int rc = make_view(s, s->A, &s->Av, nullptr, &s->own_A)) return rc;
   if (int rc = build_sell(s, 0, &s->Av)) return rc;
   if (s->precond == LSPCG_PRECOND_DIAGONAL) {
-    if (int rc = lspcg_mat_diagonal(s->A, s->d)) return rc;  // issues on ctx stream
+    if (int rc = solver_diagonal(s)) return rc;
     LSPCG_HIP(hipStreamSynchronize(s->ctx->stream));
   }
   return LSPCG_OK;
@@ -1704,7 +1714,8 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     Lu = s->Lp;
   }
   if (s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) {
-    rc = lspcg_mat_diagonal(s->A, s->d);
+    LSPCG_HIP(hipStreamSynchronize(s->stream));  // s->z is the permuted path's scratch
+    rc = solver_diagonal(s);
     if (rc) return rc;
   }
   int lflag = 3;
