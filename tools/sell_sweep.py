@@ -58,7 +58,9 @@ def main_bsr():
         y.fill_(float("nan"))
         rc = lib.sweep_bsr_run(cid, C.c_int64(n // 3), C.c_int64(B.indices.size), p(rp), p(ci), p(va), p(x), p(y), 20,
                                C.c_int64(FLUSH_BYTES), C.byref(cold), C.byref(warm))
-        print(json.dumps({"workload": "elast BSR3", "values": "fp64" if vb.value == 8 else "fp32", "QB": qb.value,
+        code = qb.value  # qb | 100 * (3: three waves per slice) | 1000 * MINW
+        print(json.dumps({"workload": "elast BSR3", "values": "fp64" if vb.value == 8 else "fp32", "QB": code % 100,
+                          "waves_per_slice": 3 if (code // 100) % 10 == 3 else 1, "minw": code // 1000,
                           "rc": rc, "cold_us": cold.value * 1e3, "warm_us": warm.value * 1e3,
                           "frac_alg_cold": alg / (cold.value * 1e-3) / 8e12, "bitexact": bool(torch.equal(y, want))}),
               flush=True)
