@@ -625,6 +625,28 @@ def main():
         loop_kernels = {}
     loop_dom = loop_dominant(loop_kernels, A, n, nnz_l) if loop_kernels else None
 
+    # ---- the same solve on views WITHOUT the value dictionary (fp32-stored values throughout): what
+    # the 1-byte A codes buy (the loop is bit-identical either way; lspcg_solver_views)
+    views = solver.views
+    no_codes = None
+    if not args.no_variants and any(v["value_bytes"] == 1 for v in views.values()):
+        os.environ["LSPCG_VALUE_CODES"] = "0"
+        try:
+            s2 = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", dtype=np.float64)
+        finally:
+            del os.environ["LSPCG_VALUE_CODES"]
+        s2.set_spai(L, args.epsilon, block_size=L.block_size)
+        x2 = torch.zeros_like(b)
+        ts2 = []
+        for _ in range(4):
+            x2.zero_()
+            it2, _c2, t2 = s2.solve(b, x2, rtol=args.rtol)
+            ts2.append(t2)
+        no_codes = {"views": s2.views, "iters": it2, "same_x": bool(torch.equal(x2, x)),
+                    "pcg_iter_us": float(np.median(ts2[1:])) / it2 * 1e6,
+                    "loop_kernels_us": {k: v * 1e6 for k, v in s2.time_kernels(b, 40).items()}}
+        del s2
+
     # ---- time-to-rtol beside the neural preconditioner (infer.py:310-321 rows): CG and Jacobi on the
     # same system and rhs, and every method with infer.py's rhs="random" (:300-302, b = A (randn ⊙ mask))
     variants = None
@@ -789,6 +811,8 @@ def main():
                 "method": "HIP events on the ctx stream; cold = a 512 MiB read before every launch, launch time = (R x (flush+SpMV) - R x flush)/R",
             },
             "pcg_loop_spmv": pcg_spmv,
+            "solver_views": views,
+            "without_value_codes": no_codes,
             "pcg_loop_kernels": loop_dom,
             "cpu_baseline": cpu,
             "c1_synthetic": c1,

@@ -63,6 +63,7 @@ SIGNATURES = {
     "lspcg_solver_set_ic_factor": (C.c_int, [vp, vp, p_f64]),
     "lspcg_solver_solve": (C.c_int, [vp, vp, vp, C.c_double, C.c_int64, p_i64, p_f64, p_f64]),
     "lspcg_solver_time_kernels": (C.c_int, [vp, vp, C.c_int64, p_f64, C.POINTER(C.c_int)]),
+    "lspcg_solver_views": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "lspcg_solver_reorder_info": (C.c_int, [vp, C.POINTER(C.c_int), p_f64, p_f64]),
     "lspcg_solver_set_dot_order": (C.c_int, [vp, C.c_int, C.c_int]),
     "lspcg_solver_destroy": (C.c_int, [vp]),

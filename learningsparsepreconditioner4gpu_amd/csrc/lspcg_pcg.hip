@@ -1096,6 +1096,8 @@ static int elem_grid(int64_t n) {  // 2 elements per lane, >= 2 pairs per lane, 
 
 using namespace lspcg;
 
+constexpr int kValCode8 = 8;  // lspcg_solver::svd: the view's slots are 1-byte dictionary codes
+
 struct lspcg_solver {
   lspcg_ctx* ctx = nullptr;
   const lspcg_mat* A = nullptr;       // the system the loop runs on: A_user, or Ap when reordered
@@ -1147,7 +1149,9 @@ struct lspcg_solver {
   SellPattern spat[3];
   const SellPattern* sp[3] = {nullptr, nullptr, nullptr};
   void* sv[3] = {nullptr, nullptr, nullptr};
-  int svd[3] = {0, 0, 0};
+  int svd[3] = {0, 0, 0};  // storage of sv[w]: LSPCG_F32 / LSPCG_F64, or kValCode8 (1-byte dictionary codes)
+  float* slut[3] = {nullptr, nullptr, nullptr};  // the dictionary of a coded view (256 floats)
+  bool codes_ok = false;   // value dictionaries allowed (single solves; LSPCG_VALUE_CODES=0 turns them off)
   double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
   int64_t dhist_cap = 0;
   int64_t small_n = kSmallNDefault;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it; also bounded by
@@ -1194,6 +1198,8 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   if (s->sv[w] || s->spat[w].gp) LSPCG_HIP(hipStreamSynchronize(s->stream));  // a solve may use them
   (void)hipFree(s->sv[w]);
   s->sv[w] = nullptr;
+  (void)hipFree(s->slut[w]);
+  s->slut[w] = nullptr;
   s->spat[w].release();
   s->sp[w] = nullptr;
   if (!s->use_sell || view->n == 0 || view->nnzb == 0) return LSPCG_OK;
@@ -1216,6 +1222,19 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   if (int rc = sell_fill_values(*P, view->colind, view->vals, vd, vd, st, &s->sv[w])) return rc;
   s->svd[w] = vd;
   s->sp[w] = P;
+  if (s->codes_ok && P->col_bits == 1 && vd == LSPCG_F32 && view->n > s->small_n) {
+    // few distinct values (a structured grid's stencil): 1-byte codes into an LDS dictionary
+    uint8_t* codes = nullptr;
+    float* lut = nullptr;
+    int nk = 0;
+    if (int rc = sdia_value_codes(*P, static_cast<const float*>(s->sv[w]), st, &codes, &lut, &nk)) return rc;
+    if (codes) {
+      (void)hipFree(s->sv[w]);
+      s->sv[w] = codes;
+      s->slut[w] = lut;
+      s->svd[w] = kValCode8;
+    }
+  }
   return LSPCG_OK;
 }
 
@@ -1245,6 +1264,10 @@ static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view) {
 template <typename T, class Gx, class Pro, class Epi>
 static int launch_it_gx(lspcg_solver* s, int w, Gx gx, Pro pro, Epi epi, hipStream_t st) {
   if (const SellPattern* P = s->sp[w]) {
+    if (s->svd[w] == kValCode8) {
+      launch_spmv_sdia<T, uint8_t>(*P, s->sv[w], gx, pro, epi, st, false, s->slut[w]);
+      return LSPCG_OK;
+    }
     if constexpr (sizeof(T) == 8) {
       if (s->svd[w] == LSPCG_F32) {
         launch_spmv_sell_cfg<T, float>(*P, s->sv[w], gx, pro, epi, st);
@@ -1636,6 +1659,8 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
   s->A_user = A;
   s->dia_ok = dia_ok;
   s->reorder_ok = reorder_ok && precond != LSPCG_PRECOND_IC;
+  s->codes_ok = reorder_ok;  // single solves only (the batched tile kernels read fp32 / fp64 views)
+  if (const char* e = std::getenv("LSPCG_VALUE_CODES")) s->codes_ok = s->codes_ok && e[0] != '0';
   s->precond = precond;
   s->dtype = A->dtype;
   s->n = A->n;
@@ -2066,6 +2091,16 @@ int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, dou
   return LSPCG_OK;
 }
 
+int lspcg_solver_views(const lspcg_solver* s, int* col_kind, int* value_bytes) {
+  LSPCG_CHECK(s && col_kind && value_bytes, LSPCG_ERR_ARG, "solver_views: NULL argument");
+  for (int w = 0; w < 3; ++w) {
+    const SellPattern* P = s->sp[w];
+    col_kind[w] = P ? P->col_bits : 0;
+    value_bytes[w] = !P ? 0 : s->svd[w] == kValCode8 ? 1 : s->svd[w] == LSPCG_F32 ? 4 : 8;
+  }
+  return LSPCG_OK;
+}
+
 int lspcg_solver_reorder_info(const lspcg_solver* s, int* applied, double* mean_offset_before,
                               double* mean_offset_after) {
   LSPCG_CHECK(s && applied, LSPCG_ERR_ARG, "reorder_info: NULL argument");
@@ -2100,6 +2135,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   for (void* p : {s->own_A, s->own_L, s->own_LT}) (void)hipFree(p);
   for (int w = 0; w < 3; ++w) {
     (void)hipFree(s->sv[w]);
+    (void)hipFree(s->slut[w]);
     s->spat[w].release();
   }
   (void)hipFree(s->flag);
