@@ -193,7 +193,8 @@ int lspcg_solver_set_dot_order(lspcg_solver* s, int order, int threads);
  * 1 (SELL-DIA: no column array), 16 / 32 (SELL-64 with 16-bit / int32 columns); value_bytes[w] = 8
  * (fp64), 4 (fp64 matrix stored exactly as fp32), 1 (one-byte codes into a <= 256-entry dictionary
  * of the view's exact values, SELL-DIA only: matrices with few distinct values, e.g. a structured
- * grid's stencil; LSPCG_VALUE_CODES=0 turns it off), 0 (no view).  Same bits in every case. */
+ * grid's stencil; opt-in with LSPCG_VALUE_CODES=1: it saves memory, not time), 0 (no view).  Same bits
+ * in every case. */
 int lspcg_solver_views(const lspcg_solver* s, int* col_kind, int* value_bytes);
 int lspcg_solver_reorder_info(const lspcg_solver* s, int* applied, double* mean_offset_before,
                               double* mean_offset_after);

@@ -1659,8 +1659,14 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
   s->A_user = A;
   s->dia_ok = dia_ok;
   s->reorder_ok = reorder_ok && precond != LSPCG_PRECOND_IC;
-  s->codes_ok = reorder_ok;  // single solves only (the batched tile kernels read fp32 / fp64 views)
-  if (const char* e = std::getenv("LSPCG_VALUE_CODES")) s->codes_ok = s->codes_ok && e[0] != '0';
+  // value dictionaries: single solves only (the batched tile kernels read fp32 / fp64 views), and
+  // opt-in -- on the headline system the coded A (15 MB instead of 61 MB) left the loop unchanged
+  // (67.5 vs 67.6 us per iteration, KC 20.9 vs 21.3 us: KC is not bound by A's value bytes; DESIGN.md
+  // §5), so it buys memory, not time.  LSPCG_VALUE_CODES=1 turns it on.
+  {
+    const char* e = std::getenv("LSPCG_VALUE_CODES");
+    s->codes_ok = reorder_ok && e && e[0] == '1';
+  }
   s->precond = precond;
   s->dtype = A->dtype;
   s->n = A->n;

@@ -2,9 +2,9 @@
 
 A matrix whose stored values take few distinct bit patterns (a structured grid's stencil: the
 headline Kuhn-tet Laplacian has 9) keeps each slot as a one-byte index into a <= 256-entry
-dictionary of the exact fp32 values, staged in LDS.  Every multiply sees the same value, so the
-solve must be BIT-identical to the fp32-value views (LSPCG_VALUE_CODES=0): count, every ‖r_k‖
-and x.  Views with more than 256 values (the GNN's L) stay fp32.
+dictionary of the exact fp32 values, staged in LDS (opt-in: LSPCG_VALUE_CODES=1).  Every
+multiply sees the same value, so the solve must be BIT-identical to the fp32-value views (the
+default): count, every ‖r_k‖ and x.  Views with more than 256 values (the GNN's L) stay fp32.
 """
 import numpy as np
 import pytest
