@@ -498,4 +498,16 @@ int lspcg_part_status(lspcg_part* p, int64_t* iter, int* done) {
   return LSPCG_OK;
 }
 
+int lspcg_part_progress(lspcg_part* p, int64_t* iter, int* done, double* rr, double* atol) {
+  LSPCG_CHECK(p && iter && done && rr && atol, LSPCG_ERR_ARG, "part_progress: NULL argument");
+  PartState h{};
+  LSPCG_HIP(hipMemcpyAsync(&h, p->S, sizeof(PartState), hipMemcpyDeviceToHost, p->ctx->stream));
+  LSPCG_HIP(hipStreamSynchronize(p->ctx->stream));
+  *iter = h.iter;
+  *done = h.done;
+  *rr = h.rr;
+  *atol = h.atol;
+  return LSPCG_OK;
+}
+
 }  // extern "C"

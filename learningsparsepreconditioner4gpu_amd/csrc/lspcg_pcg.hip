@@ -21,6 +21,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cmath>
+#include <cstring>
 #include <cstdlib>
 #include <map>
 #include <memory>
@@ -1153,7 +1154,9 @@ struct lspcg_solver {
   float* slut[3] = {nullptr, nullptr, nullptr};  // the dictionary of a coded view (256 floats)
   bool codes_ok = false;   // value dictionaries allowed (single solves; LSPCG_VALUE_CODES=0 turns them off)
   double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
+  double* hhist = nullptr;  // its pinned host mirror (the history's copy is enqueued, not a blocking copy)
   int64_t dhist_cap = 0;
+  unsigned* hflags = nullptr;  // pinned: the IC triangular solves' timeout flags, copied behind the solve
   int64_t small_n = kSmallNDefault;  // largest n solved by k_pcg_small (LSPCG_SMALL_N; 0 disables it; also bounded by
                            // 3 rows per thread at 1024 threads and the LDS of 3 vectors: 2560 in fp64)
   bool small_sell = true;  // k_pcg_small reads the SELL copies (LSPCG_SMALL_SELL=0: the CSR views)
@@ -1870,9 +1873,12 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     if (s->dhist_cap < max_iter + 2) {
       LSPCG_HIP(hipStreamSynchronize(st));
       (void)hipFree(s->dhist);
+      (void)hipHostFree(s->hhist);
       s->dhist = nullptr;
+      s->hhist = nullptr;
       s->dhist_cap = 0;
       LSPCG_HIP(hipMalloc(&s->dhist, sizeof(double) * (max_iter + 2)));
+      LSPCG_HIP(hipHostMalloc(&s->hhist, sizeof(double) * (max_iter + 2), hipHostMallocDefault));
       s->dhist_cap = max_iter + 2;
     }
     dhist = s->dhist;
@@ -1995,24 +2001,39 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     LSPCG_HIP(hipMemcpyAsync(x, src, vb, hipMemcpyDeviceToDevice, st));
   }
   LSPCG_HIP(hipEventRecord(s->ev_t1, st));
+  // the tail's device-to-host copies (IC timeout flags, the residual history) are enqueued behind the
+  // solve into pinned mirrors, so the last host wait is the only one and the submission lock is not
+  // held through it (a blocking copy under the lock serialised concurrent solves' tails)
+  const bool ic = s->precond == LSPCG_PRECOND_IC;
+  if (ic) {
+    if (!s->hflags) LSPCG_HIP(hipHostMalloc(&s->hflags, 2 * sizeof(unsigned), hipHostMallocDefault));
+    s->hflags[0] = s->hflags[1] = 0;
+    if (s->levL.head)
+      LSPCG_HIP(hipMemcpyAsync(&s->hflags[0], s->levL.head + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    if (s->levU.head)
+      LSPCG_HIP(hipMemcpyAsync(&s->hflags[1], s->levU.head + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  }
+  const int64_t it = (fin.done == 3) ? max_iter : fin.iter;
+  // history entries 0..fin.iter were written; a non-finite residual stops early while iters reports
+  // max_iter (pymathprim's count), so the rest of 0..iters is NaN-filled
+  const int64_t hcnt = std::min<int64_t>(fin.iter, max_iter) + 1;
+  if (res_hist) LSPCG_HIP(hipMemcpyAsync(s->hhist, dhist, sizeof(double) * hcnt, hipMemcpyDeviceToHost, st));
   LSPCG_HIP(hipEventRecord(s->ev_out, st));
   LSPCG_HIP(hipStreamWaitEvent(s->ctx->stream, s->ev_out, 0));
-  LSPCG_HIP(wait(s->ev_t1));
-  if (s->precond == LSPCG_PRECOND_IC) {  // a timed-out sync-free hand-off fails the solve loudly
-    if (int r2 = trsv_check_timeout(s->levL, st)) return r2;
+  sub.unlock();
+  LSPCG_HIP(hipEventSynchronize(s->ev_out));
+  if (ic && (s->hflags[0] || s->hflags[1])) {  // a timed-out sync-free hand-off fails the solve loudly
+    sub.lock();
+    if (int r2 = trsv_check_timeout(s->levL, st)) return r2;  // resets the flag, sets the message
     if (int r2 = trsv_check_timeout(s->levU, st)) return r2;
   }
   float ms = 0.f;
   LSPCG_HIP(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1));
   if (t_solve_ms) *t_solve_ms = ms;
-  const int64_t it = (fin.done == 3) ? max_iter : fin.iter;
   *iters = it;
   if (res_hist) {
-    // entries 0..fin.iter were written; a non-finite residual stops early while iters reports
-    // max_iter (pymathprim's count), so the rest of 0..iters is NaN-filled
-    const int64_t cnt = std::min<int64_t>(fin.iter, max_iter) + 1;
-    LSPCG_HIP(hipMemcpy(res_hist, dhist, sizeof(double) * cnt, hipMemcpyDeviceToHost));
-    for (int64_t k = cnt; k <= it; ++k) res_hist[k] = NAN;
+    std::memcpy(res_hist, s->hhist, sizeof(double) * hcnt);
+    for (int64_t k = hcnt; k <= it; ++k) res_hist[k] = NAN;
   }
   return (fin.done == 1) ? LSPCG_OK : LSPCG_NOT_CONVERGED;
 }
@@ -2147,6 +2168,8 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   (void)hipFree(s->flag);
   (void)hipFree(s->ob_part);
   (void)hipFree(s->dhist);
+  (void)hipHostFree(s->hhist);
+  (void)hipHostFree(s->hflags);
   (void)hipStreamDestroy(s->stream);
   delete s;
   return LSPCG_OK;

@@ -234,6 +234,22 @@ def gather_rows(t: torch.Tensor, group=None) -> np.ndarray:
     return torch.stack(parts).numpy()
 
 
+def next_chunk(chunk: int, max_chunk: int, k: int, rr: float, atol: float, max_iter: int, last):
+    """Iterations to enqueue before the next state read, and the new ``last`` = (k, ‖r_k‖²): doubling
+    while no decay has been observed, then the predicted remaining count (log(atol² / rr) over the
+    observed log-decay per iteration, as lspcg_solver_solve's poll loop), capped by ``max_chunk``
+    and ``max_iter - k``, at least 1."""
+    nxt = min(2 * chunk, max_chunk)
+    if last is not None and k > last[0] and 0.0 < rr < last[1]:
+        rate = math.log(rr / last[1]) / (k - last[0])  # < 0
+        need = math.log(atol * atol / rr) / rate if atol > 0 else float("inf")
+        rem = max(1, int(math.ceil(need))) if need > 0 else 1
+        nxt = max(1, min(rem, max_chunk, max(1, max_iter - k)))
+    if last is None or k > last[0]:
+        last = (k, rr)
+    return nxt, last
+
+
 # ---------------------------------------------------------------------------------------------
 # the solver
 # ---------------------------------------------------------------------------------------------
@@ -390,13 +406,21 @@ class DistributedPCG:
         _lib.call("lspcg_part_status", self.handle, C.byref(it), C.byref(done))
         return it.value, done.value
 
+    def _progress(self):
+        it, done, rr, atol = C.c_int64(), C.c_int(), C.c_double(), C.c_double()
+        _lib.call("lspcg_part_progress", self.handle, C.byref(it), C.byref(done), C.byref(rr), C.byref(atol))
+        return it.value, done.value, rr.value, atol.value
+
     def solve(self, b_global: np.ndarray, rtol: float = 1e-6, max_iter: int = 0, return_history: bool = False,
               max_chunk: int = 16):
         """scipy cg from x0 = 0 on the global rhs (every rank passes the same vector).  Returns
         ``(iters, converged, x_own[, history])``; x_own: this rank's rows of the solution.
-        Iterations are enqueued in chunks of 1, 2, 4, ... ``max_chunk`` with the device state read
-        once per chunk; iterations enqueued past convergence skip every update (predicated on the
-        state), so count, history and x are those of the converged iteration."""
+        Iterations are enqueued in chunks with the device state read once per chunk: 1, 2, 4, ...
+        ``max_chunk`` until the residual has decayed twice, then sized by the predicted remaining
+        iterations (next_chunk; the single-GPU solver's rule), so few iterations run past
+        convergence -- each would still pay its halo exchanges and all-gathers.  Iterations
+        enqueued past convergence skip every update (predicated on the state), so count, history
+        and x are those of the converged iteration."""
         p = self.plan
         no = p.n_own
         mi = int(max_iter) if max_iter and max_iter > 0 else self.n
@@ -417,11 +441,12 @@ class DistributedPCG:
             out = (0, True, self.x[:no].clone())
             return out + ((self.hist_dev[:1].cpu().numpy(),) if return_history else ())
         chunk = 1
+        last = None  # (iteration, ‖r‖²) of the previous state read
         while not done:
             for _ in range(chunk):
                 self._iteration()
-            k, done = self._status()
-            chunk = min(2 * chunk, int(max_chunk))
+            k, done, rr, atol = self._progress()
+            chunk, last = next_chunk(chunk, int(max_chunk), k, rr, atol, mi, last)
         iters = mi if done == 3 else k
         out = (iters, done == 1, self.x[:no].clone())
         if return_history:

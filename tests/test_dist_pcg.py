@@ -156,3 +156,19 @@ def test_from_row_blocks_validates_its_blocks():
         DistributedPCG.from_row_blocks(A, n=n, bounds=[0, n - 1])
     with pytest.raises(ValueError, match="shape"):
         DistributedPCG.from_row_blocks(A[: n - 3], n=n, bounds=[0, n])
+
+
+def test_next_chunk_prediction():
+    """dist_pcg's chunks follow the residual's decay, not a blind doubling to 16."""
+    from learningsparsepreconditioner4gpu_amd.dist_pcg import next_chunk
+
+    c, last = next_chunk(1, 16, 1, 1.0, 1e-4, 1000, None)  # no history yet: double
+    assert c == 2 and last == (1, 1.0)
+    # rr fell 1.0 -> 1e-2 over 2 iterations (a factor 10 per iteration in ‖r‖²): atol² = 1e-8 needs
+    # log(1e-8 / 1e-2) / log(0.1) = 6 more
+    c, last = next_chunk(2, 16, 3, 1e-2, 1e-4, 1000, last)
+    assert c == 6 and last == (3, 1e-2)
+    c, _ = next_chunk(2, 16, 3, 1e-2, 1e-4, 4, (1, 1.0))  # capped by max_iter - k
+    assert c == 1
+    c, _ = next_chunk(4, 16, 5, 1e-2, 1e-4, 1000, (3, 1e-2))  # no decay: double
+    assert c == 8
