@@ -60,12 +60,18 @@ __host__ __device__ constexpr int frag_size(int s1) { return s1 * 64 + 5 * 256; 
 using f2 = float __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, float c) { return __builtin_elementwise_fma(a, b, (f2)(c)); }
 constexpr float kGeluClamp = 5.75f;
+#ifdef LSPCG_GELU_DEG5
+constexpr int kGeluDeg = 5;  // experiment: 4.4e-7 in exact arithmetic
+constexpr float kGeluC[6] = {-1.000037670135498f, -1.1507878303527832f, -0.45999249815940857f,
+                             -0.05182735249400139f, 0.007084548939019442f, -0.0004733086680062115f};
+#else
 constexpr int kGeluDeg = 6;  // fitted to the GELU's absolute error |v| m(|v|) (iteratively reweighted
                               // least squares toward minimax): 5.1e-8 in exact arithmetic, 5.2e-7 with fp32
                               // evaluation -- the fp32 rounding of GELU(v) itself is 4.8e-7 at |v| = 9
 constexpr float kGeluC[7] = {-0.999993085861206f,   -1.1512017250061035f,    -0.4587709605693817f,
                              -0.05341210961341858f, 0.008080719038844109f,   -0.0007692205253988504f,
                              3.309291059849784e-05f};
+#endif
 // max(v, 0) as one v_max_i32 on the bit pattern (negative floats, -0 included, are negative
 // integers); fmaxf would add a canonicalising v_max
 __device__ __forceinline__ float relu(float v) {
@@ -215,14 +221,20 @@ constexpr int kH48W2h = 1024, kH48W2l = 1152, kH48C2 = 1280, kH48W3h = 1536, kH4
 constexpr int kH48S = 2048;
 
 // (a, b) -> packed f16 pairs hi = RNE(a, b), lo = RNE(a - hi, b - hi) (x - hi is exact in fp32).
-// Plain conversions: a three-instruction inline-asm form (v_fma_mix{lo,hi}_f16 for the residuals)
-// gives the same bits but, with the 2 wait states its MFMA consumers need inside the string (hipcc
-// pads nothing inside inline asm), measured no faster.
+// The residuals come straight from the f16 halves: v_fma_mix_f32 reads src0 as f16 (lo or hi half
+// by op_sel), so hi is never converted back to f32 and there is no packed subtract -- 4 instead of 5
+// instructions per pair, 2 of them packed-rate fewer (the compiler does not select the mix form
+// itself).  Exact, so the same bits; the asm results feed a compiler-emitted conversion, never an
+// MFMA operand (an MFMA reading a VGPR written inside inline asm needs wait states hipcc does not
+// insert -- round 4's v_fma_mix{lo,hi}_f16 form, which wrote the f16 operand itself, measured no
+// faster for that reason).  Forward 4.49 vs 4.63 ms at kuhn101 (profiles/r5_gnn_ab_mix.jsonl).
 __device__ __forceinline__ void split2(float a, float b, unsigned& hi, unsigned& lo) {
   const hf2 h = __builtin_convertvector((f2){a, b}, hf2);
-  const f2 r = (f2){a, b} - __builtin_convertvector(h, f2);
   hi = __builtin_bit_cast(unsigned, h);
-  lo = __builtin_bit_cast(unsigned, __builtin_convertvector(r, hf2));
+  float ra, rb;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(ra) : "v"(hi), "v"(a));
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(rb) : "v"(hi), "v"(b));
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f2){ra, rb}, hf2));
 }
 __device__ __forceinline__ void split4(const float* v, h4& hi, h4& lo) {
   unsigned h[2], l[2];
