@@ -60,18 +60,12 @@ __host__ __device__ constexpr int frag_size(int s1) { return s1 * 64 + 5 * 256; 
 using f2 = float __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, float c) { return __builtin_elementwise_fma(a, b, (f2)(c)); }
 constexpr float kGeluClamp = 5.75f;
-#ifdef LSPCG_GELU_DEG5
-constexpr int kGeluDeg = 5;  // experiment: 4.4e-7 in exact arithmetic
-constexpr float kGeluC[6] = {-1.000037670135498f, -1.1507878303527832f, -0.45999249815940857f,
-                             -0.05182735249400139f, 0.007084548939019442f, -0.0004733086680062115f};
-#else
 constexpr int kGeluDeg = 6;  // fitted to the GELU's absolute error |v| m(|v|) (iteratively reweighted
                               // least squares toward minimax): 5.1e-8 in exact arithmetic, 5.2e-7 with fp32
                               // evaluation -- the fp32 rounding of GELU(v) itself is 4.8e-7 at |v| = 9
 constexpr float kGeluC[7] = {-0.999993085861206f,   -1.1512017250061035f,    -0.4587709605693817f,
                              -0.05341210961341858f, 0.008080719038844109f,   -0.0007692205253988504f,
                              3.309291059849784e-05f};
-#endif
 // max(v, 0) as one v_max_i32 on the bit pattern (negative floats, -0 included, are negative
 // integers); fmaxf would add a canonicalising v_max
 __device__ __forceinline__ float relu(float v) {
