@@ -324,6 +324,10 @@ int lspcg_part_scalars(lspcg_part* p, const double* gathered, int world, int pha
 int lspcg_part_update_p_dev(lspcg_part* p, const void* z, void* p_ext);
 int lspcg_part_update_xr_dev(lspcg_part* p, const void* p_ext, const void* q, void* x, void* r_ext);
 int lspcg_part_status(lspcg_part* p, int64_t* iter, int* done);
+/* The SpMV phases (lt / l / a) of this part store and reduce own rows [r0, n_own) only (default 0):
+ * dist_pcg keeps one part for the interior rows (every column owned: computed while the halo
+ * exchange is in flight) and one with r0 = the first boundary row (after it). */
+int lspcg_part_set_rows(lspcg_part* p, int64_t r0);
 /* lspcg_part_status plus the state's ‖r_k‖² and atol: the host sizes the next chunk of enqueued
  * iterations from the residual's decay (as lspcg_solver_solve does), so few iterations are enqueued
  * past convergence -- each would still run its halo exchanges and all-gathers. */

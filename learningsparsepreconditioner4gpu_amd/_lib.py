@@ -95,6 +95,7 @@ SIGNATURES = {
     "lspcg_part_update_p_dev": (C.c_int, [vp, vp, vp]),
     "lspcg_part_update_xr_dev": (C.c_int, [vp, vp, vp, vp, vp]),
     "lspcg_part_progress": (C.c_int, [vp, p_i64, C.POINTER(C.c_int), p_f64, p_f64]),
+    "lspcg_part_set_rows": (C.c_int, [vp, C.c_int64]),
     "lspcg_part_status": (C.c_int, [vp, C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
 }
 

@@ -25,7 +25,8 @@ namespace lspcg {
 
 constexpr int kPartGroups = 64;  // group slots of a reduction buffer (kMaxGroups)
 
-// own-row store (rows >= n_own of the extended matrix are empty and skipped)
+// own-row store (rows >= n_own of the extended matrix are empty and skipped; so are rows < r0, the
+// part's first row -- lspcg_part_set_rows: a part that runs the boundary rows only)
 template <typename T>
 struct EpiOwn {
   static constexpr int NDOT = 0;
@@ -33,9 +34,10 @@ struct EpiOwn {
   int64_t n_own;
   double* partials = nullptr;
   unsigned* ticket = nullptr;
+  int64_t r0 = 0;
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ void row(int64_t i, T s, DD*) const {
-    if (i < n_own) gst(y + i, s);
+    if (i >= r0 && i < n_own) gst(y + i, s);
   }
   __device__ __forceinline__ void fin(const double*) const {}
 };
@@ -56,9 +58,10 @@ struct EpiZPart {
   unsigned* ticket;
   double* group_out;
   int gsz;
+  int64_t r0 = 0;
   __device__ __forceinline__ void prepare() { gsz = part_gsz(); }
   __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
-    if (i >= n_own) return;
+    if (i < r0 || i >= n_own) return;
     const T ri = gld(r + i);
     const T zi = s + eps * ri;
     gst(z + i, zi);
@@ -80,9 +83,10 @@ struct EpiQPart {
   unsigned* ticket;
   double* group_out;
   int gsz;
+  int64_t r0 = 0;
   __device__ __forceinline__ void prepare() { gsz = part_gsz(); }
   __device__ __forceinline__ void row(int64_t i, T s, DD* dots) const {
-    if (i >= n_own) return;
+    if (i < r0 || i >= n_own) return;
     gst(q + i, s);
     dd_fma(dots[0], double(gld(p + i)), double(s));
   }
@@ -256,6 +260,7 @@ struct lspcg_part {
   const lspcg_mat* LT = nullptr;
   int dtype = LSPCG_F64;
   int64_t n_own = 0, n_ext = 0, n_send = 0;
+  int64_t r0 = 0;               // first own row of the SpMV phases (lspcg_part_set_rows)
   int32_t* send_idx = nullptr;  // owned device copy
   double* partials = nullptr;
   unsigned* ticket = nullptr;
@@ -361,9 +366,10 @@ int lspcg_part_norms(lspcg_part* p, const void* a, const void* b, double* red) {
 
 int lspcg_part_lt(lspcg_part* p, const void* r_ext, void* t_ext) {
   LSPCG_CHECK(p && p->LT && r_ext && t_ext, LSPCG_ERR_ARG, "part_lt: NULL argument (or no L)");
-  int rc = p->dtype == LSPCG_F64
-               ? part_spmv<double>(p, p->LT, r_ext, EpiOwn<double>{static_cast<double*>(t_ext), p->n_own})
-               : part_spmv<float>(p, p->LT, r_ext, EpiOwn<float>{static_cast<float*>(t_ext), p->n_own});
+  EpiOwn<double> ed{static_cast<double*>(t_ext), p->n_own};
+  EpiOwn<float> ef{static_cast<float*>(t_ext), p->n_own};
+  ed.r0 = ef.r0 = p->r0;
+  int rc = p->dtype == LSPCG_F64 ? part_spmv<double>(p, p->LT, r_ext, ed) : part_spmv<float>(p, p->LT, r_ext, ef);
   if (rc) return rc;
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
@@ -374,14 +380,17 @@ int lspcg_part_l(lspcg_part* p, const void* t_ext, const void* r, double eps, vo
   hipStream_t st = p->ctx->stream;
   LSPCG_HIP(hipMemsetAsync(red, 0, sizeof(double) * kPartGroups * 2 * 2, st));
   int rc;
-  if (p->dtype == LSPCG_F64)
-    rc = part_spmv<double>(p, p->L, t_ext,
-                           EpiZPart<double>{static_cast<double*>(z), static_cast<const double*>(r), eps, p->n_own,
-                                            p->partials, p->ticket, red, 1});
-  else
-    rc = part_spmv<float>(p, p->L, t_ext,
-                          EpiZPart<float>{static_cast<float*>(z), static_cast<const float*>(r), float(eps), p->n_own,
-                                          p->partials, p->ticket, red, 1});
+  if (p->dtype == LSPCG_F64) {
+    EpiZPart<double> e{static_cast<double*>(z), static_cast<const double*>(r), eps, p->n_own, p->partials, p->ticket,
+                       red, 1};
+    e.r0 = p->r0;
+    rc = part_spmv<double>(p, p->L, t_ext, e);
+  } else {
+    EpiZPart<float> e{static_cast<float*>(z), static_cast<const float*>(r), float(eps), p->n_own, p->partials,
+                      p->ticket, red, 1};
+    e.r0 = p->r0;
+    rc = part_spmv<float>(p, p->L, t_ext, e);
+  }
   if (rc) return rc;
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
@@ -392,14 +401,17 @@ int lspcg_part_a(lspcg_part* p, const void* p_ext, void* q, double* red) {
   hipStream_t st = p->ctx->stream;
   LSPCG_HIP(hipMemsetAsync(red, 0, sizeof(double) * kPartGroups * 2, st));
   int rc;
-  if (p->dtype == LSPCG_F64)
-    rc = part_spmv<double>(p, p->A, p_ext,
-                           EpiQPart<double>{static_cast<double*>(q), static_cast<const double*>(p_ext), p->n_own,
-                                            p->partials, p->ticket, red, 1});
-  else
-    rc = part_spmv<float>(p, p->A, p_ext,
-                          EpiQPart<float>{static_cast<float*>(q), static_cast<const float*>(p_ext), p->n_own,
-                                          p->partials, p->ticket, red, 1});
+  if (p->dtype == LSPCG_F64) {
+    EpiQPart<double> e{static_cast<double*>(q), static_cast<const double*>(p_ext), p->n_own, p->partials, p->ticket,
+                       red, 1};
+    e.r0 = p->r0;
+    rc = part_spmv<double>(p, p->A, p_ext, e);
+  } else {
+    EpiQPart<float> e{static_cast<float*>(q), static_cast<const float*>(p_ext), p->n_own, p->partials, p->ticket,
+                      red, 1};
+    e.r0 = p->r0;
+    rc = part_spmv<float>(p, p->A, p_ext, e);
+  }
   if (rc) return rc;
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
@@ -495,6 +507,12 @@ int lspcg_part_status(lspcg_part* p, int64_t* iter, int* done) {
   LSPCG_HIP(hipStreamSynchronize(p->ctx->stream));
   *iter = h.iter;
   *done = h.done;
+  return LSPCG_OK;
+}
+
+int lspcg_part_set_rows(lspcg_part* p, int64_t r0) {
+  LSPCG_CHECK(p && r0 >= 0 && r0 <= p->n_own, LSPCG_ERR_ARG, "part_set_rows: r0 outside [0, n_own]");
+  p->r0 = r0;
   return LSPCG_OK;
 }
 

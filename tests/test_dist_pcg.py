@@ -172,3 +172,50 @@ def test_next_chunk_prediction():
     assert c == 1
     c, _ = next_chunk(4, 16, 5, 1e-2, 1e-4, 1000, (3, 1e-2))  # no decay: double
     assert c == 8
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_plans_interior_first(world):
+    """Interior-first local numbering (dist_pcg overlap): every interior row's columns are owned, the
+    local SpMV over [interior | boundary] rows reproduces scipy's rows bit for bit in global order,
+    row_range splits a local matrix into the two launches' halves exactly, and what a rank sends is
+    what its neighbours' halos hold."""
+    from learningsparsepreconditioner4gpu_amd.dist_pcg import interior_rows, row_range
+
+    mats = _mats()
+    n = mats[0].shape[0]
+    bounds = partition_rows(mats[0].indptr, world)
+    plans = [build_plan(mats, bounds, r, split=True) for r in range(world)]
+    x = np.random.default_rng(3).standard_normal(n)
+    for M in mats:
+        y = np.empty(n)
+        for r, p in enumerate(plans):
+            r0, r1 = bounds[r], bounds[r + 1]
+            assert 0 < p.n_int < p.n_own and sorted(p.order) == list(range(r0, r1))
+            ok = interior_rows([m[r0:r1] for m in mats], r0, r1)
+            assert np.array_equal(np.sort(p.order[:p.n_int]), np.arange(r0, r1)[ok])
+            xe = np.concatenate([x[p.order], x[p.halo]])
+            Ml = local_matrix(M, p)
+            assert Ml[:p.n_int].indices.max() < p.n_own  # interior rows: own columns only
+            lo, hi = row_range(Ml, 0, p.n_int), row_range(Ml, p.n_int, p.n_own)
+            assert (lo + hi - Ml).nnz == 0 and lo[p.n_int:].nnz == 0 and hi[:p.n_int].nnz == 0
+            y[p.order] = (Ml @ xe)[:p.n_own]
+        assert np.array_equal(y, M @ x)
+    for r, p in enumerate(plans):
+        for s, q in enumerate(plans):
+            if s == r:
+                continue
+            off = sum(q.send_counts[:r])
+            sent = q.order[q.send_idx[off:off + q.send_counts[r]]]
+            got = p.halo[sum(p.recv_counts[:s]):sum(p.recv_counts[:s + 1])]
+            assert np.array_equal(sent, got)
+
+
+def test_sum_groups_two_halves():
+    """Two 64-group halves per rank are summed rank-major, half by half: the same as treating every
+    half as a rank (lspcg_part_scalars with world * 2)."""
+    rng = np.random.default_rng(5)
+    g = rng.standard_normal((3, 2 * GROUPS * 2 * 2))
+    a = sum_groups(g, 2)
+    b = sum_groups(g.reshape(6, GROUPS * 2 * 2), 2)
+    assert a == b

@@ -87,10 +87,10 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, kind, q, blocks=False):
+def _rank(rank, world, port, kind, q, blocks=False, overlap=True):
     import torch.distributed as dist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LSPCG_DIST_OVERLAP="1" if overlap else "0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from learningsparsepreconditioner4gpu_amd.dist_pcg import DistributedPCG, partition_rows
@@ -108,19 +108,21 @@ def _rank(rank, world, port, kind, q, blocks=False):
     it_h, conv_h, x_h, hist_h = d.solve_host(b, rtol=1e-8, return_history=True)
     same = (it_h, conv_h) == (it, conv) and np.array_equal(hist_h, hist) and torch.equal(x_h, x)
     xg = d.gather_solution(x)
-    q.put((rank, it, bool(conv), xg, hist, d.plan.n_own, len(d.plan.halo), same))
+    q.put((rank, it, bool(conv), xg, hist, d.plan.n_own, len(d.plan.halo), same, d.split))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,blocks", [(2, False), (3, False), (3, True)])
-def test_multi_rank_matches_oracle(gpu_ctx, world, blocks):
-    """blocks: DistributedPCG.from_row_blocks -- no rank holds the global system."""
+@pytest.mark.parametrize("world,blocks,overlap", [(2, False, True), (3, False, True), (3, True, True), (2, False, False)])
+def test_multi_rank_matches_oracle(gpu_ctx, world, blocks, overlap):
+    """blocks: DistributedPCG.from_row_blocks -- no rank holds the global system.  overlap: own rows
+    numbered interior first, the interior rows' SpMVs enqueued while the halo exchange runs
+    (LSPCG_DIST_OVERLAP=0: one row range)."""
     kind = "kuhn"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, kind, q, blocks)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, kind, q, blocks, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     outs = sorted([q.get(timeout=100) for _ in range(world)], key=lambda o: o[0])
@@ -130,7 +132,8 @@ def test_multi_rank_matches_oracle(gpu_ctx, world, blocks):
     A, L, b = _system(kind)
     it_o, x_o, h_o = _oracle(A, L, b, 1e-8)
     assert sum(o[5] for o in outs) == A.shape[0] and all(o[6] > 0 for o in outs)
-    for rank, it, conv, xg, hist, _, _, same in outs:
+    for rank, it, conv, xg, hist, _, _, same, split in outs:
+        assert split == overlap, rank
         assert same, rank  # device-side scalars = the host recurrence, bit for bit
         assert conv and it == it_o, (rank, it, it_o)
         np.testing.assert_allclose(hist, h_o[: it + 1], rtol=1e-12, atol=0)
