@@ -12,16 +12,17 @@
 // numbering (b, x0 gathered in, x scattered out); the compensated dots are order-insensitive to
 // ~1 ulp.  The parity dot order (numpy's ddot order over the ORIGINAL numbering) turns it off.
 //
-// The permutation is computed on the host (one copy of the pattern, two BFS sweeps: a
-// pseudo-peripheral start per connected component, then Cuthill-McKee with neighbours by
-// increasing degree, reversed) -- scipy.sparse.csgraph.reverse_cuthill_mckee's algorithm -- and only
-// for matrices whose numbering is far from banded: mean |col - row| > 4 nb^(2/3) (a 3-D mesh in
+// The permutation is computed on the device, one BFS level per step (a pseudo-peripheral start per
+// connected component, then Cuthill-McKee with neighbours by increasing degree, reversed --
+// scipy.sparse.csgraph.reverse_cuthill_mckee's algorithm, see rcm_device), and only for matrices
+// whose numbering is far from banded: mean |col - row| > 4 nb^(2/3) (a 3-D mesh in
 // any locality-preserving order sits well below; a random numbering at ~nb / 3), measured by one
 // device reduction first.  The matrices are permuted on the device.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <memory>
@@ -119,74 +120,250 @@ int mean_abs_offset(const lspcg_mat* A, double* out) {
   return LSPCG_OK;
 }
 
-// Reverse Cuthill-McKee of the graph of (rp, ci) (rows as adjacency lists; self loops ignored):
-// order[k] = old index of the k-th new row.
-static void rcm_host(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& ci,
-                     std::vector<int32_t>& order) {
-  std::vector<int32_t> deg(n);
-  for (int64_t i = 0; i < n; ++i) deg[i] = rp[i + 1] - rp[i];
-  std::vector<int32_t> bydeg(n);
-  std::iota(bydeg.begin(), bydeg.end(), 0);
-  std::stable_sort(bydeg.begin(), bydeg.end(), [&](int32_t a, int32_t b) { return deg[a] < deg[b]; });
-  std::vector<uint8_t> done(n, 0);
-  std::vector<int32_t> stamp(n, -1);  // BFS of the pseudo-peripheral search: last component id seen
-  std::vector<int32_t> queue;
-  queue.reserve(n);
-  order.clear();
-  order.reserve(n);
-  std::vector<int32_t> nbr;
-  int64_t cursor = 0;
-  int32_t comp = 0;
-  while (int64_t(order.size()) < n) {
-    while (done[bydeg[cursor]]) ++cursor;
-    int32_t start = bydeg[cursor];
-    {  // one pseudo-peripheral step: the min-degree node (ties: index) of the BFS's last level
-      queue.clear();
-      queue.push_back(start);
-      stamp[start] = comp;
-      size_t lb = 0;
-      for (;;) {
-        const size_t le = queue.size();
-        for (size_t h = lb; h < le; ++h) {
-          const int32_t u = queue[h];
-          for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
-            const int32_t v = ci[k];
-            if (stamp[v] != comp) {
-              stamp[v] = comp;
-              queue.push_back(v);
-            }
-          }
-        }
-        if (queue.size() == le) break;  // [lb, le) was the last level
-        lb = le;
-      }
-      int32_t best = queue[lb];
-      for (size_t k = lb + 1; k < queue.size(); ++k) {
-        const int32_t v = queue[k];
-        if (deg[v] < deg[best] || (deg[v] == deg[best] && v < best)) best = v;
-      }
-      start = best;
-      ++comp;
-    }
-    // Cuthill-McKee from `start`: neighbours appended by increasing degree (ties: index)
-    size_t head = order.size();
-    order.push_back(start);
-    done[start] = 1;
-    while (head < order.size()) {
-      const int32_t u = order[head++];
-      nbr.clear();
-      for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
-        const int32_t v = ci[k];
-        if (!done[v]) {
-          done[v] = 1;
-          nbr.push_back(v);
-        }
-      }
-      std::sort(nbr.begin(), nbr.end(), [&](int32_t a, int32_t b) { return deg[a] != deg[b] ? deg[a] < deg[b] : a < b; });
-      order.insert(order.end(), nbr.begin(), nbr.end());
+// ---- reverse Cuthill-McKee on the device (level-synchronous) ---------------------------------
+// Sequential Cuthill-McKee appends, while it walks its queue, each node's unvisited neighbours by
+// increasing (degree, index); a node of BFS level L+1 is therefore appended by the FIRST node of
+// level L (in queue order) adjacent to it.  So level L+1's order is the sort of its nodes by
+// (position of that first parent in level L, degree, index) -- computed here one level at a time:
+// the frontier kernel records every unvisited neighbour's smallest parent position (atomicMin) and
+// appends it once to the next level (atomicExch on a per-level stamp), then two stable radix sorts
+// (by index, then by (parent position, degree)) order the level.  Nodes whose only neighbour is
+// themselves (Dirichlet rows) are placed first, in (degree, index) order; every other component
+// starts from its (degree, index)-smallest node, moved once to the (degree, index)-smallest node of
+// its last BFS level (one pseudo-peripheral step).  The whole order is reversed at the end.
+__global__ void k_rcm_init(int64_t n, const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                           int32_t* __restrict__ deg, uint8_t* __restrict__ iso, int32_t* __restrict__ pos,
+                           int32_t* __restrict__ pkey, int32_t* __restrict__ mark) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t b = rp[i], e = rp[i + 1];
+    bool only_self = true;
+    for (int32_t k = b; k < e; ++k) only_self = only_self && ci[k] == i;
+    deg[i] = e - b;
+    iso[i] = only_self ? uint8_t(e - b == 0 ? 1 : 2) : uint8_t(0);  // 1: empty row, 2: self loop only
+    pos[i] = -1;
+    pkey[i] = INT_MAX;
+    mark[i] = -1;
+  }
+}
+
+// the (degree, index)-smallest node with pos == -1 (or, pass >= 0, among list[0..m))
+__global__ void k_rcm_argmin(int64_t m, const int32_t* __restrict__ list, const int32_t* __restrict__ deg,
+                             const int32_t* __restrict__ pos, unsigned long long* __restrict__ best) {
+  unsigned long long b = ~0ull;
+  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < m; k += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t v = list ? list[k] : int32_t(k);
+    if (list || pos[v] == -1) {
+      const unsigned long long key = (static_cast<unsigned long long>(deg[v]) << 32) | unsigned(v);
+      b = key < b ? key : b;
     }
   }
-  std::reverse(order.begin(), order.end());
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long t = __shfl_xor(b, o);
+    b = t < b ? t : b;
+  }
+  if ((threadIdx.x & 63) == 0 && b != ~0ull) atomicMin(best, b);
+}
+
+// one BFS level: every unvisited (pos == -1) neighbour v of frontier[f] gets pkey[v] = min f and is
+// appended once (mark[v] = stamp) to next; record = false: the pseudo-peripheral BFS (no pkey)
+__global__ void k_rcm_level(int64_t m, const int32_t* __restrict__ frontier, const int32_t* __restrict__ rp,
+                            const int32_t* __restrict__ ci, const int32_t* __restrict__ pos, int32_t* __restrict__ pkey,
+                            int32_t* __restrict__ mark, int32_t stamp, int32_t* __restrict__ next,
+                            int32_t* __restrict__ cnt, int record) {
+  for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < m; f += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t u = frontier[f];
+    for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
+      const int32_t v = ci[k];
+      if (pos[v] != -1) continue;
+      if (record) {
+        atomicMin(&pkey[v], int32_t(f));  // every parent, so the level's FIRST parent wins
+      } else if (mark[v] == stamp) {
+        continue;
+      }
+      if (atomicExch(&mark[v], stamp) != stamp) next[atomicAdd(cnt, 1)] = v;
+    }
+  }
+}
+
+__global__ void k_rcm_iota(int64_t n, int32_t* __restrict__ out) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = int32_t(i);
+}
+
+__global__ void k_rcm_keys(int64_t m, const int32_t* __restrict__ ids, const int32_t* __restrict__ pkey,
+                           const int32_t* __restrict__ deg, unsigned long long* __restrict__ keys) {
+  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < m; k += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t v = ids[k];
+    keys[k] = (static_cast<unsigned long long>(unsigned(pkey[v])) << 32) | unsigned(deg[v]);
+  }
+}
+
+__global__ void k_rcm_place(int64_t m, const int32_t* __restrict__ ids, int32_t base, int32_t* __restrict__ pos,
+                            int32_t* __restrict__ order) {
+  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < m; k += int64_t(gridDim.x) * blockDim.x) {
+    pos[ids[k]] = base + int32_t(k);
+    order[base + k] = ids[k];
+  }
+}
+
+__global__ void k_rcm_flags(int64_t n, const uint8_t* __restrict__ iso, uint8_t want, uint8_t* __restrict__ flag) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    flag[i] = iso[i] == want;
+}
+
+// reversal: perm[i'] = order[n - 1 - i'], iperm[perm[i']] = i'
+__global__ void k_rcm_reverse(int64_t n, const int32_t* __restrict__ order, int32_t* __restrict__ perm,
+                              int32_t* __restrict__ iperm) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t o = order[n - 1 - i];
+    perm[i] = o;
+    iperm[o] = int32_t(i);
+  }
+}
+
+__global__ void k_abs_offset_perm(int64_t nb, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                                  const int32_t* __restrict__ iperm, unsigned long long* __restrict__ sum) {
+  unsigned long long acc = 0;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nb; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t ri = iperm[i];
+    for (int32_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+      const int64_t d = int64_t(iperm[colind[k]]) - ri;
+      acc += static_cast<unsigned long long>(d < 0 ? -d : d);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(sum, acc);
+}
+
+namespace {
+struct DevBuf {  // hipMalloc'd scratch freed on scope exit
+  std::vector<void*> p;
+  template <typename T>
+  int get(T** out, size_t count) {
+    void* v = nullptr;
+    LSPCG_HIP(hipMalloc(&v, std::max<size_t>(count, 1) * sizeof(T)));
+    p.push_back(v);
+    *out = static_cast<T*>(v);
+    return LSPCG_OK;
+  }
+  ~DevBuf() {
+    for (void* v : p) (void)hipFree(v);
+  }
+};
+}  // namespace
+
+constexpr int kRcmMaxComponents = 256;
+constexpr int kRcmTooManyComponents = -1;
+
+// perm / iperm (device, nb entries) of the reverse Cuthill-McKee order of A's block graph;
+// kRcmTooManyComponents when the graph has more than kRcmMaxComponents non-trivial components
+static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
+  hipStream_t st = A->ctx->stream;
+  const int64_t n = A->nb;
+  const int32_t *rp = A->rowptr, *ci = A->colind;
+  DevBuf B;
+  int32_t *deg, *pos, *pkey, *mark, *order, *fa, *fb, *ids, *cnt;
+  uint8_t *iso, *flag;
+  unsigned long long *keys, *keys2, *best;
+  if (int rc = B.get(&deg, n) | B.get(&pos, n) | B.get(&pkey, n) | B.get(&mark, n) | B.get(&order, n) |
+               B.get(&fa, n) | B.get(&fb, n) | B.get(&ids, n) | B.get(&cnt, 1) | B.get(&iso, n) | B.get(&flag, n) |
+               B.get(&keys, n) | B.get(&keys2, n) | B.get(&best, 1))
+    return rc;
+  size_t tb = 0, t1 = 0, t2 = 0, t3 = 0;
+  LSPCG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, fa, fb, int(n), 0, 32, st));
+  LSPCG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, keys, keys2, fa, fb, int(n), 0, 64, st));
+  LSPCG_HIP(hipcub::DeviceSelect::Flagged(nullptr, t3, fa, flag, fb, cnt, int(n), st));
+  tb = std::max({t1, t2, t3});
+  void* tmp = nullptr;
+  if (int rc = B.get(reinterpret_cast<uint8_t**>(&tmp), tb)) return rc;
+  const int g = grid_for(n);
+  hipLaunchKernelGGL(k_rcm_init, dim3(g), dim3(kThreads), 0, st, n, rp, ci, deg, iso, pos, pkey, mark);
+  auto read_cnt = [&](int32_t* h) -> int {
+    LSPCG_HIP(hipMemcpyAsync(h, cnt, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    LSPCG_HIP(hipStreamSynchronize(st));
+    return LSPCG_OK;
+  };
+  int32_t placed = 0;
+  // nodes without neighbours other than themselves: empty rows, then self-loop-only rows, by index
+  hipLaunchKernelGGL(k_rcm_iota, dim3(g), dim3(kThreads), 0, st, n, fa);
+  for (uint8_t want : {uint8_t(1), uint8_t(2)}) {
+    hipLaunchKernelGGL(k_rcm_flags, dim3(g), dim3(kThreads), 0, st, n, iso, want, flag);
+    size_t t = tb;
+    LSPCG_HIP(hipcub::DeviceSelect::Flagged(tmp, t, fa, flag, fb, cnt, int(n), st));
+    int32_t m = 0;
+    if (int rc = read_cnt(&m)) return rc;
+    if (m) hipLaunchKernelGGL(k_rcm_place, dim3(grid_for(m)), dim3(kThreads), 0, st, int64_t(m), fb, placed, pos, order);
+    placed += m;
+  }
+  int32_t stamp = 0;
+  int components = 0;
+  while (placed < n) {
+    // one host round trip per BFS level: a graph of many small components is left in its order
+    if (++components > kRcmMaxComponents) return kRcmTooManyComponents;
+    // component start: the (degree, index)-smallest unplaced node
+    const unsigned long long inf = ~0ull;
+    unsigned long long hb = 0;
+    LSPCG_HIP(hipMemcpyAsync(best, &inf, sizeof(inf), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_rcm_argmin, dim3(g), dim3(kThreads), 0, st, n, static_cast<const int32_t*>(nullptr), deg, pos, best);
+    LSPCG_HIP(hipMemcpyAsync(&hb, best, sizeof(hb), hipMemcpyDeviceToHost, st));
+    LSPCG_HIP(hipStreamSynchronize(st));
+    int32_t start = int32_t(hb & 0xffffffffu);
+    // one pseudo-peripheral step: BFS (marks only), then the smallest node of its last level
+    {
+      int32_t* cur = fa;
+      int32_t* nxt = fb;
+      LSPCG_HIP(hipMemcpyAsync(cur, &start, sizeof(int32_t), hipMemcpyHostToDevice, st));
+      const int32_t s0 = ++stamp;
+      LSPCG_HIP(hipMemcpyAsync(mark + start, &s0, sizeof(int32_t), hipMemcpyHostToDevice, st));
+      int32_t m = 1;
+      for (;;) {
+        LSPCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
+        hipLaunchKernelGGL(k_rcm_level, dim3(grid_for(m)), dim3(kThreads), 0, st, int64_t(m), cur, rp, ci, pos, pkey,
+                           mark, s0, nxt, cnt, 0);
+        int32_t mn = 0;
+        if (int rc = read_cnt(&mn)) return rc;
+        if (mn == 0) break;
+        std::swap(cur, nxt);
+        m = mn;
+      }
+      LSPCG_HIP(hipMemcpyAsync(best, &inf, sizeof(inf), hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_rcm_argmin, dim3(grid_for(m)), dim3(kThreads), 0, st, int64_t(m), cur, deg, pos, best);
+      LSPCG_HIP(hipMemcpyAsync(&hb, best, sizeof(hb), hipMemcpyDeviceToHost, st));
+      LSPCG_HIP(hipStreamSynchronize(st));
+      start = int32_t(hb & 0xffffffffu);
+    }
+    // Cuthill-McKee from start, one level at a time
+    LSPCG_HIP(hipMemcpyAsync(fa, &start, sizeof(int32_t), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_rcm_place, dim3(1), dim3(64), 0, st, int64_t(1), fa, placed, pos, order);
+    ++placed;
+    int32_t* cur = fa;
+    int32_t m = 1;
+    for (;;) {
+      const int32_t sl = ++stamp;
+      LSPCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
+      hipLaunchKernelGGL(k_rcm_level, dim3(grid_for(m)), dim3(kThreads), 0, st, int64_t(m), cur, rp, ci, pos, pkey,
+                         mark, sl, ids, cnt, 1);
+      int32_t mn = 0;
+      if (int rc = read_cnt(&mn)) return rc;
+      if (mn == 0) break;
+      int32_t* nxt = cur == fa ? fb : fa;
+      // by index, then stably by (first parent's position, degree)
+      size_t t = tb;
+      LSPCG_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, t, ids, nxt, mn, 0, 32, st));
+      hipLaunchKernelGGL(k_rcm_keys, dim3(grid_for(mn)), dim3(kThreads), 0, st, int64_t(mn), nxt, pkey, deg, keys);
+      t = tb;
+      LSPCG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, t, keys, keys2, nxt, ids, mn, 0, 64, st));
+      hipLaunchKernelGGL(k_rcm_place, dim3(grid_for(mn)), dim3(kThreads), 0, st, int64_t(mn), ids, placed, pos, order);
+      LSPCG_HIP(hipMemcpyAsync(nxt, ids, sizeof(int32_t) * mn, hipMemcpyDeviceToDevice, st));
+      placed += mn;
+      cur = nxt;
+      m = mn;
+    }
+  }
+  hipLaunchKernelGGL(k_rcm_reverse, dim3(g), dim3(kThreads), 0, st, n, order, perm, iperm);
+  LSPCG_HIP(hipGetLastError());
+  LSPCG_HIP(hipStreamSynchronize(st));  // the scratch is freed on return
+  return LSPCG_OK;
 }
 
 int rcm_reorder(const lspcg_mat* A, int mode, Reorder* out, bool* applied) {
@@ -202,29 +379,36 @@ int rcm_reorder(const lspcg_mat* A, int mode, Reorder* out, bool* applied) {
   // |col - row| of order nb^(2/3) / 4; a random one ~ nb / 3); never small systems
   if (mode < 0 && (nb < 16384 || before <= 4.0 * std::cbrt(double(nb) * double(nb)))) return LSPCG_OK;
   hipStream_t st = A->ctx->stream;
-  std::vector<int32_t> rp(nb + 1), ci(A->nnzb);
-  LSPCG_HIP(hipMemcpyAsync(rp.data(), A->rowptr, sizeof(int32_t) * (nb + 1), hipMemcpyDeviceToHost, st));
-  LSPCG_HIP(hipMemcpyAsync(ci.data(), A->colind, sizeof(int32_t) * A->nnzb, hipMemcpyDeviceToHost, st));
-  LSPCG_HIP(hipStreamSynchronize(st));
-  std::vector<int32_t> order;
-  rcm_host(nb, rp, ci, order);
-  std::vector<int32_t> iord(nb);
-  for (int64_t k = 0; k < nb; ++k) iord[order[k]] = int32_t(k);
-  double after = 0;
-  {
-    long double acc = 0;
-    for (int64_t i = 0; i < nb; ++i)
-      for (int32_t k = rp[i]; k < rp[i + 1]; ++k) acc += std::fabs(double(iord[ci[k]]) - double(iord[i]));
-    after = double(acc / (long double)std::max<int64_t>(1, A->nnzb));
-  }
-  out->off_after = after;
-  if (mode < 0 && !(after < 0.5 * before)) return LSPCG_OK;  // RCM would not help this pattern
   LSPCG_HIP(hipMalloc(&out->perm, sizeof(int32_t) * nb));
   LSPCG_HIP(hipMalloc(&out->iperm, sizeof(int32_t) * nb));
   out->nb = nb;
-  LSPCG_HIP(hipMemcpyAsync(out->perm, order.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, st));
-  LSPCG_HIP(hipMemcpyAsync(out->iperm, iord.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, st));
-  LSPCG_HIP(hipStreamSynchronize(st));
+  if (int rc = rcm_device(A, out->perm, out->iperm)) {
+    out->release();
+    out->off_before = before;
+    out->off_after = before;
+    return rc == kRcmTooManyComponents ? LSPCG_OK : rc;
+  }
+  {
+    unsigned long long* d = nullptr;
+    LSPCG_HIP(hipMalloc(&d, sizeof(unsigned long long)));
+    LSPCG_HIP(hipMemsetAsync(d, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_abs_offset_perm, dim3(grid_for(nb)), dim3(kThreads), 0, st, nb, A->rowptr, A->colind,
+                       out->iperm, d);
+    unsigned long long h = 0;
+    const hipError_t e1 = hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, st);
+    const hipError_t e2 = hipStreamSynchronize(st);
+    (void)hipFree(d);
+    LSPCG_HIP(e1);
+    LSPCG_HIP(e2);
+    out->off_after = double(h) / double(A->nnzb);
+  }
+  if (mode < 0 && !(out->off_after < 0.5 * before)) {  // RCM would not help this pattern
+    const double b = out->off_before, a = out->off_after;
+    out->release();
+    out->off_before = b;
+    out->off_after = a;
+    return LSPCG_OK;
+  }
   *applied = true;
   return LSPCG_OK;
 }

@@ -161,3 +161,38 @@ def test_reordered_bsr3_equals_oracle(gpu_ctx, monkeypatch):
     for mode, (it, conv, x, h) in res.items():
         assert conv and it == it_o, (mode, it, it_o)
         assert np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o), mode
+
+
+@pytest.mark.parametrize("kind", ["kuhn27rand", "poisson160rand"])
+def test_device_rcm_quality_matches_scipy(gpu_ctx, monkeypatch, kind):
+    """The device's level-synchronous Cuthill-McKee reaches scipy's reverse_cuthill_mckee bandwidth
+    (mean |col - row| within 15 %; the orders differ only in start-node and tie choices)."""
+    from scipy.sparse.csgraph import reverse_cuthill_mckee
+
+    A, L, _ = _system(kind)
+    monkeypatch.setenv("LSPCG_REORDER", "1")
+    info = _solver(A, L, "none").reorder_info
+    p = reverse_cuthill_mckee(A, symmetric_mode=True)
+    ip = np.empty_like(p)
+    ip[p] = np.arange(p.size)
+    C = A.tocoo()
+    ref = np.abs(ip[C.col].astype(np.int64) - ip[C.row]).mean()
+    assert info["applied"] and info["mean_offset_after"] <= 1.15 * ref, (info, ref)
+
+
+def test_many_components_left_in_order(gpu_ctx, monkeypatch):
+    """A graph of more than 256 non-trivial components is not reordered (one host round trip per BFS
+    level would dominate); the solve still equals the oracle."""
+    rng = np.random.default_rng(5)
+    blocks = [sp.csr_matrix(np.array([[4.0, -1.0], [-1.0, 3.0 + k % 3]])) for k in range(400)]
+    A0 = sp.block_diag(blocks, format="csr")
+    pm = rng.permutation(A0.shape[0])
+    A = sp.csr_matrix(A0[pm][:, pm])
+    A.sort_indices()
+    b = rng.standard_normal(A.shape[0])
+    monkeypatch.setenv("LSPCG_REORDER", "1")
+    s = _solver(A, None, "none")
+    assert not s.reorder_info["applied"]
+    it, conv, x, _ = _run(s, b)
+    it_o, x_o, _ = O.pcg(A, b, None, rtol=1e-8, dot="exact")
+    assert conv and it == it_o and np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
