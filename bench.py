@@ -682,9 +682,15 @@ def main():
     ms_cold = A.spmv_timed(p, q, args.spmv_reps, flush_bytes=FLUSH_BYTES)
     ms_warm = A.spmv_timed(p, q, args.spmv_reps * 3)
     if A.block_size == 3:
-        kernel = (f"k_spmv_bsell3<double,double,int{kind}> BSELL-64 block copy of the fp64 BSR 3x3 A (one {kind}-bit "
-                  "column per block, 16-B value loads), bit-exact scipy bsr_matvec order" if kind else
-                  "k_spmv<double,3> staged BSR 3x3 SpMV of A, bit-exact scipy bsr_matvec order")
+        if kind == 1:
+            kernel = ("k_spmv_bsdia3<double,double> BSELL-DIA block copy of the fp64 BSR 3x3 A (one slot per "
+                      "distinct block offset of the 64-block-row slice, no columns, 16-B value loads), bit-exact "
+                      "scipy bsr_matvec order")
+        elif kind:
+            kernel = (f"k_spmv_bsell3<double,double,int{kind}> BSELL-64 block copy of the fp64 BSR 3x3 A (one "
+                      f"{kind}-bit column per block, 16-B value loads), bit-exact scipy bsr_matvec order")
+        else:
+            kernel = "k_spmv<double,3> staged BSR 3x3 SpMV of A, bit-exact scipy bsr_matvec order"
         alg = bsr3_bytes(n // 3, A.nnzb)
         alg_formula = "(72+4)·nnzb + 4·(N_b+1) + 24·N_b + 24·N_b (SURVEY.md 8(d), BSR b=3)"
     else:

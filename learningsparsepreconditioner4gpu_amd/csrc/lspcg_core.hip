@@ -500,7 +500,8 @@ int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind) {
   hipStream_t st = A->ctx->stream;
   std::unique_ptr<SellCopy> c(new SellCopy());
   const bool blk = A->block_size == 3;  // BSR 3x3: the BSELL-64 block layout
-  int rc = blk ? bsell_build_pattern(A->nb, A->nnzb, A->rowptr, A->colind, sell_max_pad(), true, st, &c->P)
+  int rc = blk ? bsell_build_pattern(A->nb, A->nnzb, A->rowptr, A->colind, sell_max_pad(), true, bsdia_allowed(), st,
+                                     &c->P)
                : sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, sell_max_pad(), kSellCol16 | kSellColDia, st,
                                     &c->P);
   if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // irregular rows: the CSR / BSR kernel stays

@@ -1250,8 +1250,8 @@ static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view) {
   if (shared) {
     P = s->sp[0];
   } else {
-    const int rc = bsell_build_pattern(view->nb, view->nnzb, view->rowptr, view->colind, sell_max_pad(), true, st,
-                                       &s->spat[w]);
+    const int rc = bsell_build_pattern(view->nb, view->nnzb, view->rowptr, view->colind, sell_max_pad(), true,
+                                       s->dia_ok && bsdia_allowed(), st, &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: the staged block kernel
     if (rc) return rc;
     P = &s->spat[w];

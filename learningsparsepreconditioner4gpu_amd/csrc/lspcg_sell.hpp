@@ -419,6 +419,82 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_bsell3(SellArgs<VT, CT> a, Pr
   finish_epi_dots<Epi>(d, epi);
 }
 
+// BSR 3x3 over the BSELL-DIA layout (SELL-DIA's slot dictionary on the block graph + BSELL-64's
+// 9-value lane chunks): one lane = one block row = 3 scalar rows; slot j of the slice holds the
+// block at block column I + dict[j] (mask bit j), so the x entries of a slot are three contiguous
+// 64-block loads at a wave-uniform offset and no column is loaded at all.  SB slots per batch, all
+// value and x loads of a batch issued before the first add; the slot order is the row's block
+// column order, c = 0, 1, 2 inside a block: the expanded scalar CSR's summation order.
+template <typename T, typename VT, int SB, int TH, int MINW, class Pro, class Gx, class Epi>
+__global__ void __launch_bounds__(TH, MINW) k_spmv_bsdia3(SdiaArgs<VT> a, Pro pro, Gx gx, Epi epi) {
+  constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int64_t nb = a.n / 3;
+  const int64_t ntiles = (nb + TH - 1) / TH;
+  int32_t g0 = 0, g1 = 0;
+  unsigned msk = 0;
+  int32_t dct[kSdiaMax];
+  auto meta = [&](int64_t sl) {
+    g0 = a.gp[sl];
+    g1 = a.gp[sl + 1];
+    msk = gld(a.mask + kSellC * sl + lane);
+    const int32_t* dp = a.dict + kSdiaMax * sl;
+#pragma unroll
+    for (int j = 0; j < kSdiaMax; ++j) dct[j] = dp[j];
+  };
+  {
+    const int64_t s = int64_t(blockIdx.x) * (TH / 64) + w;
+    if (int64_t(blockIdx.x) < ntiles && s < a.ns) meta(s);
+  }
+  if (pro.exit()) return;
+  gx.prepare();
+  epi.prepare();
+  DD d[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) d[j] = dd_zero();
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t s = tile * (TH / 64) + w;
+    const int64_t I = tile * TH + threadIdx.x;
+    if (s < a.ns) {  // wave-uniform
+      if (tile != int64_t(blockIdx.x)) meta(s);
+      const int nd = g1 - g0;
+      const int32_t base = int32_t(s * kSellC);
+      const int32_t brow = base + lane;
+      T acc[3] = {T(0), T(0), T(0)};
+#pragma unroll
+      for (int j0 = 0; j0 < kSdiaMax; j0 += SB) {
+        if (j0 >= nd) break;  // wave-uniform
+        VT v[SB][9];
+        T xv[SB][3];
+        bool m[SB];
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+          const int j = j0 + u;
+          m[u] = (j < nd) && ((msk >> j) & 1u);
+          const int64_t c = 3 * int64_t(m[u] ? brow + dct[j] : base);
+          bsell_load_block(a.vals + 576 * int64_t(g0 + min(j, nd - 1)), v[u]);
+#pragma unroll
+          for (int cc = 0; cc < 3; ++cc) xv[u][cc] = gx(c + cc);
+        }
+#pragma unroll
+        for (int u = 0; u < SB; ++u)
+          if (m[u]) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+              for (int cc = 0; cc < 3; ++cc) acc[r] = acc[r] + T(v[u][3 * r + cc]) * xv[u][cc];
+          }
+      }
+      if (I < nb) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) epi.row(3 * I + r, acc[r], d);
+      }
+    }
+  }
+  finish_epi_dots<Epi>(d, epi);
+}
+
 // Reducing launches use a resident grid: 6 workgroups per CU (the compact-value kernels'
 // __launch_bounds__ guarantee), i.e. 1536 on MI355X -- one wave of workgroups, each walking its
 // row tiles, so no straggler round delays the ticket (8 per CU / 2048 measured the same; caps of
@@ -491,13 +567,28 @@ inline void launch_spmv_sdia(const SellPattern& P, const void* vals, Gx gx, Pro 
                      0, st, a, pro, gx, epi);
 }
 
+// BSELL-DIA launch: 256 block rows (4 slices) per row tile, as BSELL-64
+constexpr int kBsdiaSB = 2;  // block slots per batch (18 values, 6 x loads)
+template <typename T, typename VT, class Pro, class Gx, class Epi>
+inline void launch_spmv_bsdia3(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
+                               bool one_tile_per_wg = false) {
+  int64_t grid = (P.nb + kSellWG - 1) / kSellWG;
+  if (!one_tile_per_wg) grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
+  if (grid <= 0) return;
+  SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals)};
+  constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? 1536 / kSellWG : 1;
+  hipLaunchKernelGGL((k_spmv_bsdia3<T, VT, kBsdiaSB, kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)),
+                     dim3(kSellWG), 0, st, a, pro, gx, epi);
+}
+
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
                                  bool one_tile_per_wg = false) {
   if constexpr (std::is_same<VT, uint8_t>::value) {
     return;  // coded views are SELL-DIA only: launch_spmv_sdia with their dictionary
   }
-  if (P.col_bits == 1) launch_spmv_sdia<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
+  if (P.col_bits == 1 && P.bs == 3) launch_spmv_bsdia3<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
+  else if (P.col_bits == 1) launch_spmv_sdia<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else launch_spmv_sell_th<T, VT, int32_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
 }
@@ -530,8 +621,14 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
                      hipStream_t st, void** out);
 // BSELL-64 pattern of a BSR 3x3 (nb block rows, nnzb blocks, sorted block columns); the same
 // padding rule on block slots (64 x groups <= max_pad x nnzb) and 16-bit block-column offsets.
+// allow_dia: BSELL-DIA (col_bits 1) when every slice has <= 16 distinct block offsets and it
+// stores at most 1/16 more block slots than BSELL-64 (env LSPCG_BSDIA=0 turns it off: bsdia_allowed()).
 int bsell_build_pattern(int64_t nb, int64_t nnzb, const int32_t* rowptr, const int32_t* colind, double max_pad,
-                        bool allow16, hipStream_t st, SellPattern* out);
+                        bool allow16, bool allow_dia, hipStream_t st, SellPattern* out);
+inline bool bsdia_allowed() {
+  const char* e = std::getenv("LSPCG_BSDIA");
+  return !(e && e[0] == '0');
+}
 // its block values (16-B lane chunks) from the BSR's [nnzb][3][3] array
 int bsell_fill_values(const SellPattern& P, const void* src, int src_dtype, int dst_dtype, hipStream_t st, void** out);
 // Value dictionary of a SELL-DIA view's fp32 value array: when it holds <= 256 distinct bit

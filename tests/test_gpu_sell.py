@@ -255,13 +255,17 @@ def test_pcg_bsr3_sell_equals_block_kernel(gpu_ctx, precond, monkeypatch):
     assert np.array_equal(out[0][2], out[1][2])
 
 
+@pytest.mark.parametrize("bsdia", ["1", "0"])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("case", ["elast", "elast-zeros", "ragged"])
-def test_prepare_spmv_bsr3_keeps_bits(gpu_ctx, dtype, case):
-    """BSR 3x3 analysis step: the BSELL-64 block copy (one column per block, plane-major values)
-    gives scipy's bsr_matvec bits (per block row: blocks in column order, c = 0, 1, 2 inside)."""
+def test_prepare_spmv_bsr3_keeps_bits(gpu_ctx, monkeypatch, dtype, case, bsdia):
+    """BSR 3x3 analysis step: the BSELL-DIA block copy (a structured mesh: <= 16 block offsets per
+    64-block-row slice, no columns) or the BSELL-64 one (one column per block; LSPCG_BSDIA=0, and the
+    ragged pattern) gives scipy's bsr_matvec bits (per block row: blocks in column order, c = 0, 1, 2
+    inside)."""
     from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
 
+    monkeypatch.setenv("LSPCG_BSDIA", bsdia)
     if case == "ragged":  # block rows of 1..40 blocks, some empty, columns up to the whole range
         rng = np.random.default_rng(4)
         nb = 700
@@ -288,7 +292,10 @@ def test_prepare_spmv_bsr3_keeps_bits(gpu_ctx, dtype, case):
     Ad = DeviceMatrix.from_scipy(B, dtype=dtype, block_size=3)
     y0 = Ad.matvec(torch.from_numpy(x).cuda()).cpu().numpy()  # staged block kernel
     kind = Ad.prepare_spmv()
-    assert kind in (16, 32) if case != "ragged" else kind in (0, 16, 32)
+    if case == "ragged":
+        assert kind in (0, 16, 32)
+    else:
+        assert kind == (1 if bsdia == "1" else 16), kind
     y = Ad.matvec(torch.from_numpy(x).cuda()).cpu().numpy()
     assert np.array_equal(y0, ref) and np.array_equal(y, ref), (case, kind)
 
