@@ -568,7 +568,15 @@ inline void launch_spmv_sdia(const SellPattern& P, const void* vals, Gx gx, Pro 
 }
 
 // BSELL-DIA launch: 256 block rows (4 slices) per row tile, as BSELL-64
-constexpr int kBsdiaSB = 2;  // block slots per batch (18 values, 6 x loads)
+#ifndef LSPCG_BSDIA_SB64
+#define LSPCG_BSDIA_SB64 2
+#endif
+#ifndef LSPCG_BSDIA_SB32
+#define LSPCG_BSDIA_SB32 2
+#endif
+// block slots per batch (2: 18 values, 6 x loads) by value size
+template <typename VT>
+constexpr int bsdia_sb() { return sizeof(VT) == 8 ? LSPCG_BSDIA_SB64 : LSPCG_BSDIA_SB32; }
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_bsdia3(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
                                bool one_tile_per_wg = false) {
@@ -577,7 +585,7 @@ inline void launch_spmv_bsdia3(const SellPattern& P, const void* vals, Gx gx, Pr
   if (grid <= 0) return;
   SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals)};
   constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? 1536 / kSellWG : 1;
-  hipLaunchKernelGGL((k_spmv_bsdia3<T, VT, kBsdiaSB, kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)),
+  hipLaunchKernelGGL((k_spmv_bsdia3<T, VT, bsdia_sb<VT>(), kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)),
                      dim3(kSellWG), 0, st, a, pro, gx, epi);
 }
 

@@ -3,6 +3,7 @@ compiler flags, linked with the in-tree objects of the others (build/lspcg/*.o, 
 build first).  Measurement only: load it with LSPCG_LIB=<path> (tools/gnn_ab.py).
 
     python tools/build_variant.py exp/liblspcg_gs.so lspcg_gnn.hip -DLSPCG_GELU_SCALAR
+    python tools/build_variant.py tools/_variants/libx.so lspcg_pcg.hip,lspcg_core.hip -DX=1  (several units)
 """
 import subprocess
 import sys
@@ -13,16 +14,20 @@ from learningsparsepreconditioner4gpu_amd import _build as B
 
 
 def main():
-    out, src, flags = Path(sys.argv[1]), sys.argv[2], sys.argv[3:]
+    out, srcs, flags = Path(sys.argv[1]), sys.argv[2].split(","), sys.argv[3:]
     B.build(verbose=False)
     out.parent.mkdir(parents=True, exist_ok=True)
-    obj = out.with_suffix(".o")
-    cmd = B._cmd(src, B.tree_hash())
-    cmd = cmd[:-2] + list(flags) + ["-o", str(obj)]
-    subprocess.run(cmd, check=True)
-    objs = [str(obj) if s == src else str(B._obj(s)) for s in B.SOURCES]
+    objs_v = {}
+    for src in srcs:
+        obj = out.with_name(out.stem + "_" + Path(src).stem + ".o")
+        cmd = B._cmd(src, B.tree_hash())
+        cmd = cmd[:-2] + list(flags) + ["-o", str(obj)]
+        subprocess.run(cmd, check=True)
+        objs_v[src] = obj
+    objs = [str(objs_v[s]) if s in objs_v else str(B._obj(s)) for s in B.SOURCES]
     subprocess.run([B.hipcc(), "-shared", f"--offload-arch={B.ARCH}", *objs, "-o", str(out)], check=True)
-    obj.unlink()
+    for obj in objs_v.values():
+        obj.unlink()
     print(out)
 
 
