@@ -94,6 +94,14 @@ int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out);
 int lspcg_mat_diagonal(const lspcg_mat* A, void* d);
 /* A <- A diag(d): column scaling, d device pointer of the matrix dtype, length n */
 int lspcg_mat_scale_columns(lspcg_mat* A, const void* d);
+/* The solver's reordering analysis on its own (DESIGN.md §2 "Reordering"): perm (device int32,
+ * one entry per block row) <- the reverse Cuthill-McKee order of A's block graph, new row i' = old row
+ * perm[i'] (isolated rows -- empty or diagonal-only -- last, each component from a pseudo-peripheral
+ * node, children by (row length, index)); *applied = 0 and perm untouched when the graph is left in
+ * its order (more than 256 non-trivial components, or a row longer than 1024 blocks).  Mean |col -
+ * row| before / after (either pointer may be NULL). */
+int lspcg_mat_rcm(const lspcg_mat* A, int32_t* perm, int* applied, double* mean_offset_before,
+                  double* mean_offset_after);
 
 /* ---- kernels ---- */
 /* y = A x (scipy csr_matvec bit pattern: per-row sequential sum in index order) */

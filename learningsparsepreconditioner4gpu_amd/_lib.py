@@ -46,6 +46,7 @@ SIGNATURES = {
     "lspcg_mat_copy_out": (C.c_int, [vp, vp, vp, vp]),
     "lspcg_mat_transpose": (C.c_int, [vp, pp]),
     "lspcg_mat_diagonal": (C.c_int, [vp, vp]),
+    "lspcg_mat_rcm": (C.c_int, [vp, vp, C.POINTER(C.c_int), p_f64, p_f64]),
     "lspcg_mat_scale_columns": (C.c_int, [vp, vp]),
     "lspcg_spmv": (C.c_int, [vp, vp, vp, vp]),
     "lspcg_spmv_timed": (C.c_int, [vp, vp, vp, vp, C.c_int, C.c_int64, p_f64]),

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdint>
 #include <cmath>
 #include <cstdlib>
 #include <memory>
@@ -123,30 +124,36 @@ int mean_abs_offset(const lspcg_mat* A, double* out) {
 // ---- reverse Cuthill-McKee on the device (level-synchronous) ---------------------------------
 // Sequential Cuthill-McKee appends, while it walks its queue, each node's unvisited neighbours by
 // increasing (degree, index); a node of BFS level L+1 is therefore appended by the FIRST node of
-// level L (in queue order) adjacent to it.  So level L+1's order is the sort of its nodes by
-// (position of that first parent in level L, degree, index) -- computed here one level at a time:
-// the frontier kernel records every unvisited neighbour's smallest parent position (atomicMin) and
-// appends it once to the next level (atomicExch on a per-level stamp), then two stable radix sorts
-// (by index, then by (parent position, degree)) order the level.  Nodes whose only neighbour is
-// themselves (Dirichlet rows) are placed first, in (degree, index) order; every other component
-// starts from its (degree, index)-smallest node, moved once to the (degree, index)-smallest node of
-// its last BFS level (one pseudo-peripheral step).  The whole order is reversed at the end.
+// level L (in queue order) adjacent to it, and level L+1 in order is: for each level-L node f in
+// order, the children it owns (those whose first parent is f) by (degree, index).  Computed one
+// level at a time with no sort and no host round trip: k_rcm_expand records every unvisited
+// neighbour's smallest parent position (atomicMin) and stamps it, k_rcm_count counts each parent's
+// owned children, an exclusive scan gives each parent its output range, and k_rcm_emit writes each
+// parent's children there by (degree, index) -- level sizes and bases stay on the device, and the
+// host reads them back once per kRcmBatch levels.  Nodes whose only neighbour is themselves
+// (Dirichlet rows) are placed first, by index; every other component starts from its (degree,
+// index)-smallest node, moved once to the (degree, index)-smallest node of its last BFS level (one
+// pseudo-peripheral step).  The whole order is reversed at the end.
 __global__ void k_rcm_init(int64_t n, const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
                            int32_t* __restrict__ deg, uint8_t* __restrict__ iso, int32_t* __restrict__ pos,
-                           int32_t* __restrict__ pkey, int32_t* __restrict__ mark) {
+                           int32_t* __restrict__ pkey, int32_t* __restrict__ mark, int32_t* __restrict__ maxdeg) {
+  int32_t md = 0;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     const int32_t b = rp[i], e = rp[i + 1];
     bool only_self = true;
     for (int32_t k = b; k < e; ++k) only_self = only_self && ci[k] == i;
     deg[i] = e - b;
+    md = max(md, e - b);
     iso[i] = only_self ? uint8_t(e - b == 0 ? 1 : 2) : uint8_t(0);  // 1: empty row, 2: self loop only
     pos[i] = -1;
     pkey[i] = INT_MAX;
     mark[i] = -1;
   }
+  for (int o = 32; o > 0; o >>= 1) md = max(md, __shfl_xor(md, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(maxdeg, md);
 }
 
-// the (degree, index)-smallest node with pos == -1 (or, pass >= 0, among list[0..m))
+// the (degree, index)-smallest node with pos == -1 (list == nullptr), or among list[0..m)
 __global__ void k_rcm_argmin(int64_t m, const int32_t* __restrict__ list, const int32_t* __restrict__ deg,
                              const int32_t* __restrict__ pos, unsigned long long* __restrict__ best) {
   unsigned long long b = ~0ull;
@@ -164,23 +171,92 @@ __global__ void k_rcm_argmin(int64_t m, const int32_t* __restrict__ list, const 
   if ((threadIdx.x & 63) == 0 && b != ~0ull) atomicMin(best, b);
 }
 
-// one BFS level: every unvisited (pos == -1) neighbour v of frontier[f] gets pkey[v] = min f and is
-// appended once (mark[v] = stamp) to next; record = false: the pseudo-peripheral BFS (no pkey)
-__global__ void k_rcm_level(int64_t m, const int32_t* __restrict__ frontier, const int32_t* __restrict__ rp,
-                            const int32_t* __restrict__ ci, const int32_t* __restrict__ pos, int32_t* __restrict__ pkey,
-                            int32_t* __restrict__ mark, int32_t stamp, int32_t* __restrict__ next,
-                            int32_t* __restrict__ cnt, int record) {
+// pseudo-peripheral BFS level lv (marks only): the lvm[lv] nodes of `frontier` append their
+// unvisited neighbours (mark != stamp) once to `next`, counted in lvm[lv + 1]
+__global__ void k_rcm_pp_level(int lv, int32_t* __restrict__ lvm, const int32_t* __restrict__ frontier,
+                               const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                               const int32_t* __restrict__ pos, int32_t* __restrict__ mark, int32_t stamp,
+                               int32_t* __restrict__ next) {
+  const int64_t m = lvm[lv];
+  for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < m; f += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t u = frontier[f];
+    for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
+      const int32_t v = ci[k];
+      if (pos[v] != -1 || mark[v] == stamp) continue;
+      if (atomicExch(&mark[v], stamp) != stamp) next[atomicAdd(&lvm[lv + 1], 1)] = v;
+    }
+  }
+}
+
+// Cuthill-McKee level lv, step 1: every unplaced neighbour v of frontier[f] gets pkey[v] = the
+// smallest such f and mark[v] = stamp (the level's stamp)
+__global__ void k_rcm_expand(int lv, const int32_t* __restrict__ lvm, const int32_t* __restrict__ frontier,
+                             const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                             const int32_t* __restrict__ pos, int32_t* __restrict__ pkey, int32_t* __restrict__ mark,
+                             int32_t stamp) {
+  const int64_t m = lvm[lv];
   for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < m; f += int64_t(gridDim.x) * blockDim.x) {
     const int32_t u = frontier[f];
     for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
       const int32_t v = ci[k];
       if (pos[v] != -1) continue;
-      if (record) {
-        atomicMin(&pkey[v], int32_t(f));  // every parent, so the level's FIRST parent wins
-      } else if (mark[v] == stamp) {
-        continue;
+      atomicMin(&pkey[v], int32_t(f));
+      mark[v] = stamp;
+    }
+  }
+}
+
+// step 2: cnt[f] = the children frontier[f] owns (stamped this level, first parent f); 0 past m
+// up to nscan (the scan's length)
+__global__ void k_rcm_count(int lv, const int32_t* __restrict__ lvm, const int32_t* __restrict__ frontier,
+                            const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                            const int32_t* __restrict__ pkey, const int32_t* __restrict__ mark, int32_t stamp,
+                            int64_t nscan, int32_t* __restrict__ cnt) {
+  const int64_t m = lvm[lv];
+  for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < nscan; f += int64_t(gridDim.x) * blockDim.x) {
+    int32_t c = 0;
+    if (f < m) {
+      const int32_t u = frontier[f];
+      for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
+        const int32_t v = ci[k];
+        c += (mark[v] == stamp && pkey[v] == int32_t(f)) ? 1 : 0;
       }
-      if (atomicExch(&mark[v], stamp) != stamp) next[atomicAdd(cnt, 1)] = v;
+    }
+    cnt[f] = c;
+  }
+}
+
+// step 3 (after the exclusive scan off = scan(cnt)): frontier[f] writes its owned children by
+// (degree, index) to next[off[f] ..] and places them at lvbase[lv] + m + off[f] + k; the last
+// parent publishes the next level's size and base
+__global__ void k_rcm_emit(int lv, int32_t* __restrict__ lvm, int32_t* __restrict__ lvbase,
+                           const int32_t* __restrict__ frontier, const int32_t* __restrict__ rp,
+                           const int32_t* __restrict__ ci, const int32_t* __restrict__ deg,
+                           const int32_t* __restrict__ pkey, const int32_t* __restrict__ mark, int32_t stamp,
+                           const int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
+                           int32_t* __restrict__ next, int32_t* __restrict__ pos, int32_t* __restrict__ order) {
+  const int64_t m = lvm[lv];
+  const int32_t base = lvbase[lv] + int32_t(m);
+  for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < m; f += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t u = frontier[f], c = cnt[f], o = off[f];
+    long long last = -1;  // (degree << 32 | index) of the child emitted last
+    for (int32_t j = 0; j < c; ++j) {
+      long long best = LLONG_MAX;
+      for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
+        const int32_t v = ci[k];
+        if (mark[v] != stamp || pkey[v] != int32_t(f)) continue;
+        const long long key = (static_cast<long long>(deg[v]) << 32) | unsigned(v);
+        if (key > last && key < best) best = key;
+      }
+      const int32_t v = int32_t(best & 0xffffffff);
+      next[o + j] = v;
+      pos[v] = base + o + j;
+      order[base + o + j] = v;
+      last = best;
+    }
+    if (f == m - 1) {
+      lvm[lv + 1] = o + c;
+      lvbase[lv + 1] = base;
     }
   }
 }
@@ -188,14 +264,6 @@ __global__ void k_rcm_level(int64_t m, const int32_t* __restrict__ frontier, con
 __global__ void k_rcm_iota(int64_t n, int32_t* __restrict__ out) {
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
     out[i] = int32_t(i);
-}
-
-__global__ void k_rcm_keys(int64_t m, const int32_t* __restrict__ ids, const int32_t* __restrict__ pkey,
-                           const int32_t* __restrict__ deg, unsigned long long* __restrict__ keys) {
-  for (int64_t k = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < m; k += int64_t(gridDim.x) * blockDim.x) {
-    const int32_t v = ids[k];
-    keys[k] = (static_cast<unsigned long long>(unsigned(pkey[v])) << 32) | unsigned(deg[v]);
-  }
 }
 
 __global__ void k_rcm_place(int64_t m, const int32_t* __restrict__ ids, int32_t base, int32_t* __restrict__ pos,
@@ -253,111 +321,130 @@ struct DevBuf {  // hipMalloc'd scratch freed on scope exit
 }  // namespace
 
 constexpr int kRcmMaxComponents = 256;
-constexpr int kRcmTooManyComponents = -1;
+constexpr int kRcmMaxDegree = 1024;  // k_rcm_emit orders a parent's children in O(degree^2)
+constexpr int kRcmBatch = 16;        // BFS levels enqueued per host read-back
+constexpr int kRcmSkip = -1;
 
 // perm / iperm (device, nb entries) of the reverse Cuthill-McKee order of A's block graph;
-// kRcmTooManyComponents when the graph has more than kRcmMaxComponents non-trivial components
+// kRcmSkip (left in its order) for more than kRcmMaxComponents non-trivial components or a row
+// longer than kRcmMaxDegree
 static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
   hipStream_t st = A->ctx->stream;
   const int64_t n = A->nb;
   const int32_t *rp = A->rowptr, *ci = A->colind;
+  // level slots over all components: each uses its levels + 1 empty slot + 1, and a batch may run
+  // kRcmBatch slots past its end
+  const int64_t nlv = n + 2 * kRcmMaxComponents + 2 * kRcmBatch + 4;
   DevBuf B;
-  int32_t *deg, *pos, *pkey, *mark, *order, *fa, *fb, *ids, *cnt;
+  int32_t *deg, *pos, *pkey, *mark, *order, *fa, *fb, *cnt, *off, *lvm, *lvbase, *ppm, *misc;
   uint8_t *iso, *flag;
-  unsigned long long *keys, *keys2, *best;
+  unsigned long long* best;
   if (int rc = B.get(&deg, n) | B.get(&pos, n) | B.get(&pkey, n) | B.get(&mark, n) | B.get(&order, n) |
-               B.get(&fa, n) | B.get(&fb, n) | B.get(&ids, n) | B.get(&cnt, 1) | B.get(&iso, n) | B.get(&flag, n) |
-               B.get(&keys, n) | B.get(&keys2, n) | B.get(&best, 1))
+               B.get(&fa, n) | B.get(&fb, n) | B.get(&cnt, n) | B.get(&off, n) | B.get(&lvm, nlv) |
+               B.get(&lvbase, nlv) | B.get(&ppm, nlv) | B.get(&misc, 2) | B.get(&iso, n) | B.get(&flag, n) |
+               B.get(&best, 1))
     return rc;
-  size_t tb = 0, t1 = 0, t2 = 0, t3 = 0;
-  LSPCG_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, fa, fb, int(n), 0, 32, st));
-  LSPCG_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, keys, keys2, fa, fb, int(n), 0, 64, st));
-  LSPCG_HIP(hipcub::DeviceSelect::Flagged(nullptr, t3, fa, flag, fb, cnt, int(n), st));
-  tb = std::max({t1, t2, t3});
+  size_t t1 = 0, t2 = 0;
+  LSPCG_HIP(hipcub::DeviceSelect::Flagged(nullptr, t1, fa, flag, fb, misc, int(n), st));
+  LSPCG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, cnt, off, int(n), st));
+  const size_t tb = std::max(t1, t2);
   void* tmp = nullptr;
   if (int rc = B.get(reinterpret_cast<uint8_t**>(&tmp), tb)) return rc;
+  LSPCG_HIP(hipMemsetAsync(lvm, 0, sizeof(int32_t) * nlv, st));
+  LSPCG_HIP(hipMemsetAsync(ppm, 0, sizeof(int32_t) * nlv, st));
+  LSPCG_HIP(hipMemsetAsync(misc, 0, sizeof(int32_t) * 2, st));
   const int g = grid_for(n);
-  hipLaunchKernelGGL(k_rcm_init, dim3(g), dim3(kThreads), 0, st, n, rp, ci, deg, iso, pos, pkey, mark);
-  auto read_cnt = [&](int32_t* h) -> int {
-    LSPCG_HIP(hipMemcpyAsync(h, cnt, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    LSPCG_HIP(hipStreamSynchronize(st));
-    return LSPCG_OK;
-  };
+  hipLaunchKernelGGL(k_rcm_init, dim3(g), dim3(kThreads), 0, st, n, rp, ci, deg, iso, pos, pkey, mark, misc + 1);
   int32_t placed = 0;
   // nodes without neighbours other than themselves: empty rows, then self-loop-only rows, by index
   hipLaunchKernelGGL(k_rcm_iota, dim3(g), dim3(kThreads), 0, st, n, fa);
   for (uint8_t want : {uint8_t(1), uint8_t(2)}) {
     hipLaunchKernelGGL(k_rcm_flags, dim3(g), dim3(kThreads), 0, st, n, iso, want, flag);
     size_t t = tb;
-    LSPCG_HIP(hipcub::DeviceSelect::Flagged(tmp, t, fa, flag, fb, cnt, int(n), st));
-    int32_t m = 0;
-    if (int rc = read_cnt(&m)) return rc;
-    if (m) hipLaunchKernelGGL(k_rcm_place, dim3(grid_for(m)), dim3(kThreads), 0, st, int64_t(m), fb, placed, pos, order);
-    placed += m;
+    LSPCG_HIP(hipcub::DeviceSelect::Flagged(tmp, t, fa, flag, fb, misc, int(n), st));
+    int32_t h[2] = {0, 0};
+    LSPCG_HIP(hipMemcpyAsync(h, misc, sizeof(h), hipMemcpyDeviceToHost, st));
+    LSPCG_HIP(hipStreamSynchronize(st));
+    if (h[1] > kRcmMaxDegree) return kRcmSkip;
+    if (h[0]) hipLaunchKernelGGL(k_rcm_place, dim3(grid_for(h[0])), dim3(kThreads), 0, st, int64_t(h[0]), fb, placed, pos, order);
+    placed += h[0];
   }
+  // level-parallel kernels: a resident-sized grid striding over the level (its size is on the device)
+  const int lg = int(std::min<int64_t>(grid_for(n), 1024));
   int32_t stamp = 0;
   int components = 0;
+  int lv = 0, pl = 0;  // next free slots of lvm / lvbase and of ppm
+  std::vector<int32_t> hb(kRcmBatch + 1);
   while (placed < n) {
-    // one host round trip per BFS level: a graph of many small components is left in its order
-    if (++components > kRcmMaxComponents) return kRcmTooManyComponents;
+    if (++components > kRcmMaxComponents) return kRcmSkip;
     // component start: the (degree, index)-smallest unplaced node
     const unsigned long long inf = ~0ull;
-    unsigned long long hb = 0;
+    unsigned long long hbest = 0;
     LSPCG_HIP(hipMemcpyAsync(best, &inf, sizeof(inf), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_rcm_argmin, dim3(g), dim3(kThreads), 0, st, n, static_cast<const int32_t*>(nullptr), deg, pos, best);
-    LSPCG_HIP(hipMemcpyAsync(&hb, best, sizeof(hb), hipMemcpyDeviceToHost, st));
+    LSPCG_HIP(hipMemcpyAsync(&hbest, best, sizeof(hbest), hipMemcpyDeviceToHost, st));
     LSPCG_HIP(hipStreamSynchronize(st));
-    int32_t start = int32_t(hb & 0xffffffffu);
-    // one pseudo-peripheral step: BFS (marks only), then the smallest node of its last level
+    int32_t start = int32_t(hbest & 0xffffffffu);
+    // one pseudo-peripheral step: BFS (marks only), then the smallest node of its last level;
+    // level l's list is in (l even ? fa : fb)
     {
-      int32_t* cur = fa;
-      int32_t* nxt = fb;
-      LSPCG_HIP(hipMemcpyAsync(cur, &start, sizeof(int32_t), hipMemcpyHostToDevice, st));
       const int32_t s0 = ++stamp;
+      const int32_t one = 1;
+      LSPCG_HIP(hipMemcpyAsync(fa, &start, sizeof(int32_t), hipMemcpyHostToDevice, st));
       LSPCG_HIP(hipMemcpyAsync(mark + start, &s0, sizeof(int32_t), hipMemcpyHostToDevice, st));
-      int32_t m = 1;
-      for (;;) {
-        LSPCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
-        hipLaunchKernelGGL(k_rcm_level, dim3(grid_for(m)), dim3(kThreads), 0, st, int64_t(m), cur, rp, ci, pos, pkey,
-                           mark, s0, nxt, cnt, 0);
-        int32_t mn = 0;
-        if (int rc = read_cnt(&mn)) return rc;
-        if (mn == 0) break;
-        std::swap(cur, nxt);
-        m = mn;
+      LSPCG_HIP(hipMemcpyAsync(ppm + pl, &one, sizeof(int32_t), hipMemcpyHostToDevice, st));
+      int l0 = 0, last = -1;
+      while (last < 0) {
+        for (int l = l0; l < l0 + kRcmBatch; ++l)
+          hipLaunchKernelGGL(k_rcm_pp_level, dim3(lg), dim3(kThreads), 0, st, pl + l, ppm, (l & 1) ? fb : fa, rp, ci,
+                             pos, mark, s0, (l & 1) ? fa : fb);
+        LSPCG_HIP(hipMemcpyAsync(hb.data(), ppm + pl + l0, sizeof(int32_t) * (kRcmBatch + 1), hipMemcpyDeviceToHost, st));
+        LSPCG_HIP(hipStreamSynchronize(st));
+        for (int k = 1; k <= kRcmBatch && last < 0; ++k)
+          if (hb[k] == 0) last = l0 + k - 1;
+        l0 += kRcmBatch;
       }
       LSPCG_HIP(hipMemcpyAsync(best, &inf, sizeof(inf), hipMemcpyHostToDevice, st));
-      hipLaunchKernelGGL(k_rcm_argmin, dim3(grid_for(m)), dim3(kThreads), 0, st, int64_t(m), cur, deg, pos, best);
-      LSPCG_HIP(hipMemcpyAsync(&hb, best, sizeof(hb), hipMemcpyDeviceToHost, st));
+      const int32_t mlast = hb[last - (l0 - kRcmBatch)];
+      hipLaunchKernelGGL(k_rcm_argmin, dim3(grid_for(mlast)), dim3(kThreads), 0, st, int64_t(mlast),
+                         (last & 1) ? fb : fa, deg, pos, best);
+      LSPCG_HIP(hipMemcpyAsync(&hbest, best, sizeof(hbest), hipMemcpyDeviceToHost, st));
       LSPCG_HIP(hipStreamSynchronize(st));
-      start = int32_t(hb & 0xffffffffu);
+      start = int32_t(hbest & 0xffffffffu);
+      pl += last + 2;
     }
-    // Cuthill-McKee from start, one level at a time
-    LSPCG_HIP(hipMemcpyAsync(fa, &start, sizeof(int32_t), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_rcm_place, dim3(1), dim3(64), 0, st, int64_t(1), fa, placed, pos, order);
-    ++placed;
-    int32_t* cur = fa;
-    int32_t m = 1;
-    for (;;) {
-      const int32_t sl = ++stamp;
-      LSPCG_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
-      hipLaunchKernelGGL(k_rcm_level, dim3(grid_for(m)), dim3(kThreads), 0, st, int64_t(m), cur, rp, ci, pos, pkey,
-                         mark, sl, ids, cnt, 1);
-      int32_t mn = 0;
-      if (int rc = read_cnt(&mn)) return rc;
-      if (mn == 0) break;
-      int32_t* nxt = cur == fa ? fb : fa;
-      // by index, then stably by (first parent's position, degree)
-      size_t t = tb;
-      LSPCG_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, t, ids, nxt, mn, 0, 32, st));
-      hipLaunchKernelGGL(k_rcm_keys, dim3(grid_for(mn)), dim3(kThreads), 0, st, int64_t(mn), nxt, pkey, deg, keys);
-      t = tb;
-      LSPCG_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, t, keys, keys2, nxt, ids, mn, 0, 64, st));
-      hipLaunchKernelGGL(k_rcm_place, dim3(grid_for(mn)), dim3(kThreads), 0, st, int64_t(mn), ids, placed, pos, order);
-      LSPCG_HIP(hipMemcpyAsync(nxt, ids, sizeof(int32_t) * mn, hipMemcpyDeviceToDevice, st));
-      placed += mn;
-      cur = nxt;
-      m = mn;
+    // Cuthill-McKee from start: level 0 = {start} at position `placed`
+    {
+      const int32_t h0[2] = {1, placed};
+      LSPCG_HIP(hipMemcpyAsync(fa, &start, sizeof(int32_t), hipMemcpyHostToDevice, st));
+      LSPCG_HIP(hipMemcpyAsync(lvm + lv, &h0[0], sizeof(int32_t), hipMemcpyHostToDevice, st));
+      LSPCG_HIP(hipMemcpyAsync(lvbase + lv, &h0[1], sizeof(int32_t), hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_rcm_place, dim3(1), dim3(64), 0, st, int64_t(1), fa, placed, pos, order);
+      int l0 = 0, last = -1;
+      while (last < 0) {
+        for (int l = l0; l < l0 + kRcmBatch; ++l) {
+          const int32_t sl = ++stamp;
+          const int32_t* cur = (l & 1) ? fb : fa;
+          int32_t* nxt = (l & 1) ? fa : fb;
+          hipLaunchKernelGGL(k_rcm_expand, dim3(lg), dim3(kThreads), 0, st, lv + l, lvm, cur, rp, ci, pos, pkey, mark, sl);
+          hipLaunchKernelGGL(k_rcm_count, dim3(g), dim3(kThreads), 0, st, lv + l, lvm, cur, rp, ci, pkey, mark, sl, n, cnt);
+          size_t t = tb;
+          LSPCG_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, t, cnt, off, int(n), st));
+          hipLaunchKernelGGL(k_rcm_emit, dim3(lg), dim3(kThreads), 0, st, lv + l, lvm, lvbase, cur, rp, ci, deg, pkey,
+                             mark, sl, cnt, off, nxt, pos, order);
+        }
+        LSPCG_HIP(hipMemcpyAsync(hb.data(), lvm + lv + l0, sizeof(int32_t) * (kRcmBatch + 1), hipMemcpyDeviceToHost, st));
+        LSPCG_HIP(hipStreamSynchronize(st));
+        for (int k = 1; k <= kRcmBatch && last < 0; ++k)
+          if (hb[k] == 0) last = l0 + k - 1;
+        l0 += kRcmBatch;
+      }
+      // nodes placed by this component: the sum of its level sizes
+      std::vector<int32_t> sizes(last + 1);
+      LSPCG_HIP(hipMemcpyAsync(sizes.data(), lvm + lv, sizeof(int32_t) * (last + 1), hipMemcpyDeviceToHost, st));
+      LSPCG_HIP(hipStreamSynchronize(st));
+      for (int32_t m : sizes) placed += m;
+      lv += last + 2;
     }
   }
   hipLaunchKernelGGL(k_rcm_reverse, dim3(g), dim3(kThreads), 0, st, n, order, perm, iperm);
@@ -386,7 +473,7 @@ int rcm_reorder(const lspcg_mat* A, int mode, Reorder* out, bool* applied) {
     out->release();
     out->off_before = before;
     out->off_after = before;
-    return rc == kRcmTooManyComponents ? LSPCG_OK : rc;
+    return rc == kRcmSkip ? LSPCG_OK : rc;
   }
   {
     unsigned long long* d = nullptr;
@@ -462,3 +549,22 @@ int vec_permute(int dtype, int64_t nb, int bs, const int32_t* perm, const void* 
 }
 
 }  // namespace lspcg
+
+using namespace lspcg;
+
+int lspcg_mat_rcm(const lspcg_mat* A, int32_t* perm, int* applied, double* mean_offset_before,
+                  double* mean_offset_after) {
+  LSPCG_CHECK(A && perm && applied, LSPCG_ERR_ARG, "mat_rcm: NULL argument");
+  Reorder R;
+  bool ap = false;
+  if (int rc = rcm_reorder(A, 1, &R, &ap)) return rc;
+  *applied = ap ? 1 : 0;
+  if (mean_offset_before) *mean_offset_before = R.off_before;
+  if (mean_offset_after) *mean_offset_after = R.off_after;
+  hipError_t e = hipSuccess;
+  if (ap) e = hipMemcpyAsync(perm, R.perm, sizeof(int32_t) * A->nb, hipMemcpyDeviceToDevice, A->ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(A->ctx->stream);
+  R.release();
+  LSPCG_HIP(e);
+  return LSPCG_OK;
+}

@@ -186,6 +186,16 @@ class DeviceMatrix:
         _lib.call("lspcg_trsv", self.handle, int(bool(lower)), _ptr(b), _ptr(x))
         return x
 
+    def rcm(self):
+        """The solver's reordering analysis (lspcg_mat_rcm): (perm | None, mean |col - row| before,
+        after) -- perm[i'] = the old block row placed at i' (reverse Cuthill-McKee), None when the
+        graph is left in its order."""
+        perm = torch.empty(self.n // self.block_size, dtype=torch.int32, device=self.ctx.torch_device)
+        applied = C.c_int(0)
+        before, after = C.c_double(0.0), C.c_double(0.0)
+        _lib.call("lspcg_mat_rcm", self.handle, _ptr(perm), C.byref(applied), C.byref(before), C.byref(after))
+        return (perm if applied.value else None), before.value, after.value
+
     def diagonal(self) -> torch.Tensor:
         d = self.empty_vector()
         _lib.call("lspcg_mat_diagonal", self.handle, _ptr(d))

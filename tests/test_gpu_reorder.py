@@ -196,3 +196,107 @@ def test_many_components_left_in_order(gpu_ctx, monkeypatch):
     it, conv, x, _ = _run(s, b)
     it_o, x_o, _ = O.pcg(A, b, None, rtol=1e-8, dot="exact")
     assert conv and it == it_o and np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
+
+
+def _cuthill_mckee_reference(A):
+    """Sequential restatement of the device analysis (lspcg_reorder.hip rcm_device): rows with no
+    neighbour but themselves first (empty rows, then diagonal-only rows, by index); each remaining
+    component from its (row length, index)-smallest row, moved to the smallest row of the last level
+    of a BFS from there; Cuthill-McKee appending each row's unplaced neighbours by (row length,
+    index); reversed."""
+    A = sp.csr_matrix(A)
+    n, rp, ci = A.shape[0], A.indptr, A.indices
+    deg = np.diff(rp)
+    pos = np.full(n, -1)
+    order = []
+
+    def place(v):
+        pos[v] = len(order)
+        order.append(v)
+
+    only_self = np.array([np.all(ci[rp[i]:rp[i + 1]] == i) for i in range(n)])
+    for want_empty in (True, False):
+        for i in range(n):
+            if only_self[i] and (deg[i] == 0) == want_empty:
+                place(i)
+    key = lambda v: (deg[v], v)
+    while len(order) < n:
+        start = min(np.flatnonzero(pos == -1), key=key)
+        seen, level = {start}, [start]
+        while True:
+            nxt = []
+            for u in level:
+                for v in ci[rp[u]:rp[u + 1]]:
+                    if pos[v] == -1 and v not in seen:
+                        seen.add(v)
+                        nxt.append(v)
+            if not nxt:
+                break
+            level = nxt
+        start = min(level, key=key)
+        place(start)
+        head = len(order) - 1
+        while head < len(order):
+            u = order[head]
+            head += 1
+            for v in sorted({int(v) for v in ci[rp[u]:rp[u + 1]] if pos[v] == -1}, key=key):
+                place(v)
+    return np.asarray(order[::-1], dtype=np.int32)
+
+
+def _rcm_cases():
+    rng = np.random.default_rng(11)
+    A1, _ = P.renumber(*P.kuhn_dirichlet(17), "rand")
+    A2 = sp.csr_matrix(P.renumber(sp.csr_matrix(P.poisson2d_grid(60, 50)[0]), np.ones(3000), "rand")[0])
+    # three components, empty rows and diagonal-only rows, random extra edges
+    R = sp.random(600, 600, density=0.004, random_state=3, format="csr")
+    R = (R + R.T + sp.diags(np.where(np.arange(600) % 7 == 0, 1.0, 0.0))).tocsr()
+    C = sp.csr_matrix(P.kuhn_dirichlet(6)[0])  # 216 rows
+    # random graph (several components) | Kuhn grid | 20 empty rows | 20 diagonal-only rows | 14 empty
+    D = sp.diags(np.r_[np.zeros(20), 2.0 * np.ones(20), np.zeros(14)])
+    B = sp.block_diag([R, C, D], format="csr")
+    B.eliminate_zeros()
+    B.sort_indices()
+    pb = rng.permutation(B.shape[0])
+    B = sp.csr_matrix(B[pb][:, pb])
+    B.sort_indices()
+    return {"kuhn17rand": sp.csr_matrix(A1), "poisson60x50rand": A2, "components": B}
+
+
+@pytest.mark.parametrize("case", ["kuhn17rand", "poisson60x50rand", "components"])
+def test_device_rcm_equals_sequential_cuthill_mckee(gpu_ctx, case):
+    """lspcg_mat_rcm's level-synchronous order (no sort, sizes kept on the device) equals the
+    sequential Cuthill-McKee restatement above, index for index."""
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    A = _rcm_cases()[case]
+    A.sort_indices()
+    Ad = DeviceMatrix.from_scipy(A, dtype=np.float64)
+    perm, before, after = Ad.rcm()
+    assert perm is not None
+    ref = _cuthill_mckee_reference(A)
+    got = perm.cpu().numpy()
+    assert np.array_equal(np.sort(got), np.arange(A.shape[0]))
+    assert np.array_equal(got, ref), (case, np.flatnonzero(got != ref)[:10])
+    ip = np.empty_like(ref)
+    ip[ref] = np.arange(ref.size)
+    C = A.tocoo()
+    assert after == pytest.approx(np.abs(ip[C.col].astype(np.int64) - ip[C.row]).mean(), rel=1e-12)
+
+
+def test_device_rcm_block_graph(gpu_ctx):
+    """BSR 3x3: the analysis runs on the block graph (one entry per block row)."""
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    A0, _, _ = P.elasticity_box(12, 6, 5)
+    nb = A0.shape[0] // 3
+    pb = np.random.default_rng(2).permutation(nb)
+    perm3 = (3 * pb[:, None] + np.arange(3)[None, :]).ravel()
+    A = sp.csr_matrix(sp.csr_matrix(A0)[perm3][:, perm3])
+    A.sort_indices()
+    B = sp.bsr_matrix(A, blocksize=(3, 3))
+    B.sort_indices()
+    Ad = DeviceMatrix.from_scipy(B, dtype=np.float64, block_size=3)
+    perm, _, _ = Ad.rcm()
+    G = sp.csr_matrix((np.ones(B.indices.size), B.indices, B.indptr), shape=(nb, nb))
+    assert np.array_equal(perm.cpu().numpy(), _cuthill_mckee_reference(G))
