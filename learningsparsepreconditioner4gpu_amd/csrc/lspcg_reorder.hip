@@ -22,6 +22,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <climits>
 #include <cstdint>
 #include <cmath>
@@ -128,9 +130,9 @@ int mean_abs_offset(const lspcg_mat* A, double* out) {
 // order, the children it owns (those whose first parent is f) by (degree, index).  Computed one
 // level at a time with no sort and no host round trip: k_rcm_expand records every unvisited
 // neighbour's smallest parent position (atomicMin) and stamps it, k_rcm_count counts each parent's
-// owned children, an exclusive scan gives each parent its output range, and k_rcm_emit writes each
-// parent's children there by (degree, index) -- level sizes and bases stay on the device, and the
-// host reads them back once per kRcmBatch levels.  Nodes whose only neighbour is themselves
+// owned children, k_rcm_emit scans those counts (each parent's output range) and emits each
+// parent's children there by (degree, index) -- level sizes and bases stay on the device (the
+// kernels size their work from them), and the host reads them back once per kRcmBatch levels.  Nodes whose only neighbour is themselves
 // (Dirichlet rows) are placed first, by index; every other component starts from its (degree,
 // index)-smallest node, moved once to the (degree, index)-smallest node of its last BFS level (one
 // pseudo-peripheral step).  The whole order is reversed at the end.
@@ -171,21 +173,64 @@ __global__ void k_rcm_argmin(int64_t m, const int32_t* __restrict__ list, const 
   if ((threadIdx.x & 63) == 0 && b != ~0ull) atomicMin(best, b);
 }
 
-// pseudo-peripheral BFS level lv (marks only): the lvm[lv] nodes of `frontier` append their
-// unvisited neighbours (mark != stamp) once to `next`, counted in lvm[lv + 1]
-__global__ void k_rcm_pp_level(int lv, int32_t* __restrict__ lvm, const int32_t* __restrict__ frontier,
-                               const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
-                               const int32_t* __restrict__ pos, int32_t* __restrict__ mark, int32_t stamp,
-                               int32_t* __restrict__ next) {
-  const int64_t m = lvm[lv];
-  for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < m; f += int64_t(gridDim.x) * blockDim.x) {
-    const int32_t u = frontier[f];
-    for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
-      const int32_t v = ci[k];
-      if (pos[v] != -1 || mark[v] == stamp) continue;
-      if (atomicExch(&mark[v], stamp) != stamp) next[atomicAdd(&lvm[lv + 1], 1)] = v;
-    }
+// A row's neighbours are visited kRcmChunk at a time with every load of a chunk issued before its
+// first use (a node's neighbour loop otherwise makes one dependent memory round trip per neighbour,
+// and a BFS level takes as long as its slowest row).
+constexpr int kRcmChunk = 16;
+struct RowChunk {
+  int32_t v[kRcmChunk];
+  int cnt;
+  __device__ __forceinline__ void load(const int32_t* __restrict__ ci, int32_t k0, int32_t e) {
+    cnt = min(kRcmChunk, e - k0);
+#pragma unroll
+    for (int j = 0; j < kRcmChunk; ++j) v[j] = j < cnt ? ci[k0 + j] : 0;
   }
+  __device__ __forceinline__ void gather(const int32_t* __restrict__ a, int32_t (&out)[kRcmChunk]) const {
+#pragma unroll
+    for (int j = 0; j < kRcmChunk; ++j) out[j] = j < cnt ? a[v[j]] : 0;
+  }
+};
+
+// pseudo-peripheral BFS level l (marks only, no lists): every node marked base + l marks its
+// neighbours not yet reached by this pass (mark < base) base + l + 1 -- plain stores, all of one
+// value, so no atomics -- and raises flag[l + 1]
+__global__ void k_rcm_pp_mark(int64_t n, int32_t base, int l, int32_t* __restrict__ mark,
+                              const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                              int32_t* __restrict__ flag) {
+  for (int64_t u = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; u < n; u += int64_t(gridDim.x) * blockDim.x) {
+    if (mark[u] != base + l) continue;
+    bool any = false;
+    const int32_t e = rp[u + 1];
+    for (int32_t k0 = rp[u]; k0 < e; k0 += kRcmChunk) {
+      RowChunk r;
+      r.load(ci, k0, e);
+      int32_t mk[kRcmChunk];
+      r.gather(mark, mk);
+#pragma unroll
+      for (int j = 0; j < kRcmChunk; ++j)
+        if (j < r.cnt && mk[j] < base) {
+          mark[r.v[j]] = base + l + 1;
+          any = true;
+        }
+    }
+    if (any) flag[l + 1] = 1;
+  }
+}
+
+// the (degree, index)-smallest node marked `value`
+__global__ void k_rcm_argmin_mark(int64_t n, const int32_t* __restrict__ mark, int32_t value,
+                                  const int32_t* __restrict__ deg, unsigned long long* __restrict__ best) {
+  unsigned long long b = ~0ull;
+  for (int64_t v = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; v < n; v += int64_t(gridDim.x) * blockDim.x)
+    if (mark[v] == value) {
+      const unsigned long long key = (static_cast<unsigned long long>(deg[v]) << 32) | unsigned(v);
+      b = key < b ? key : b;
+    }
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long t = __shfl_xor(b, o);
+    b = t < b ? t : b;
+  }
+  if ((threadIdx.x & 63) == 0 && b != ~0ull) atomicMin(best, b);
 }
 
 // Cuthill-McKee level lv, step 1: every unplaced neighbour v of frontier[f] gets pkey[v] = the
@@ -197,49 +242,151 @@ __global__ void k_rcm_expand(int lv, const int32_t* __restrict__ lvm, const int3
   const int64_t m = lvm[lv];
   for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < m; f += int64_t(gridDim.x) * blockDim.x) {
     const int32_t u = frontier[f];
-    for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
-      const int32_t v = ci[k];
-      if (pos[v] != -1) continue;
-      atomicMin(&pkey[v], int32_t(f));
-      mark[v] = stamp;
+    const int32_t e = rp[u + 1];
+    for (int32_t k0 = rp[u]; k0 < e; k0 += kRcmChunk) {
+      RowChunk r;
+      r.load(ci, k0, e);
+      int32_t ps[kRcmChunk];
+      r.gather(pos, ps);
+#pragma unroll
+      for (int j = 0; j < kRcmChunk; ++j)
+        if (j < r.cnt && ps[j] == -1) {
+          atomicMin(&pkey[r.v[j]], int32_t(f));
+          mark[r.v[j]] = stamp;
+        }
     }
   }
 }
 
-// step 2: cnt[f] = the children frontier[f] owns (stamped this level, first parent f); 0 past m
-// up to nscan (the scan's length)
-__global__ void k_rcm_count(int lv, const int32_t* __restrict__ lvm, const int32_t* __restrict__ frontier,
-                            const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
-                            const int32_t* __restrict__ pkey, const int32_t* __restrict__ mark, int32_t stamp,
-                            int64_t nscan, int32_t* __restrict__ cnt) {
-  const int64_t m = lvm[lv];
-  for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < nscan; f += int64_t(gridDim.x) * blockDim.x) {
-    int32_t c = 0;
-    if (f < m) {
-      const int32_t u = frontier[f];
-      for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
-        const int32_t v = ci[k];
-        c += (mark[v] == stamp && pkey[v] == int32_t(f)) ? 1 : 0;
-      }
-    }
+// Steps 2-4 run on kRcmParts workgroups, part b taking parents [b c, (b+1) c), c = ceil(m / parts),
+// so their cost follows the level's size (read on the device), not n.
+constexpr int kRcmParts = 256;
+
+__device__ __forceinline__ void rcm_part(int64_t m, int64_t* lo, int64_t* hi) {
+  const int64_t c = (m + kRcmParts - 1) / kRcmParts;
+  *lo = std::min<int64_t>(m, int64_t(blockIdx.x) * c);
+  *hi = std::min<int64_t>(m, *lo + c);
+}
+
+__device__ __forceinline__ int32_t rcm_owned(int32_t u, int64_t f, const int32_t* __restrict__ rp,
+                                             const int32_t* __restrict__ ci, const int32_t* __restrict__ pkey,
+                                             const int32_t* __restrict__ mark, int32_t stamp) {
+  int32_t c = 0;
+  const int32_t e = rp[u + 1];
+  for (int32_t k0 = rp[u]; k0 < e; k0 += kRcmChunk) {
+    RowChunk r;
+    r.load(ci, k0, e);
+    int32_t mk[kRcmChunk], pk[kRcmChunk];
+    r.gather(mark, mk);
+    r.gather(pkey, pk);
+#pragma unroll
+    for (int j = 0; j < kRcmChunk; ++j) c += (j < r.cnt && mk[j] == stamp && pk[j] == int32_t(f)) ? 1 : 0;
+  }
+  return c;
+}
+
+// 256-thread workgroup sum / exclusive scan through LDS (sh: 256 ints)
+__device__ __forceinline__ int32_t block_excl_scan(int32_t x, int32_t* sh, int32_t* total) {
+  const int t = threadIdx.x;
+  sh[t] = x;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int32_t y = t >= o ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += y;
+    __syncthreads();
+  }
+  const int32_t incl = sh[t];
+  *total = sh[255];
+  __syncthreads();
+  return incl - x;
+}
+
+// step 2: cnt[f] = the children frontier[f] owns (stamped this level, first parent f); psum[b] =
+// the part's total
+__global__ void __launch_bounds__(256) k_rcm_count(int lv, const int32_t* __restrict__ lvm,
+                                                   const int32_t* __restrict__ frontier, const int32_t* __restrict__ rp,
+                                                   const int32_t* __restrict__ ci, const int32_t* __restrict__ pkey,
+                                                   const int32_t* __restrict__ mark, int32_t stamp,
+                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ psum) {
+  __shared__ int32_t sh[256];
+  int64_t lo, hi;
+  rcm_part(lvm[lv], &lo, &hi);
+  int32_t acc = 0;
+  for (int64_t f = lo + threadIdx.x; f < hi; f += 256) {
+    const int32_t c = rcm_owned(frontier[f], f, rp, ci, pkey, mark, stamp);
     cnt[f] = c;
+    acc += c;
   }
+  int32_t total;
+  block_excl_scan(acc, sh, &total);
+  if (threadIdx.x == 0) psum[blockIdx.x] = total;
 }
 
-// step 3 (after the exclusive scan off = scan(cnt)): frontier[f] writes its owned children by
-// (degree, index) to next[off[f] ..] and places them at lvbase[lv] + m + off[f] + k; the last
-// parent publishes the next level's size and base
-__global__ void k_rcm_emit(int lv, int32_t* __restrict__ lvm, int32_t* __restrict__ lvbase,
-                           const int32_t* __restrict__ frontier, const int32_t* __restrict__ rp,
-                           const int32_t* __restrict__ ci, const int32_t* __restrict__ deg,
-                           const int32_t* __restrict__ pkey, const int32_t* __restrict__ mark, int32_t stamp,
-                           const int32_t* __restrict__ cnt, const int32_t* __restrict__ off,
-                           int32_t* __restrict__ next, int32_t* __restrict__ pos, int32_t* __restrict__ order) {
+// step 3: each parent writes its owned children by (degree, index) to next[off ..] and places them
+// at lvbase[lv] + m + off + j, off = the totals of the parts before its own (summed by every
+// workgroup from psum) + the prefix of cnt inside the part; workgroup 0 publishes the next level's
+// size and base
+__global__ void __launch_bounds__(256) k_rcm_emit(int lv, const int32_t* __restrict__ lvm,
+                                                  const int32_t* __restrict__ lvbase, const int32_t* __restrict__ frontier,
+                                                  const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
+                                                  const int32_t* __restrict__ deg, const int32_t* __restrict__ pkey,
+                                                  const int32_t* __restrict__ mark, int32_t stamp,
+                                                  const int32_t* __restrict__ cnt, const int32_t* __restrict__ psum,
+                                                  int32_t* __restrict__ next, int32_t* __restrict__ pos,
+                                                  int32_t* __restrict__ order, int32_t* __restrict__ lvm_next,
+                                                  int32_t* __restrict__ lvbase_next) {
+  __shared__ int32_t sh[256];
   const int64_t m = lvm[lv];
+  int64_t lo, hi;
+  rcm_part(m, &lo, &hi);
   const int32_t base = lvbase[lv] + int32_t(m);
-  for (int64_t f = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; f < m; f += int64_t(gridDim.x) * blockDim.x) {
-    const int32_t u = frontier[f], c = cnt[f], o = off[f];
+  int32_t total;
+  const int32_t before = block_excl_scan(psum[threadIdx.x], sh, &total);  // kRcmParts == blockDim
+  if (blockIdx.x == 0 && threadIdx.x == 0 && m > 0) {
+    *lvm_next = total;
+    *lvbase_next = base;
+  }
+  if (lo >= hi) return;  // workgroup-uniform
+  if (threadIdx.x == blockIdx.x) sh[0] = before;  // this part's offset
+  __syncthreads();
+  int32_t carry = sh[0];
+  __syncthreads();
+  for (int64_t f0 = lo; f0 < hi; f0 += 256) {  // workgroup-uniform
+    const int64_t f = f0 + threadIdx.x;
+    const int32_t c = f < hi ? cnt[f] : 0;
+    int32_t tile;
+    const int32_t o = carry + block_excl_scan(c, sh, &tile);
+    carry += tile;
+    if (f >= hi) continue;
+    const int32_t u = frontier[f];
     long long last = -1;  // (degree << 32 | index) of the child emitted last
+    const int32_t k0 = rp[u], e = rp[u + 1];
+    if (e - k0 <= kRcmChunk) {  // the row's owned children ordered in registers
+      RowChunk r;
+      r.load(ci, k0, e);
+      int32_t mk[kRcmChunk], pk[kRcmChunk], dg[kRcmChunk];
+      r.gather(mark, mk);
+      r.gather(pkey, pk);
+      r.gather(deg, dg);
+      long long key[kRcmChunk];
+#pragma unroll
+      for (int j = 0; j < kRcmChunk; ++j)
+        key[j] = (j < r.cnt && mk[j] == stamp && pk[j] == int32_t(f))
+                     ? (static_cast<long long>(dg[j]) << 32) | unsigned(r.v[j]) : LLONG_MAX;
+      for (int32_t j = 0; j < c; ++j) {
+        long long best = LLONG_MAX;
+#pragma unroll
+        for (int q = 0; q < kRcmChunk; ++q)
+          if (key[q] > last && key[q] < best) best = key[q];
+        const int32_t v = int32_t(best & 0xffffffff);
+        next[o + j] = v;
+        pos[v] = base + o + j;
+        order[base + o + j] = v;
+        last = best;
+      }
+      continue;
+    }
     for (int32_t j = 0; j < c; ++j) {
       long long best = LLONG_MAX;
       for (int32_t k = rp[u]; k < rp[u + 1]; ++k) {
@@ -253,10 +400,6 @@ __global__ void k_rcm_emit(int lv, int32_t* __restrict__ lvm, int32_t* __restric
       pos[v] = base + o + j;
       order[base + o + j] = v;
       last = best;
-    }
-    if (f == m - 1) {
-      lvm[lv + 1] = o + c;
-      lvbase[lv + 1] = base;
     }
   }
 }
@@ -328,26 +471,39 @@ constexpr int kRcmSkip = -1;
 // perm / iperm (device, nb entries) of the reverse Cuthill-McKee order of A's block graph;
 // kRcmSkip (left in its order) for more than kRcmMaxComponents non-trivial components or a row
 // longer than kRcmMaxDegree
+// LSPCG_REORDER_PROFILE=1: phase times of the analysis on stderr (host clock after each sync)
+static bool reorder_profile() {
+  static const bool on = [] {
+    const char* e = std::getenv("LSPCG_REORDER_PROFILE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
   hipStream_t st = A->ctx->stream;
+  const double t_start = now_ms();
+  double t_pp = 0, t_cm = 0;
+  int lv_pp = 0, lv_cm = 0;
   const int64_t n = A->nb;
   const int32_t *rp = A->rowptr, *ci = A->colind;
-  // level slots over all components: each uses its levels + 1 empty slot + 1, and a batch may run
-  // kRcmBatch slots past its end
-  const int64_t nlv = n + 2 * kRcmMaxComponents + 2 * kRcmBatch + 4;
+  // level slots over all components: a component's passes use its levels rounded up to whole
+  // batches + 2, and the last read-back looks kRcmBatch slots further
+  const int64_t nlv = n + int64_t(kRcmMaxComponents) * (kRcmBatch + 2) + 2 * kRcmBatch + 4;
   DevBuf B;
-  int32_t *deg, *pos, *pkey, *mark, *order, *fa, *fb, *cnt, *off, *lvm, *lvbase, *ppm, *misc;
+  int32_t *deg, *pos, *pkey, *mark, *order, *fa, *fb, *cnt, *parts, *lvm, *lvbase, *ppm, *misc;
   uint8_t *iso, *flag;
   unsigned long long* best;
   if (int rc = B.get(&deg, n) | B.get(&pos, n) | B.get(&pkey, n) | B.get(&mark, n) | B.get(&order, n) |
-               B.get(&fa, n) | B.get(&fb, n) | B.get(&cnt, n) | B.get(&off, n) | B.get(&lvm, nlv) |
+               B.get(&fa, n) | B.get(&fb, n) | B.get(&cnt, n) | B.get(&parts, 2 * kRcmParts) | B.get(&lvm, nlv) |
                B.get(&lvbase, nlv) | B.get(&ppm, nlv) | B.get(&misc, 2) | B.get(&iso, n) | B.get(&flag, n) |
                B.get(&best, 1))
     return rc;
-  size_t t1 = 0, t2 = 0;
-  LSPCG_HIP(hipcub::DeviceSelect::Flagged(nullptr, t1, fa, flag, fb, misc, int(n), st));
-  LSPCG_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, cnt, off, int(n), st));
-  const size_t tb = std::max(t1, t2);
+  size_t tb = 0;
+  LSPCG_HIP(hipcub::DeviceSelect::Flagged(nullptr, tb, fa, flag, fb, misc, int(n), st));
   void* tmp = nullptr;
   if (int rc = B.get(reinterpret_cast<uint8_t**>(&tmp), tb)) return rc;
   LSPCG_HIP(hipMemsetAsync(lvm, 0, sizeof(int32_t) * nlv, st));
@@ -385,19 +541,18 @@ static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
     LSPCG_HIP(hipMemcpyAsync(&hbest, best, sizeof(hbest), hipMemcpyDeviceToHost, st));
     LSPCG_HIP(hipStreamSynchronize(st));
     int32_t start = int32_t(hbest & 0xffffffffu);
-    // one pseudo-peripheral step: BFS (marks only), then the smallest node of its last level;
-    // level l's list is in (l even ? fa : fb)
+    const double t0 = now_ms();
+    // one pseudo-peripheral step: BFS from start by marks (level l = mark base + l), then the
+    // smallest node of its last level
     {
-      const int32_t s0 = ++stamp;
+      const int32_t base = stamp + 1;
       const int32_t one = 1;
-      LSPCG_HIP(hipMemcpyAsync(fa, &start, sizeof(int32_t), hipMemcpyHostToDevice, st));
-      LSPCG_HIP(hipMemcpyAsync(mark + start, &s0, sizeof(int32_t), hipMemcpyHostToDevice, st));
+      LSPCG_HIP(hipMemcpyAsync(mark + start, &base, sizeof(int32_t), hipMemcpyHostToDevice, st));
       LSPCG_HIP(hipMemcpyAsync(ppm + pl, &one, sizeof(int32_t), hipMemcpyHostToDevice, st));
       int l0 = 0, last = -1;
       while (last < 0) {
         for (int l = l0; l < l0 + kRcmBatch; ++l)
-          hipLaunchKernelGGL(k_rcm_pp_level, dim3(lg), dim3(kThreads), 0, st, pl + l, ppm, (l & 1) ? fb : fa, rp, ci,
-                             pos, mark, s0, (l & 1) ? fa : fb);
+          hipLaunchKernelGGL(k_rcm_pp_mark, dim3(g), dim3(kThreads), 0, st, n, base, l, mark, rp, ci, ppm + pl);
         LSPCG_HIP(hipMemcpyAsync(hb.data(), ppm + pl + l0, sizeof(int32_t) * (kRcmBatch + 1), hipMemcpyDeviceToHost, st));
         LSPCG_HIP(hipStreamSynchronize(st));
         for (int k = 1; k <= kRcmBatch && last < 0; ++k)
@@ -405,14 +560,15 @@ static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
         l0 += kRcmBatch;
       }
       LSPCG_HIP(hipMemcpyAsync(best, &inf, sizeof(inf), hipMemcpyHostToDevice, st));
-      const int32_t mlast = hb[last - (l0 - kRcmBatch)];
-      hipLaunchKernelGGL(k_rcm_argmin, dim3(grid_for(mlast)), dim3(kThreads), 0, st, int64_t(mlast),
-                         (last & 1) ? fb : fa, deg, pos, best);
+      hipLaunchKernelGGL(k_rcm_argmin_mark, dim3(lg), dim3(kThreads), 0, st, n, mark, base + last, deg, best);
       LSPCG_HIP(hipMemcpyAsync(&hbest, best, sizeof(hbest), hipMemcpyDeviceToHost, st));
       LSPCG_HIP(hipStreamSynchronize(st));
       start = int32_t(hbest & 0xffffffffu);
-      pl += last + 2;
+      stamp = base + last + kRcmBatch + 1;  // past every mark this pass (and its trailing batch) wrote
+      pl += l0 + 2;
+      lv_pp += last + 1;
     }
+    const double t1 = now_ms();
     // Cuthill-McKee from start: level 0 = {start} at position `placed`
     {
       const int32_t h0[2] = {1, placed};
@@ -427,11 +583,10 @@ static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
           const int32_t* cur = (l & 1) ? fb : fa;
           int32_t* nxt = (l & 1) ? fa : fb;
           hipLaunchKernelGGL(k_rcm_expand, dim3(lg), dim3(kThreads), 0, st, lv + l, lvm, cur, rp, ci, pos, pkey, mark, sl);
-          hipLaunchKernelGGL(k_rcm_count, dim3(g), dim3(kThreads), 0, st, lv + l, lvm, cur, rp, ci, pkey, mark, sl, n, cnt);
-          size_t t = tb;
-          LSPCG_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, t, cnt, off, int(n), st));
-          hipLaunchKernelGGL(k_rcm_emit, dim3(lg), dim3(kThreads), 0, st, lv + l, lvm, lvbase, cur, rp, ci, deg, pkey,
-                             mark, sl, cnt, off, nxt, pos, order);
+          hipLaunchKernelGGL(k_rcm_count, dim3(kRcmParts), dim3(256), 0, st, lv + l, lvm, cur, rp, ci, pkey, mark, sl,
+                             cnt, parts);
+          hipLaunchKernelGGL(k_rcm_emit, dim3(kRcmParts), dim3(256), 0, st, lv + l, lvm, lvbase, cur, rp, ci, deg, pkey,
+                             mark, sl, cnt, parts, nxt, pos, order, lvm + lv + l + 1, lvbase + lv + l + 1);
         }
         LSPCG_HIP(hipMemcpyAsync(hb.data(), lvm + lv + l0, sizeof(int32_t) * (kRcmBatch + 1), hipMemcpyDeviceToHost, st));
         LSPCG_HIP(hipStreamSynchronize(st));
@@ -445,11 +600,18 @@ static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
       LSPCG_HIP(hipStreamSynchronize(st));
       for (int32_t m : sizes) placed += m;
       lv += last + 2;
+      lv_cm += last + 1;
     }
+    t_pp += t1 - t0;
+    t_cm += now_ms() - t1;
   }
   hipLaunchKernelGGL(k_rcm_reverse, dim3(g), dim3(kThreads), 0, st, n, order, perm, iperm);
   LSPCG_HIP(hipGetLastError());
   LSPCG_HIP(hipStreamSynchronize(st));  // the scratch is freed on return
+  if (reorder_profile())
+    std::fprintf(stderr, "[lspcg reorder] rcm n=%lld components=%d: %.2f ms (pseudo-peripheral %.2f ms / %d levels, "
+                 "Cuthill-McKee %.2f ms / %d levels)\n", static_cast<long long>(n), components, now_ms() - t_start,
+                 t_pp, lv_pp, t_cm, lv_cm);
   return LSPCG_OK;
 }
 
