@@ -260,10 +260,18 @@ def _rcm_cases():
     pb = rng.permutation(B.shape[0])
     B = sp.csr_matrix(B[pb][:, pb])
     B.sort_indices()
-    return {"kuhn17rand": sp.csr_matrix(A1), "poisson60x50rand": A2, "components": B}
+    # unsymmetric pattern with rows of 1..60 entries (the 16-entry register path and the long-row path)
+    rows, cols = [], []
+    for i in range(1500):
+        k = int(rng.integers(1, 60)) if i % 9 == 0 else int(rng.integers(1, 8))
+        rows += [i] * k
+        cols += list(rng.choice(1500, size=k, replace=False))
+    U = sp.csr_matrix((np.ones(len(rows)), (rows, cols)), shape=(1500, 1500))
+    U.sum_duplicates()
+    return {"kuhn17rand": sp.csr_matrix(A1), "poisson60x50rand": A2, "components": B, "unsym-long-rows": U}
 
 
-@pytest.mark.parametrize("case", ["kuhn17rand", "poisson60x50rand", "components"])
+@pytest.mark.parametrize("case", ["kuhn17rand", "poisson60x50rand", "components", "unsym-long-rows"])
 def test_device_rcm_equals_sequential_cuthill_mckee(gpu_ctx, case):
     """lspcg_mat_rcm's level-synchronous order (no sort, sizes kept on the device) equals the
     sequential Cuthill-McKee restatement above, index for index."""
