@@ -192,11 +192,12 @@ struct RowChunk {
 };
 
 // pseudo-peripheral BFS level l (marks only, no lists): every node marked base + l marks its
-// neighbours not yet reached by this pass (mark < base) base + l + 1 -- plain stores, all of one
-// value, so no atomics -- and raises flag[l + 1]
+// unplaced neighbours not yet reached by this pass (mark < base) base + l + 1 -- plain stores, all
+// of one value, so no atomics -- and raises flag[l + 1].  (Placed nodes are skipped: a directed
+// pattern can reach rows an earlier component placed.)
 __global__ void k_rcm_pp_mark(int64_t n, int32_t base, int l, int32_t* __restrict__ mark,
-                              const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
-                              int32_t* __restrict__ flag) {
+                              const int32_t* __restrict__ pos, const int32_t* __restrict__ rp,
+                              const int32_t* __restrict__ ci, int32_t* __restrict__ flag) {
   for (int64_t u = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; u < n; u += int64_t(gridDim.x) * blockDim.x) {
     if (mark[u] != base + l) continue;
     bool any = false;
@@ -204,11 +205,12 @@ __global__ void k_rcm_pp_mark(int64_t n, int32_t base, int l, int32_t* __restric
     for (int32_t k0 = rp[u]; k0 < e; k0 += kRcmChunk) {
       RowChunk r;
       r.load(ci, k0, e);
-      int32_t mk[kRcmChunk];
+      int32_t mk[kRcmChunk], ps[kRcmChunk];
       r.gather(mark, mk);
+      r.gather(pos, ps);
 #pragma unroll
       for (int j = 0; j < kRcmChunk; ++j)
-        if (j < r.cnt && mk[j] < base) {
+        if (j < r.cnt && mk[j] < base && ps[j] == -1) {
           mark[r.v[j]] = base + l + 1;
           any = true;
         }
@@ -552,7 +554,7 @@ static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
       int l0 = 0, last = -1;
       while (last < 0) {
         for (int l = l0; l < l0 + kRcmBatch; ++l)
-          hipLaunchKernelGGL(k_rcm_pp_mark, dim3(g), dim3(kThreads), 0, st, n, base, l, mark, rp, ci, ppm + pl);
+          hipLaunchKernelGGL(k_rcm_pp_mark, dim3(g), dim3(kThreads), 0, st, n, base, l, mark, pos, rp, ci, ppm + pl);
         LSPCG_HIP(hipMemcpyAsync(hb.data(), ppm + pl + l0, sizeof(int32_t) * (kRcmBatch + 1), hipMemcpyDeviceToHost, st));
         LSPCG_HIP(hipStreamSynchronize(st));
         for (int k = 1; k <= kRcmBatch && last < 0; ++k)
