@@ -1933,11 +1933,14 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
     ++npend;
     return LSPCG_OK;
   };
+  int64_t launched = 0, nlaunch = 0;  // iterations / graphs enqueued (LSPCG_SOLVE_PROFILE)
   auto launch = [&](int c) -> int {
     hipGraphExec_t ex = nullptr;
     int r = get_graph(s, c, &ex);
     if (r) return r;
     LSPCG_HIP(hipGraphLaunch(ex, st));
+    launched += c;
+    ++nlaunch;
     for (int j = 0; j < npend; ++j) queued[(head + j) & 1] += c;
     return post();
   };
@@ -2030,6 +2033,14 @@ int lspcg_solver_solve(lspcg_solver* s, const void* b, void* x, double rtol, int
   float ms = 0.f;
   LSPCG_HIP(hipEventElapsedTime(&ms, s->ev_t0, s->ev_t1));
   if (t_solve_ms) *t_solve_ms = ms;
+  static const bool prof = [] {
+    const char* e = std::getenv("LSPCG_SOLVE_PROFILE");
+    return e && e[0] == '1';
+  }();
+  if (prof)
+    std::fprintf(stderr, "[lspcg solve] n=%lld iters=%lld launched=%lld in %lld graphs, %.3f ms\n",
+                 static_cast<long long>(n), static_cast<long long>(it), static_cast<long long>(launched),
+                 static_cast<long long>(nlaunch), double(ms));
   *iters = it;
   if (res_hist) {
     std::memcpy(res_hist, s->hhist, sizeof(double) * hcnt);
