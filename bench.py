@@ -814,7 +814,7 @@ def main():
                 "achieved_warm": gbs_warm,
                 "csr_staged_ms_cold": csr_cold, "csr_staged_ms_warm": csr_warm,
                 "csr_staged_achieved": alg / (csr_cold * 1e-3) / 1e9,
-                "method": "HIP events on the ctx stream; cold = a 512 MiB read before every launch, launch time = (R x (flush+SpMV) - R x flush)/R",
+                "method": "cold = a 512 MiB read before every launch; launch time = the SpMV kernel's own start/end stamps (hipExtLaunchKernelGGL events on the ctx stream, the duration rocprofv3's kernel trace reports), averaged over the launches",
             },
             "pcg_loop_spmv": pcg_spmv,
             "solver_views": views,

@@ -9,6 +9,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -58,6 +59,27 @@ std::mutex& submit_mutex();
 // ---------------------------------------------------------------------------
 // Launch geometry
 // ---------------------------------------------------------------------------
+// One-shot kernel timing for the standalone SpMV measurement (spmv_timed_impl): while set, the next
+// SpMV launch of this host thread goes through hipExtLaunchKernelGGL with these events, which the
+// runtime stamps at that kernel's own start and end -- the duration rocprofv3's kernel trace
+// reports, without the in-stream kernel boundaries an event pair around the launch would add.
+struct KernelTimer {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+inline KernelTimer*& kernel_timer() {
+  thread_local KernelTimer* t = nullptr;
+  return t;
+}
+#define LSPCG_LAUNCH_SPMV(kernel, grid, block, shmem, stream, ...)                                      \
+  do {                                                                                                   \
+    if (::lspcg::KernelTimer* kt_ = ::lspcg::kernel_timer()) {                                           \
+      ::lspcg::kernel_timer() = nullptr;                                                                 \
+      hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, kt_->start, kt_->stop, 0, __VA_ARGS__);  \
+    } else {                                                                                             \
+      hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                               \
+    }                                                                                                    \
+  } while (0)
+
 constexpr int kThreads = 256;       // 4 wave64 per workgroup
 constexpr int kElemBlocksMax = 2048;  // grid cap for streaming elementwise kernels
 // grid_reduce_dd ticket buffer: [top | group 0 | group 1 | ...], one 128-B line each

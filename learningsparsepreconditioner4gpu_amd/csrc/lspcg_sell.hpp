@@ -542,7 +542,7 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
   if constexpr (!std::is_same<CT, uint16_t>::value) {  // BSELL-64 has no dictionary columns
     if (P.bs == 3) {
       // 2 block slots (18 values, 6 gathers) per batch
-      hipLaunchKernelGGL((k_spmv_bsell3<T, VT, CT, 2, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st,
+      LSPCG_LAUNCH_SPMV((k_spmv_bsell3<T, VT, CT, 2, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st,
                          a, pro, gx, epi);
       return;
     }
@@ -550,7 +550,7 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
   // 2 groups of 4 entries per batch (tools/sell_sweep.py on kuhn101, dictionary columns, cold:
   // fp64 values 32.2 us vs 33.8 with 4 groups and 46.0 with 8; fp32 values 22.7 vs 24.1 / 37.0)
   constexpr int QB = 2;
-  hipLaunchKernelGGL((k_spmv_sell<T, VT, CT, QB, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a,
+  LSPCG_LAUNCH_SPMV((k_spmv_sell<T, VT, CT, QB, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st, a,
                      pro, gx, epi);
 }
 
@@ -563,7 +563,7 @@ inline void launch_spmv_sdia(const SellPattern& P, const void* vals, Gx gx, Pro 
   if (grid <= 0) return;
   SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals), lut};
   constexpr int MINW = (sizeof(VT) <= 4 && std::is_same<Gx, GatherVec<T>>::value) ? 1536 / kSellWG : 1;
-  hipLaunchKernelGGL((k_spmv_sdia<T, VT, kSdiaSB, kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
+  LSPCG_LAUNCH_SPMV((k_spmv_sdia<T, VT, kSdiaSB, kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
                      0, st, a, pro, gx, epi);
 }
 
@@ -585,7 +585,7 @@ inline void launch_spmv_bsdia3(const SellPattern& P, const void* vals, Gx gx, Pr
   if (grid <= 0) return;
   SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals)};
   constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? 1536 / kSellWG : 1;
-  hipLaunchKernelGGL((k_spmv_bsdia3<T, VT, bsdia_sb<VT>(), kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)),
+  LSPCG_LAUNCH_SPMV((k_spmv_bsdia3<T, VT, bsdia_sb<VT>(), kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)),
                      dim3(kSellWG), 0, st, a, pro, gx, epi);
 }
 

@@ -311,7 +311,7 @@ inline void launch_spmv_cfg(const lspcg_mat* A, Gx gx, Pro pro, Epi epi, hipStre
   if (XCD) grid = std::min<int64_t>(((grid + 7) / 8) * 8, cap);
   else if (Epi::NDOT > 0 && grid > cap) grid = cap;
   if (grid > 0)
-    hipLaunchKernelGGL((k_spmv<T, VT, BS, THREADS, GPT, NT, Pro, Gx, Epi, LANEC, XCD>), dim3(unsigned(grid)),
+    LSPCG_LAUNCH_SPMV((k_spmv<T, VT, BS, THREADS, GPT, NT, Pro, Gx, Epi, LANEC, XCD>), dim3(unsigned(grid)),
                        dim3(THREADS), 0, st, a, pro, gx, epi);
 }
 
