@@ -1124,8 +1124,8 @@ struct lspcg_solver {
   int split_mode = -1;  // -1 auto (by grid size), 1 groups, 2 no groups (LSPCG_SPLIT_REDUCE)
   double* groups = nullptr;  // [GZ: <= 4096 x 2 dots x DD | GQ: <= 4096 x DD]
   int gsz_l = 1, ng_l = 1, gsz_a = 1, ng_a = 1;  // group size / count of the KB and KC launches
-  hipEvent_t* tev = nullptr;  // lspcg_solver_time_kernels: an event recorded after every launch
-  int tev_i = 0;
+  KernelTimer* tk = nullptr;  // lspcg_solver_time_kernels: start / end stamps armed for each launch
+  int tk_i = 0;
   PcgState* S = nullptr;
   PcgState* hS = nullptr;  // pinned host mirrors [2] (poll slots)
   double* partials = nullptr;
@@ -1353,8 +1353,9 @@ static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const
 }
 
 // lspcg_solver_time_kernels only: record the next timing event behind the launch just enqueued
-static void mark(lspcg_solver* s, hipStream_t st) {
-  if (s->tev) (void)hipEventRecord(s->tev[s->tev_i++], st);
+// lspcg_solver_time_kernels: the next launch is stamped with its own start / end events
+static void arm(lspcg_solver* s) {
+  if (s->tk) kernel_timer() = &s->tk[s->tk_i++];
 }
 
 template <typename T, bool SC>
@@ -1371,23 +1372,24 @@ static int enqueue_iteration_split(lspcg_solver* s, hipStream_t st) {
   double* gz = s->groups;
   double* gq = s->groups + 4096 * 2 * 2;
   const int eg = elem_vec_grid<T>(n);
+  arm(s);
   int rc = launch_it<T>(s, 2, static_cast<const T*>(r), ProDone{S}, EpiT<T, SC>{t, d}, st);
   if (rc) return rc;
-  mark(s, st);
+  arm(s);
   rc = launch_it<T>(s, 1, static_cast<const T*>(t), ProDone{S},
                     EpiZG<T, SC>{z, r, d, T(s->eps), s->partials, s->ticket, gz, s->gsz_l}, st);
   if (rc) return rc;
-  mark(s, st);
-  hipLaunchKernelGGL(k_update_p_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
-                     static_cast<const T*>(z), p, x);
-  mark(s, st);
+  arm(s);
+  LSPCG_LAUNCH_SPMV(k_update_p_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_l,
+                    static_cast<const T*>(z), p, x);
+  arm(s);
   rc = launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQG<T>{q, p, s->partials, s->ticket, gq, s->gsz_a},
                     st);
   if (rc) return rc;
-  mark(s, st);
-  hipLaunchKernelGGL(k_update_r_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gq), s->ng_a,
-                     static_cast<const T*>(q), r);
-  mark(s, st);
+  arm(s);
+  LSPCG_LAUNCH_SPMV(k_update_r_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gq), s->ng_a,
+                    static_cast<const T*>(q), r);
+  kernel_timer() = nullptr;
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }
@@ -2102,25 +2104,33 @@ int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, dou
   LSPCG_HIP(hipMemcpyAsync(s->S, s->hS, sizeof(PcgState), hipMemcpyHostToDevice, st));
   int rc = s->dtype == LSPCG_F64 ? enqueue_init<double>(s, st) : enqueue_init<float>(s, st);
   if (rc) return rc;
+  // each launch timed by its own start / end stamps (KernelTimer: the kernel durations rocprofv3's
+  // trace reports, without the in-stream boundaries event pairs between launches would add)
   constexpr int K = 5;
-  hipEvent_t ev[K + 1];
-  for (auto& e : ev) LSPCG_HIP(hipEventCreate(&e));
+  KernelTimer kt[K];
+  for (auto& t : kt) {
+    LSPCG_HIP(hipEventCreate(&t.start));
+    LSPCG_HIP(hipEventCreate(&t.stop));
+  }
   double acc[K] = {0, 0, 0, 0, 0};
   for (int64_t it = 0; it < iters && rc == LSPCG_OK; ++it) {
-    LSPCG_HIP(hipEventRecord(ev[0], st));
-    s->tev = ev;
-    s->tev_i = 1;
+    s->tk = kt;
+    s->tk_i = 0;
     rc = s->dtype == LSPCG_F64 ? enqueue_iteration<double>(s, st) : enqueue_iteration<float>(s, st);
-    s->tev = nullptr;
+    s->tk = nullptr;
+    kernel_timer() = nullptr;
     if (rc) break;
-    LSPCG_HIP(hipEventSynchronize(ev[K]));
+    LSPCG_HIP(hipEventSynchronize(kt[K - 1].stop));
     for (int k = 0; k < K; ++k) {
       float ms = 0.f;
-      LSPCG_HIP(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      LSPCG_HIP(hipEventElapsedTime(&ms, kt[k].start, kt[k].stop));
       acc[k] += ms;
     }
   }
-  for (auto& e : ev) (void)hipEventDestroy(e);
+  for (auto& t : kt) {
+    (void)hipEventDestroy(t.start);
+    (void)hipEventDestroy(t.stop);
+  }
   if (rc) return rc;
   for (int k = 0; k < K; ++k) kernel_ms[k] = acc[k] / double(iters);
   *nk = K;
