@@ -98,7 +98,8 @@ int lspcg_mat_scale_columns(lspcg_mat* A, const void* d);
  * one entry per block row) <- the reverse Cuthill-McKee order of A's block graph, new row i' = old row
  * perm[i'] (isolated rows -- empty or diagonal-only -- last, each component from a pseudo-peripheral
  * node, children by (row length, index)); *applied = 0 and perm untouched when the graph is left in
- * its order (more than 256 non-trivial components, or a row longer than 1024 blocks).  Mean |col -
+ * its order (more than 256 non-trivial components, a row longer than 1024 blocks, or a row whose
+ * columns are not strictly increasing).  Mean |col -
  * row| before / after (either pointer may be NULL). */
 int lspcg_mat_rcm(const lspcg_mat* A, int32_t* perm, int* applied, double* mean_offset_before,
                   double* mean_offset_after);

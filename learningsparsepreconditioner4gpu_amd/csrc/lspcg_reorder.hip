@@ -142,10 +142,15 @@ __global__ void k_rcm_init(int64_t n, const int32_t* __restrict__ rp, const int3
   int32_t md = 0;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     const int32_t b = rp[i], e = rp[i + 1];
-    bool only_self = true;
-    for (int32_t k = b; k < e; ++k) only_self = only_self && ci[k] == i;
+    bool only_self = true, sorted = true;
+    for (int32_t k = b; k < e; ++k) {
+      only_self = only_self && ci[k] == i;
+      sorted = sorted && (k == b || ci[k] > ci[k - 1]);
+    }
     deg[i] = e - b;
-    md = max(md, e - b);
+    // a row with an unsorted or repeated column would count a child twice: report it as an
+    // over-long row, which leaves the matrix in its order
+    md = max(md, sorted ? e - b : INT_MAX);
     iso[i] = only_self ? uint8_t(e - b == 0 ? 1 : 2) : uint8_t(0);  // 1: empty row, 2: self loop only
     pos[i] = -1;
     pkey[i] = INT_MAX;
@@ -471,8 +476,8 @@ constexpr int kRcmBatch = 16;        // BFS levels enqueued per host read-back
 constexpr int kRcmSkip = -1;
 
 // perm / iperm (device, nb entries) of the reverse Cuthill-McKee order of A's block graph;
-// kRcmSkip (left in its order) for more than kRcmMaxComponents non-trivial components or a row
-// longer than kRcmMaxDegree
+// kRcmSkip (left in its order) for more than kRcmMaxComponents non-trivial components, a row
+// longer than kRcmMaxDegree, or a row whose columns are not strictly increasing
 // LSPCG_REORDER_PROFILE=1: phase times of the analysis on stderr (host clock after each sync)
 static bool reorder_profile() {
   static const bool on = [] {

@@ -308,3 +308,24 @@ def test_device_rcm_block_graph(gpu_ctx):
     perm, _, _ = Ad.rcm()
     G = sp.csr_matrix((np.ones(B.indices.size), B.indices, B.indptr), shape=(nb, nb))
     assert np.array_equal(perm.cpu().numpy(), _cuthill_mckee_reference(G))
+
+
+def test_device_rcm_leaves_unsorted_or_repeated_rows_in_order(gpu_ctx):
+    """A row whose columns are not strictly increasing (unsorted or repeated: a CSR uploaded with
+    keep_order) would count a child twice; the analysis leaves such a matrix in its order."""
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    A = sp.csr_matrix(_rcm_cases()["kuhn17rand"])
+    A.sort_indices()
+    for how in ("unsorted", "repeated"):
+        B = A.copy()
+        r = 100
+        a, b = B.indptr[r], B.indptr[r + 1]
+        if how == "unsorted":
+            B.indices[a:b] = B.indices[a:b][::-1].copy()
+        else:
+            B.indices[a + 1] = B.indices[a]
+        B.has_sorted_indices = False
+        Bd = DeviceMatrix.from_scipy(B, dtype=np.float64, keep_order=True)
+        perm, before, after = Bd.rcm()
+        assert perm is None and after == before, how
