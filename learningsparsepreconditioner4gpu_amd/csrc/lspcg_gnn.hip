@@ -296,8 +296,10 @@ __device__ __forceinline__ void ff2_48(const float* fa, const float* fb, const f
     split4(va, xah, xal);
     split4(vb, xbh, xbl);
   }
-  oa = layer16h(fa, kH48W3h, kH48W3l, kH48C3, us[2], xah, xal, lane);
-  ob = layer16h(fb, kH48W3h, kH48W3l, kH48C3, us[5], xbh, xbl, lane);
+  // the last layer's accumulators are returned as they stand (2^s3 times the outputs): the
+  // caller folds the unscale into the message aggregation / the edge residual's FMA
+  oa = layer16h(fa, kH48W3h, kH48W3l, kH48C3, 1.0f, xah, xal, lane);
+  ob = layer16h(fb, kH48W3h, kH48W3l, kH48C3, 1.0f, xbh, xbl, lane);
 }
 
 // FeedForward(16 -> 16 -> 16 -> 16) (the node MLP) on split operands: block [W1 hi | W1 lo | C1 | W2 hi |
@@ -818,9 +820,17 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
         v[2 * j + 1] = w[j].y;
       }
       f4 m, u;
-      if constexpr (F32) ff2_48(fmsg, fedge, v, lane, m, u);
-      else ff2_48(fmsg, fedge, v, lane, m, u, us);
-      if (edge_res) u += ea;
+      if constexpr (F32) {
+        ff2_48(fmsg, fedge, v, lane, m, u);
+        if (edge_res) u += ea;
+      } else {
+        // m stays 2^s3 times the message (unscaled once per node after the sum: power-of-two
+        // scaling commutes with every rounding of the sum, so the same bits); the edge output's
+        // unscale is exact, so unscale + residual is one FMA with the same result
+        ff2_48(fmsg, fedge, v, lane, m, u, us);
+        if (edge_res) u = __builtin_elementwise_fma(u, (f4)(us[5]), ea);
+        else u *= us[5];
+      }
       if (valid) {
         st4(e + int64_t(k) * H + 4 * q, u);
         st4(msg + (k - c0) * H + 4 * q, m);
@@ -842,7 +852,7 @@ __global__ void __launch_bounds__(256, 4) k_mp_layer(int64_t N, const float* __r
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int i = n0 + (wave + 4 * j) * 16 + it;
-    const f4 a = agg[j];
+    const f4 a = F32 ? agg[j] : agg[j] * us[2];  // split-f16: the messages were summed 2^s3-scaled
     const float mean = quad_sum((a.x + a.y) + (a.z + a.w)) * (1.0f / 16.0f);
     float v[4] = {a.x - mean, a.y - mean, a.z - mean, a.w - mean};
     const float sq = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
