@@ -136,6 +136,62 @@ void launch_clu(const SellPattern& P, const void* vals, const double* x, double*
                      static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals), x, y);
 }
 
+// Experiment (round 5): each wave takes NS consecutive slices, loading all their metadata at once and
+// then every value / vector load of all NS slices before the first add -- one metadata round trip and
+// one data round trip per NS slices (the product kernel's one-tile workgroups pay both per slice).
+template <typename VT, int NS, int MINW>
+__global__ void __launch_bounds__(256, MINW) k_sdia_multi(int64_t n, int64_t ns, const int32_t* __restrict__ gp,
+                                                          const uint16_t* __restrict__ mask,
+                                                          const int32_t* __restrict__ dict, const VT* __restrict__ vals,
+                                                          const double* __restrict__ x, double* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int64_t s0 = (int64_t(blockIdx.x) * 4 + w) * NS;
+  int g0[NS], nd[NS];
+  unsigned msk[NS];
+  int32_t dct[NS][kSdiaMax];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int64_t s = min(s0 + k, ns - 1);
+    g0[k] = gp[s];
+    nd[k] = s0 + k < ns ? gp[s + 1] - g0[k] : 0;
+    msk[k] = mask[kSellC * s + lane];
+    const int32_t* dp = dict + kSdiaMax * s;
+#pragma unroll
+    for (int j = 0; j < kSdiaMax; ++j) dct[k][j] = dp[j];
+  }
+  VT v[NS][kSdiaMax];
+  double xv[NS][kSdiaMax];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int32_t base = int32_t(min(s0 + k, ns - 1) * kSellC), row = base + lane;
+#pragma unroll
+    for (int j = 0; j < kSdiaMax; ++j) {
+      if (j < nd[k]) {
+        const bool m = (msk[k] >> j) & 1u;
+        v[k][j] = gld(vals + kSellC * int64_t(g0[k] + j) + lane);
+        xv[k][j] = gld(x + (m ? row + dct[k][j] : base));
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int64_t row = (s0 + k) * kSellC + lane;
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < kSdiaMax; ++j)
+      if (j < nd[k] && ((msk[k] >> j) & 1u)) acc = acc + double(v[k][j]) * xv[k][j];
+    if (s0 + k < ns && row < n) y[row] = acc;
+  }
+}
+
+template <typename VT, int NS, int MINW>
+void launch_multi(const SellPattern& P, const void* vals, const double* x, double* y, hipStream_t st) {
+  const int64_t waves = (P.ns + NS - 1) / NS;
+  hipLaunchKernelGGL((k_sdia_multi<VT, NS, MINW>), dim3(unsigned((waves + 3) / 4)), dim3(256), 0, st, P.n, P.ns, P.gp,
+                     static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals), x, y);
+}
+
 using Fn = void (*)(const SellPattern&, const void*, const double*, double*, hipStream_t);
 
 // config id -> (value bytes, slots per batch SB, MINW, transposed)
@@ -151,6 +207,8 @@ const Cfg kCfgs[] = {
     {8, 8, 1, 3, launch_xconst<double, 8, 1>}, {4, 8, 6, 3, launch_xconst<float, 8, 6>},
     {8, 16, 1, 4, launch_clu<double, 2, 1>}, {8, 16, 1, 5, launch_clu<double, 0, 1>}, {8, 16, 1, 6, launch_clu<double, 1, 1>},
     {4, 16, 6, 4, launch_clu<float, 2, 6>},  {4, 16, 6, 5, launch_clu<float, 0, 6>},  {4, 16, 6, 6, launch_clu<float, 1, 6>},
+    {8, 1, 1, 7, launch_multi<double, 1, 1>}, {8, 2, 1, 7, launch_multi<double, 2, 1>}, {8, 3, 1, 7, launch_multi<double, 3, 1>},
+    {8, 4, 1, 7, launch_multi<double, 4, 1>},
 };
 
 template <typename VT, int QB, int MINW>
@@ -301,7 +359,7 @@ int sweep_bsr_run(int id, int64_t nb, int64_t nnzb, const int32_t* rowptr, const
   if (id < 0 || id >= sweep_bsr_count()) return -1;
   hipStream_t st = nullptr;
   SellPattern P;
-  if (bsell_build_pattern(nb, nnzb, rowptr, colind, 1e30, true, st, &P) || P.col_bits != 16) return -2;
+  if (bsell_build_pattern(nb, nnzb, rowptr, colind, 1e30, true, false, st, &P) || P.col_bits != 16) return -2;
   void* v = nullptr;
   if (bsell_fill_values(P, vals, LSPCG_F64, kBsrCfgs[id].vbytes == 4 ? LSPCG_F32 : LSPCG_F64, st, &v)) return -3;
   int4* fl = nullptr;
