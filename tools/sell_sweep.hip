@@ -192,6 +192,62 @@ void launch_multi(const SellPattern& P, const void* vals, const double* x, doubl
                      static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals), x, y);
 }
 
+// Experiment (round 5): TWO waves per slice.  Wave h of a pair loads slots [8h, 8h + 8) and forms
+// their products; wave 0 folds its products in slot order, hands the partial row sums to wave 1
+// through LDS, and wave 1 continues the fold with its own products in slot order -- the same
+// sequential sum (products are rounded before each add either way), with twice the waves.
+template <typename VT, int MINW>
+__global__ void __launch_bounds__(256, MINW) k_sdia_split2(int64_t n, int64_t ns, const int32_t* __restrict__ gp,
+                                                           const uint16_t* __restrict__ mask,
+                                                           const int32_t* __restrict__ dict, const VT* __restrict__ vals,
+                                                           const double* __restrict__ x, double* __restrict__ y) {
+  __shared__ double sh[2][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int h = w & 1, pr = w >> 1;
+  const int64_t s = int64_t(blockIdx.x) * 2 + pr;
+  const bool live = s < ns;  // wave-uniform
+  const int64_t sc = live ? s : ns - 1;
+  const int g0 = gp[sc], nd = live ? gp[sc + 1] - g0 : 0;
+  const unsigned msk = mask[kSellC * sc + lane];
+  const int32_t* dp = dict + kSdiaMax * sc + 8 * h;
+  int32_t dct[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dct[j] = dp[j];
+  const int32_t base = int32_t(sc * kSellC), row = base + lane;
+  double prod[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int jj = 8 * h + j;
+    const bool m = jj < nd && ((msk >> jj) & 1u);
+    const VT v = gld(vals + kSellC * int64_t(g0 + min(jj, max(nd - 1, 0))) + lane);
+    const double xv = gld(x + (m ? row + dct[j] : base));
+    prod[j] = double(v) * xv;
+  }
+  double acc = 0.0;
+  if (h == 1) {
+    __syncthreads();
+    acc = sh[pr][lane];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int jj = 8 * h + j;
+    if (jj < nd && ((msk >> jj) & 1u)) acc = acc + prod[j];
+  }
+  if (h == 0) {
+    sh[pr][lane] = acc;
+    __syncthreads();
+  } else if (live && row < n) {
+    y[row] = acc;
+  }
+}
+
+template <typename VT, int MINW>
+void launch_split2(const SellPattern& P, const void* vals, const double* x, double* y, hipStream_t st) {
+  hipLaunchKernelGGL((k_sdia_split2<VT, MINW>), dim3(unsigned((P.ns + 1) / 2)), dim3(256), 0, st, P.n, P.ns, P.gp,
+                     static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals), x, y);
+}
+
 using Fn = void (*)(const SellPattern&, const void*, const double*, double*, hipStream_t);
 
 // config id -> (value bytes, slots per batch SB, MINW, transposed)
@@ -209,6 +265,7 @@ const Cfg kCfgs[] = {
     {4, 16, 6, 4, launch_clu<float, 2, 6>},  {4, 16, 6, 5, launch_clu<float, 0, 6>},  {4, 16, 6, 6, launch_clu<float, 1, 6>},
     {8, 1, 1, 7, launch_multi<double, 1, 1>}, {8, 2, 1, 7, launch_multi<double, 2, 1>}, {8, 3, 1, 7, launch_multi<double, 3, 1>},
     {8, 4, 1, 7, launch_multi<double, 4, 1>},
+    {8, 8, 1, 8, launch_split2<double, 1>}, {4, 8, 6, 8, launch_split2<float, 6>}, {4, 8, 8, 8, launch_split2<float, 8>},
 };
 
 template <typename VT, int QB, int MINW>
