@@ -539,6 +539,92 @@ __global__ void __launch_bounds__(kThreads) k_update_r_g(int64_t n, PcgState* S,
   for (int64_t i = nv * W + jt; i < n; i += ts) r[i] = r[i] - alpha * q[i];
 }
 
+// UR of the split CG / Jacobi schedule (no preconditioner or the diagonal one): as k_update_r_g --
+// α_k = ρ_k/π_k from KC's groups, r_{k+1} = r_k - α_k q -- plus, for the next iteration's UP, the
+// groups of ρ_{k+1} = r·z (z = r / d for Jacobi; r·r without a preconditioner) and ‖r_{k+1}‖², the
+// dots the ext_spai schedule takes from KB.
+template <typename T, int PRE>
+__global__ void __launch_bounds__(kThreads) k_update_r_gd(int64_t n, PcgState* S, const double* __restrict__ gq,
+                                                          int ngq, const T* __restrict__ q, T* __restrict__ r,
+                                                          const T* __restrict__ d, T* __restrict__ z,
+                                                          double* partials, unsigned* ticket, int gsz,
+                                                          double* __restrict__ gz) {
+  using V = typename VecT<T>::type;
+  constexpr int W = VecT<T>::W;
+  const int64_t nv = n / W;
+  const int64_t ts = int64_t(gridDim.x) * blockDim.x;
+  const int64_t jt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  V rr[kElemUnroll], qq[kElemUnroll];
+  auto load = [&](int64_t j0) {
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        rr[u] = reinterpret_cast<const V*>(r)[j];
+        qq[u] = reinterpret_cast<const V*>(q)[j];
+      }
+    }
+  };
+  load(jt);  // first chunk, group totals and state line together (as in UP)
+  const int32_t done = S->done;
+  const int64_t k = S->iter;
+  const double rho_prev = S->rho;
+  const double rho = S->rho_k;
+  double vq[1];
+  group_sum_dd<1>(gq, ngq, vq);
+  if (done) return;  // uniform: UP exits too, nobody reads the groups
+  const double pq = round_to<T>(vq[0]);
+  const T alpha = T(rho) / T(pq);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    S->rho_prev = rho_prev;
+    S->rho = rho;
+    S->pq = pq;
+    S->alpha = double(alpha);
+    S->iter = k + 1;
+  }
+  DD dots[2] = {dd_zero(), dd_zero()};  // ρ_{k+1}, ‖r_{k+1}‖²
+  auto elem = [&](T ri, int64_t i) {
+    dd_fma(dots[1], double(ri), double(ri));
+    if constexpr (PRE == LSPCG_PRECOND_DIAGONAL) {
+      const T zi = ri / d[i];
+      z[i] = zi;
+      dd_fma(dots[0], double(ri), double(zi));
+    } else {
+      dd_fma(dots[0], double(ri), double(ri));
+    }
+  };
+  for (int64_t j0 = jt; j0 < nv; j0 += ts * kElemUnroll) {
+    if (j0 != jt) load(j0);
+#pragma unroll
+    for (int u = 0; u < kElemUnroll; ++u) {
+      const int64_t j = j0 + u * ts;
+      if (j < nv) {
+        const V rn = rr[u] - alpha * qq[u];
+        reinterpret_cast<V*>(r)[j] = rn;
+#pragma unroll
+        for (int c = 0; c < W; ++c) elem(rn[c], j * W + c);
+      }
+    }
+  }
+  for (int64_t i = nv * W + jt; i < n; i += ts) {
+    const T ri = r[i] - alpha * q[i];
+    r[i] = ri;
+    elem(ri, i);
+  }
+  grid_partial_groups<2>(dots, partials, ticket, gsz, gz);
+}
+
+// the split CG / Jacobi schedule's first UP reads ρ_0 from the groups: group 0 <- (ρ_0, ‖r_0‖²) of
+// the init launch's state, the other groups <- 0 (exact in the dd sums)
+__global__ void k_seed_groups(const PcgState* S, double* __restrict__ gz, int ng) {
+  for (int i = threadIdx.x; i < 4 * ng; i += blockDim.x) {
+    double v = 0.0;
+    if (i == 0) v = S->rho;
+    if (i == 2) v = S->rr;
+    gz[i] = v;
+  }
+}
+
 // ---- small systems: the whole solve in ONE workgroup --------------------------------------
 // Below a few thousand unknowns an iteration of the multi-kernel schedules is 5 dependent
 // launches of almost no work (~16 us per iteration at n = 900).  k_pcg_small runs
@@ -1124,6 +1210,8 @@ struct lspcg_solver {
   int split_mode = -1;  // -1 auto (by grid size), 1 groups, 2 no groups (LSPCG_SPLIT_REDUCE)
   double* groups = nullptr;  // [GZ: <= 4096 x 2 dots x DD | GQ: <= 4096 x DD]
   int gsz_l = 1, ng_l = 1, gsz_a = 1, ng_a = 1;  // group size / count of the KB and KC launches
+  bool split_cg = false;  // CG / Jacobi on the split reductions (UP, KC, UR with the dots of ρ, ‖r‖²)
+  int gsz_r = 1, ng_r = 1;  // ... group size / count of that UR launch
   KernelTimer* tk = nullptr;  // lspcg_solver_time_kernels: start / end stamps armed for each launch
   int tk_i = 0;
   PcgState* S = nullptr;
@@ -1410,6 +1498,26 @@ static int enqueue_iteration(lspcg_solver* s, hipStream_t st) {
   PcgState* S = s->S;
   const int eg = elem_vec_grid<T>(n);
   int rc = LSPCG_OK;
+  if (s->split_cg) {  // UP (ρ_k, ‖r_k‖² from UR's groups) -> KC (π groups) -> UR (+ next dots' groups)
+    double* gz = s->groups;
+    double* gq = s->groups + 4096 * 2 * 2;
+    const bool jac = s->precond == LSPCG_PRECOND_DIAGONAL;
+    hipLaunchKernelGGL(k_update_p_g<T>, dim3(eg), dim3(kThreads), 0, st, n, S, static_cast<const double*>(gz), s->ng_r,
+                       static_cast<const T*>(jac ? z : r), p, x);
+    rc = launch_it<T>(s, 0, static_cast<const T*>(p), ProDone{S}, EpiQG<T>{q, p, s->partials, s->ticket, gq, s->gsz_a},
+                      st);
+    if (rc) return rc;
+    if (jac)
+      hipLaunchKernelGGL((k_update_r_gd<T, LSPCG_PRECOND_DIAGONAL>), dim3(eg), dim3(kThreads), 0, st, n, S,
+                         static_cast<const double*>(gq), s->ng_a, static_cast<const T*>(q), r, d, z, s->partials,
+                         s->ticket, s->gsz_r, gz);
+    else
+      hipLaunchKernelGGL((k_update_r_gd<T, LSPCG_PRECOND_NONE>), dim3(eg), dim3(kThreads), 0, st, n, S,
+                         static_cast<const double*>(gq), s->ng_a, static_cast<const T*>(q), r, d, z, s->partials,
+                         s->ticket, s->gsz_r, gz);
+    LSPCG_HIP(hipGetLastError());
+    return LSPCG_OK;
+  }
   switch (s->precond) {
     case LSPCG_PRECOND_EXT_SPAI:
     case LSPCG_PRECOND_EXT_SPAI_SCALED: {
@@ -1494,6 +1602,7 @@ static int enqueue_init(lspcg_solver* s, hipStream_t st) {
                                           EpiResid<T, LSPCG_PRECOND_NONE>{r, b, d, z, s->S, s->partials, s->ticket},
                                           st);
   if (rc) return rc;
+  if (s->split_cg) hipLaunchKernelGGL(k_seed_groups, dim3(1), dim3(256), 0, st, s->S, s->groups, s->ng_r);
   if (s->precond == LSPCG_PRECOND_DIAGONAL) enqueue_ob<kObInit, true>(s, st, 3, r, r, b, b, r, z);
   else enqueue_ob<kObInit>(s, st, 2, r, r, b, b);
   LSPCG_HIP(hipGetLastError());
@@ -1626,6 +1735,33 @@ static int solver_diagonal(lspcg_solver* s) {
   return vec_permute(s->dtype, s->n / bs, bs, s->ro.perm, s->z, s->d, false, s->ctx->stream);
 }
 
+// reducing grid of iteration view 0's SpMV (the SELL / SELL-DIA copy, else the staged CSR kernel)
+static int64_t view0_reduce_grid(const lspcg_solver* s) {
+  if (s->sp[0]) return sell_grid(*s->sp[0], true);
+  const int64_t cap = std::min<int64_t>(kReduceGridMax, kElemBlocksMax);
+  const int64_t g = s->Av.block_size == 3 ? spmv_grid_t<256, 3>(s->Av.nb) : spmv_grid_t<256, 1>(s->Av.nb);
+  return std::min<int64_t>(g, cap);
+}
+
+// group size / count of a reducing launch of `grid` workgroups (see lspcg_solver_set_spai)
+static void split_groups(int mode, int64_t grid, int* gsz, int* ng) {
+  const bool nogroups = mode == 2 || (mode < 0 && grid <= kNoGroupGrid);
+  *gsz = nogroups ? 1 : int((grid + kMaxGroups - 1) / kMaxGroups);
+  *ng = int((grid + *gsz - 1) / *gsz);
+}
+
+// CG / Jacobi on the split reductions: compensated dot order, fp64 / fp32 alike, the multi-kernel
+// schedule (the one-workgroup solve has its own loop)
+static void setup_split_cg(lspcg_solver* s) {
+  s->split_cg = false;
+  if (!(s->precond == LSPCG_PRECOND_NONE || s->precond == LSPCG_PRECOND_DIAGONAL)) return;
+  if (!s->allow_split || s->dot_order != LSPCG_DOT_COMPENSATED || s->n == 0) return;
+  split_groups(s->split_mode, view0_reduce_grid(s), &s->gsz_a, &s->ng_a);
+  const int64_t eg = s->dtype == LSPCG_F64 ? elem_vec_grid<double>(s->n) : elem_vec_grid<float>(s->n);
+  split_groups(s->split_mode, eg, &s->gsz_r, &s->ng_r);
+  s->split_cg = s->gsz_a <= kMaxGroups && s->gsz_r <= kMaxGroups && s->ng_a <= 4096 && s->ng_r <= 4096;
+}
+
 // The A side of the solver: (optionally) the permuted system, its iteration view and SELL copy,
 // the diagonal of the Jacobi preconditioner.
 static int setup_A(lspcg_solver* s) {
@@ -1645,6 +1781,7 @@ static int setup_A(lspcg_solver* s) {
   }
   if (int rc = make_view(s, s->A, &s->Av, nullptr, &s->own_A)) return rc;
   if (int rc = build_sell(s, 0, &s->Av)) return rc;
+  setup_split_cg(s);
   if (s->precond == LSPCG_PRECOND_DIAGONAL) {
     if (int rc = solver_diagonal(s)) return rc;
     LSPCG_HIP(hipStreamSynchronize(s->ctx->stream));
@@ -1767,14 +1904,8 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     // round trip costs more than the consumers' extra loads (Poisson 256^2: 20.6 vs 22.0 us per
     // iteration; at 1 M rows, 1536 workgroups, the groups win: 91.4 vs 94.3).
     // LSPCG_SPLIT_REDUCE=1 / 2 force groups / no groups.
-    const int mode = s->split_mode;
-    auto groups = [mode](int64_t grid, int* gsz, int* ng) {
-      const bool nogroups = mode == 2 || (mode < 0 && grid <= kNoGroupGrid);
-      *gsz = nogroups ? 1 : int((grid + kMaxGroups - 1) / kMaxGroups);
-      *ng = int((grid + *gsz - 1) / *gsz);
-    };
-    groups(sell_grid(*s->sp[1], true), &s->gsz_l, &s->ng_l);
-    groups(sell_grid(*s->sp[0], true), &s->gsz_a, &s->ng_a);
+    split_groups(s->split_mode, sell_grid(*s->sp[1], true), &s->gsz_l, &s->ng_l);
+    split_groups(s->split_mode, sell_grid(*s->sp[0], true), &s->gsz_a, &s->ng_a);
     LSPCG_CHECK(s->gsz_l <= kMaxGroups && s->gsz_a <= kMaxGroups, LSPCG_ERR_UNSUPPORTED,
                 "set_spai: reducing grid too large for one-wave group sums");
   }
@@ -2073,6 +2204,7 @@ int lspcg_solver_set_dot_order(lspcg_solver* s, int order, int threads) {
     }
   }
   s->split = s->split_ok && order == LSPCG_DOT_COMPENSATED;
+  setup_split_cg(s);
   for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
   s->graphs.clear();
