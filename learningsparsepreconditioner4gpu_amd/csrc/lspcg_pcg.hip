@@ -1735,11 +1735,12 @@ static int solver_diagonal(lspcg_solver* s) {
   return vec_permute(s->dtype, s->n / bs, bs, s->ro.perm, s->z, s->d, false, s->ctx->stream);
 }
 
-// reducing grid of iteration view 0's SpMV (the SELL / SELL-DIA copy, else the staged CSR kernel)
-static int64_t view0_reduce_grid(const lspcg_solver* s) {
-  if (s->sp[0]) return sell_grid(*s->sp[0], true);
+// reducing grid of iteration view w's SpMV (the SELL / SELL-DIA copy, else the staged CSR kernel)
+static int64_t view_reduce_grid(const lspcg_solver* s, int w) {
+  if (s->sp[w]) return sell_grid(*s->sp[w], true);
+  const lspcg_mat& V = w == 0 ? s->Av : (w == 1 ? s->Lv : s->LTv);
   const int64_t cap = std::min<int64_t>(kReduceGridMax, kElemBlocksMax);
-  const int64_t g = s->Av.block_size == 3 ? spmv_grid_t<256, 3>(s->Av.nb) : spmv_grid_t<256, 1>(s->Av.nb);
+  const int64_t g = V.block_size == 3 ? spmv_grid_t<256, 3>(V.nb) : spmv_grid_t<256, 1>(V.nb);
   return std::min<int64_t>(g, cap);
 }
 
@@ -1756,7 +1757,7 @@ static void setup_split_cg(lspcg_solver* s) {
   s->split_cg = false;
   if (!(s->precond == LSPCG_PRECOND_NONE || s->precond == LSPCG_PRECOND_DIAGONAL)) return;
   if (!s->allow_split || s->dot_order != LSPCG_DOT_COMPENSATED || s->n == 0) return;
-  split_groups(s->split_mode, view0_reduce_grid(s), &s->gsz_a, &s->ng_a);
+  split_groups(s->split_mode, view_reduce_grid(s, 0), &s->gsz_a, &s->ng_a);
   const int64_t eg = s->dtype == LSPCG_F64 ? elem_vec_grid<double>(s->n) : elem_vec_grid<float>(s->n);
   split_groups(s->split_mode, eg, &s->gsz_r, &s->ng_r);
   s->split_cg = s->gsz_a <= kMaxGroups && s->gsz_r <= kMaxGroups && s->ng_a <= 4096 && s->ng_r <= 4096;
@@ -1896,7 +1897,9 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT, lt_same ? &lflag : nullptr))) return rc;
   if ((rc = build_sell(s, 1, &s->Lv))) return rc;
   if ((rc = build_sell(s, 2, &s->LTv))) return rc;
-  s->split_ok = s->allow_split && s->sp[0] && s->sp[1] && s->sp[2];
+  // the split schedule runs on any iteration views (SELL copies or the staged CSR kernel, whose
+  // epilogues finish their dots the same way; round 5 -- before, it needed SELL views of A, L, Lᵀ)
+  s->split_ok = s->allow_split;
   s->split = s->split_ok && s->dot_order == LSPCG_DOT_COMPENSATED;
   if (s->split_ok) {
     // <= 64 groups per reducing launch; no groups at all (the consumers sum every workgroup's
@@ -1904,8 +1907,8 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     // round trip costs more than the consumers' extra loads (Poisson 256^2: 20.6 vs 22.0 us per
     // iteration; at 1 M rows, 1536 workgroups, the groups win: 91.4 vs 94.3).
     // LSPCG_SPLIT_REDUCE=1 / 2 force groups / no groups.
-    split_groups(s->split_mode, sell_grid(*s->sp[1], true), &s->gsz_l, &s->ng_l);
-    split_groups(s->split_mode, sell_grid(*s->sp[0], true), &s->gsz_a, &s->ng_a);
+    split_groups(s->split_mode, view_reduce_grid(s, 1), &s->gsz_l, &s->ng_l);
+    split_groups(s->split_mode, view_reduce_grid(s, 0), &s->gsz_a, &s->ng_a);
     LSPCG_CHECK(s->gsz_l <= kMaxGroups && s->gsz_a <= kMaxGroups, LSPCG_ERR_UNSUPPORTED,
                 "set_spai: reducing grid too large for one-wave group sums");
   }
@@ -2215,7 +2218,7 @@ int lspcg_solver_set_dot_order(lspcg_solver* s, int order, int threads) {
 int lspcg_solver_time_kernels(lspcg_solver* s, const void* b, int64_t iters, double* kernel_ms, int* nk) {
   LSPCG_CHECK(s && b && kernel_ms && nk && iters > 0, LSPCG_ERR_ARG, "time_kernels: bad argument");
   *nk = 0;
-  LSPCG_CHECK(s->split, LSPCG_ERR_UNSUPPORTED, "time_kernels: only the split ext_spai schedule (set_spai on SELL views)");
+  LSPCG_CHECK(s->split, LSPCG_ERR_UNSUPPORTED, "time_kernels: only the split ext_spai schedule (LSPCG_SPLIT_REDUCE != 0)");
   LSPCG_HIP(hipSetDevice(s->ctx->device));
   const int64_t n = s->n;
   hipStream_t st = s->stream;

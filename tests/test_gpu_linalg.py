@@ -260,11 +260,16 @@ def test_time_kernels_reports_five_launches(gpu_ctx, monkeypatch):
     it, conv, _ = s.solve(b, x, rtol=1e-8)
     L = _cases.spai_like(A)
     assert conv and it == O.pcg(A, A @ np.ones(A.shape[0]), O.spai_operator(L, 3e-3), rtol=1e-8, dot="exact")[0]
-    monkeypatch.setenv("LSPCG_NO_SELL", "1")  # staged CSR views: not instrumented
+    monkeypatch.setenv("LSPCG_NO_SELL", "1")  # staged CSR views: the same split schedule (round 5)
     s2 = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai")
     s2.set_spai(L, 3e-3)
+    k2 = s2.time_kernels(b, 5)
+    assert list(k2) == list(s.KERNELS) and all(v > 0 for v in k2.values())
+    monkeypatch.setenv("LSPCG_SPLIT_REDUCE", "0")  # last-arriver reductions: not instrumented
+    s3 = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai")
+    s3.set_spai(L, 3e-3)
     with pytest.raises(RuntimeError):
-        s2.time_kernels(b, 5)
+        s3.time_kernels(b, 5)
 
 
 def test_solve_many_matches_one_by_one(gpu_ctx):
