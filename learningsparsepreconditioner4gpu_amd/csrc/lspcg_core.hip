@@ -367,18 +367,36 @@ int lspcg_mat_copy_out(const lspcg_mat* A, int32_t* indptr, int32_t* indices, vo
   return LSPCG_OK;
 }
 
-int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out) { return lspcg::mat_transpose(A, out, nullptr); }
+int lspcg_mat_transpose(const lspcg_mat* A, lspcg_mat** out) {
+  return lspcg::mat_transpose(A, out, nullptr, nullptr);
+}
 
 }  // extern "C"
 
-int lspcg::mat_transpose(const lspcg_mat* A, lspcg_mat** out, bool* same_pattern) {
+bool lspcg::mat_reusable(const lspcg_mat* old, const lspcg_mat* like) {
+  return old && like && old != like && old->ctx == like->ctx && old->nb == like->nb && old->nnzb == like->nnzb &&
+         old->block_size == like->block_size && old->dtype == like->dtype &&
+         old->storage_dtype() == like->storage_dtype() && !old->sell;
+}
+
+int lspcg::mat_transpose(const lspcg_mat* A, lspcg_mat** out, bool* same_pattern, lspcg_mat* reuse) {
   LSPCG_CHECK(A && out, LSPCG_ERR_ARG, "transpose: NULL");
   if (same_pattern) *same_pattern = false;
   lspcg_ctx* ctx = A->ctx;
   hipStream_t st = ctx->stream;
   lspcg_mat* Tm = nullptr;
-  int rc = mat_alloc(ctx, A->nb, A->nnzb, A->block_size, A->dtype, &Tm);
-  if (rc) return rc;
+  // a previous transpose of a matrix of the same shape is overwritten in place (a new ext_spai factor
+  // on the same solver: no free / allocate of the entry arrays, and its addresses stay valid)
+  if (A->storage_dtype() == A->dtype && mat_reusable(reuse, A)) {
+    Tm = reuse;
+  } else {
+    reuse = nullptr;
+    int rc = mat_alloc(ctx, A->nb, A->nnzb, A->block_size, A->dtype, &Tm);
+    if (rc) return rc;
+  }
+  auto drop = [&]() {
+    if (Tm != reuse) lspcg_mat_destroy(Tm);
+  };
   {  // symmetric pattern (the ext_spai factor always has A's pattern): value permutation only
     int* flag = nullptr;
     int h = 1;
@@ -411,7 +429,7 @@ int lspcg::mat_transpose(const lspcg_mat* A, lspcg_mat** out, bool* same_pattern
     (void)hipFree(flag);
     if (e != hipSuccess) {
       set_error(std::string("transpose: ") + hipGetErrorString(e));
-      lspcg_mat_destroy(Tm);
+      drop();
       return LSPCG_ERR_HIP;
     }
     if (h == 0) {
@@ -426,7 +444,7 @@ int lspcg::mat_transpose(const lspcg_mat* A, lspcg_mat** out, bool* same_pattern
     set_error(std::string("transpose: ") + hipGetErrorString(e));
     (void)hipFree(cnt);
     (void)hipFree(tsrc);
-    lspcg_mat_destroy(Tm);
+    drop();
     return LSPCG_ERR_HIP;
   };
   hipError_t e = hipMalloc(&cnt, sizeof(int32_t) * (A->nb + 1));

@@ -422,7 +422,10 @@ int mat_alloc_entries(lspcg_mat* m, int64_t nnzb);
 int mat_alloc(lspcg_ctx* ctx, int64_t nb, int64_t nnzb, int bs, int dtype, lspcg_mat** out);
 // lspcg_mat_transpose; *same_pattern (optional) <- the symmetric-pattern path ran, i.e. Aᵀ has
 // A's rowptr / colind and its values are a permutation of A's
-int mat_transpose(const lspcg_mat* A, lspcg_mat** out, bool* same_pattern);
+// reuse: an owned matrix of A's shape to overwrite instead of allocating (kept by the caller when
+// not taken: *out != reuse)
+int mat_transpose(const lspcg_mat* A, lspcg_mat** out, bool* same_pattern, lspcg_mat* reuse);
+bool mat_reusable(const lspcg_mat* old, const lspcg_mat* like);
 
 // Bandwidth-reducing row placement (lspcg_reorder.hip): perm[i'] = original (block) row of row
 // i', iperm its inverse (device arrays, nb entries); off_* = mean |col - row| of the pattern in the
@@ -440,7 +443,7 @@ int mean_abs_offset(const lspcg_mat* A, double* out);
 // banded, and only if RCM halves the mean offset).  *applied <- out holds a permutation.
 int rcm_reorder(const lspcg_mat* A, int mode, Reorder* out, bool* applied);
 // P M P^T with every row's entries in their original order (columns renamed): same row sums
-int mat_permute(const lspcg_mat* M, const Reorder& R, lspcg_mat** out);
+int mat_permute(const lspcg_mat* M, const Reorder& R, lspcg_mat** out, lspcg_mat* reuse = nullptr);
 // dst[i'] = src[perm[i']] (scatter = false) or dst[perm[i']] = src[i'] (scatter = true), bs scalars per row
 int vec_permute(int dtype, int64_t nb, int bs, const int32_t* perm, const void* src, void* dst, bool scatter,
                 hipStream_t st);

@@ -1196,6 +1196,7 @@ struct lspcg_solver {
   Reorder ro;
   lspcg_mat* Ap = nullptr;   // owned P A Pᵀ
   lspcg_mat* Lp = nullptr;   // owned P L Pᵀ
+  lspcg_mat* LTo = nullptr;  // owned Lᵀ in the original numbering (reordered ext_spai; kept for reuse)
   int reorder_mode = -1;     // LSPCG_REORDER: -1 auto, 0 off, 1 always
   bool reorder_ok = false;   // single solves in the compensated order only (not batches, IC, parity)
   int precond = LSPCG_PRECOND_NONE;
@@ -1227,6 +1228,7 @@ struct lspcg_solver {
   void* own_A = nullptr;
   void* own_L = nullptr;
   void* own_LT = nullptr;
+  int64_t own_L_n = -1, own_LT_n = -1;  // entries of the fp32 copies above (refilled in place)
   int* flag = nullptr;
   // IC(0): factor, its explicit transpose and their level sets
   lspcg_mat* icL = nullptr;
@@ -1287,6 +1289,15 @@ static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view);
 static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   hipStream_t st = s->ctx->stream;
   if (s->sv[w] || s->spat[w].gp) LSPCG_HIP(hipStreamSynchronize(s->stream));  // a solve may use them
+  // L / Lᵀ on A's pattern again (a new L for the same system): refill the value array in place, so
+  // its address -- and with it every captured iteration graph -- stays valid (get_graph)
+  if (w > 0 && s->use_sell && s->sv[w] && !s->slut[w] && s->sp[w] && s->sp[w] == s->sp[0] &&
+      view->rowptr == s->Av.rowptr && view->colind == s->Av.colind && view->storage_dtype() == s->svd[w]) {
+    const SellPattern* P = s->sp[w];
+    const int vd = view->storage_dtype();
+    return P->bs == 3 ? bsell_fill_values(*P, view->vals, vd, vd, st, &s->sv[w])
+                      : sell_fill_values(*P, view->colind, view->vals, vd, vd, st, &s->sv[w]);
+  }
   (void)hipFree(s->sv[w]);
   s->sv[w] = nullptr;
   (void)hipFree(s->slut[w]);
@@ -1391,15 +1402,17 @@ static int flag_run(lspcg_solver* s, hipStream_t st, int* out) {
 // symmetric-pattern transpose has L's pattern and a permutation of L's values.  Returns the
 // flag in *flag_out (optional).
 static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const lspcg_mat* base, void** own,
-                     const int* known = nullptr, int* flag_out = nullptr) {
+                     const int* known = nullptr, int* flag_out = nullptr, int64_t* own_n = nullptr) {
   hipStream_t st = s->ctx->stream;
+  const int64_t ne = M->nnzb * M->block_size * M->block_size;
   if (*own) {
     LSPCG_HIP(hipStreamSynchronize(s->stream));
-    (void)hipFree(*own);
-    *own = nullptr;
+    if (!own_n || *own_n != ne) {  // an fp32 copy of the same length is refilled in place below
+      (void)hipFree(*own);
+      *own = nullptr;
+    }
   }
   *view = *M;
-  const int64_t ne = M->nnzb * M->block_size * M->block_size;
   const bool try_compact = M->dtype == LSPCG_F64 && M->storage_dtype() == LSPCG_F64 && ne > 0;
   const bool try_share = base && base != M && base->nb == M->nb && base->nnzb == M->nnzb &&
                          base->block_size == M->block_size;
@@ -1423,11 +1436,18 @@ static int make_view(lspcg_solver* s, const lspcg_mat* M, lspcg_mat* view, const
     if (!try_share) f |= 2;
   }
   if (flag_out) *flag_out = f;
+  if (*own && !(try_compact && !(f & 1))) {  // the new matrix is not stored compactly
+    (void)hipFree(*own);
+    *own = nullptr;
+  }
   if (try_compact && !(f & 1)) {
-    float* v = nullptr;
-    LSPCG_HIP(hipMalloc(&v, sizeof(float) * (ne + kEntryPad)));
-    *own = v;
-    LSPCG_HIP(hipMemsetAsync(v + ne, 0, sizeof(float) * kEntryPad, st));
+    float* v = static_cast<float*>(*own);
+    if (!v) {
+      LSPCG_HIP(hipMalloc(&v, sizeof(float) * (ne + kEntryPad)));
+      *own = v;
+      if (own_n) *own_n = ne;
+      LSPCG_HIP(hipMemsetAsync(v + ne, 0, sizeof(float) * kEntryPad, st));
+    }
     hipLaunchKernelGGL(k_to_f32, dim3(elem_grid(ne)), dim3(kThreads), 0, st, ne, static_cast<const double*>(M->vals), v);
     view->vals = v;
     view->val_dtype = LSPCG_F32;
@@ -1857,6 +1877,43 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
   return LSPCG_OK;
 }
 
+// Everything a captured iteration graph holds by value besides the solver's own fixed buffers: the
+// views' arrays (SELL copies or CSR views), their value types, the reduction geometry and ε.  A
+// new L whose views land at the same addresses keeps the graphs (build_sell / make_view refill in
+// place), so a sample-by-sample loop does not re-capture every chunk size per sample.
+struct GraphKey {
+  const void* p[15];
+  int64_t i[16];
+  double eps;
+  bool operator==(const GraphKey& o) const {
+    return std::memcmp(p, o.p, sizeof(p)) == 0 && std::memcmp(i, o.i, sizeof(i)) == 0 && eps == o.eps;
+  }
+};
+static GraphKey graph_key(const lspcg_solver* s) {
+  GraphKey k{};
+  int a = 0, b = 0;
+  for (int w = 0; w < 3; ++w) {
+    const lspcg_mat& V = w == 0 ? s->Av : (w == 1 ? s->Lv : s->LTv);
+    k.p[a++] = s->sp[w];
+    k.p[a++] = s->sv[w];
+    k.p[a++] = s->slut[w];
+    k.p[a++] = V.rowptr;
+    k.p[a++] = V.vals;
+    k.i[b++] = s->svd[w];
+    k.i[b++] = V.val_dtype;
+    k.i[b++] = reinterpret_cast<intptr_t>(V.colind);
+  }
+  k.i[b++] = s->split;
+  k.i[b++] = s->split_cg;
+  k.i[b++] = s->gsz_l;
+  k.i[b++] = s->ng_l;
+  k.i[b++] = s->gsz_a;
+  k.i[b++] = s->ng_a;
+  k.i[b++] = s->dot_order;
+  k.eps = s->eps;
+  return k;
+}
+
 int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, double* t_prec_ms) {
   LSPCG_CHECK(s && L, LSPCG_ERR_ARG, "set_spai: NULL");
   LSPCG_CHECK(s->precond == LSPCG_PRECOND_EXT_SPAI || s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED, LSPCG_ERR_ARG,
@@ -1864,27 +1921,31 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   LSPCG_CHECK(L->n == s->n, LSPCG_ERR_ARG, "set_spai: L has a different size than A");
   LSPCG_CHECK(L->dtype == s->dtype, LSPCG_ERR_ARG, "set_spai: L dtype differs from A dtype");
   hipStream_t cst = s->ctx->stream;
+  const GraphKey key_before = graph_key(s);
+  LSPCG_HIP(hipStreamSynchronize(s->stream));  // Lᵀ below may be referenced by a running solve
   LSPCG_HIP(hipEventRecord(s->ev_t0, cst));
-  if (s->LT) {
-    lspcg_mat_destroy(s->LT);
-    s->LT = nullptr;
-  }
-  if (s->Lp) {
-    lspcg_mat_destroy(s->Lp);
-    s->Lp = nullptr;
-  }
+  // Lᵀ (and, reordered, P L Pᵀ / P Lᵀ Pᵀ) of the previous factor are overwritten in place when the
+  // new L has its shape: no free / allocate per sample, and the iteration views keep their addresses
+  // (so the captured graphs survive, graph_key below)
+  auto renew = [](lspcg_mat** slot, lspcg_mat* keep, int rc) {
+    if (keep && keep != *slot) lspcg_mat_destroy(keep);
+    return rc;
+  };
   bool lt_same = false;
-  int rc = mat_transpose(L, &s->LT, &lt_same);  // in the ORIGINAL numbering: Lᵀ's rows in scipy's order
+  lspcg_mat** raw_slot = s->ro.perm ? &s->LTo : &s->LT;  // Lᵀ in the ORIGINAL numbering: rows in scipy's order
+  lspcg_mat* keep = *raw_slot;
+  *raw_slot = nullptr;
+  int rc = renew(raw_slot, keep, mat_transpose(L, raw_slot, &lt_same, keep));
   if (rc) return rc;
   const lspcg_mat* Lu = L;
   if (s->ro.perm) {  // reordered solver: P L Pᵀ and P Lᵀ Pᵀ, every row's entries in their original order
     LSPCG_CHECK(L->block_size == s->A->block_size, LSPCG_ERR_ARG, "set_spai: L and A block sizes differ");
-    if ((rc = mat_permute(L, s->ro, &s->Lp))) return rc;
-    lspcg_mat* LTp = nullptr;
-    rc = mat_permute(s->LT, s->ro, &LTp);
-    lspcg_mat_destroy(s->LT);
-    s->LT = LTp;
-    if (rc) return rc;
+    keep = s->Lp;
+    s->Lp = nullptr;
+    if ((rc = renew(&s->Lp, keep, mat_permute(L, s->ro, &s->Lp, keep)))) return rc;
+    keep = s->LT;
+    s->LT = nullptr;
+    if ((rc = renew(&s->LT, keep, mat_permute(s->LTo, s->ro, &s->LT, keep)))) return rc;
     Lu = s->Lp;
   }
   if (s->precond == LSPCG_PRECOND_EXT_SPAI_SCALED) {
@@ -1893,8 +1954,9 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
     if (rc) return rc;
   }
   int lflag = 3;
-  if ((rc = make_view(s, Lu, &s->Lv, &s->Av, &s->own_L, nullptr, &lflag))) return rc;
-  if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT, lt_same ? &lflag : nullptr))) return rc;
+  if ((rc = make_view(s, Lu, &s->Lv, &s->Av, &s->own_L, nullptr, &lflag, &s->own_L_n))) return rc;
+  if ((rc = make_view(s, s->LT, &s->LTv, &s->Av, &s->own_LT, lt_same ? &lflag : nullptr, nullptr, &s->own_LT_n)))
+    return rc;
   if ((rc = build_sell(s, 1, &s->Lv))) return rc;
   if ((rc = build_sell(s, 2, &s->LTv))) return rc;
   // the split schedule runs on any iteration views (SELL copies or the staged CSR kernel, whose
@@ -1919,11 +1981,13 @@ int lspcg_solver_set_spai(lspcg_solver* s, const lspcg_mat* L, double epsilon, d
   if (t_prec_ms) *t_prec_ms = ms;
   s->L = L;
   s->eps = epsilon;
-  // graphs capture matrix pointers: drop them when the preconditioner changes
-  for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
-  for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
-  s->graphs.clear();
-  s->graph_defs.clear();
+  // graphs capture the views' addresses and ε: drop them unless the new L kept every one of them
+  if (!(graph_key(s) == key_before)) {
+    for (auto& kv : s->graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : s->graph_defs) (void)hipGraphDestroy(kv.second);
+    s->graphs.clear();
+    s->graph_defs.clear();
+  }
   return LSPCG_OK;
 }
 
@@ -2309,6 +2373,7 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   for (hipEvent_t e : {s->ev_in, s->ev_out, s->ev_poll, s->ev_poll2, s->ev_t0, s->ev_t1}) (void)hipEventDestroy(e);
   if (s->LT) lspcg_mat_destroy(s->LT);
   if (s->Lp) lspcg_mat_destroy(s->Lp);
+  if (s->LTo) lspcg_mat_destroy(s->LTo);
   if (s->Ap) lspcg_mat_destroy(s->Ap);
   s->ro.release();
   if (s->icL) lspcg_mat_destroy(s->icL);

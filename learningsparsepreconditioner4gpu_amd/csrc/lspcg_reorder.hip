@@ -669,12 +669,17 @@ int rcm_reorder(const lspcg_mat* A, int mode, Reorder* out, bool* applied) {
   return LSPCG_OK;
 }
 
-int mat_permute(const lspcg_mat* M, const Reorder& R, lspcg_mat** out) {
+int mat_permute(const lspcg_mat* M, const Reorder& R, lspcg_mat** out, lspcg_mat* reuse) {
   LSPCG_CHECK(R.perm && M->nb == R.nb, LSPCG_ERR_ARG, "mat_permute: permutation size differs from the matrix");
   hipStream_t st = M->ctx->stream;
   lspcg_mat* P = nullptr;
-  if (int rc = mat_alloc(M->ctx, M->nb, M->nnzb, M->block_size, M->dtype, &P)) return rc;
-  std::unique_ptr<lspcg_mat, int (*)(lspcg_mat*)> guard(P, lspcg_mat_destroy);
+  if (mat_reusable(reuse, M)) {  // overwrite a previous P M Pᵀ of the same shape (caller keeps it on failure)
+    P = reuse;
+  } else {
+    reuse = nullptr;
+    if (int rc = mat_alloc(M->ctx, M->nb, M->nnzb, M->block_size, M->dtype, &P)) return rc;
+  }
+  std::unique_ptr<lspcg_mat, int (*)(lspcg_mat*)> guard(reuse ? nullptr : P, lspcg_mat_destroy);
   P->val_dtype = M->val_dtype;
   const int64_t nb = M->nb;
   int32_t* len = nullptr;
@@ -699,7 +704,8 @@ int mat_permute(const lspcg_mat* M, const Reorder& R, lspcg_mat** out) {
                        static_cast<uint32_t*>(P->vals));
   LSPCG_HIP(hipGetLastError());
   LSPCG_HIP(hipStreamSynchronize(st));  // len / tmp are freed on return
-  *out = guard.release();
+  guard.release();
+  *out = P;
   return LSPCG_OK;
 }
 

@@ -375,8 +375,9 @@ int bsell_build_pattern(int64_t nb, int64_t nnzb, const int32_t* rowptr, const i
 
 int bsell_fill_values(const SellPattern& P, const void* src, int src_dtype, int dst_dtype, hipStream_t st, void** out) {
   const size_t es = dst_dtype == LSPCG_F32 ? 4 : 8;
-  void* v = nullptr;
-  LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(576 * P.groups, 1)));
+  void* v = *out;  // an existing array of this pattern and dtype is refilled in place
+  const bool mine = v == nullptr;
+  if (!v) LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(576 * P.groups, 1)));
   const dim3 g(slice_grid(P.ns)), b(256);
   const int32_t* nocol = nullptr;
   if (P.ns && P.col_bits == 1) {
@@ -413,7 +414,7 @@ int bsell_fill_values(const SellPattern& P, const void* src, int src_dtype, int 
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
-    (void)hipFree(v);
+    if (mine) (void)hipFree(v);
     set_error(std::string("bsell_fill_values: ") + hipGetErrorString(e));
     return LSPCG_ERR_HIP;
   }
@@ -540,9 +541,10 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
 int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* src, int src_dtype, int dst_dtype,
                      hipStream_t st, void** out) {
   const size_t es = dst_dtype == LSPCG_F32 ? 4 : 8;
-  void* v = nullptr;
+  void* v = *out;  // an existing array of this pattern and dtype is refilled in place
+  const bool mine = v == nullptr;
   const int64_t slots = P.col_bits == 1 ? kSellC * P.groups : 256 * P.groups;
-  LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(slots, 1)));
+  if (!v) LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(slots, 1)));
   const dim3 g(slice_grid(P.ns)), b(256);
   if (P.ns && P.col_bits == 1) {
     const auto* m = static_cast<const uint16_t*>(P.col);
@@ -574,7 +576,7 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
-    (void)hipFree(v);
+    if (mine) (void)hipFree(v);
     set_error(std::string("sell_fill_values: ") + hipGetErrorString(e));
     return LSPCG_ERR_HIP;
   }

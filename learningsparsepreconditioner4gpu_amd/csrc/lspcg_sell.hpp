@@ -623,8 +623,9 @@ namespace lspcg {
 // than the 4-entry groups would, else 16-bit offsets when they fit.
 int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
                        int cols, hipStream_t st, SellPattern* out);
-// Allocates and fills the SELL value array of a CSR with the same pattern.  src_dtype /
-// dst_dtype: LSPCG_F32 or LSPCG_F64 (fp64 -> fp32 only for exactly representable values).
+// Allocates and fills the SELL value array of a CSR with the same pattern (*out == nullptr), or
+// refills *out in place (an array of this pattern and dst_dtype).  src_dtype / dst_dtype:
+// LSPCG_F32 or LSPCG_F64 (fp64 -> fp32 only for exactly representable values).
 int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* src, int src_dtype, int dst_dtype,
                      hipStream_t st, void** out);
 // BSELL-64 pattern of a BSR 3x3 (nb block rows, nnzb blocks, sorted block columns); the same

@@ -332,3 +332,53 @@ def test_solve_many_fresh_solvers_concurrent_capture(gpu_ctx):
         for (it, conv, x), (it2, conv2, _), (_, _, x2) in zip(ref, out, jobs):
             assert (it, conv) == (it2, conv2)
             assert torch.equal(x, x2)
+
+
+@pytest.mark.parametrize("case", ["sdia", "csr", "bsr3", "scaled", "fp32", "reordered"])
+def test_new_spai_on_the_same_solver_equals_a_fresh_solver(gpu_ctx, monkeypatch, case):
+    """set_spai with a new L on a solver that has solved before refills its L / Lᵀ views in place and
+    keeps its captured iteration graphs when every address and ε are unchanged (GraphKey); the
+    solve must equal a fresh solver's on the new L bit for bit -- also after an ε change (graphs
+    dropped) and back."""
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    dtype = np.float32 if case == "fp32" else np.float64
+    bs = 3 if case == "bsr3" else 1
+    pre = "ext_spai_scaled" if case == "scaled" else "ext_spai"
+    if case == "csr":
+        monkeypatch.setenv("LSPCG_NO_SELL", "1")
+    if case == "reordered":  # P L Pᵀ, Lᵀ and P Lᵀ Pᵀ overwritten in place too
+        monkeypatch.setenv("LSPCG_REORDER", "1")
+    if bs == 3:
+        A0, _, _ = P.elasticity_box(16, 8, 8)
+        A = sp.csr_matrix(A0)
+    else:
+        A = sp.csr_matrix(P.kuhn_laplacian(30, 1e-2))
+    A.sort_indices()
+    A.data = A.data.astype(np.float32).astype(np.float64)
+    Ls = []
+    for seed in (1, 2):
+        L = _cases.spai_like(A, seed=seed)
+        L.data = L.data.astype(np.float32).astype(np.float64)
+        Ls.append(L)
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    b = torch.from_numpy(A @ np.ones(A.shape[0])).to(tdt).cuda()
+    rtol = 1e-8 if dtype == np.float64 else 1e-5
+
+    def run(s):
+        x = torch.zeros_like(b)
+        it, conv, _, h = s.solve(b, x, rtol=rtol, return_history=True)
+        return it, x.cpu().numpy(), h
+
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=pre, dtype=dtype, block_size=bs)
+    seq = [(Ls[0], 3e-3), (Ls[1], 3e-3), (Ls[1], 2e-3), (Ls[0], 3e-3)]
+    for L, eps in seq:
+        s.set_spai(L, eps, block_size=bs)
+        got = run(s)
+        got2 = run(s)  # the graphs of this L (kept or re-captured) replayed again
+        f = PreconditionedConjugateGradient(A, device="cuda", preconditioner=pre, dtype=dtype, block_size=bs)
+        f.set_spai(L, eps, block_size=bs)
+        want = run(f)
+        del f
+        for g in (got, got2):
+            assert g[0] == want[0] and np.array_equal(g[1], want[1]) and np.array_equal(g[2], want[2]), (case, eps)
