@@ -650,9 +650,10 @@ __global__ void __launch_bounds__(256) k_encode(int64_t M, int fin, const float*
 // out[e] = edge_dec(cat[e_attr, x[src], x[dst]])  (gnns.py:88-95; original edge order).  Visits
 // edges e, gathering each 64-B edge-state row from its CSC slot inv[e]: measured faster than
 // visiting slots and scattering the OUT-float results (0.59 vs 0.67 ms at E = 15.2 M).
-template <bool F32, int OUT>
+template <bool F32, int OUT, typename IT>
 __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __restrict__ fr,
-                                                 const int64_t* __restrict__ ei, const int32_t* __restrict__ inv,
+                                                 const IT* __restrict__ ra, const IT* __restrict__ rb,
+                                                 const int32_t* __restrict__ inv,
                                                  const float* __restrict__ ecsc, const float* __restrict__ x,
                                                  float* __restrict__ out) {
   // the decoder's fragment block in LDS (8 KiB): the per-tile weight reads stay off the gathers'
@@ -669,7 +670,7 @@ __global__ void __launch_bounds__(256) k_edge_dec(int64_t E, const float* __rest
     const bool valid = e < E;
     const int64_t ee = valid ? e : E - 1;
     float in[12];
-    pack12(ld4(ecsc + int64_t(inv[ee]) * H + 4 * q), ld4(x + ei[ee] * H + 4 * q), ld4(x + ei[E + ee] * H + 4 * q), in);
+    pack12(ld4(ecsc + int64_t(inv[ee]) * H + 4 * q), ld4(x + int64_t(ra[ee]) * H + 4 * q), ld4(x + int64_t(rb[ee]) * H + 4 * q), in);
     f4 o;
     if constexpr (F32) o = ff_tile<12>(wd, in, lane);
     else o = ff1_48(wd, in, lane, us);
@@ -1317,9 +1318,27 @@ int lspcg_gnn_forward(lspcg_gnn* g, int64_t N, int64_t E, const float* x, const 
   }
   // decoder
   const float* fd = g->frag + g->o_dec;
-  auto dec = g->f32 ? (d.edge_out == 1 ? k_edge_dec<true, 1> : d.edge_out == 4 ? k_edge_dec<true, 4> : k_edge_dec<true, 9>)
-                    : (d.edge_out == 1 ? k_edge_dec<false, 1> : d.edge_out == 4 ? k_edge_dec<false, 4> : k_edge_dec<false, 9>);
-  hipLaunchKernelGGL(dec, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, inv, g->ecsc, xc, out);
+  // endpoints in edge order: the symmetric fast path's int32 dst / src are exactly edge_index's
+  // rows (k_csc_sym: slot e's endpoints are (ei[E+e], ei[e])), half the index bytes of the int64 rows
+  if (!hflag) {
+    auto dec = g->f32 ? (d.edge_out == 1   ? k_edge_dec<true, 1, int32_t>
+                         : d.edge_out == 4 ? k_edge_dec<true, 4, int32_t>
+                                           : k_edge_dec<true, 9, int32_t>)
+                      : (d.edge_out == 1   ? k_edge_dec<false, 1, int32_t>
+                         : d.edge_out == 4 ? k_edge_dec<false, 4, int32_t>
+                                           : k_edge_dec<false, 9, int32_t>);
+    hipLaunchKernelGGL(dec, dim3(tgrid(E)), dim3(256), 0, st, E, fd, static_cast<const int32_t*>(g->dst),
+                       static_cast<const int32_t*>(g->src), inv, g->ecsc, xc, out);
+  } else {
+    auto dec = g->f32 ? (d.edge_out == 1   ? k_edge_dec<true, 1, int64_t>
+                         : d.edge_out == 4 ? k_edge_dec<true, 4, int64_t>
+                                           : k_edge_dec<true, 9, int64_t>)
+                      : (d.edge_out == 1   ? k_edge_dec<false, 1, int64_t>
+                         : d.edge_out == 4 ? k_edge_dec<false, 4, int64_t>
+                                           : k_edge_dec<false, 9, int64_t>);
+    hipLaunchKernelGGL(dec, dim3(tgrid(E)), dim3(256), 0, st, E, fd, edge_index, edge_index + E, inv, g->ecsc, xc,
+                       out);
+  }
   LSPCG_HIP(hipGetLastError());
   return LSPCG_OK;
 }

@@ -1882,34 +1882,45 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
 // new L whose views land at the same addresses keeps the graphs (build_sell / make_view refill in
 // place), so a sample-by-sample loop does not re-capture every chunk size per sample.
 struct GraphKey {
-  const void* p[15];
-  int64_t i[16];
-  double eps;
-  bool operator==(const GraphKey& o) const {
-    return std::memcmp(p, o.p, sizeof(p)) == 0 && std::memcmp(i, o.i, sizeof(i)) == 0 && eps == o.eps;
-  }
+  std::vector<int64_t> v;  // pointers, kinds and sizes, in a fixed order
+  double eps = 0.0;
+  bool operator==(const GraphKey& o) const { return v == o.v && eps == o.eps; }
 };
 static GraphKey graph_key(const lspcg_solver* s) {
-  GraphKey k{};
-  int a = 0, b = 0;
+  GraphKey k;
+  auto put = [&](auto x) {
+    if constexpr (std::is_pointer<decltype(x)>::value) k.v.push_back(int64_t(reinterpret_cast<intptr_t>(x)));
+    else k.v.push_back(int64_t(x));
+  };
   for (int w = 0; w < 3; ++w) {
     const lspcg_mat& V = w == 0 ? s->Av : (w == 1 ? s->Lv : s->LTv);
-    k.p[a++] = s->sp[w];
-    k.p[a++] = s->sv[w];
-    k.p[a++] = s->slut[w];
-    k.p[a++] = V.rowptr;
-    k.p[a++] = V.vals;
-    k.i[b++] = s->svd[w];
-    k.i[b++] = V.val_dtype;
-    k.i[b++] = reinterpret_cast<intptr_t>(V.colind);
+    put(s->sp[w]);
+    if (const SellPattern* P = s->sp[w]) {  // its contents too: a rebuilt pattern may reuse the host address
+      put(P->gp);
+      put(P->col);
+      put(P->dict);
+      put(P->rowptr);
+      put(P->col_bits);
+      put(P->bs);
+      put(P->n);
+      put(P->ns);
+      put(P->groups);
+    }
+    put(s->sv[w]);
+    put(s->slut[w]);
+    put(V.rowptr);
+    put(V.colind);
+    put(V.vals);
+    put(s->svd[w]);
+    put(V.val_dtype);
   }
-  k.i[b++] = s->split;
-  k.i[b++] = s->split_cg;
-  k.i[b++] = s->gsz_l;
-  k.i[b++] = s->ng_l;
-  k.i[b++] = s->gsz_a;
-  k.i[b++] = s->ng_a;
-  k.i[b++] = s->dot_order;
+  put(s->split);
+  put(s->split_cg);
+  put(s->gsz_l);
+  put(s->ng_l);
+  put(s->gsz_a);
+  put(s->ng_a);
+  put(s->dot_order);
   k.eps = s->eps;
   return k;
 }

@@ -339,7 +339,8 @@ def test_new_spai_on_the_same_solver_equals_a_fresh_solver(gpu_ctx, monkeypatch,
     """set_spai with a new L on a solver that has solved before refills its L / Lᵀ views in place and
     keeps its captured iteration graphs when every address and ε are unchanged (GraphKey); the
     solve must equal a fresh solver's on the new L bit for bit -- also after an ε change (graphs
-    dropped) and back."""
+    dropped) and back, and through an L of another pattern (its views rebuilt: the key holds the
+    patterns' arrays, not just their host addresses)."""
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
 
     dtype = np.float32 if case == "fp32" else np.float64
@@ -361,6 +362,9 @@ def test_new_spai_on_the_same_solver_equals_a_fresh_solver(gpu_ctx, monkeypatch,
         L = _cases.spai_like(A, seed=seed)
         L.data = L.data.astype(np.float32).astype(np.float64)
         Ls.append(L)
+    Lc = Ls[1].tocoo()  # block-lower-triangular part: a pattern other than A's
+    keep = (Lc.row // bs) >= (Lc.col // bs)
+    Ls.append(sp.csr_matrix((Lc.data[keep], (Lc.row[keep], Lc.col[keep])), shape=Lc.shape))
     tdt = torch.float64 if dtype == np.float64 else torch.float32
     b = torch.from_numpy(A @ np.ones(A.shape[0])).to(tdt).cuda()
     rtol = 1e-8 if dtype == np.float64 else 1e-5
@@ -371,7 +375,8 @@ def test_new_spai_on_the_same_solver_equals_a_fresh_solver(gpu_ctx, monkeypatch,
         return it, x.cpu().numpy(), h
 
     s = PreconditionedConjugateGradient(A, device="cuda", preconditioner=pre, dtype=dtype, block_size=bs)
-    seq = [(Ls[0], 3e-3), (Ls[1], 3e-3), (Ls[1], 2e-3), (Ls[0], 3e-3)]
+    seq = [(Ls[0], 3e-3), (Ls[1], 3e-3), (Ls[1], 2e-3), (Ls[0], 3e-3), (Ls[2], 3e-3), (Ls[2], 3e-3),
+           (Ls[0], 3e-3)]
     for L, eps in seq:
         s.set_spai(L, eps, block_size=bs)
         got = run(s)
