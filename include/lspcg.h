@@ -199,7 +199,9 @@ int lspcg_solver_set_dot_order(lspcg_solver* s, int order, int threads);
  * (which switches a reordered solver back).  *applied = 1 if the solver runs permuted;
  * mean |col - row| before / after (either pointer may be NULL). */
 /* The iteration views the solver built for A (0), L (1), Lᵀ (2): col_kind[w] = 0 (staged CSR kernel),
- * 1 (SELL-DIA: no column array), 16 / 32 (SELL-64 with 16-bit / int32 columns); value_bytes[w] = 8
+ * 1 (SELL-DIA: no column array), 16 / 32 (SELL-64 with 16-bit / int32 columns), 8 (SELL-64C: one-byte
+ * codes into per-slice dictionaries of <= 64 row-relative offsets, 16-bit columns for slices with
+ * more; unstructured orderings, LSPCG_SELLC=0 turns it off); value_bytes[w] = 8
  * (fp64), 4 (fp64 matrix stored exactly as fp32), 1 (one-byte codes into a <= 256-entry dictionary
  * of the view's exact values, SELL-DIA only: matrices with few distinct values, e.g. a structured
  * grid's stencil; opt-in with LSPCG_VALUE_CODES=1: it saves memory, not time), 0 (no view).  Same bits

@@ -1315,7 +1315,8 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
     // groups with one 16-B load; slot-by-slot loads measured 16.0 vs 9.8 us per iteration at n = 900)
     const bool dia = s->dia_ok && view->n > std::min<int64_t>(s->small_n, int64_t(kSmallThreadsBig) * 3);
     const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(),
-                                      kSellCol16 | (dia ? kSellColDia : 0), st, &s->spat[w]);
+                                      kSellCol16 | (dia ? kSellColDia : 0) | (dia && sellc_allowed() ? kSellColCode : 0),
+                                      st, &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: CSR kernel
     if (rc) return rc;
     P = &s->spat[w];
@@ -1650,7 +1651,7 @@ static CsrView csr_view(const lspcg_solver* s, int w, const lspcg_mat& M) {
   CsrView v{M.rowptr, M.colind, M.vals, M.storage_dtype() == LSPCG_F32 ? 1 : 0, nullptr, nullptr, nullptr, 0, 0};
   if (const SellPattern* P = s->sp[w]) {
     // (SELL-DIA views are never built for systems this kernel solves: build_sell / lspcg_batch_create)
-    if (s->small_sell && s->sv[w] && P->bs == 1 && P->groups > 0 && P->col_bits != 1) {
+    if (s->small_sell && s->sv[w] && P->bs == 1 && P->groups > 0 && (P->col_bits == 16 || P->col_bits == 32)) {
       v.gp = P->gp;
       v.scol = P->col;
       v.sv = s->sv[w];
@@ -1899,6 +1900,8 @@ static GraphKey graph_key(const lspcg_solver* s) {
       put(P->gp);
       put(P->col);
       put(P->dict);
+      put(P->rgp);
+      put(P->col2);
       put(P->rowptr);
       put(P->col_bits);
       put(P->bs);

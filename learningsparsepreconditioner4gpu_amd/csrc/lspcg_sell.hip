@@ -155,6 +155,107 @@ __global__ void k_sdia_fill(int64_t n, int64_t ns, const int32_t* __restrict__ g
   }
 }
 
+// ---- SELL-64C (layout: lspcg_sell.hpp kSellCodeMax) ------------------------------------------
+// Dictionary of slice s: the distinct row-relative offsets col - row of its 64 rows, gathered in a
+// per-wave LDS hash set (linear probing, 256 slots), so rows need not be sorted (a reordered solver's
+// permuted rows keep their original entry order).  Entries are numbered in slot order: the order is
+// immaterial -- a code only names its offset, and slot k stays entry k of its row, so the sum order
+// is the CSR's.  dict[64 s + j] (0 past the count); raw[s] = the slice's groups when it has more
+// than kSellCodeMax offsets (kept as 16-bit offsets), else 0.
+constexpr int kSellcHash = 256;
+constexpr int kSellcEmpty = INT_MIN;  // never an offset: |col - row| < 2^31 - 1
+__global__ void __launch_bounds__(256) k_sellc_dict(int64_t n, int64_t ns, const int32_t* __restrict__ rowptr,
+                                                    const int32_t* __restrict__ colind, const int32_t* __restrict__ gp,
+                                                    int32_t* __restrict__ dict, int32_t* __restrict__ raw) {
+  __shared__ int tab[4][kSellcHash];
+  __shared__ int dd[4][kSellCodeMax];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t s = int64_t(blockIdx.x) * 4 + w;
+  if (s >= ns) return;  // wave-uniform; only this wave's tables are used below
+  for (int j = lane; j < kSellcHash; j += 64) tab[w][j] = kSellcEmpty;
+  dd[w][lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  const int64_t i = s * kSellC + lane;
+  int32_t k = 0, e = 0;
+  if (i < n) {
+    k = rowptr[i];
+    e = rowptr[i + 1];
+  }
+  bool over = false;
+  for (; k < e && !over; ++k) {
+    const int off = int(int64_t(colind[k]) - i);
+    unsigned h = (unsigned(off) * 0x9E3779B1u) >> 24;  // 8 bits: kSellcHash slots
+    int probe = 0;
+    for (; probe < kSellcHash; ++probe) {
+      const int prev = atomicCAS(&tab[w][h], kSellcEmpty, off);
+      if (prev == kSellcEmpty || prev == off) break;
+      h = (h + 1) & (kSellcHash - 1);
+    }
+    over = probe == kSellcHash;  // > 256 distinct offsets
+  }
+  __builtin_amdgcn_wave_barrier();
+  int total = 0;
+  for (int c = 0; c < kSellcHash / 64; ++c) {
+    const int v = tab[w][64 * c + lane];
+    const bool used = v != kSellcEmpty;
+    const unsigned long long bal = __ballot(used);
+    const int pos = total + __popcll(bal & ((1ull << lane) - 1ull));
+    if (used && pos < kSellCodeMax) dd[w][pos] = v;
+    total += __popcll(bal);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const bool raw_slice = __any(over) || total > kSellCodeMax;
+  dict[kSellCodeMax * s + lane] = raw_slice ? 0 : dd[w][lane];
+  if (lane == 0) raw[s] = raw_slice ? gp[s + 1] - gp[s] : 0;
+}
+
+// rgp[s] = the first col2 group of an uncoded slice (exclusive prefix of raw), -1 for a coded one
+__global__ void k_sellc_rgp(int64_t ns, const int32_t* __restrict__ raw, const int32_t* __restrict__ rscan,
+                            int32_t* __restrict__ rgp) {
+  for (int64_t s = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; s < ns; s += int64_t(gridDim.x) * blockDim.x)
+    rgp[s] = raw[s] ? rscan[s] : -1;
+}
+
+// codes (coded slices) or 16-bit offsets (the others), every slot written, in k_sell_fill's order
+__global__ void __launch_bounds__(256) k_sellc_fill(int64_t n, int64_t ns, const int32_t* __restrict__ gp,
+                                                    const int32_t* __restrict__ rowptr,
+                                                    const int32_t* __restrict__ colind, const int32_t* __restrict__ dict,
+                                                    const int32_t* __restrict__ rgp, uint8_t* __restrict__ col8,
+                                                    int16_t* __restrict__ col2) {
+  __shared__ int32_t sd[kSellCodeMax];
+  for (int64_t s = blockIdx.x; s < ns; s += gridDim.x) {
+    __syncthreads();  // the previous slice's lookups are done
+    if (threadIdx.x < kSellCodeMax) sd[threadIdx.x] = dict[kSellCodeMax * s + threadIdx.x];
+    __syncthreads();
+    const int32_t r0 = rgp[s];
+    const int64_t base = 256 * int64_t(gp[s]);
+    const int32_t slots = 256 * (gp[s + 1] - gp[s]);
+    for (int32_t p = threadIdx.x; p < slots; p += blockDim.x) {
+      const int64_t i = s * kSellC + ((p & 255) >> 2);
+      const int32_t k = 4 * (p >> 8) + (p & 3);
+      int32_t b = 0, len = 0;
+      if (i < n) {
+        b = rowptr[i];
+        len = rowptr[i + 1] - b;
+      }
+      const bool real = k < len;
+      if (r0 < 0) {
+        uint8_t code = kSellCodePad;
+        if (real) {
+          const int off = int(int64_t(colind[b + k]) - i);
+          int j = 0;
+          while (j < kSellCodeMax - 1 && sd[j] != off) ++j;  // present, once: the dictionary is the slice's set
+          code = uint8_t(j);
+        }
+        col8[base + p] = code;
+      } else {
+        col8[base + p] = kSellCodePad;
+        col2[256 * int64_t(r0) + p] = real ? int16_t(colind[b + k] - int32_t(s * kSellC)) : kSellPad16;
+      }
+    }
+  }
+}
+
 static int slice_grid(int64_t ns) { return int(std::max<int64_t>(1, std::min<int64_t>(ns, 16384))); }
 
 static int fill_grid(int64_t n) {
@@ -523,6 +624,50 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
   (void)hipFree(dgp);
   (void)hipFree(P.dict);
   P.dict = nullptr;
+  if ((cols & kSellColCode) && !fit16 && n && P.groups > 0) {
+    // SELL-64C when at least half of the slots lie in slices of <= 64 distinct offsets
+    int32_t* raw = nullptr;
+    int32_t* rscan = nullptr;
+    int32_t rawg = 0;
+    e = hipMalloc(&P.dict, sizeof(int32_t) * kSellCodeMax * P.ns);
+    if (e == hipSuccess) e = hipMalloc(&raw, sizeof(int32_t) * (P.ns + 1));
+    if (e == hipSuccess) e = hipMalloc(&rscan, sizeof(int32_t) * (P.ns + 1));
+    if (e == hipSuccess) e = hipMemsetAsync(raw, 0, sizeof(int32_t) * (P.ns + 1), st);
+    if (e == hipSuccess)
+      hipLaunchKernelGGL(k_sellc_dict, dim3(unsigned((P.ns + 3) / 4)), dim3(256), 0, st, n, P.ns, rowptr, colind, P.gp,
+                         P.dict, raw);
+    size_t tb3 = 0;
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, raw, rscan, int(P.ns + 1), st);
+    if (e == hipSuccess) e = hipMalloc(&tmp, tb3 ? tb3 : 1);
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb3, raw, rscan, int(P.ns + 1), st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&rawg, rscan + P.ns, sizeof(int32_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(tmp);
+    tmp = nullptr;
+    if (e == hipSuccess && int64_t(rawg) * 2 <= P.groups) {
+      e = hipMalloc(&P.rgp, sizeof(int32_t) * P.ns);
+      if (e == hipSuccess) e = hipMalloc(&P.col, std::max<size_t>(size_t(256) * size_t(P.groups), 1));
+      if (e == hipSuccess) e = hipMalloc(&P.col2, sizeof(int16_t) * std::max<size_t>(size_t(256) * size_t(rawg), 1));
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_sellc_rgp, dim3(fill_grid(P.ns)), dim3(kThreads), 0, st, P.ns, raw, rscan, P.rgp);
+        hipLaunchKernelGGL(k_sellc_fill, dim3(slice_grid(P.ns)), dim3(256), 0, st, n, P.ns, P.gp, rowptr, colind, P.dict,
+                           P.rgp, static_cast<uint8_t*>(P.col), P.col2);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess) e = hipStreamSynchronize(st);  // raw / rscan are freed below
+      (void)hipFree(raw);
+      (void)hipFree(rscan);
+      if (e != hipSuccess) return fail(e);
+      P.col_bits = 8;
+      *out = P;
+      return LSPCG_OK;
+    }
+    (void)hipFree(raw);
+    (void)hipFree(rscan);
+    (void)hipFree(P.dict);
+    P.dict = nullptr;
+    if (e != hipSuccess) return fail(e);
+  }
   P.col_bits = fit16 ? 32 : 16;
   // the fill writes every slot (padding included)
   const size_t cbytes = size_t(P.col_bits / 8) * size_t(std::max<int64_t>(256 * P.groups, 1));

@@ -44,6 +44,16 @@ constexpr int kSdiaMax = 16;       // slots (distinct offsets) per slice
 // column-storage choices for sell_build_pattern (bit mask); int32 columns are always possible
 constexpr int kSellCol16 = 1;
 constexpr int kSellColDia = 2;
+constexpr int kSellColCode = 4;
+// Coded SELL-64 ("SELL-64C", col_bits == 8; unstructured orderings after a bandwidth-reducing
+// permutation, where a slice's rows share few row-relative offsets col - row but more than SELL-DIA's
+// 16): SELL-64's slot layout and values, with ONE byte per slot -- the rank of the slot's offset in
+// its slice's ascending dictionary dict[64 s + j] (<= 64 entries, kSellCodePad for padding) --
+// instead of a 16-bit column offset.  The lane's dictionary entry sits in one register and a code
+// is decoded with one ds_bpermute (no LDS allocation).  Slices with more than 64 distinct offsets
+// keep 16-bit offsets in a second array: rgp[s] = their first group there (-1: coded slice).
+constexpr int kSellCodeMax = 64;
+constexpr uint8_t kSellCodePad = 0xff;
 
 // Pattern shared by every matrix with the same CSR (rowptr, colind).
 //
@@ -68,15 +78,22 @@ struct SellPattern {
   void* col = nullptr;             // [256*groups] (bs 1) / [64*groups] (bs 3) int32 columns or int16 offsets;
                                    // SELL-DIA (col_bits 1): [64*ns] uint16 row masks
   int col_bits = 32;
-  int32_t* dict = nullptr;         // SELL-DIA: [16*ns] ascending row-relative offsets per slice
+  int32_t* dict = nullptr;         // SELL-DIA: [16*ns] ascending row-relative offsets per slice;
+                                   // SELL-64C (col_bits 8): [64*ns], col = [256*groups] uint8 codes
+  int32_t* rgp = nullptr;          // SELL-64C: [ns] group start in col2 of a slice kept uncoded, or -1
+  int16_t* col2 = nullptr;         // SELL-64C: 16-bit offsets of the uncoded slices
   const int32_t* rowptr = nullptr; // CSR row pointer (row lengths), not owned
   void release() {
     (void)hipFree(gp);
     (void)hipFree(col);
     (void)hipFree(dict);
+    (void)hipFree(rgp);
+    (void)hipFree(col2);
     gp = nullptr;
     col = nullptr;
     dict = nullptr;
+    rgp = nullptr;
+    col2 = nullptr;
   }
 };
 
@@ -88,6 +105,9 @@ struct SellArgs {
   const CT* col;
   const int32_t* rowptr;
   const VT* vals;
+  const int32_t* dict = nullptr;  // SELL-64C (CT = uint8_t): see kSellCodeMax
+  const int32_t* rgp = nullptr;
+  const int16_t* col2 = nullptr;
 };
 
 template <typename VT>
@@ -141,15 +161,21 @@ template <typename T, typename VT, typename CT, int QB, int TH, int MINW, class 
 __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
   constexpr bool C16 = std::is_same<CT, int16_t>::value;
+  constexpr bool C8 = std::is_same<CT, uint8_t>::value;  // SELL-64C
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int64_t ntiles = (a.n + TH - 1) / TH;
   // the first tile's slice range is loaded before the prologue's state read, so the two
   // dependent-free loads share one memory latency (the state line was written by another CU)
   int32_t gb[2] = {0, 0};
+  [[maybe_unused]] int32_t rg = -1, dl = 0;  // SELL-64C: uncoded group start, this lane's dictionary entry
   if (int64_t(blockIdx.x) * (TH / 64) + w < a.ns) {
     gb[0] = a.gp[int64_t(blockIdx.x) * (TH / 64) + w];
     gb[1] = a.gp[int64_t(blockIdx.x) * (TH / 64) + w + 1];
+    if constexpr (C8) {
+      rg = a.rgp[int64_t(blockIdx.x) * (TH / 64) + w];
+      dl = a.dict[kSellCodeMax * (int64_t(blockIdx.x) * (TH / 64) + w) + lane];
+    }
   }
   if (pro.exit()) return;
   gx.prepare();
@@ -164,12 +190,17 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
       if (tile != int64_t(blockIdx.x)) {
         gb[0] = a.gp[s];
         gb[1] = a.gp[s + 1];
+        if constexpr (C8) {
+          rg = a.rgp[s];
+          dl = a.dict[kSellCodeMax * s + lane];
+        }
       }
       const int32_t g0 = gb[0];
       const int nq = gb[1] - g0;
       const int32_t base = int32_t(s * kSellC);
       const VT* vp = a.vals + 256 * int64_t(g0) + 4 * lane;
       const CT* cp = a.col + 256 * int64_t(g0) + 4 * lane;
+      [[maybe_unused]] const int16_t* cp2 = C8 ? a.col2 + 256 * int64_t(rg) + 4 * lane : nullptr;
       T acc = T(0);
       T pf = T(0);
       if constexpr (epi_prefetch<Epi>::value) {
@@ -183,7 +214,26 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
         for (int u = 0; u < QB; ++u) {
           const int q = min(q0 + u, nq - 1);
           Vec4Ld<VT>::load(vp + 256 * q, v[u]);
-          if constexpr (C16) {
+          if constexpr (C8) {
+            if (rg < 0) {  // wave-uniform: a coded slice
+              const unsigned cc = *(const __attribute__((address_space(1))) unsigned*)(cp + 256 * q);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const unsigned b = (cc >> (8 * j)) & 0xffu;
+                const int off = __builtin_amdgcn_ds_bpermute(int((b & 63u) << 2), dl);
+                m[u][j] = (b != kSellCodePad) && (q0 + u < nq);
+                c[u][j] = b != kSellCodePad ? base + lane + off : base;  // padding gathers row base
+              }
+            } else {
+              const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(cp2 + 256 * q);
+              const int o[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                m[u][j] = (o[j] != kSellPad16) && (q0 + u < nq);
+                c[u][j] = base + (o[j] != kSellPad16 ? o[j] : 0);
+              }
+            }
+          } else if constexpr (C16) {
             const i16x4 cc = *(const __attribute__((address_space(1))) i16x4*)(cp + 256 * q);
             const int o[4] = {cc.x, cc.y, cc.z, cc.w};
 #pragma unroll
@@ -536,10 +586,11 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
   // that tile's and its prologue may test the tile's own system
   if (!one_tile_per_wg) grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
-  SellArgs<VT, CT> a{P.n, P.ns, P.gp, static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
+  SellArgs<VT, CT> a{P.n,      P.ns,  P.gp,  static_cast<const CT*>(P.col), P.rowptr, static_cast<const VT*>(vals),
+                     P.dict, P.rgp, P.col2};
   // compact-value kernels: registers for 6 workgroups per CU (the resident reducing grid)
   constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? (TH <= 1536 ? 1536 / TH : 1) : 1;
-  if constexpr (!std::is_same<CT, uint16_t>::value) {  // BSELL-64 has no dictionary columns
+  if constexpr (!std::is_same<CT, uint16_t>::value && !std::is_same<CT, uint8_t>::value) {  // BSELL-64: int16 / int32 columns
     if (P.bs == 3) {
       // 2 block slots (18 values, 6 gathers) per batch
       LSPCG_LAUNCH_SPMV((k_spmv_bsell3<T, VT, CT, 2, TH, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(TH), 0, st,
@@ -598,6 +649,7 @@ inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, 
   if (P.col_bits == 1 && P.bs == 3) launch_spmv_bsdia3<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 1) launch_spmv_sdia<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
+  else if (P.col_bits == 8) launch_spmv_sell_th<T, VT, uint8_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else launch_spmv_sell_th<T, VT, int32_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
 }
 
@@ -618,9 +670,11 @@ namespace lspcg {
 // Host-side construction (lspcg_sell.hip), enqueued on `st`.
 // Builds the SELL-64 pattern of a scalar CSR (n rows); fails with LSPCG_ERR_UNSUPPORTED when the
 // padded size exceeds max_pad x nnz (irregular row lengths: the CSR kernel is used instead).
-// cols (kSellCol16 | kSellColDia): the column storages allowed besides int32; SELL-DIA is taken
-// when every slice has <= 16 distinct offsets, every row is sorted and it stores no more slots
-// than the 4-entry groups would, else 16-bit offsets when they fit.
+// cols (kSellCol16 | kSellColDia | kSellColCode): the column storages allowed besides int32; SELL-DIA
+// is taken when every slice has <= 16 distinct offsets, every row is sorted and it stores no more
+// slots than the 4-entry groups would, else (kSellColCode, 16-bit offsets fit, rows sorted) SELL-64C
+// when at least half of the slots fall in slices of <= 64 distinct offsets, else 16-bit offsets
+// when they fit.
 int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int32_t* colind, double max_pad,
                        int cols, hipStream_t st, SellPattern* out);
 // Allocates and fills the SELL value array of a CSR with the same pattern (*out == nullptr), or
@@ -634,6 +688,11 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
 // stores at most 1/16 more block slots than BSELL-64 (env LSPCG_BSDIA=0 turns it off: bsdia_allowed()).
 int bsell_build_pattern(int64_t nb, int64_t nnzb, const int32_t* rowptr, const int32_t* colind, double max_pad,
                         bool allow16, bool allow_dia, hipStream_t st, SellPattern* out);
+// SELL-64C for the solver's large views (env LSPCG_SELLC=0 turns it off)
+inline bool sellc_allowed() {
+  const char* e = std::getenv("LSPCG_SELLC");
+  return !(e && e[0] == '0');
+}
 inline bool bsdia_allowed() {
   const char* e = std::getenv("LSPCG_BSDIA");
   return !(e && e[0] == '0');

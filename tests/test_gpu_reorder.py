@@ -329,3 +329,77 @@ def test_device_rcm_leaves_unsorted_or_repeated_rows_in_order(gpu_ctx):
         Bd = DeviceMatrix.from_scipy(B, dtype=np.float64, keep_order=True)
         perm, before, after = Bd.rcm()
         assert perm is None and after == before, how
+
+
+def _hubbed(A, hubs=6, far=80, seed=5):
+    """A plus a few rows with `far` long-range symmetric couplings each (diagonally compensated, so
+    still SPD): their slices hold more than 64 distinct offsets and stay uncoded in SELL-64C."""
+    rng = np.random.default_rng(seed)
+    n = A.shape[0]
+    rows = np.repeat(np.linspace(0, n - 1, hubs).astype(np.int64), far)
+    cols = rng.integers(0, n, rows.size)
+    keep = rows != cols
+    S = sp.csr_matrix((np.full(keep.sum(), -2.0 ** -10), (rows[keep], cols[keep])), shape=A.shape)
+    S = S + S.T
+    S = S + sp.diags(np.asarray(abs(S).sum(axis=1)).ravel())
+    B = sp.csr_matrix(A + S)
+    B.sum_duplicates()
+    B.sort_indices()
+    return B
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("pre", ["none", "ext_spai"])
+@pytest.mark.parametrize("kind", ["rcm", "rcm_hubs", "rcm_unsorted"])
+def test_sellc_views_equal_sell16_and_csr(gpu_ctx, monkeypatch, kind, pre, dtype):
+    """SELL-64C (one-byte codes into per-slice offset dictionaries, 16-bit offsets for slices with
+    more than 64) sums every row in the CSR order: the solve equals the 16-bit SELL-64 views' and the
+    staged CSR kernel's bit for bit, and the oracle's.  rcm_unsorted: every row of A stored in a
+    shuffled entry order (as a reordered solver's permuted rows are), summed in that order by all
+    three paths and by scipy."""
+    A, m = P.renumber(*P.kuhn_dirichlet(27), "rcm")
+    A = sp.csr_matrix(A)
+    A.sort_indices()
+    if kind == "rcm_hubs":
+        A = _hubbed(A)
+    A.data = A.data.astype(np.float32).astype(np.float64)
+    L = _cases.spai_like(A, seed=4)
+    L.data = L.data.astype(np.float32).astype(np.float64)
+    if kind == "rcm_unsorted":
+        rng = np.random.default_rng(9)
+        idx, dat = A.indices.copy(), A.data.copy()
+        for i in range(A.shape[0]):
+            p = A.indptr[i] + rng.permutation(A.indptr[i + 1] - A.indptr[i])
+            idx[A.indptr[i]:A.indptr[i + 1]], dat[A.indptr[i]:A.indptr[i + 1]] = A.indices[p], A.data[p]
+        A = sp.csr_matrix((dat, idx, A.indptr.copy()), shape=A.shape)
+        assert not A.has_sorted_indices
+    b = A @ np.asarray(m, dtype=np.float64).ravel()
+    monkeypatch.setenv("LSPCG_REORDER", "0")
+    rtol = 1e-8 if dtype == np.float64 else 1e-5
+    runs = {}
+    for name, env in (("sellc", {"LSPCG_SELLC": "1"}), ("sell16", {"LSPCG_SELLC": "0"}), ("csr", {"LSPCG_NO_SELL": "1"})):
+        for k in ("LSPCG_SELLC", "LSPCG_NO_SELL"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        Ad = A
+        if kind == "rcm_unsorted":  # upload the rows in their stored order (from_scipy sorts by default)
+            from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+            Ad = DeviceMatrix.from_scipy(A, dtype=dtype, keep_order=True)
+        s = _solver(Ad, L, pre, dtype=dtype)
+        views = s.views
+        want = "csr" if name == "csr" else name
+        assert views["A"]["columns"] == want, (name, views)
+        if pre == "ext_spai":
+            assert views["L"]["columns"] == want and views["LT"]["columns"] == want, (name, views)
+        runs[name] = _run(s, b, rtol=rtol, dtype=dtype)
+        del s
+    it, conv, x, h = runs["sellc"]
+    assert conv
+    for other in ("sell16", "csr"):
+        it2, conv2, x2, h2 = runs[other]
+        assert it == it2 and np.array_equal(x, x2) and np.array_equal(h, h2), (kind, pre, other)
+    if dtype == np.float64:
+        it_o, x_o, _ = O.pcg(A, b, O.spai_operator(L, 3e-3) if pre == "ext_spai" else None, rtol=1e-8, dot="exact")
+        assert it == it_o and np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
