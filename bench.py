@@ -100,6 +100,7 @@ def reduce_timing(elapsed: float, iters: float, device) -> tuple:
 
 KERNEL_NAME = {1: "k_spmv_sdia", 16: "k_spmv_sell<int16 columns>", 32: "k_spmv_sell<int32 columns>"}
 KIND_TEXT = {1: "SELL-DIA: one slot per distinct row-relative offset of the 64-row slice, 2-B row masks, no columns",
+             8: "SELL-64C: one-byte codes into per-slice dictionaries of <= 64 row-relative offsets",
              16: "16-bit column offsets", 32: "int32 columns"}
 
 
@@ -359,7 +360,7 @@ def irregular_row(workload: str, eps: float, rtol: float, reps: int) -> dict:
             "solver_reorder": s.reorder_info, "solver_setup_ms": setup_ms,
             "distinct_offsets_per_slice": {"mean": float(dc.mean()), "max": int(dc.max())},
             "bandwidth": int(np.abs(Ah.indices - np.repeat(np.arange(A.n), np.diff(Ah.indptr))).max()),
-            "column_storage": KIND_TEXT[kind_loop], "iters": it, "converged": bool(conv),
+            "spmv_column_storage": KIND_TEXT[kind_loop], "solver_views": s.views, "iters": it, "converged": bool(conv),
             "time_to_rtol_ms": med * 1e3, "pcg_iter_us": med / it * 1e6,
             "loop_kernels_us": {k: v * 1e6 for k, v in loop.items()},
             "spmv": {"kernel": f"{KERNEL_NAME.get(kind, 'k_spmv')}<double,double>", "avg_launch_ms_cold": cold,

@@ -1315,7 +1315,7 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
     // groups with one 16-B load; slot-by-slot loads measured 16.0 vs 9.8 us per iteration at n = 900)
     const bool dia = s->dia_ok && view->n > std::min<int64_t>(s->small_n, int64_t(kSmallThreadsBig) * 3);
     const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(),
-                                      kSellCol16 | (dia ? kSellColDia : 0) | (dia && sellc_allowed() ? kSellColCode : 0),
+                                      kSellCol16 | (dia ? kSellColDia : 0) | (dia && sellc_allowed(view->n) ? kSellColCode : 0),
                                       st, &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: CSR kernel
     if (rc) return rc;

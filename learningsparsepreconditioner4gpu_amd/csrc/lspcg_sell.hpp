@@ -688,10 +688,16 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
 // stores at most 1/16 more block slots than BSELL-64 (env LSPCG_BSDIA=0 turns it off: bsdia_allowed()).
 int bsell_build_pattern(int64_t nb, int64_t nnzb, const int32_t* rowptr, const int32_t* colind, double max_pad,
                         bool allow16, bool allow_dia, hipStream_t st, SellPattern* out);
-// SELL-64C for the solver's large views (env LSPCG_SELLC=0 turns it off)
-inline bool sellc_allowed() {
+// SELL-64C for the solver's views of >= LSPCG_SELLC_MIN_N rows (env LSPCG_SELLC=0 turns it off): the
+// byte codes pay where the loop streams matrix bytes; below, the decode's ds_bpermute in the gathers'
+// dependency chain costs more than the bytes save (us per iteration, SELL-64C vs 16-bit: bunny 6.3 k
+// rows 17.4 vs 16.6, kuhn41rcm 69 k 28.6 vs 27.1, kuhn64rcm 262 k 37.7 vs 37.4, kuhn80rcm 512 k 53.0 vs
+// 55.5, kuhn101rcm 1 M 86.7 vs 90.2)
+inline bool sellc_allowed(int64_t n) {
   const char* e = std::getenv("LSPCG_SELLC");
-  return !(e && e[0] == '0');
+  if (e && e[0] == '0') return false;
+  const char* m = std::getenv("LSPCG_SELLC_MIN_N");
+  return n >= (m ? std::atoll(m) : int64_t(400000));
 }
 inline bool bsdia_allowed() {
   const char* e = std::getenv("LSPCG_BSDIA");

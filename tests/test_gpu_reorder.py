@@ -377,8 +377,10 @@ def test_sellc_views_equal_sell16_and_csr(gpu_ctx, monkeypatch, kind, pre, dtype
     monkeypatch.setenv("LSPCG_REORDER", "0")
     rtol = 1e-8 if dtype == np.float64 else 1e-5
     runs = {}
-    for name, env in (("sellc", {"LSPCG_SELLC": "1"}), ("sell16", {"LSPCG_SELLC": "0"}), ("csr", {"LSPCG_NO_SELL": "1"})):
-        for k in ("LSPCG_SELLC", "LSPCG_NO_SELL"):
+    variants = (("sellc", {"LSPCG_SELLC": "1", "LSPCG_SELLC_MIN_N": "0"}),  # (the default takes >= 2^19 rows)
+                ("sell16", {"LSPCG_SELLC": "0"}), ("csr", {"LSPCG_NO_SELL": "1"}))
+    for name, env in variants:
+        for k in ("LSPCG_SELLC", "LSPCG_SELLC_MIN_N", "LSPCG_NO_SELL"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
