@@ -330,19 +330,44 @@ __global__ void __launch_bounds__(256) k_rcm_count(int lv, const int32_t* __rest
   if (threadIdx.x == 0) psum[blockIdx.x] = total;
 }
 
+// the next level's step 1 for one of its nodes, v = next[fn], run by the thread that emits v: its
+// neighbours neither placed nor in v's own level (stamped `stamp` by this level's step 1; some of
+// them may still be unplaced while this kernel runs) get pkey = min(pkey, fn), mark = stamp_next --
+// the same sets and keys as k_rcm_expand over the finished level (round 5: one launch per level
+// fewer)
+__device__ __forceinline__ void rcm_expand_one(int32_t v, int32_t fn, const int32_t* __restrict__ rp,
+                                               const int32_t* __restrict__ ci, const int32_t* __restrict__ pos,
+                                               int32_t* __restrict__ pkey, int32_t* __restrict__ mark, int32_t stamp,
+                                               int32_t stamp_next) {
+  const int32_t e = rp[v + 1];
+  for (int32_t k0 = rp[v]; k0 < e; k0 += kRcmChunk) {
+    RowChunk r;
+    r.load(ci, k0, e);
+    int32_t ps[kRcmChunk], mk[kRcmChunk];
+    r.gather(pos, ps);
+    r.gather(mark, mk);
+#pragma unroll
+    for (int j = 0; j < kRcmChunk; ++j)
+      if (j < r.cnt && ps[j] == -1 && mk[j] != stamp) {
+        atomicMin(&pkey[r.v[j]], fn);
+        mark[r.v[j]] = stamp_next;
+      }
+  }
+}
+
 // step 3: each parent writes its owned children by (degree, index) to next[off ..] and places them
 // at lvbase[lv] + m + off + j, off = the totals of the parts before its own (summed by every
 // workgroup from psum) + the prefix of cnt inside the part; workgroup 0 publishes the next level's
-// size and base
+// size and base.  Then step 1 of the next level for each child (rcm_expand_one).
 __global__ void __launch_bounds__(256) k_rcm_emit(int lv, const int32_t* __restrict__ lvm,
                                                   const int32_t* __restrict__ lvbase, const int32_t* __restrict__ frontier,
                                                   const int32_t* __restrict__ rp, const int32_t* __restrict__ ci,
-                                                  const int32_t* __restrict__ deg, const int32_t* __restrict__ pkey,
-                                                  const int32_t* __restrict__ mark, int32_t stamp,
+                                                  const int32_t* __restrict__ deg, int32_t* __restrict__ pkey,
+                                                  int32_t* __restrict__ mark, int32_t stamp,
                                                   const int32_t* __restrict__ cnt, const int32_t* __restrict__ psum,
                                                   int32_t* __restrict__ next, int32_t* __restrict__ pos,
                                                   int32_t* __restrict__ order, int32_t* __restrict__ lvm_next,
-                                                  int32_t* __restrict__ lvbase_next) {
+                                                  int32_t* __restrict__ lvbase_next, int fuse) {
   __shared__ int32_t sh[256];
   const int64_t m = lvm[lv];
   int64_t lo, hi;
@@ -392,6 +417,8 @@ __global__ void __launch_bounds__(256) k_rcm_emit(int lv, const int32_t* __restr
         order[base + o + j] = v;
         last = best;
       }
+      if (fuse)
+        for (int32_t j = 0; j < c; ++j) rcm_expand_one(next[o + j], o + j, rp, ci, pos, pkey, mark, stamp, stamp + 1);
       continue;
     }
     for (int32_t j = 0; j < c; ++j) {
@@ -408,6 +435,8 @@ __global__ void __launch_bounds__(256) k_rcm_emit(int lv, const int32_t* __restr
       order[base + o + j] = v;
       last = best;
     }
+    if (fuse)
+      for (int32_t j = 0; j < c; ++j) rcm_expand_one(next[o + j], o + j, rp, ci, pos, pkey, mark, stamp, stamp + 1);
   }
 }
 
@@ -583,17 +612,27 @@ static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
       LSPCG_HIP(hipMemcpyAsync(lvm + lv, &h0[0], sizeof(int32_t), hipMemcpyHostToDevice, st));
       LSPCG_HIP(hipMemcpyAsync(lvbase + lv, &h0[1], sizeof(int32_t), hipMemcpyHostToDevice, st));
       hipLaunchKernelGGL(k_rcm_place, dim3(1), dim3(64), 0, st, int64_t(1), fa, placed, pos, order);
+      // step 1 of level 0; every later level's runs inside the previous level's emit, stamped one
+      // past that level's stamp
+      // (LSPCG_RCM_FUSE=0: a k_rcm_expand launch per level, as before round 5's fold)
+      static const int fuse = [] {
+        const char* e = std::getenv("LSPCG_RCM_FUSE");
+        return e && e[0] == '0' ? 0 : 1;
+      }();
+      if (fuse)
+        hipLaunchKernelGGL(k_rcm_expand, dim3(lg), dim3(kThreads), 0, st, lv, lvm, fa, rp, ci, pos, pkey, mark, ++stamp);
       int l0 = 0, last = -1;
       while (last < 0) {
         for (int l = l0; l < l0 + kRcmBatch; ++l) {
-          const int32_t sl = ++stamp;
+          const int32_t sl = fuse ? stamp++ : ++stamp;  // level l's stamp; a fused emit stamps level l + 2's nodes sl + 1
           const int32_t* cur = (l & 1) ? fb : fa;
           int32_t* nxt = (l & 1) ? fa : fb;
-          hipLaunchKernelGGL(k_rcm_expand, dim3(lg), dim3(kThreads), 0, st, lv + l, lvm, cur, rp, ci, pos, pkey, mark, sl);
+          if (!fuse)
+            hipLaunchKernelGGL(k_rcm_expand, dim3(lg), dim3(kThreads), 0, st, lv + l, lvm, cur, rp, ci, pos, pkey, mark, sl);
           hipLaunchKernelGGL(k_rcm_count, dim3(kRcmParts), dim3(256), 0, st, lv + l, lvm, cur, rp, ci, pkey, mark, sl,
                              cnt, parts);
           hipLaunchKernelGGL(k_rcm_emit, dim3(kRcmParts), dim3(256), 0, st, lv + l, lvm, lvbase, cur, rp, ci, deg, pkey,
-                             mark, sl, cnt, parts, nxt, pos, order, lvm + lv + l + 1, lvbase + lv + l + 1);
+                             mark, sl, cnt, parts, nxt, pos, order, lvm + lv + l + 1, lvbase + lv + l + 1, fuse);
         }
         LSPCG_HIP(hipMemcpyAsync(hb.data(), lvm + lv + l0, sizeof(int32_t) * (kRcmBatch + 1), hipMemcpyDeviceToHost, st));
         LSPCG_HIP(hipStreamSynchronize(st));
