@@ -98,10 +98,19 @@ def reduce_timing(elapsed: float, iters: float, device) -> tuple:
     return float(mx[0]), float(sm[0])
 
 
-KERNEL_NAME = {1: "k_spmv_sdia", 16: "k_spmv_sell<int16 columns>", 32: "k_spmv_sell<int32 columns>"}
+KERNEL_NAME = {1: "k_spmv_sdia", 16: "k_spmv_sell<int16 columns>", 17: "k_spmv_sellj", 18: "k_spmv_sellj<XS>",
+               32: "k_spmv_sell<int32 columns>"}
 KIND_TEXT = {1: "SELL-DIA: one slot per distinct row-relative offset of the 64-row slice, 2-B row masks, no columns",
              8: "SELL-64C: one-byte codes into per-slice dictionaries of <= 64 row-relative offsets",
-             16: "16-bit column offsets", 32: "int32 columns"}
+             16: "16-bit column offsets",
+             17: "SELL-64J: lanes sorted by row length inside each 64-row slice, groups stored for their active "
+                 "lanes only, 16-bit column offsets",
+             18: "SELL-64X: SELL-64J whose 16-bit column words index an LDS copy of the 256-row tile's x blocks "
+                 "(16 entries each, loaded once per tile)",
+             32: "int32 columns"}
+JAG_PAD = 1.15  # csrc/lspcg_sell.hpp kSellJagPad
+XS_MAX = 256    # csrc/lspcg_sell.hpp kSellXMax: x blocks per 256-row tile
+XS_MIN_N = 262144  # csrc/lspcg_sell.hpp kSellXMinN
 
 
 def sell_slots(indptr: np.ndarray) -> int:
@@ -114,6 +123,20 @@ def sell_slots(indptr: np.ndarray) -> int:
     return int(256 * ((pad.reshape(ns, 64).max(axis=1) + 3) // 4).sum())
 
 
+def jag_elems(indptr: np.ndarray) -> int:
+    """Stored entries of the SELL-64J layout (csrc/lspcg_sell.hpp kSellJag): every row's entries
+    rounded up to whole 4-entry groups (a group stores only the lanes whose rows reach it)."""
+    return int(4 * ((np.diff(indptr) + 3) // 4).sum())
+
+
+def xs_blocks(indptr: np.ndarray, indices: np.ndarray) -> np.ndarray:
+    """Distinct 16-entry x blocks (col // 16) each 256-row tile reads (the SELL-64X staged lists)."""
+    n = indptr.size - 1
+    rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
+    key = np.unique((rows // 256) * (1 << 32) + indices.astype(np.int64) // 16)
+    return np.bincount(key >> 32, minlength=(n + 255) // 256)
+
+
 def dia_counts(indptr: np.ndarray, indices: np.ndarray) -> np.ndarray:
     """Distinct row-relative offsets col - row per 64-row slice (SELL-DIA slots per row)."""
     n = indptr.size - 1
@@ -124,8 +147,9 @@ def dia_counts(indptr: np.ndarray, indices: np.ndarray) -> np.ndarray:
 
 def sell_kind(indptr: np.ndarray, indices: np.ndarray) -> int:
     """Column storage the SELL-64 build picks (csrc/lspcg_sell.hip, sorted rows): 1 = SELL-DIA
-    (<= 16 distinct offsets col - row per 64-row slice, no more slots than 4-entry groups), 16 =
-    16-bit offsets from the slice's first row, 32 = int32 columns."""
+    (<= 16 distinct offsets col - row per 64-row slice, no more slots than 4-entry groups), 17 =
+    SELL-64J (16-bit offsets, SELL-64 would pad more than JAG_PAD x nnz, no row beyond 64 entries),
+    16 = 16-bit offsets from the slice's first row, 32 = int32 columns."""
     n = indptr.size - 1
     rows = np.repeat(np.arange(n, dtype=np.int64), np.diff(indptr))
     if rows.size == 0:
@@ -133,16 +157,25 @@ def sell_kind(indptr: np.ndarray, indices: np.ndarray) -> int:
     d = dia_counts(indptr, indices)
     if d.max() <= 16 and 64 * d.sum() <= sell_slots(indptr):
         return 1
-    return 16 if np.all(np.abs(indices.astype(np.int64) - (rows // 64) * 64) <= 32767) else 32
+    if not np.all(np.abs(indices.astype(np.int64) - (rows // 64) * 64) <= 32767):
+        return 32
+    if sell_slots(indptr) > JAG_PAD * rows.size and np.diff(indptr).max() <= 64:
+        return 18 if n >= XS_MIN_N and xs_blocks(indptr, indices).max() <= XS_MAX else 17
+    return 16
 
 
 def sell_format_bytes(indptr: np.ndarray, indices: np.ndarray, kind: int, value_bytes: int) -> int:
     """Matrix bytes one SELL-64 SpMV streams.  SELL-DIA: 64 x D_s value slots per slice + the 2-B row
     masks (128 B per slice) + the slice's 16-entry int32 offset dictionary (64 B); otherwise every
     stored slot's value and column (2 B offset or 4 B index)."""
+    ns = (indptr.size + 62) // 64
     if kind == 1:
-        ns = (indptr.size + 62) // 64
         return int(64 * dia_counts(indptr, indices).sum() * value_bytes) + ns * (128 + 64)
+    if kind == 17:  # + the lane -> row bytes (64) and group counts (16) per slice
+        return int(jag_elems(indptr) * (value_bytes + 2)) + ns * (64 + 16)
+    if kind == 18:  # + the tiles' block lists (4 B per block, 4 B per tile)
+        return (int(jag_elems(indptr) * (value_bytes + 2)) + ns * (64 + 16)
+                + 4 * int(xs_blocks(indptr, indices).sum()) + 4 * ((indptr.size + 254) // 256))
     return int(sell_slots(indptr) * (value_bytes + {16: 2, 32: 4}[kind]))
 
 
@@ -157,7 +190,8 @@ def pcg_loop_spmv(A, p, q, reps: int, kind: int) -> dict:
     out = {}
     for label, flush in (("cold", FLUSH_BYTES), ("warm", 0)):
         ms = C.c_double()
-        _lib.call("lspcg_spmv_sell_timed", A.ctx.handle, A.handle, 3 | (8 if kind == 1 else 0), C.c_void_p(p.data_ptr()),
+        _lib.call("lspcg_spmv_sell_timed", A.ctx.handle, A.handle, 3 | (8 if kind == 1 else 0) | (16 if kind in (17, 18) else 0) | (32 if kind == 18 else 0),
+                  C.c_void_p(p.data_ptr()),
                   C.c_void_p(q.data_ptr()), reps if flush else 3 * reps, flush, C.byref(ms))
         out[label] = ms.value
     As = A.to_scipy()
@@ -354,9 +388,15 @@ def irregular_row(workload: str, eps: float, rtol: float, reps: int) -> dict:
     warm = A.spmv_timed(p, q, 3 * reps)
     alg = spmv_bytes(A.n, A.nnz)
     dc = dia_counts(Ah.indptr, Ah.indices)
-    how = "random symmetric permutation + RCM" if workload.endswith("rcm") else "random symmetric permutation"
-    return {"workload": f"{workload}: the headline system renumbered ({how}), "
-                        f"n={A.n}, nnz={A.nnz}, ext_spai, rtol {rtol:g}",
+    how = ("random symmetric permutation + RCM" if workload.endswith("rcm") else
+           "random symmetric permutation" if workload.endswith("rand") else "the generator's spatial bucket order")
+    what = ("the unstructured Delaunay heat system (problems.delaunay_heat: qhull tets of a seeded uniform point "
+            "cloud, P1 Laplacian + lumped mass, heat_tetmesh.py)" if workload.startswith("delaunay")
+            else "the headline system renumbered")
+    lens = np.diff(Ah.indptr)
+    return {"workload": f"{workload}: {what} ({how}), n={A.n}, nnz={A.nnz}, ext_spai, rtol {rtol:g}",
+            "row_entries": {"mean": float(lens.mean()), "min": int(lens.min()), "max": int(lens.max())},
+            "sell_slots_per_nnz": sell_slots(Ah.indptr) / max(A.nnz, 1),
             "solver_reorder": s.reorder_info, "solver_setup_ms": setup_ms,
             "distinct_offsets_per_slice": {"mean": float(dc.mean()), "max": int(dc.max())},
             "bandwidth": int(np.abs(Ah.indices - np.repeat(np.arange(A.n), np.diff(Ah.indptr))).max()),

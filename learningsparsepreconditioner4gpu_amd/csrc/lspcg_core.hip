@@ -520,7 +520,8 @@ int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind) {
   const bool blk = A->block_size == 3;  // BSR 3x3: the BSELL-64 block layout
   int rc = blk ? bsell_build_pattern(A->nb, A->nnzb, A->rowptr, A->colind, sell_max_pad(), true, bsdia_allowed(), st,
                                      &c->P)
-               : sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, sell_max_pad(), kSellCol16 | kSellColDia, st,
+               : sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, sell_max_pad(),
+                                    kSellCol16 | kSellColDia | kSellColJag | kSellColXs, st,
                                     &c->P);
   if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // irregular rows: the CSR / BSR kernel stays
   if (rc) return rc;
@@ -696,8 +697,9 @@ int lspcg_spmv_sell_timed(lspcg_ctx* ctx, const lspcg_mat* A, int compact, const
               LSPCG_ERR_ARG, "spmv_sell_timed: fp64 scalar CSR required");
   hipStream_t st = ctx->stream;
   SellPattern P;
-  // any padding; compact bit 1: 16-bit offsets allowed, bit 3: SELL-DIA allowed
-  const int cols = ((compact & 2) ? kSellCol16 : 0) | ((compact & 8) ? kSellColDia : 0);
+  // any padding; compact bit 1: 16-bit offsets allowed, bit 3: SELL-DIA allowed, bit 4: SELL-64J allowed, bit 5: SELL-64X allowed
+  const int cols = ((compact & 2) ? kSellCol16 : 0) | ((compact & 8) ? kSellColDia : 0) |
+                   ((compact & 16) ? kSellColJag : 0) | ((compact & 32) && !(compact & 4) ? kSellColXs : 0);
   int rc = sell_build_pattern(A->n, A->nnzb, A->rowptr, A->colind, 1e30, cols, st, &P);
   if (rc) return rc;
   void* v = nullptr;

@@ -1241,6 +1241,7 @@ struct lspcg_solver {
   const SellPattern* sp[3] = {nullptr, nullptr, nullptr};
   void* sv[3] = {nullptr, nullptr, nullptr};
   int svd[3] = {0, 0, 0};  // storage of sv[w]: LSPCG_F32 / LSPCG_F64, or kValCode8 (1-byte dictionary codes)
+  int64_t svn[3] = {0, 0, 0};  // entries sv[w] was allocated for (an in-place refill must fit them)
   float* slut[3] = {nullptr, nullptr, nullptr};  // the dictionary of a coded view (256 floats)
   bool codes_ok = false;   // value dictionaries allowed (single solves; LSPCG_VALUE_CODES=0 turns them off)
   double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
@@ -1291,8 +1292,11 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   if (s->sv[w] || s->spat[w].gp) LSPCG_HIP(hipStreamSynchronize(s->stream));  // a solve may use them
   // L / Lᵀ on A's pattern again (a new L for the same system): refill the value array in place, so
   // its address -- and with it every captured iteration graph -- stays valid (get_graph)
+  // (the pattern may have been rebuilt at the same host address -- set_dot_order's switch back to the
+  // unpermuted A -- so the array's entry count must match the pattern's, not just the pointers)
   if (w > 0 && s->use_sell && s->sv[w] && !s->slut[w] && s->sp[w] && s->sp[w] == s->sp[0] &&
-      view->rowptr == s->Av.rowptr && view->colind == s->Av.colind && view->storage_dtype() == s->svd[w]) {
+      view->rowptr == s->Av.rowptr && view->colind == s->Av.colind && view->storage_dtype() == s->svd[w] &&
+      s->svn[w] == s->sp[w]->slots()) {
     const SellPattern* P = s->sp[w];
     const int vd = view->storage_dtype();
     return P->bs == 3 ? bsell_fill_values(*P, view->vals, vd, vd, st, &s->sv[w])
@@ -1315,7 +1319,8 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
     // groups with one 16-B load; slot-by-slot loads measured 16.0 vs 9.8 us per iteration at n = 900)
     const bool dia = s->dia_ok && view->n > std::min<int64_t>(s->small_n, int64_t(kSmallThreadsBig) * 3);
     const int rc = sell_build_pattern(view->n, view->nnzb, view->rowptr, view->colind, sell_max_pad(),
-                                      kSellCol16 | (dia ? kSellColDia : 0) | (dia && sellc_allowed(view->n) ? kSellColCode : 0),
+                                      kSellCol16 | (dia ? kSellColDia | kSellColJag | kSellColXs : 0) |
+                                          (dia && sellc_allowed(view->n) ? kSellColCode : 0),
                                       st, &s->spat[w]);
     if (rc == LSPCG_ERR_UNSUPPORTED) return LSPCG_OK;  // padding too large: CSR kernel
     if (rc) return rc;
@@ -1324,6 +1329,7 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   const int vd = view->storage_dtype();
   if (int rc = sell_fill_values(*P, view->colind, view->vals, vd, vd, st, &s->sv[w])) return rc;
   s->svd[w] = vd;
+  s->svn[w] = P->slots();
   s->sp[w] = P;
   if (s->codes_ok && P->col_bits == 1 && vd == LSPCG_F32 && view->n > s->small_n) {
     // few distinct values (a structured grid's stencil): 1-byte codes into an LDS dictionary
@@ -1359,6 +1365,7 @@ static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view) {
   const int vd = view->storage_dtype();
   if (int rc = bsell_fill_values(*P, view->vals, vd, vd, st, &s->sv[w])) return rc;
   s->svd[w] = vd;
+  s->svn[w] = P->slots();
   s->sp[w] = P;
   return LSPCG_OK;
 }

@@ -256,7 +256,306 @@ __global__ void __launch_bounds__(256) k_sellc_fill(int64_t n, int64_t ns, const
   }
 }
 
+// ---- SELL-64J (layout: lspcg_sell.hpp kSellJag) ---------------------------------------------
+// One wave per slice: the lanes' ranks by (row length descending, row ascending) -> lmap, the
+// per-group lane counts -> jc, the slice's stored entries -> etot.  flag |= 1 when a row has more
+// than 16 groups (64 entries): no jagged layout.
+__global__ void k_jag_meta(int64_t n, int64_t ns, const int32_t* __restrict__ rowptr, uint8_t* __restrict__ lmap,
+                           uint8_t* __restrict__ jc, int32_t* __restrict__ etot, int* __restrict__ flag) {
+  const int64_t s = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (s >= ns) return;  // wave-uniform
+  const int64_t i = s * kSellC + lane;
+  const int len = i < n ? rowptr[i + 1] - rowptr[i] : 0;
+  const int g = (len + 3) >> 2;
+  if (__any(g > kSellJagMaxG)) {
+    if (lane == 0) atomicOr(flag, 1);
+    return;
+  }
+  int rank = 0;
+  for (int j = 0; j < 64; ++j) {
+    const int lj = __shfl(len, j, 64);
+    rank += (lj > len) || (lj == len && j < lane);
+  }
+  lmap[kSellC * s + rank] = uint8_t(lane);
+  int total = 0;
+#pragma unroll
+  for (int q = 0; q < kSellJagMaxG; ++q) {
+    const int c = __popcll(__ballot(g > q));
+    if (lane == q) jc[kSellJagMaxG * s + q] = uint8_t(c);
+    total += c;
+  }
+  if (lane == 0) etot[s] = 4 * total;
+}
+
+// Element-parallel fill: one workgroup per slice, threads over its stored entries in storage order
+// (coalesced writes): element p of the slice -> group q (the counts' prefix in LDS), lane (p - start_q)
+// / 4, entry 4 q + p % 4 of that lane's row.  16-bit offsets (col16) and / or values (dst); entries
+// past the row's end get kSellPad16 / 0.
+template <typename VS, typename VD>
+__global__ void __launch_bounds__(256) k_jag_fill(int64_t n, int64_t ns, const int32_t* __restrict__ gp,
+                                                  const uint8_t* __restrict__ jc, const uint8_t* __restrict__ lmap,
+                                                  const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colind,
+                                                  const VS* __restrict__ src, int16_t* __restrict__ col16,
+                                                  VD* __restrict__ dst) {
+  __shared__ int32_t start[kSellJagMaxG + 1];
+  for (int64_t s = blockIdx.x; s < ns; s += gridDim.x) {
+    __syncthreads();  // the previous slice's lookups are done
+    if (threadIdx.x == 0) {
+      int32_t e = 0;
+      for (int q = 0; q < kSellJagMaxG; ++q) {
+        start[q] = e;
+        e += 4 * jc[kSellJagMaxG * s + q];
+      }
+      start[kSellJagMaxG] = e;
+    }
+    __syncthreads();
+    const int64_t e0 = gp[s];
+    const int32_t total = start[kSellJagMaxG];
+    for (int32_t p = threadIdx.x; p < total; p += blockDim.x) {
+      int q = 0;
+      while (q + 1 < kSellJagMaxG && start[q + 1] <= p) ++q;
+      const int l = (p - start[q]) >> 2;
+      const int64_t i = s * kSellC + lmap[kSellC * s + l];
+      const int32_t k = 4 * q + (p & 3);
+      int32_t b = 0, len = 0;
+      if (i < n) {
+        b = rowptr[i];
+        len = rowptr[i + 1] - b;
+      }
+      const bool real = k < len;
+      if (col16) col16[e0 + p] = real ? int16_t(colind[b + k] - int32_t(s * kSellC)) : kSellPad16;
+      if (dst) dst[e0 + p] = real ? VD(src[b + k]) : VD(0);
+    }
+  }
+}
+
+// ---- SELL-64X (layout: lspcg_sell.hpp kSellJagX) --------------------------------------------
+// The distinct x blocks (col / 16) of one 256-row tile in an LDS hash set (one workgroup per tile,
+// one row per thread); returns the count, or kSellXMax + 1 once the set outgrows the limit.
+constexpr int kXsHash = 1024;
+__device__ int xs_tile_set(int64_t n, int64_t tile, const int32_t* __restrict__ rowptr,
+                           const int32_t* __restrict__ colind, int* tab, int* count, int* maxcol = nullptr) {
+  for (int j = threadIdx.x; j < kXsHash; j += blockDim.x) tab[j] = -1;
+  if (threadIdx.x == 0) *count = 0;
+  __syncthreads();
+  const int64_t i = tile * kSellWG + threadIdx.x;
+  if (i < n) {
+    for (int32_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+      const int b = colind[k] / kSellXBlk;
+      if (maxcol) atomicMax(maxcol, colind[k]);
+      unsigned h = (unsigned(b) * 0x9E3779B1u) >> 22;  // 10 bits
+      for (int probe = 0; probe < kXsHash; ++probe, h = (h + 1) & (kXsHash - 1)) {
+        const int prev = atomicCAS(&tab[h], -1, b);
+        if (prev == -1) {
+          atomicAdd(count, 1);
+          break;
+        }
+        if (prev == b) break;
+      }
+      if (*count > kSellXMax) break;  // (racy read: only ends the insertion early, the flag follows)
+    }
+  }
+  __syncthreads();
+  return *count;
+}
+
+__global__ void __launch_bounds__(256) k_xs_count(int64_t n, int64_t ntiles, const int32_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ colind, int32_t* __restrict__ cnt,
+                                                  int* __restrict__ flag) {
+  __shared__ int tab[kXsHash];
+  __shared__ int count;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int c = xs_tile_set(n, t, rowptr, colind, tab, &count, flag + 3);
+    if (threadIdx.x == 0) {
+      cnt[t] = c;
+      if (c > kSellXMax) atomicOr(flag, 1);
+      atomicMax(flag + 1, c);
+    }
+    __syncthreads();
+  }
+}
+
+// The tile's ascending block list (xl at xlp[t]) and every stored entry's word: slot * 16 + col % 16
+// (the jagged storage order of k_jag_fill; padding keeps kSellPad16).
+__global__ void __launch_bounds__(256) k_xs_fill(int64_t n, int64_t ns, int64_t ntiles, const int32_t* __restrict__ rowptr,
+                                                 const int32_t* __restrict__ colind, const int32_t* __restrict__ xlp,
+                                                 const int32_t* __restrict__ gp, const uint8_t* __restrict__ jc,
+                                                 const uint8_t* __restrict__ lmap, int32_t* __restrict__ xl,
+                                                 int16_t* __restrict__ code) {
+  __shared__ int tab[kXsHash];
+  __shared__ int sorted[kSellXMax];
+  __shared__ int count;
+  __shared__ int32_t start[kSellJagMaxG + 1];
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int c = xs_tile_set(n, t, rowptr, colind, tab, &count);
+    for (int j = threadIdx.x; j < kXsHash; j += blockDim.x) {  // rank = number of smaller keys
+      const int b = tab[j];
+      if (b < 0) continue;
+      int r = 0;
+      for (int k = 0; k < kXsHash; ++k) r += (tab[k] >= 0 && tab[k] < b);
+      sorted[r] = b;
+      xl[xlp[t] + r] = b;
+    }
+    __syncthreads();
+    for (int w = 0; w < kSellWG / kSellC; ++w) {
+      const int64_t s = t * (kSellWG / kSellC) + w;
+      if (s >= ns) break;  // uniform
+      if (threadIdx.x == 0) {
+        int32_t e = 0;
+        for (int q = 0; q < kSellJagMaxG; ++q) {
+          start[q] = e;
+          e += 4 * jc[kSellJagMaxG * s + q];
+        }
+        start[kSellJagMaxG] = e;
+      }
+      __syncthreads();
+      const int64_t e0 = gp[s];
+      for (int32_t p = threadIdx.x; p < start[kSellJagMaxG]; p += blockDim.x) {
+        int q = 0;
+        while (q + 1 < kSellJagMaxG && start[q + 1] <= p) ++q;
+        const int64_t i = s * kSellC + lmap[kSellC * s + ((p - start[q]) >> 2)];
+        const int32_t k = 4 * q + (p & 3);
+        int16_t word = kSellPad16;
+        if (i < n && k < rowptr[i + 1] - rowptr[i]) {
+          const int col = colind[rowptr[i] + k];
+          const int b = col / kSellXBlk;
+          int lo = 0, hi = c - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sorted[mid] < b) lo = mid + 1;
+            else hi = mid;
+          }
+          word = int16_t(lo * kSellXBlk + col % kSellXBlk);
+        }
+        code[e0 + p] = word;
+      }
+      __syncthreads();  // start[] is rewritten for the next slice
+    }
+  }
+}
+
 static int slice_grid(int64_t ns) { return int(std::max<int64_t>(1, std::min<int64_t>(ns, 16384))); }
+
+// SELL-64X from a SELL-64J pattern (*taken = true when every tile touches <= kSellXMax blocks): the
+// column words are rewritten as LDS positions, the block lists added.
+static int xs_try(int64_t n, const int32_t* rowptr, const int32_t* colind, hipStream_t st, SellPattern* P,
+                  bool* taken) {
+  *taken = false;
+  const int64_t ntiles = (n + kSellWG - 1) / kSellWG;
+  int32_t *cnt = nullptr, *xlp = nullptr, *xl = nullptr;
+  int* flag = nullptr;
+  void* tmp = nullptr;
+  auto done = [&](hipError_t e) {
+    (void)hipFree(cnt);
+    (void)hipFree(xlp);
+    (void)hipFree(xl);
+    (void)hipFree(flag);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) {
+      set_error(std::string("sell_build_pattern (x-staged): ") + hipGetErrorString(e));
+      return LSPCG_ERR_HIP;
+    }
+    return LSPCG_OK;
+  };
+  int flag_h[4] = {1, 0, 0, 0};  // [over the limit, longest list, total, largest column]
+  hipError_t e = hipMalloc(&flag, 4 * sizeof(int));
+  if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 4 * sizeof(int), st);
+  if (e == hipSuccess) e = hipMalloc(&cnt, sizeof(int32_t) * (ntiles + 1));
+  if (e == hipSuccess) e = hipMalloc(&xlp, sizeof(int32_t) * (ntiles + 1));
+  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, sizeof(int32_t) * (ntiles + 1), st);
+  const int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, 8192)));
+  if (e == hipSuccess) hipLaunchKernelGGL(k_xs_count, dim3(grid), dim3(256), 0, st, n, ntiles, rowptr, colind, cnt, flag);
+  size_t tb = 0;
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, xlp, int(ntiles + 1), st);
+  if (e == hipSuccess) e = hipMalloc(&tmp, tb ? tb : 1);
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, xlp, int(ntiles + 1), st);
+  if (e == hipSuccess) e = hipMemcpyAsync(flag + 2, xlp + ntiles, sizeof(int), hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(flag_h, flag, 4 * sizeof(int), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess || (flag_h[0] & 1)) return done(e);
+  e = hipMalloc(&xl, sizeof(int32_t) * std::max(flag_h[2], 1));
+  if (e == hipSuccess)
+    hipLaunchKernelGGL(k_xs_fill, dim3(grid), dim3(256), 0, st, n, P->ns, ntiles, rowptr, colind, xlp, P->gp, P->jc,
+                       P->lmap, xl, static_cast<int16_t*>(P->col));
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) return done(e);
+  P->xlp = xlp;
+  P->xl = xl;
+  P->kx = flag_h[1];
+  P->xn = int64_t(flag_h[3]) + 1;
+  P->col_bits = kSellJagX;
+  xlp = nullptr;
+  xl = nullptr;
+  *taken = true;
+  return done(hipSuccess);
+}
+
+// SELL-64J pattern (P: the SELL-64 pattern with 16-bit offsets, already sized): *taken = true when
+// every row has <= 64 entries; P's gp becomes the element prefix, col the jagged 16-bit offsets.
+static int jag_try(int64_t n, const int32_t* rowptr, const int32_t* colind, hipStream_t st, SellPattern* P,
+                   bool* taken) {
+  *taken = false;
+  int32_t *etot = nullptr, *egp = nullptr;
+  uint8_t *lmap = nullptr, *jc = nullptr;
+  int16_t* col = nullptr;
+  int* flag = nullptr;
+  void* tmp = nullptr;
+  auto done = [&](hipError_t e) {
+    (void)hipFree(etot);
+    (void)hipFree(egp);
+    (void)hipFree(lmap);
+    (void)hipFree(jc);
+    (void)hipFree(col);
+    (void)hipFree(flag);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) {
+      set_error(std::string("sell_build_pattern (jagged): ") + hipGetErrorString(e));
+      return LSPCG_ERR_HIP;
+    }
+    return LSPCG_OK;
+  };
+  const int64_t ns = P->ns;
+  int flag_h[2] = {1, 0};
+  hipError_t e = hipMalloc(&flag, 2 * sizeof(int));
+  if (e == hipSuccess) e = hipMemsetAsync(flag, 0, 2 * sizeof(int), st);
+  if (e == hipSuccess) e = hipMalloc(&etot, sizeof(int32_t) * (ns + 1));
+  if (e == hipSuccess) e = hipMalloc(&egp, sizeof(int32_t) * (ns + 1));
+  if (e == hipSuccess) e = hipMalloc(&lmap, size_t(kSellC) * ns);
+  if (e == hipSuccess) e = hipMalloc(&jc, size_t(kSellJagMaxG) * ns);
+  if (e == hipSuccess) e = hipMemsetAsync(etot, 0, sizeof(int32_t) * (ns + 1), st);
+  if (e == hipSuccess)
+    hipLaunchKernelGGL(k_jag_meta, dim3(unsigned((ns + 3) / 4)), dim3(256), 0, st, n, ns, rowptr, lmap, jc, etot, flag);
+  size_t tb = 0;
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, etot, egp, int(ns + 1), st);
+  if (e == hipSuccess) e = hipMalloc(&tmp, tb ? tb : 1);
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, etot, egp, int(ns + 1), st);
+  if (e == hipSuccess) e = hipMemcpyAsync(flag + 1, egp + ns, sizeof(int), hipMemcpyDeviceToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(flag_h, flag, 2 * sizeof(int), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess || (flag_h[0] & 1)) return done(e);
+  const int64_t elems = flag_h[1];
+  e = hipMalloc(&col, sizeof(int16_t) * std::max<int64_t>(elems, 1));
+  if (e == hipSuccess)
+    hipLaunchKernelGGL((k_jag_fill<float, float>), dim3(slice_grid(ns)), dim3(256), 0, st, n, ns, egp, jc, lmap, rowptr,
+                       colind, static_cast<const float*>(nullptr), col, static_cast<float*>(nullptr));
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) return done(e);
+  (void)hipFree(P->gp);
+  (void)hipFree(P->col);
+  P->gp = egp;
+  P->col = col;
+  P->lmap = lmap;
+  P->jc = jc;
+  P->elems = elems;
+  P->col_bits = kSellJag;
+  egp = nullptr;
+  col = nullptr;
+  lmap = nullptr;
+  jc = nullptr;
+  *taken = true;
+  return done(hipSuccess);
+}
 
 static int fill_grid(int64_t n) {
   return int(std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, kElemBlocksMax)));
@@ -557,11 +856,15 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
   cnt = nullptr;
   tmp = nullptr;
   P.groups = groups;
-  if (double(256) * double(groups) > max_pad * double(std::max<int64_t>(nnz, 1))) {
+  // padding past max_pad: only the jagged layout (which pads just each row's last group) may remain
+  const bool overpad = double(256) * double(groups) > max_pad * double(std::max<int64_t>(nnz, 1));
+  auto reject = [&]() {
     P.release();
     set_error("sell: padding exceeds the limit (irregular row lengths)");
     return LSPCG_ERR_UNSUPPORTED;
-  }
+  };
+  if (overpad && !(cols & kSellColJag)) return reject();
+  if (overpad) cols &= ~(kSellColDia | kSellColCode);
   // SELL-DIA: dictionaries and slot counts first; one host read of (flag, DIA slot total) decides
   int fit16 = 0;  // 1 = some column out of 16-bit offset range
   int flag_h[2] = {1, 0};  // [flags (bit 0: no SELL-DIA, bit 1: no 16-bit offsets), SELL-DIA slots]
@@ -668,6 +971,25 @@ int sell_build_pattern(int64_t n, int64_t nnz, const int32_t* rowptr, const int3
     P.dict = nullptr;
     if (e != hipSuccess) return fail(e);
   }
+  if ((cols & kSellColJag) && !fit16 && n && double(256) * double(P.groups) > kSellJagPad * double(nnz)) {
+    bool taken = false;  // irregular row lengths: the jagged layout stores ~1.1 x nnz instead
+    if (int rc = jag_try(n, rowptr, colind, st, &P, &taken)) {
+      P.release();
+      return rc;
+    }
+    if (taken && (cols & kSellColXs) && n >= kSellXMinN) {  // stage each tile's x blocks in LDS where they fit
+      bool xs = false;
+      if (int rc = xs_try(n, rowptr, colind, st, &P, &xs)) {
+        P.release();
+        return rc;
+      }
+    }
+    if (taken) {
+      *out = P;
+      return LSPCG_OK;
+    }
+  }
+  if (overpad) return reject();
   P.col_bits = fit16 ? 32 : 16;
   // the fill writes every slot (padding included)
   const size_t cbytes = size_t(P.col_bits / 8) * size_t(std::max<int64_t>(256 * P.groups, 1));
@@ -688,10 +1010,23 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
   const size_t es = dst_dtype == LSPCG_F32 ? 4 : 8;
   void* v = *out;  // an existing array of this pattern and dtype is refilled in place
   const bool mine = v == nullptr;
-  const int64_t slots = P.col_bits == 1 ? kSellC * P.groups : 256 * P.groups;
-  if (!v) LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(slots, 1)));
+  if (!v) LSPCG_HIP(hipMalloc(&v, es * std::max<int64_t>(P.slots(), 1)));
   const dim3 g(slice_grid(P.ns)), b(256);
-  if (P.ns && P.col_bits == 1) {
+  if (P.ns && P.jagged()) {
+    int16_t* nc = nullptr;
+    if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F64)
+      hipLaunchKernelGGL((k_jag_fill<double, double>), g, b, 0, st, P.n, P.ns, P.gp, P.jc, P.lmap, P.rowptr, colind,
+                         static_cast<const double*>(src), nc, static_cast<double*>(v));
+    else if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F32)
+      hipLaunchKernelGGL((k_jag_fill<double, float>), g, b, 0, st, P.n, P.ns, P.gp, P.jc, P.lmap, P.rowptr, colind,
+                         static_cast<const double*>(src), nc, static_cast<float*>(v));
+    else if (src_dtype == LSPCG_F32 && dst_dtype == LSPCG_F32)
+      hipLaunchKernelGGL((k_jag_fill<float, float>), g, b, 0, st, P.n, P.ns, P.gp, P.jc, P.lmap, P.rowptr, colind,
+                         static_cast<const float*>(src), nc, static_cast<float*>(v));
+    else
+      hipLaunchKernelGGL((k_jag_fill<float, double>), g, b, 0, st, P.n, P.ns, P.gp, P.jc, P.lmap, P.rowptr, colind,
+                         static_cast<const float*>(src), nc, static_cast<double*>(v));
+  } else if (P.ns && P.col_bits == 1) {
     const auto* m = static_cast<const uint16_t*>(P.col);
     if (src_dtype == LSPCG_F64 && dst_dtype == LSPCG_F64)
       hipLaunchKernelGGL((k_sdia_fill<double, double>), g, b, 0, st, P.n, P.ns, P.gp, m, P.rowptr,

@@ -54,6 +54,38 @@ constexpr int kSellColCode = 4;
 // keep 16-bit offsets in a second array: rgp[s] = their first group there (-1: coded slice).
 constexpr int kSellCodeMax = 64;
 constexpr uint8_t kSellCodePad = 0xff;
+// Jagged SELL-64 ("SELL-64J", col_bits == kSellJag: 16-bit offsets; unstructured meshes, whose rows
+// in one 64-row slice range from 4 to ~35 entries, so SELL-64's 64 x longest-row slots pad 1.6x).
+// Inside each slice the LANES are sorted by descending row length (ties by row): lane l owns row
+// 64 s + lmap[64 s + l], and group q (entries 4q .. 4q+3) holds only the cnt_q = jc[16 s + q] lanes
+// whose rows reach it, a prefix of the lanes -- stored densely:
+//     entry k of lane l at  gp[s] + 4 (cnt_0 + ... + cnt_{q-1}) + 4 l + k % 4,   q = k / 4, l < cnt_q,
+// with gp[s] the slice's first ELEMENT.  Padding is only the row's last group (16.1 -> 17.6 entries
+// per row on the 1 M Delaunay mesh, vs 26.1 for SELL-64).  Rows move only inside their slice, so x
+// gathers and y / r / p accesses hit the same cache lines as before, and slot k is still entry k of
+// its row: scipy's sum order, the same bits.  Rows of more than 64 entries (16 groups) keep SELL-64.
+constexpr int kSellJag = 17;
+constexpr int kSellJagMaxG = 16;   // groups per slice (jc bytes per slice)
+constexpr int kSellColJag = 8;     // sell_build_pattern: jagged 16-bit layout allowed
+constexpr double kSellJagPad = 1.15;  // taken when SELL-64 stores more than this x nnz slots
+// x-staged SELL-64J ("SELL-64X", col_bits == kSellJagX): the jagged layout whose 16-bit column words
+// are positions in an LDS copy of the vector blocks the row tile (4 slices, 256 rows) touches.  An
+// unstructured mesh's 64-row slice gathers ~14 distinct 128-B lines per 64-lane gather (Kuhn grid: 4),
+// mostly L1 misses (a slice's x footprint is ~11 KB, 24 resident slices per CU), and those gathers
+// cost 40 % of the jagged SpMV (tools/jag_probe.py: 43.8 vs 26.8 us with contiguous gathers, delaunay1m).
+// Here a tile's distinct 16-element x blocks (xl[xlp[t] .. xlp[t+1]), ascending; ~170 on delaunay1m)
+// are loaded ONCE per tile with 16-B loads into LDS (barrier), and entry k's word is
+// slot * 16 + col % 16 with slot the block's rank in the list: the gathers become LDS reads of the
+// same values, so the bits are unchanged.  kx = the largest list (LDS: kx * 16 * sizeof(x) per
+// workgroup); patterns whose tiles touch more than kSellXMax blocks keep SELL-64J.
+constexpr int kSellJagX = 18;
+constexpr int kSellColXs = 16;  // sell_build_pattern: the x-staged layout allowed (GatherVec only)
+constexpr int kSellXMax = 256;  // blocks per tile (32 KB of fp64)
+constexpr int kSellXBlk = 16;   // vector entries per staged block
+// smallest pattern staged: below it the per-tile staging latency and barriers cost more than the
+// gathers they replace (us per iteration, SELL-64X vs SELL-64J: delaunay1m 127.0 vs 134.9, delaunay64k
+// 31.5 vs 28.6, bunny 18.8 vs 16.9; profiles/r6_sellx_probe.jsonl)
+constexpr int64_t kSellXMinN = 262144;
 
 // Pattern shared by every matrix with the same CSR (rowptr, colind).
 //
@@ -82,18 +114,40 @@ struct SellPattern {
                                    // SELL-64C (col_bits 8): [64*ns], col = [256*groups] uint8 codes
   int32_t* rgp = nullptr;          // SELL-64C: [ns] group start in col2 of a slice kept uncoded, or -1
   int16_t* col2 = nullptr;         // SELL-64C: 16-bit offsets of the uncoded slices
+  uint8_t* lmap = nullptr;         // SELL-64J: [64*ns] row (within the slice) of each lane
+  uint8_t* jc = nullptr;           // SELL-64J: [16*ns] lanes per group (non-increasing, 0 past the last)
+  int64_t elems = 0;               // SELL-64J: stored entries (gp is an element prefix, not a group prefix)
+  int32_t* xlp = nullptr;          // SELL-64X: [ntiles+1] block-list prefix per 256-row tile
+  int32_t* xl = nullptr;           // SELL-64X: the tiles' ascending x-block lists
+  int kx = 0;                      // SELL-64X: the longest list
+  int64_t xn = 0;                  // SELL-64X: vector entries read (largest column + 1; > n for dist_pcg's halo)
   const int32_t* rowptr = nullptr; // CSR row pointer (row lengths), not owned
+  // the jagged element layout (SELL-64J / SELL-64X): gp is an element prefix
+  bool jagged() const { return col_bits == kSellJag || col_bits == kSellJagX; }
+  // entries of a value array of this pattern (sell_fill_values allocates this many)
+  int64_t slots() const {
+    if (bs == 3) return int64_t(576) * groups;  // BSELL-64 / BSELL-DIA: 9 values per block slot
+    return jagged() ? elems : (col_bits == 1 ? int64_t(64) : int64_t(256)) * groups;
+  }
   void release() {
     (void)hipFree(gp);
     (void)hipFree(col);
     (void)hipFree(dict);
     (void)hipFree(rgp);
     (void)hipFree(col2);
+    (void)hipFree(lmap);
+    (void)hipFree(jc);
+    (void)hipFree(xlp);
+    (void)hipFree(xl);
+    xlp = nullptr;
+    xl = nullptr;
     gp = nullptr;
     col = nullptr;
     dict = nullptr;
     rgp = nullptr;
     col2 = nullptr;
+    lmap = nullptr;
+    jc = nullptr;
   }
 };
 
@@ -108,6 +162,11 @@ struct SellArgs {
   const int32_t* dict = nullptr;  // SELL-64C (CT = uint8_t): see kSellCodeMax
   const int32_t* rgp = nullptr;
   const int16_t* col2 = nullptr;
+  const uint8_t* lmap = nullptr;  // SELL-64J: see kSellJag
+  const uint8_t* jc = nullptr;
+  const int32_t* xlp = nullptr;   // SELL-64X: see kSellJagX
+  const int32_t* xl = nullptr;
+  int64_t xn = 0;
 };
 
 template <typename VT>
@@ -141,6 +200,7 @@ struct Vec4Ld<double> {
 };
 
 using i16x4 = short __attribute__((ext_vector_type(4)));
+using xs_u4 = unsigned __attribute__((ext_vector_type(4)));  // 16-B staging part (SELL-64X)
 
 // Epilogues with a PREFETCH member (a device pointer) read one own-row value in row(); the SELL
 // kernel loads it before the row's slot loop so it does not add a memory latency after the
@@ -261,6 +321,127 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sell(SellArgs<VT, CT> a, Pro 
 #pragma unroll
           for (int j = 0; j < 4; ++j)
             if (m[u][j]) acc = acc + T(v[u][j]) * xv[u][j];
+      }
+      if constexpr (epi_prefetch<Epi>::value) {
+        if (i < a.n) epi.row_pf(i, acc, d, pf);
+      } else {
+        if (i < a.n) epi.row(i, acc, d);
+      }
+    }
+  }
+  finish_epi_dots<Epi>(d, epi);
+}
+
+// SELL-64J SpMV (layout: see kSellJag): one wave = one 64-row slice; lane l sums row 64 s + lmap[l].
+// The slice's metadata is its first element gp[s], the 16 group counts (two 8-byte scalar loads)
+// and the lane's row byte, loaded in one batch (the first tile's before the prologue's state read).
+// Group q's loads are issued only by its cnt_q active lanes (a prefix of the wave): a shorter row's
+// lane neither loads nor adds past its last group.  The counts are consumed from a 128-bit scalar
+// shift register, QB groups per batch, every load of a batch before the first add.
+// XS (SELL-64X, kSellJagX): the column words index the tile's LDS copy of its x blocks (dynamic
+// shared memory, kx * 16 entries), staged by the whole workgroup between two barriers per tile.
+template <typename T, typename VT, int QB, int TH, int MINW, bool XS, class Pro, class Gx, class Epi>
+__global__ void __launch_bounds__(TH, MINW) k_spmv_sellj(SellArgs<VT, int16_t> a, Pro pro, Gx gx, Epi epi) {
+  static_assert(QB >= 1 && QB <= 4, "QB groups per batch");
+  static_assert(!XS || std::is_same<Gx, GatherVec<T>>::value, "SELL-64X stages a plain vector");
+  constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
+  [[maybe_unused]] extern __shared__ __attribute__((aligned(16))) unsigned char sx_raw[];
+  [[maybe_unused]] T* sx = reinterpret_cast<T*>(sx_raw);
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int64_t ntiles = (a.n + TH - 1) / TH;
+  int32_t e0 = 0;
+  uint64_t c0 = 0, c1 = 0;
+  int rl = 0;
+  auto meta = [&](int64_t sl) {
+    e0 = a.gp[sl];
+    const uint64_t* cp = reinterpret_cast<const uint64_t*>(a.jc + kSellJagMaxG * sl);
+    c0 = cp[0];
+    c1 = cp[1];
+    rl = a.lmap[kSellC * sl + lane];
+  };
+  {
+    const int64_t s = int64_t(blockIdx.x) * (TH / 64) + w;
+    if (int64_t(blockIdx.x) < ntiles && s < a.ns) meta(s);
+  }
+  if (pro.exit()) return;
+  gx.prepare();
+  epi.prepare();
+  DD d[ND];
+#pragma unroll
+  for (int j = 0; j < ND; ++j) d[j] = dd_zero();
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    if constexpr (XS) {  // the tile's x blocks -> LDS (16-B loads; a block past n element by element)
+      if (tile != int64_t(blockIdx.x)) __syncthreads();  // the previous tile's LDS reads are done
+      const int32_t b0 = a.xlp[tile], nbk = a.xlp[tile + 1] - b0;
+      constexpr int W = 16 / int(sizeof(T));   // entries per 16-B part
+      constexpr int PPB = kSellXBlk / W;       // parts per block
+      const T* xg = gx.x;
+      for (int p = threadIdx.x; p < nbk * PPB; p += TH) {
+        const int64_t e = int64_t(a.xl[b0 + p / PPB]) * kSellXBlk + (p % PPB) * W;
+        T* dst = sx + (p / PPB) * kSellXBlk + (p % PPB) * W;
+        if (e + W <= a.xn) {
+          *reinterpret_cast<xs_u4*>(dst) = *(const __attribute__((address_space(1))) xs_u4*)(xg + e);
+        } else {
+#pragma unroll
+          for (int k = 0; k < W; ++k) dst[k] = e + k < a.xn ? xg[e + k] : T(0);
+        }
+      }
+      __syncthreads();
+    }
+    const int64_t s = tile * (TH / 64) + w;
+    if (s < a.ns) {  // wave-uniform
+      if (tile != int64_t(blockIdx.x)) meta(s);
+      const int32_t base = int32_t(s * kSellC);
+      const int64_t i = int64_t(base) + rl;
+      T acc = T(0);
+      T pf = T(0);
+      if constexpr (epi_prefetch<Epi>::value) {
+        if (i < a.n) pf = epi.prefetch(i);
+      }
+      uint64_t lo = c0, hi = c1;
+      int32_t eo = e0;
+      while (lo & 0xffu) {  // wave-uniform: groups left
+        VT v[QB][4];
+        int c[QB][4];
+        bool m[QB][4];
+        [[maybe_unused]] int o16[QB][4];
+        int32_t eu = eo;
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+          const int cq = int((lo >> (8 * u)) & 0xffu);
+          const bool act = lane < cq;
+          i16x4 cc = {kSellPad16, kSellPad16, kSellPad16, kSellPad16};
+          v[u][0] = v[u][1] = v[u][2] = v[u][3] = VT(0);
+          if (act) {
+            Vec4Ld<VT>::load(a.vals + int64_t(eu) + 4 * lane, v[u]);
+            cc = *(const __attribute__((address_space(1))) i16x4*)(a.col + int64_t(eu) + 4 * lane);
+          }
+          const int o[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            m[u][j] = o[j] != kSellPad16;
+            c[u][j] = base + (o[j] != kSellPad16 ? o[j] : 0);
+            o16[u][j] = o[j];
+          }
+          eu += 4 * cq;
+        }
+        T xv[QB][4];
+#pragma unroll
+        for (int u = 0; u < QB; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if constexpr (XS) xv[u][j] = sx[m[u][j] ? o16[u][j] : 0];
+            else xv[u][j] = gx(c[u][j]);
+          }
+#pragma unroll
+        for (int u = 0; u < QB; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (m[u][j]) acc = acc + T(v[u][j]) * xv[u][j];
+        eo = eu;
+        lo = (lo >> (8 * QB)) | (hi << (64 - 8 * QB));
+        hi >>= 8 * QB;
       }
       if constexpr (epi_prefetch<Epi>::value) {
         if (i < a.n) epi.row_pf(i, acc, d, pf);
@@ -640,13 +821,41 @@ inline void launch_spmv_bsdia3(const SellPattern& P, const void* vals, Gx gx, Pr
                      dim3(kSellWG), 0, st, a, pro, gx, epi);
 }
 
+// SELL-64J / SELL-64X launch: 256-row tiles (4 slices), the SELL-64 grid rules
+template <typename T, typename VT, class Pro, class Gx, class Epi>
+inline void launch_spmv_sellj(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
+                              bool one_tile_per_wg = false) {
+  int64_t grid = (P.nb + kSellWG - 1) / kSellWG;
+  if (!one_tile_per_wg) grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
+  if (grid <= 0) return;
+  SellArgs<VT, int16_t> a{P.n, P.ns, P.gp, static_cast<const int16_t*>(P.col), P.rowptr, static_cast<const VT*>(vals)};
+  a.lmap = P.lmap;
+  a.jc = P.jc;
+  a.xlp = P.xlp;
+  a.xl = P.xl;
+  a.xn = P.xn;
+  constexpr int MINW = (sizeof(VT) == 4 && std::is_same<Gx, GatherVec<T>>::value) ? 1536 / kSellWG : 1;
+  if constexpr (std::is_same<Gx, GatherVec<T>>::value) {
+    if (P.col_bits == kSellJagX) {
+      const size_t lds = size_t(P.kx) * kSellXBlk * sizeof(T);
+      LSPCG_LAUNCH_SPMV((k_spmv_sellj<T, VT, 2, kSellWG, MINW, true, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
+                         lds, st, a, pro, gx, epi);
+      return;
+    }
+  }
+  if (P.col_bits != kSellJag) return;  // (SELL-64X needs a plain vector gather: sell_build_pattern's callers)
+  LSPCG_LAUNCH_SPMV((k_spmv_sellj<T, VT, 2, kSellWG, MINW, false, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
+                     0, st, a, pro, gx, epi);
+}
+
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
                                  bool one_tile_per_wg = false) {
   if constexpr (std::is_same<VT, uint8_t>::value) {
     return;  // coded views are SELL-DIA only: launch_spmv_sdia with their dictionary
   }
-  if (P.col_bits == 1 && P.bs == 3) launch_spmv_bsdia3<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
+  if (P.jagged()) launch_spmv_sellj<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
+  else if (P.col_bits == 1 && P.bs == 3) launch_spmv_bsdia3<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 1) launch_spmv_sdia<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 16) launch_spmv_sell_th<T, VT, int16_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 8) launch_spmv_sell_th<T, VT, uint8_t, kSellWG>(P, vals, gx, pro, epi, st, one_tile_per_wg);

@@ -106,6 +106,13 @@ def synthetic_dataset(name: str) -> List[GraphSample]:
             A, mask, feats = P.heat_tet(k, k, max(4, nv // (k * k)), rho=float(rng.uniform(1e-4, 5e-4)), seed=s)
             out.append(make_sample(A, mask, node_features=feats))
         return out
+    if name == "delaunay_batch8":  # C5 on unstructured Delaunay tet meshes: 8 systems, 400-32000 vertices
+        rng = np.random.default_rng(0)
+        out = []
+        for s in range(8):
+            A, mask, nodes = P.delaunay_heat(int(rng.integers(400, 32000)), seed=s)
+            out.append(make_sample(A, mask, node_features=nodes))
+        return out
     if name == "heat_bunny":  # C3: heat on the voxelised bunny, F_in = 5 (field, xyz, mask)
         A, mask, feats = P.heat_bunny()
         return [make_sample(A, mask, node_features=feats)]

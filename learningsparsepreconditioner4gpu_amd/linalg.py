@@ -157,7 +157,7 @@ class PreconditionedConjugateGradient:
         slot (8, 4, or 1 = dictionary codes)."""
         ck, vb = (C.c_int * 3)(), (C.c_int * 3)()
         _lib.call("lspcg_solver_views", self.handle, ck, vb)
-        names = {0: "csr", 1: "sdia", 8: "sellc", 16: "sell16", 32: "sell32"}
+        names = {0: "csr", 1: "sdia", 8: "sellc", 16: "sell16", 17: "sell16j", 18: "sell16x", 32: "sell32"}
         return {m: {"columns": names.get(ck[w], str(ck[w])), "value_bytes": vb[w]}
                 for w, m in enumerate(("A", "L", "LT"))}
 

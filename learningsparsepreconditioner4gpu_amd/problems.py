@@ -377,7 +377,7 @@ def kuhn_dirichlet(n: int = 101, shift: float = 1e-4):
     return A, mask
 
 
-def renumber(A: sp.csr_matrix, mask: np.ndarray, order: str, seed: int = 0):
+def renumber(A: sp.csr_matrix, mask: np.ndarray, order: str, seed: int = 0, return_perm: bool = False):
     """``A`` and ``mask`` under a symmetric renumbering (P A Pᵀ, P mask): ``"rand"`` = a seeded random
     permutation (no locality at all), ``"rcm"`` = that random permutation followed by reverse
     Cuthill-McKee (scipy.sparse.csgraph) -- a banded but irregular ordering like an RCM-ordered
@@ -393,7 +393,143 @@ def renumber(A: sp.csr_matrix, mask: np.ndarray, order: str, seed: int = 0):
         raise ValueError(order)
     B = sp.csr_matrix(sp.csr_matrix(A)[perm][:, perm])
     B.sort_indices()
+    if return_perm:
+        return B, mask[perm], perm
     return B, mask[perm]
+
+
+# ---------------------------------------------------------------------------
+# Unstructured tet meshes (datagen/heat_tetmesh.py on tetgen meshes)
+# ---------------------------------------------------------------------------
+def delaunay_tets(n_pts: int, seed: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """Unstructured tet mesh of the unit cube with about ``n_pts`` vertices: the 3-D Delaunay
+    triangulation (scipy.spatial / qhull) of a seeded UNIFORM random point cloud -- no lattice, so no
+    stencil: vertex degrees vary (rows of 4 to ~35 entries, ~15.7 on average), like the tetgen meshes
+    the reference's heat data come from (``neural_cg/datagen_helper.py:113-137``, 400-32 k vertices,
+    ``preprocess/msh_to_npy.py:77-86``).  The cloud fills a box one mean spacing h = n^(-1/3) larger
+    than the cube on every side and only the tets with all four vertices inside the cube are kept: the
+    hull's flat slivers (4 nearly coplanar points on a face, stiffness entries ~1e5 x the median) never
+    enter, interior tets keep the diagonal within ~35 x its median.  Vertices are numbered by a spatial
+    bucket sort (cells of size h, x slowest, z fastest; the cell's points by x), the locality-preserving
+    numbering a meshing tool emits; ``renumber`` gives the irregular ones.  Only elementwise numpy
+    and qhull: the same bits on every host (tests pin A's sha256)."""
+    from scipy.spatial import Delaunay
+
+    h = float(n_pts) ** (-1.0 / 3.0)
+    n_gen = int(round(n_pts * (1.0 + 2.0 * h) ** 3))
+    rng = np.random.default_rng(seed)
+    pts = rng.uniform(-h, 1.0 + h, size=(n_gen, 3))
+    tets = Delaunay(pts).simplices.astype(np.int64)
+    inside = np.all((pts >= 0.0) & (pts <= 1.0), axis=1)
+    tets = tets[inside[tets].all(axis=1)]
+    used = np.unique(tets)
+    cells = np.minimum((pts[used] / h).astype(np.int64), int(1.0 / h) + 1)
+    m = int(cells.max()) + 1
+    key = (cells[:, 0] * m + cells[:, 1]) * m + cells[:, 2]
+    order = np.lexsort((pts[used, 0], key))  # by cell, then x inside the cell
+    new = np.empty(n_gen, dtype=np.int64)
+    new[used[order]] = np.arange(used.size)
+    tets = new[tets]
+    # orient every tet positively (det > 0): swap its last two vertices where needed
+    nodes = pts[used[order]]
+    d = _tet_dets(nodes, tets)
+    neg = d < 0
+    tets[neg, 2], tets[neg, 3] = tets[neg, 3].copy(), tets[neg, 2].copy()
+    return nodes, tets
+
+
+def _tet_dets(nodes: np.ndarray, tets: np.ndarray) -> np.ndarray:
+    X = nodes[tets]
+    a, b, c = X[:, 1] - X[:, 0], X[:, 2] - X[:, 0], X[:, 3] - X[:, 0]
+    return (a[:, 0] * (b[:, 1] * c[:, 2] - b[:, 2] * c[:, 1]) - a[:, 1] * (b[:, 0] * c[:, 2] - b[:, 2] * c[:, 0])
+            + a[:, 2] * (b[:, 0] * c[:, 1] - b[:, 1] * c[:, 0]))
+
+
+def p1_laplacian_exact(nodes: np.ndarray, tets: np.ndarray) -> Tuple[sp.csr_matrix, np.ndarray]:
+    """P1 stiffness (cotangent Laplacian, ``pymathprim.geometry.laplacian`` as heat_tetmesh.py:26
+    calls it) and the lumped mass (``lumped_mass``, :27) of a positively oriented tet mesh, with
+    explicit cofactor arithmetic only (no LAPACK / BLAS, so the bits do not depend on the host's
+    BLAS kernels): grad λ_a = cofactor row / det, K_ab += vol · (g_a · g_b), M_a += vol / 4."""
+    X = nodes[tets]
+    a, b, c = X[:, 1] - X[:, 0], X[:, 2] - X[:, 0], X[:, 3] - X[:, 0]
+    cross = lambda u, v: np.stack([u[:, 1] * v[:, 2] - u[:, 2] * v[:, 1], u[:, 2] * v[:, 0] - u[:, 0] * v[:, 2],
+                                   u[:, 0] * v[:, 1] - u[:, 1] * v[:, 0]], 1)
+    bc, ca, ab = cross(b, c), cross(c, a), cross(a, b)
+    det = a[:, 0] * bc[:, 0] + a[:, 1] * bc[:, 1] + a[:, 2] * bc[:, 2]
+    g1, g2, g3 = bc / det[:, None], ca / det[:, None], ab / det[:, None]
+    g0 = -(g1 + g2 + g3)
+    G = np.stack([g0, g1, g2, g3], 1)  # [T, 4, 3]
+    vol = det / 6.0
+    K = (G[:, :, None, 0] * G[:, None, :, 0] + G[:, :, None, 1] * G[:, None, :, 1]
+         + G[:, :, None, 2] * G[:, None, :, 2]) * vol[:, None, None]
+    n = nodes.shape[0]
+    r = np.repeat(tets, 4, axis=1).ravel()
+    cidx = np.tile(tets, (1, 4)).ravel()
+    S = _canon(sp.coo_matrix((K.ravel(), (r, cidx)), shape=(n, n)))
+    S = _canon(sp.triu(S) + sp.triu(S, 1).T)  # exactly symmetric (duplicate sums run in sort order)
+    mass = np.bincount(tets.ravel(), weights=np.repeat(vol / 4.0, 4), minlength=n)
+    return S, mass
+
+
+def smooth_random_field(points: np.ndarray, seed: int, cells: int = 4) -> np.ndarray:
+    """Seeded smooth random field (stand-in for heat_tetmesh.py:29-31's gstools Gaussian SRF; gstools
+    is absent): trilinear interpolation of uniform random values on a ``cells``³ lattice over the
+    points' bounding box -- additions and multiplications only, so host-independent bits."""
+    rng = np.random.default_rng(seed)
+    v = rng.uniform(0.0, 1.0, size=(cells + 1,) * 3)
+    lo = points.min(0)
+    span = np.maximum(points.max(0) - lo, 1e-300)
+    u = (points - lo) / span * cells
+    i = np.minimum(u.astype(np.int64), cells - 1)
+    f = u - i
+    out = np.zeros(points.shape[0])
+    for dx in (0, 1):
+        wx = f[:, 0] if dx else 1.0 - f[:, 0]
+        for dy in (0, 1):
+            wy = f[:, 1] if dy else 1.0 - f[:, 1]
+            for dz in (0, 1):
+                wz = f[:, 2] if dz else 1.0 - f[:, 2]
+                out += wx * wy * wz * v[i[:, 0] + dx, i[:, 1] + dy, i[:, 2] + dz]
+    return out
+
+
+def delaunay_heat(n_pts: int, seed: int = 0, min_density: float = 1e-4, max_density: float = 5e-4,
+                  dirichlet: bool = True):
+    """Heat on an unstructured Delaunay tet mesh, ``datagen/heat_tetmesh.py:17-56``: ``S = L +
+    diag(M · ρ)`` with ``L`` the P1 Laplacian, ``M`` the lumped mass and ``ρ`` a smooth random field
+    renormalised into [min_density, max_density] (config/heat_tetmesh.yaml: 1e-4, 5e-4) as
+    heat_tetmesh.py:32-34 does.  Dirichlet (``dirichlet``): the vertices within one mean spacing of
+    the x = 0 face (mask 0; heat_tetmesh has none -- SURVEY 8(d) adds them so the masked assembly
+    runs).  Node features = xyz (heat_tetmesh.py:99 returns the nodes); make_data appends the mask.
+
+    Returns ``(A_raw, mask[N,1], features[N,3])``."""
+    nodes, tets = delaunay_tets(n_pts, seed)
+    S, mass = p1_laplacian_exact(nodes, tets)
+    field = smooth_random_field(nodes, seed + 1)
+    field = field - field.min()
+    field = field / (field.max() + 1e-4)
+    field = field * (max_density - min_density) + min_density
+    A = _canon(S + sp.diags(mass * field))
+    mask = np.ones((A.shape[0], 1))
+    if dirichlet:
+        mask[nodes[:, 0] < float(n_pts) ** (-1.0 / 3.0)] = 0.0
+    return A, mask, nodes
+
+
+def matrix_sha256(A: sp.csr_matrix) -> str:
+    """sha256 of a CSR matrix's (indptr int64, indices int64, data float64) bytes."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for arr, dt in ((A.indptr, np.int64), (A.indices, np.int64), (A.data, np.float64)):
+        h.update(np.ascontiguousarray(arr, dtype=dt).tobytes())
+    return h.hexdigest()
+
+
+def _count(tok: str) -> int:
+    """'1m' -> 1,000,000, '64k' -> 64,000, '5000' -> 5,000."""
+    mult = {"k": 1000, "m": 1000000}.get(tok[-1:], 1)
+    return int(tok[:-1] if mult > 1 else tok) * mult
 
 
 def workload(name: str):
@@ -401,7 +537,9 @@ def workload(name: str):
 
     ``kuhn<N>`` is the structured Kuhn-tet grid (N³ vertices, Dirichlet face); ``kuhn<N>rcm`` and
     ``kuhn<N>rand`` are the same system renumbered (``renumber``): irregular orderings of the same
-    1M-row problem, the shape of the reference's tetgen meshes (datagen/heat_tetmesh.py)."""
+    1M-row problem.  ``delaunay<N>`` (``delaunay1m``, ``delaunay64k``, ...) is the unstructured
+    Delaunay heat system of about N vertices (``delaunay_heat``: the shape of the reference's tetgen
+    meshes, datagen/heat_tetmesh.py), ``delaunay<N>rcm`` / ``rand`` its renumberings."""
     import re
 
     m = re.fullmatch(r"kuhn(\d*)(rcm|rand)?", name)
@@ -411,6 +549,13 @@ def workload(name: str):
         if m.group(2):
             A, mask = renumber(A, mask, m.group(2))
         return A, mask, None, 1, "disable"
+    m = re.fullmatch(r"delaunay(\d+[km]?)(rcm|rand)?", name)
+    if m:
+        A, mask, nodes = delaunay_heat(_count(m.group(1)))
+        if m.group(2):
+            A, mask, perm = renumber(A, mask, m.group(2), return_perm=True)
+            nodes = nodes[perm]
+        return A, mask, nodes, 1, "disable"
     if name.startswith("poisson"):
         n = int(name[7:] or 256)
         A, mask, _ = poisson2d_grid(n, n)

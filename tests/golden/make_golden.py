@@ -756,10 +756,40 @@ def bunny_grid():
     print("bunny grid", tuple(shape), "inside vertices", int(inside.sum()))
 
 
+def delaunay_sha():
+    """delaunay_sha.json: sha256 of the unstructured Delaunay systems' A (problems.delaunay_heat: qhull
+    + elementwise numpy only) as this container builds them, so a GPU box whose qhull / numpy gave a
+    different mesh or different bits fails loudly instead of comparing against the wrong system."""
+    import json
+
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.infer import synthetic_dataset
+
+    out = {}
+    for name in ("delaunay20k", "delaunay1m"):
+        A, mask, _, _, _ = P.workload(name)
+        lens = np.diff(A.indptr)
+        out[name] = {"n": int(A.shape[0]), "nnz": int(A.nnz), "A_sha256": P.matrix_sha256(A),
+                     "dirichlet": int((np.asarray(mask) == 0).sum()),
+                     "row_entries": [int(lens.min()), float(lens.mean()), int(lens.max())]}
+        print(name, out[name], flush=True)
+    rows = []
+    for smp in synthetic_dataset("delaunay_batch8"):
+        rows.append({"n": int(smp.num_nodes), "E": int(smp.edge_index.shape[1]),
+                     "values_sha256": _sha(smp.matrix_values.numpy(), smp.edge_index.numpy())})
+    out["delaunay_batch8"] = rows
+    print("delaunay_batch8", [r["n"] for r in rows], flush=True)
+    (OUT / "delaunay_sha.json").write_text(json.dumps(out, indent=1) + "\n")
+
+
 def main():
     install_shims()
     if sys.argv[1:] == ["bunny"]:
         bunny_grid()
+        return
+    if sys.argv[1:] == ["delaunay"]:
+        sys.path.insert(0, str(ROOT))
+        delaunay_sha()
         return
     if sys.argv[1:] == ["traj"]:
         from neural_cg.utils import validate as rval

@@ -177,11 +177,13 @@ def _dia_slots(A):
     return int(cnt.max()), int(cnt.sum())
 
 
-def _expected_kind(A, max_pad=2.0, dia=True):
-    """lspcg_mat_prepare_spmv's rule: SELL-64 if the padded slots stay <= max_pad * nnz; then SELL-DIA
-    (kind 1) if every 64-row slice has <= 16 distinct offsets col - row and the slices' offset counts
-    sum to no more than the 4-entry groups' slots (sorted rows), else 16-bit column offsets if every
-    |col - 64*slice| <= 32767, else int32 columns."""
+def _expected_kind(A, max_pad=2.0, dia=True, jag=True):
+    """lspcg_mat_prepare_spmv's rule: SELL-DIA (kind 1) if SELL-64's padded slots stay <= max_pad * nnz,
+    every 64-row slice has <= 16 distinct offsets col - row and the slices' offset counts sum to no more
+    than the 4-entry groups' slots (sorted rows); else, where 16-bit column offsets fit (every
+    |col - 64*slice| <= 32767), SELL-64J (kind 17) when SELL-64 would pad more than 1.15 * nnz and no
+    row has more than 64 entries -- SELL-64X (18) when n >= 2^18 and every 256-row tile reads <= 256
+    16-entry x blocks; else none (0) past max_pad; else 16-bit offsets or int32 columns."""
     n = A.shape[0]
     lens = np.diff(A.indptr)
     if n == 0 or A.nnz == 0:
@@ -190,14 +192,19 @@ def _expected_kind(A, max_pad=2.0, dia=True):
     pad = np.zeros(ns * 64, dtype=np.int64)
     pad[:n] = lens
     groups = ((pad.reshape(ns, 64).max(axis=1) + 3) // 4).sum()
-    if 256 * groups > max_pad * A.nnz:
-        return 0
+    overpad = 256 * groups > max_pad * A.nnz
     mx, tot = _dia_slots(A)
-    if dia and mx <= 16 and tot <= 4 * groups:
+    if not overpad and dia and mx <= 16 and tot <= 4 * groups:
         return 1
     rows = np.repeat(np.arange(n), lens)
     off = A.indices - (rows // 64) * 64
-    return 16 if np.all(np.abs(off) <= 32767) else 32
+    fit16 = bool(np.all(np.abs(off) <= 32767))
+    if jag and fit16 and 256 * groups > 1.15 * A.nnz and lens.max() <= 64:
+        key = np.unique((rows // 256) * (1 << 32) + A.indices.astype(np.int64) // 16)
+        return 18 if n >= 262144 and np.bincount(key >> 32).max() <= 256 else 17  # SELL-64X: large, tiles fit
+    if overpad:
+        return 0
+    return 16 if fit16 else 32
 
 
 @pytest.mark.parametrize("which", list(MATS))
@@ -344,7 +351,8 @@ def test_dia_rule_and_bits(gpu_ctx, case):
 
 def test_dia_unsorted_rows_fall_back(gpu_ctx):
     """Rows uploaded in a stored, unsorted order (keep_order): SELL-DIA's slot order would not be the
-    row's order, so the build takes 16-bit offsets and the sums keep the stored order."""
+    row's order, so the build takes 16-bit offsets (here the jagged SELL-64J layout: the rows' lengths
+    vary) and the sums keep the stored order."""
     from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
 
     A = _offset_matrix(9000, [-300, -1, 0, 1, 300], 4)
@@ -357,7 +365,7 @@ def test_dia_unsorted_rows_fall_back(gpu_ctx):
     x = np.random.default_rng(5).normal(size=B.shape[0])
     ref = B @ x  # scipy's csr_matvec sums each row in stored order
     Ad = DeviceMatrix.from_scipy(B, keep_order=True)
-    assert Ad.prepare_spmv() == 16
+    assert Ad.prepare_spmv() == _expected_kind(B, dia=False) == 17
     assert np.array_equal(Ad.matvec(torch.from_numpy(x).cuda()).cpu().numpy(), ref)
 
 

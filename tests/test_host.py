@@ -218,8 +218,38 @@ def test_sell_format_model_matches_layouts():
     assert bench.sell_kind(A.indptr, A.indices) == 1
     d = bench.dia_counts(A.indptr, A.indices)
     assert bench.sell_format_bytes(A.indptr, A.indices, 1, 4) == 64 * int(d.sum()) * 4 + ns * (128 + 64)
-    R, _, _, _, _ = P.workload("kuhn17rcm")
+    R, _, _, _, _ = P.workload("kuhn41rcm")  # SELL-64 pads 1.11 x nnz: 16-bit offsets
     assert bench.sell_kind(R.indptr, R.indices) == 16
     assert bench.sell_format_bytes(R.indptr, R.indices, 16, 4) == bench.sell_slots(R.indptr) * 6
+    J, _, _, _, _ = P.workload("kuhn17rcm")  # pads 1.17 x nnz: the jagged layout (x-staged only from 2^18 rows)
+    assert bench.sell_kind(J.indptr, J.indices) == 17
+    nsj = (J.shape[0] + 63) // 64
+    assert bench.sell_format_bytes(J.indptr, J.indices, 17, 4) == bench.jag_elems(J.indptr) * 6 + nsj * 80
+    assert bench.jag_elems(J.indptr) < bench.sell_slots(J.indptr)
+    xb = bench.xs_blocks(J.indptr, J.indices)
+    assert xb.max() <= bench.XS_MAX and bench.sell_format_bytes(J.indptr, J.indices, 18, 4) == (
+        bench.jag_elems(J.indptr) * 6 + nsj * 80 + 4 * int(xb.sum()) + 4 * xb.size)
     X, _, _, _, _ = P.workload("kuhn41rand")
     assert bench.sell_kind(X.indptr, X.indices) == 32
+
+
+def test_delaunay_heat_generator_pinned():
+    """problems.delaunay_heat (qhull tets of a seeded uniform point cloud, P1 Laplacian + lumped mass,
+    heat_tetmesh.py:17-56): this host builds the recorded matrix bits (tests/golden/delaunay_sha.json,
+    written by make_golden.py delaunay), an unstructured pattern (rows of 4 to ~31 entries, no
+    stencil: >16 distinct offsets per 64-row slice), SPD with a Dirichlet face."""
+    import json
+
+    import bench
+
+    fx = json.loads((Path(__file__).parent / "golden" / "delaunay_sha.json").read_text())["delaunay20k"]
+    A, m, nodes, bs, _ = P.workload("delaunay20k")
+    assert bs == 1 and nodes.shape == (A.shape[0], 3)
+    assert (A.shape[0], A.nnz) == (fx["n"], fx["nnz"]) and P.matrix_sha256(A) == fx["A_sha256"]
+    assert int((m == 0).sum()) == fx["dirichlet"]
+    lens = np.diff(A.indptr)
+    assert lens.min() >= 4 and lens.max() > 2 * lens.min() and abs(A - A.T).max() == 0
+    assert bench.dia_counts(A.indptr, A.indices).min() > 16 and bench.sell_kind(A.indptr, A.indices) == 17
+    assert np.all(A.diagonal() > 0)
+    B = P.apply_dbc_masking(A, m)
+    assert np.linalg.eigvalsh(B[:400, :400].toarray()).min() > 0
