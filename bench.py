@@ -666,27 +666,7 @@ def main():
         loop_kernels = {}
     loop_dom = loop_dominant(loop_kernels, A, n, nnz_l) if loop_kernels else None
 
-    # ---- the same solve on views WITH the opt-in value dictionary (1-byte codes of A's few distinct
-    # values; bit-identical): what the 4x smaller A buys (lspcg_solver_views)
     views = solver.views
-    no_codes = None
-    if not args.no_variants and os.environ.get("LSPCG_VALUE_CODES", "0") != "1":
-        os.environ["LSPCG_VALUE_CODES"] = "1"
-        try:
-            s2 = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", dtype=np.float64)
-        finally:
-            del os.environ["LSPCG_VALUE_CODES"]
-        s2.set_spai(L, args.epsilon, block_size=L.block_size)
-        x2 = torch.zeros_like(b)
-        ts2 = []
-        for _ in range(4):
-            x2.zero_()
-            it2, _c2, t2 = s2.solve(b, x2, rtol=args.rtol)
-            ts2.append(t2)
-        no_codes = {"views": s2.views, "iters": it2, "same_x": bool(torch.equal(x2, x)),
-                    "pcg_iter_us": float(np.median(ts2[1:])) / it2 * 1e6,
-                    "loop_kernels_us": {k: v * 1e6 for k, v in s2.time_kernels(b, 40).items()}}
-        del s2
 
     # ---- time-to-rtol beside the neural preconditioner (infer.py:310-321 rows): CG and Jacobi on the
     # same system and rhs, and every method with infer.py's rhs="random" (:300-302, b = A (randn ⊙ mask))
@@ -859,7 +839,6 @@ def main():
             },
             "pcg_loop_spmv": pcg_spmv,
             "solver_views": views,
-            "with_value_codes": no_codes,
             "pcg_loop_kernels": loop_dom,
             "cpu_baseline": cpu,
             "c1_synthetic": c1,

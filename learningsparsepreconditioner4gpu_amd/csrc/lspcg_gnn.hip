@@ -1066,6 +1066,50 @@ double ln_ff_hidden_bound(const FF& f, const float* gamma, const float* beta) {
   }
   return std::max(h1, h2 * h1 + b2 + 0.17);
 }
+// The split-f16 GEMMs carry each layer's result scaled by 2^s (s: emit_frag_h_any's exponent, max |W|
+// 2^s in [2^10, 2^11)); the last layer's messages are summed over a node's edges while still scaled.
+// A matrix of tiny weights beside O(1) biases (2^s large, the bias scaled alike) could push those
+// scaled values past fp32's range, which the per-message unscale never reached.  Returns
+// the largest scaled magnitude, 2^s x (|W| row bound x input bound + max |bias|), over the three
+// layers; gnn_create runs the fp32-MFMA kernels (no scaling) when it exceeds 2^96, which leaves 2^32
+// for a node's message sum.  (Seeded / trained weights: ~2^20.)
+double ln_ff_scaled_bound(const FF& f, const float* gamma, const float* beta) {
+  auto sexp = [](double mx) {
+    if (mx == 0) return 0;
+    int e;
+    std::frexp(mx, &e);
+    return 11 - e;
+  };
+  double w1 = 0, w2 = 0, w3 = 0, r1 = 0, r2 = 0, r3 = 0, b1 = 0, b2 = 0, b3 = 0;
+  for (int i = 0; i < H; ++i) {
+    double r = 0, bb = f.b1[i];
+    for (int k = 0; k < f.in; ++k) {
+      const double w = double(f.W1[i * f.in + k]) * gamma[k];
+      w1 = std::max(w1, std::fabs(w));
+      r += std::fabs(w);
+      bb += double(f.W1[i * f.in + k]) * beta[k];
+    }
+    r1 = std::max(r1, r);
+    b1 = std::max(b1, std::fabs(bb));
+    double q2 = 0, q3 = 0;
+    for (int k = 0; k < H; ++k) {
+      w2 = std::max(w2, std::fabs(double(f.W2[i * H + k])));
+      q2 += std::fabs(double(f.W2[i * H + k]));
+      if (i < f.out) {
+        w3 = std::max(w3, std::fabs(double(f.W3[i * H + k])));
+        q3 += std::fabs(double(f.W3[i * H + k]));
+      }
+    }
+    r2 = std::max(r2, q2);
+    r3 = std::max(r3, q3);
+    b2 = std::max(b2, std::fabs(double(f.b2[i])));
+    if (i < f.out) b3 = std::max(b3, std::fabs(double(f.b3[i])));
+  }
+  const double x1 = std::sqrt(double(f.in - 1));            // LayerNorm output bound
+  const double h1 = r1 * x1 + b1 + 0.17, h2 = r2 * h1 + b2 + 0.17;  // GELU outputs
+  return std::max({std::ldexp(r1 * x1 + b1, sexp(w1)), std::ldexp(r2 * h1 + b2, sexp(w2)),
+                   std::ldexp(r3 * h2 + b3, sexp(w3))});
+}
 void emit_frag_h(std::vector<float>& o, const FF& f, const float* gamma, const float* beta) {
   emit_frag_h_any(o, f, gamma, beta, true);  // kH48 dwords
 }
@@ -1169,6 +1213,7 @@ int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* we
   // MLPs could exceed that run the exact fp32-MFMA kernels instead (same results to ~1e-7, 1.2x slower)
   {
     int64_t ob = ff_size(d.node_in, H) + ff_size(d.edge_in, H);
+    double scaled = 0;  // ln_ff_scaled_bound over the layers
     for (int l = 0; l < d.num_mp_layers; ++l) {
       const float* node = w.data() + ob;
       const float* edge = node + 2 * H + ff_size(H, H);
@@ -1177,9 +1222,12 @@ int lspcg_gnn_create(lspcg_ctx* ctx, const lspcg_gnn_desc* desc, const float* we
       g->hidden_bound = std::max({g->hidden_bound, ln_ff_hidden_bound(ff_at(msgp + 6 * H, 3 * H, H), msgp, msgp + 3 * H),
                                   ln_ff_hidden_bound(ff_at(edge + 6 * H, 3 * H, H), edge, edge + 3 * H),
                                   ln_ff_hidden_bound(ff_at(node + 2 * H, H, H), node, node + H)});
+      scaled = std::max({scaled, ln_ff_scaled_bound(ff_at(msgp + 6 * H, 3 * H, H), msgp, msgp + 3 * H),
+                         ln_ff_scaled_bound(ff_at(edge + 6 * H, 3 * H, H), edge, edge + 3 * H),
+                         ln_ff_scaled_bound(ff_at(node + 2 * H, H, H), node, node + H)});
     }
     const char* ev = std::getenv("LSPCG_GNN_F32");
-    g->f32 = !(g->hidden_bound < 32768.0) || (ev && ev[0] == '1');
+    g->f32 = !(g->hidden_bound < 32768.0) || !(scaled <= std::ldexp(1.0, 96)) || (ev && ev[0] == '1');
   }
   const bool f32 = g->f32;
   std::vector<float> fr;

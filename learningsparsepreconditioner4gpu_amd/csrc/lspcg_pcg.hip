@@ -1183,8 +1183,6 @@ static int elem_grid(int64_t n) {  // 2 elements per lane, >= 2 pairs per lane, 
 
 using namespace lspcg;
 
-constexpr int kValCode8 = 8;  // lspcg_solver::svd: the view's slots are 1-byte dictionary codes
-
 struct lspcg_solver {
   lspcg_ctx* ctx = nullptr;
   const lspcg_mat* A = nullptr;       // the system the loop runs on: A_user, or Ap when reordered
@@ -1240,10 +1238,8 @@ struct lspcg_solver {
   SellPattern spat[3];
   const SellPattern* sp[3] = {nullptr, nullptr, nullptr};
   void* sv[3] = {nullptr, nullptr, nullptr};
-  int svd[3] = {0, 0, 0};  // storage of sv[w]: LSPCG_F32 / LSPCG_F64, or kValCode8 (1-byte dictionary codes)
+  int svd[3] = {0, 0, 0};  // storage of sv[w]: LSPCG_F32 / LSPCG_F64
   int64_t svn[3] = {0, 0, 0};  // entries sv[w] was allocated for (an in-place refill must fit them)
-  float* slut[3] = {nullptr, nullptr, nullptr};  // the dictionary of a coded view (256 floats)
-  bool codes_ok = false;   // value dictionaries allowed (single solves; LSPCG_VALUE_CODES=0 turns them off)
   double* dhist = nullptr;  // device residual history (lspcg_solver_solve with res_hist), grown on demand
   double* hhist = nullptr;  // its pinned host mirror (the history's copy is enqueued, not a blocking copy)
   int64_t dhist_cap = 0;
@@ -1294,7 +1290,7 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   // its address -- and with it every captured iteration graph -- stays valid (get_graph)
   // (the pattern may have been rebuilt at the same host address -- set_dot_order's switch back to the
   // unpermuted A -- so the array's entry count must match the pattern's, not just the pointers)
-  if (w > 0 && s->use_sell && s->sv[w] && !s->slut[w] && s->sp[w] && s->sp[w] == s->sp[0] &&
+  if (w > 0 && s->use_sell && s->sv[w] && s->sp[w] && s->sp[w] == s->sp[0] &&
       view->rowptr == s->Av.rowptr && view->colind == s->Av.colind && view->storage_dtype() == s->svd[w] &&
       s->svn[w] == s->sp[w]->slots()) {
     const SellPattern* P = s->sp[w];
@@ -1304,8 +1300,6 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   }
   (void)hipFree(s->sv[w]);
   s->sv[w] = nullptr;
-  (void)hipFree(s->slut[w]);
-  s->slut[w] = nullptr;
   s->spat[w].release();
   s->sp[w] = nullptr;
   if (!s->use_sell || view->n == 0 || view->nnzb == 0) return LSPCG_OK;
@@ -1331,19 +1325,6 @@ static int build_sell(lspcg_solver* s, int w, const lspcg_mat* view) {
   s->svd[w] = vd;
   s->svn[w] = P->slots();
   s->sp[w] = P;
-  if (s->codes_ok && P->col_bits == 1 && vd == LSPCG_F32 && view->n > s->small_n) {
-    // few distinct values (a structured grid's stencil): 1-byte codes into an LDS dictionary
-    uint8_t* codes = nullptr;
-    float* lut = nullptr;
-    int nk = 0;
-    if (int rc = sdia_value_codes(*P, static_cast<const float*>(s->sv[w]), st, &codes, &lut, &nk)) return rc;
-    if (codes) {
-      (void)hipFree(s->sv[w]);
-      s->sv[w] = codes;
-      s->slut[w] = lut;
-      s->svd[w] = kValCode8;
-    }
-  }
   return LSPCG_OK;
 }
 
@@ -1374,10 +1355,6 @@ static int build_sell_bsr3(lspcg_solver* s, int w, const lspcg_mat* view) {
 template <typename T, class Gx, class Pro, class Epi>
 static int launch_it_gx(lspcg_solver* s, int w, Gx gx, Pro pro, Epi epi, hipStream_t st) {
   if (const SellPattern* P = s->sp[w]) {
-    if (s->svd[w] == kValCode8) {
-      launch_spmv_sdia<T, uint8_t>(*P, s->sv[w], gx, pro, epi, st, false, s->slut[w]);
-      return LSPCG_OK;
-    }
     if constexpr (sizeof(T) == 8) {
       if (s->svd[w] == LSPCG_F32) {
         launch_spmv_sell_cfg<T, float>(*P, s->sv[w], gx, pro, epi, st);
@@ -1830,14 +1807,6 @@ static int solver_create(lspcg_ctx* ctx, const lspcg_mat* A, int precond, bool d
   s->A_user = A;
   s->dia_ok = dia_ok;
   s->reorder_ok = reorder_ok && precond != LSPCG_PRECOND_IC;
-  // value dictionaries: single solves only (the batched tile kernels read fp32 / fp64 views), and
-  // opt-in -- on the headline system the coded A (15 MB instead of 61 MB) left the loop unchanged
-  // (67.5 vs 67.6 us per iteration, KC 20.9 vs 21.3 us: KC is not bound by A's value bytes; DESIGN.md
-  // §5), so it buys memory, not time.  LSPCG_VALUE_CODES=1 turns it on.
-  {
-    const char* e = std::getenv("LSPCG_VALUE_CODES");
-    s->codes_ok = reorder_ok && e && e[0] == '1';
-  }
   s->precond = precond;
   s->dtype = A->dtype;
   s->n = A->n;
@@ -1917,7 +1886,6 @@ static GraphKey graph_key(const lspcg_solver* s) {
       put(P->groups);
     }
     put(s->sv[w]);
-    put(s->slut[w]);
     put(V.rowptr);
     put(V.colind);
     put(V.vals);
@@ -2364,7 +2332,7 @@ int lspcg_solver_views(const lspcg_solver* s, int* col_kind, int* value_bytes) {
   for (int w = 0; w < 3; ++w) {
     const SellPattern* P = s->sp[w];
     col_kind[w] = P ? P->col_bits : 0;
-    value_bytes[w] = !P ? 0 : s->svd[w] == kValCode8 ? 1 : s->svd[w] == LSPCG_F32 ? 4 : 8;
+    value_bytes[w] = !P ? 0 : s->svd[w] == LSPCG_F32 ? 4 : 8;
   }
   return LSPCG_OK;
 }
@@ -2404,7 +2372,6 @@ int lspcg_solver_destroy(lspcg_solver* s) {
   for (void* p : {s->own_A, s->own_L, s->own_LT}) (void)hipFree(p);
   for (int w = 0; w < 3; ++w) {
     (void)hipFree(s->sv[w]);
-    (void)hipFree(s->slut[w]);
     s->spat[w].release();
   }
   (void)hipFree(s->flag);

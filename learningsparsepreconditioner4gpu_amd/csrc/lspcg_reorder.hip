@@ -613,22 +613,16 @@ static int rcm_device(const lspcg_mat* A, int32_t* perm, int32_t* iperm) {
       LSPCG_HIP(hipMemcpyAsync(lvbase + lv, &h0[1], sizeof(int32_t), hipMemcpyHostToDevice, st));
       hipLaunchKernelGGL(k_rcm_place, dim3(1), dim3(64), 0, st, int64_t(1), fa, placed, pos, order);
       // step 1 of level 0; every later level's runs inside the previous level's emit, stamped one
-      // past that level's stamp
-      // (LSPCG_RCM_FUSE=0: a k_rcm_expand launch per level, as before round 5's fold)
-      static const int fuse = [] {
-        const char* e = std::getenv("LSPCG_RCM_FUSE");
-        return e && e[0] == '0' ? 0 : 1;
-      }();
-      if (fuse)
-        hipLaunchKernelGGL(k_rcm_expand, dim3(lg), dim3(kThreads), 0, st, lv, lvm, fa, rp, ci, pos, pkey, mark, ++stamp);
+      // past that level's stamp (round 5's fold; the separate per-level k_rcm_expand launch it
+      // replaced measured no faster and was removed in round 6)
+      constexpr int fuse = 1;
+      hipLaunchKernelGGL(k_rcm_expand, dim3(lg), dim3(kThreads), 0, st, lv, lvm, fa, rp, ci, pos, pkey, mark, ++stamp);
       int l0 = 0, last = -1;
       while (last < 0) {
         for (int l = l0; l < l0 + kRcmBatch; ++l) {
-          const int32_t sl = fuse ? stamp++ : ++stamp;  // level l's stamp; a fused emit stamps level l + 2's nodes sl + 1
+          const int32_t sl = stamp++;  // level l's stamp; the emit stamps level l + 2's nodes sl + 1
           const int32_t* cur = (l & 1) ? fb : fa;
           int32_t* nxt = (l & 1) ? fa : fb;
-          if (!fuse)
-            hipLaunchKernelGGL(k_rcm_expand, dim3(lg), dim3(kThreads), 0, st, lv + l, lvm, cur, rp, ci, pos, pkey, mark, sl);
           hipLaunchKernelGGL(k_rcm_count, dim3(kRcmParts), dim3(256), 0, st, lv + l, lvm, cur, rp, ci, pkey, mark, sl,
                              cnt, parts);
           hipLaunchKernelGGL(k_rcm_emit, dim3(kRcmParts), dim3(256), 0, st, lv + l, lvm, lvbase, cur, rp, ci, deg, pkey,

@@ -1065,135 +1065,4 @@ int sell_fill_values(const SellPattern& P, const int32_t* colind, const void* sr
 }
 
 
-// ---- value dictionary of a SELL-DIA fp32 value array (sdia_value_codes) ------------------------
-constexpr unsigned kCodeEmpty = 0xffffffffu;  // a NaN pattern: reserved as the empty hash slot
-constexpr int kCodeHash = 512;                // open-addressing table (<= 256 keys: load <= 1/2)
-
-__device__ __forceinline__ unsigned code_hash(unsigned k) { return (k * 2654435761u) >> 23; }  // 9 bits
-
-// insert k into table[kCodeHash] (LDS or global); returns false when the table is full
-template <typename Tab>
-__device__ __forceinline__ bool code_insert(Tab* table, unsigned k, unsigned* fresh) {
-  unsigned h = code_hash(k);
-  for (int probe = 0; probe < kCodeHash; ++probe, h = (h + 1) & (kCodeHash - 1)) {
-    const unsigned cur = table[h];
-    if (cur == k) return true;
-    if (cur == kCodeEmpty) {
-      const unsigned old = atomicCAS(&table[h], kCodeEmpty, k);
-      if (old == kCodeEmpty) {
-        *fresh = 1;
-        return true;
-      }
-      if (old == k) return true;
-    }
-  }
-  return false;
-}
-
-// pass 1: distinct bit patterns per workgroup in an LDS table, then merged into the global table;
-// flag[0] |= 1 on more than 256 distinct values (or the reserved pattern), flag[1] counts keys
-__global__ void __launch_bounds__(256) k_code_distinct(int64_t m, const unsigned* __restrict__ v,
-                                                       unsigned* __restrict__ gtab, int* __restrict__ flag) {
-  __shared__ unsigned tab[kCodeHash];
-  __shared__ int cnt, over;
-  for (int i = threadIdx.x; i < kCodeHash; i += blockDim.x) tab[i] = kCodeEmpty;
-  if (threadIdx.x == 0) {
-    cnt = 0;
-    over = 0;
-  }
-  __syncthreads();
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
-    if (over) break;
-    const unsigned k = v[i];
-    unsigned fresh = 0;
-    if (k == kCodeEmpty || !code_insert(tab, k, &fresh)) over = 1;
-    if (fresh && atomicAdd(&cnt, 1) >= 256) over = 1;
-  }
-  __syncthreads();
-  if (over) {
-    if (threadIdx.x == 0) atomicOr(&flag[0], 1);
-    return;
-  }
-  for (int i = threadIdx.x; i < kCodeHash; i += blockDim.x) {
-    const unsigned k = tab[i];
-    if (k == kCodeEmpty) continue;
-    unsigned fresh = 0;
-    if (!code_insert(gtab, k, &fresh)) atomicOr(&flag[0], 1);
-    if (fresh && atomicAdd(&flag[1], 1) >= 256) atomicOr(&flag[0], 1);
-  }
-}
-
-// pass 2 (one workgroup): the <= 256 keys in ascending bit-pattern order -> lut[rank]
-__global__ void __launch_bounds__(512) k_code_lut(const unsigned* __restrict__ gtab, float* __restrict__ lut) {
-  __shared__ unsigned keys[kCodeHash];
-  keys[threadIdx.x] = gtab[threadIdx.x];
-  __syncthreads();
-  const unsigned k = keys[threadIdx.x];
-  if (k == kCodeEmpty) return;
-  int rank = 0;
-  for (int j = 0; j < kCodeHash; ++j) rank += (keys[j] != kCodeEmpty && keys[j] < k);
-  lut[rank] = __builtin_bit_cast(float, k);
-}
-
-// pass 3: codes[i] = the rank of v[i] in the ascending LUT (binary search in LDS)
-__global__ void __launch_bounds__(256) k_code_fill(int64_t m, int nkeys, const unsigned* __restrict__ v,
-                                                   const float* __restrict__ lut, uint8_t* __restrict__ codes) {
-  __shared__ unsigned keys[256];
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) keys[i] = i < nkeys ? __builtin_bit_cast(unsigned, lut[i]) : ~0u;
-  __syncthreads();
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
-    const unsigned k = v[i];
-    int lo = 0, hi = nkeys - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (keys[mid] < k) lo = mid + 1;
-      else hi = mid;
-    }
-    codes[i] = uint8_t(lo);
-  }
-}
-
-int sdia_value_codes(const SellPattern& P, const float* vals, hipStream_t st, uint8_t** codes, float** lut,
-                     int* nkeys) {
-  *codes = nullptr;
-  *lut = nullptr;
-  *nkeys = 0;
-  const int64_t m = kSellC * P.groups;
-  if (P.col_bits != 1 || m == 0) return LSPCG_OK;
-  unsigned* gtab = nullptr;
-  int* flag = nullptr;
-  LSPCG_HIP(hipMalloc(&gtab, sizeof(unsigned) * kCodeHash));
-  std::unique_ptr<unsigned, void (*)(unsigned*)> g1(gtab, [](unsigned* p) { (void)hipFree(p); });
-  LSPCG_HIP(hipMalloc(&flag, sizeof(int) * 2));
-  std::unique_ptr<int, void (*)(int*)> g2(flag, [](int* p) { (void)hipFree(p); });
-  LSPCG_HIP(hipMemsetAsync(gtab, 0xff, sizeof(unsigned) * kCodeHash, st));
-  LSPCG_HIP(hipMemsetAsync(flag, 0, sizeof(int) * 2, st));
-  const int grid = int(std::min<int64_t>((m + 255) / 256, 2048));
-  hipLaunchKernelGGL(k_code_distinct, dim3(grid), dim3(256), 0, st, m, reinterpret_cast<const unsigned*>(vals), gtab,
-                     flag);
-  int hf[2] = {0, 0};
-  LSPCG_HIP(hipMemcpyAsync(hf, flag, sizeof(hf), hipMemcpyDeviceToHost, st));
-  LSPCG_HIP(hipStreamSynchronize(st));
-  if (hf[0] || hf[1] > 256 || hf[1] < 1) return LSPCG_OK;  // no dictionary: the fp32 values stay
-  float* l = nullptr;
-  uint8_t* c = nullptr;
-  LSPCG_HIP(hipMalloc(&l, sizeof(float) * 256));
-  LSPCG_HIP(hipMemsetAsync(l, 0, sizeof(float) * 256, st));
-  LSPCG_HIP(hipMalloc(&c, std::max<int64_t>(m, 1)));
-  hipLaunchKernelGGL(k_code_lut, dim3(1), dim3(kCodeHash), 0, st, gtab, l);
-  hipLaunchKernelGGL(k_code_fill, dim3(grid), dim3(256), 0, st, m, hf[1], reinterpret_cast<const unsigned*>(vals), l, c);
-  const hipError_t e = hipGetLastError();
-  if (e == hipSuccess) LSPCG_HIP(hipStreamSynchronize(st));
-  if (e != hipSuccess) {
-    (void)hipFree(l);
-    (void)hipFree(c);
-    set_error(std::string("sdia_value_codes: ") + hipGetErrorString(e));
-    return LSPCG_ERR_HIP;
-  }
-  *codes = c;
-  *lut = l;
-  *nkeys = hf[1];
-  return LSPCG_OK;
-}
-
 }  // namespace lspcg

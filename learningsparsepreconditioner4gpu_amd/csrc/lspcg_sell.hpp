@@ -177,7 +177,6 @@ struct SdiaArgs {
   const uint16_t* mask;
   const int32_t* dict;
   const VT* vals;
-  const float* lut = nullptr;  // VT = uint8_t: the value dictionary (codes index it; sdia_value_codes)
 };
 
 // ---- the SpMV ----------------------------------------------------------------
@@ -460,20 +459,9 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sellj(SellArgs<VT, int16_t> a
 // never used, masked lanes read x[base]) and its row masks -- is loaded in one batch, and the
 // first tile's batch before the prologue's state read: one memory latency before the value /
 // vector loads instead of three in a row (state, gp, dictionary).
-//
-// VT = uint8_t: the slots hold 1-byte codes into a <= 256-entry dictionary of the view's exact
-// fp32 values (sdia_value_codes; a matrix with few distinct values -- a structured grid's stencil),
-// staged in LDS once per workgroup: value = lut[code], the same value and the same bits, a quarter
-// of the value bytes.
 template <typename T, typename VT, int SB, int TH, int MINW, class Pro, class Gx, class Epi>
 __global__ void __launch_bounds__(TH, MINW) k_spmv_sdia(SdiaArgs<VT> a, Pro pro, Gx gx, Epi epi) {
   constexpr int ND = Epi::NDOT > 0 ? Epi::NDOT : 1;
-  constexpr bool CODED = std::is_same<VT, uint8_t>::value;
-  [[maybe_unused]] __shared__ float slut[CODED ? 256 : 1];
-  if constexpr (CODED) {
-    for (int i = threadIdx.x; i < 256; i += TH) slut[i] = a.lut[i];
-    __syncthreads();
-  }
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   const int64_t ntiles = (a.n + TH - 1) / TH;
@@ -526,13 +514,8 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sdia(SdiaArgs<VT> a, Pro pro,
           xv[u] = gx(c);
         }
 #pragma unroll
-        for (int u = 0; u < SB; ++u) {
-          if constexpr (CODED) {
-            if (m[u]) acc = acc + T(slut[v[u]]) * xv[u];
-          } else {
-            if (m[u]) acc = acc + T(v[u]) * xv[u];
-          }
-        }
+        for (int u = 0; u < SB; ++u)
+          if (m[u]) acc = acc + T(v[u]) * xv[u];
       }
       if constexpr (epi_prefetch<Epi>::value) {
         if (i < a.n) epi.row_pf(i, acc, d, pf);
@@ -786,14 +769,14 @@ inline void launch_spmv_sell_th(const SellPattern& P, const void* vals, Gx gx, P
                      pro, gx, epi);
 }
 
-// SELL-DIA launch (lut: the dictionary of a coded view, VT = uint8_t)
+// SELL-DIA launch
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sdia(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
-                             bool one_tile_per_wg = false, const float* lut = nullptr) {
+                             bool one_tile_per_wg = false) {
   int64_t grid = (P.nb + kSellWG - 1) / kSellWG;
   if (!one_tile_per_wg) grid = std::min<int64_t>(grid, sell_cap(Epi::NDOT > 0));
   if (grid <= 0) return;
-  SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals), lut};
+  SdiaArgs<VT> a{P.n, P.ns, P.gp, static_cast<const uint16_t*>(P.col), P.dict, static_cast<const VT*>(vals)};
   constexpr int MINW = (sizeof(VT) <= 4 && std::is_same<Gx, GatherVec<T>>::value) ? 1536 / kSellWG : 1;
   LSPCG_LAUNCH_SPMV((k_spmv_sdia<T, VT, kSdiaSB, kSellWG, MINW, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
                      0, st, a, pro, gx, epi);
@@ -851,9 +834,6 @@ inline void launch_spmv_sellj(const SellPattern& P, const void* vals, Gx gx, Pro
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
                                  bool one_tile_per_wg = false) {
-  if constexpr (std::is_same<VT, uint8_t>::value) {
-    return;  // coded views are SELL-DIA only: launch_spmv_sdia with their dictionary
-  }
   if (P.jagged()) launch_spmv_sellj<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 1 && P.bs == 3) launch_spmv_bsdia3<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
   else if (P.col_bits == 1) launch_spmv_sdia<T, VT>(P, vals, gx, pro, epi, st, one_tile_per_wg);
@@ -914,9 +894,4 @@ inline bool bsdia_allowed() {
 }
 // its block values (16-B lane chunks) from the BSR's [nnzb][3][3] array
 int bsell_fill_values(const SellPattern& P, const void* src, int src_dtype, int dst_dtype, hipStream_t st, void** out);
-// Value dictionary of a SELL-DIA view's fp32 value array: when it holds <= 256 distinct bit
-// patterns, *codes = one byte per slot (the rank of the slot's value) and *lut = the 256-float
-// dictionary (ascending bit patterns, *nkeys used); otherwise all three stay null / 0.
-int sdia_value_codes(const SellPattern& P, const float* vals, hipStream_t st, uint8_t** codes, float** lut,
-                     int* nkeys);
 }  // namespace lspcg

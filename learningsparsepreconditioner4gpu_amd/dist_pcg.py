@@ -159,6 +159,16 @@ def plan_device(group=None) -> torch.device:
     return torch.device("cpu")
 
 
+def all_ranks_agree(flag: bool, group=None) -> bool:
+    """True when ``flag`` holds on EVERY rank of the group (one all-reduce MIN; the local flag without
+    a process group): decisions that change the collectives' sizes must be taken together."""
+    if _backend(group) is None:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=plan_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
 def build_plan_exchanged(rows: Sequence[sp.csr_matrix], bounds: List[int], rank: int, group=None,
                          split: bool = False) -> HaloPlan:
     """build_plan from this rank's OWN rows only (``rows``: the rank's row blocks, global column
@@ -406,8 +416,11 @@ class DistributedPCG:
         mats = blocks
         L = blocks[1] if has_L else None
         p = self.plan
-        if self.split and not 0 < p.n_int < p.n_own:
-            self.split = False  # nothing to overlap (no interior rows, or no boundary rows)
+        if self.split:
+            # nothing to overlap on a rank with no interior or no boundary rows; the halves of the
+            # reductions are gathered from every rank, so the choice is collective (any rank without
+            # both kinds of rows turns the split off everywhere)
+            self.split = all_ranks_agree(0 < p.n_int < p.n_own, group)
         sidx = np.ascontiguousarray(p.send_idx, dtype=np.int32)
 
         def make_part(local, n_own, r0):

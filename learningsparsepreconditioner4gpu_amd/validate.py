@@ -78,6 +78,15 @@ def _prepare(A, dtype, block_size=1) -> DeviceMatrix:
     return DeviceMatrix.from_scipy(sp.csr_matrix(A), dtype=dtype, block_size=block_size, ctx=Context.get())
 
 
+def _no_device_options(info, dot_order, dot_threads):
+    """``info`` / ``dot_order`` / ``dot_threads`` are options of the HIP path (not in the reference's
+    signatures): the cpu row is pymathprim's own solver, which has neither, so asking for them with
+    device="cpu" (the reference's default) is an error, not a silently empty ``info``."""
+    if info is not None or dot_order != "compensated" or dot_threads != 1:
+        raise ValueError("info / dot_order / dot_threads apply to device='cuda' only: device='cpu' is the "
+                         "reference's pymathprim row (pass device='cuda' for the HIP solver)")
+
+
 def _host_pcg_sequence(A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, method, raise_on_max):
     """The reference's CPU rows as it runs them (validate.py:64-86 / 99-121 / 134-160): host
     ``b = A @ gt``, then per repeat one solver from ``PreconditionedConjugateGradient(device="cpu")``
@@ -119,6 +128,7 @@ def get_cg_iter_time(A, gt, rtol=1e-6, max_iter=0, dtype=np.float64, repeat=1, d
     ``"openblas"`` = parity mode (linalg.PreconditionedConjugateGradient.set_dot_order).
     ``device="cpu"`` (the reference's default) is the reference's pymathprim row (module doc)."""
     if is_cpu_device(device):
+        _no_device_options(info, dot_order, dot_threads)
         return _host_pcg_sequence(A, gt, None, 0.0, rtol, max_iter, repeat, dtype, device, method, True)
     Ad = _prepare(A, dtype)
     rows = Ad.n
@@ -152,6 +162,7 @@ def relative_residual(A: DeviceMatrix, x: torch.Tensor, b: torch.Tensor) -> floa
 def _pcg_generic(method, A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, info=None,
                  dot_order="compensated", dot_threads=1):
     if is_cpu_device(device):
+        _no_device_options(info, dot_order, dot_threads)
         return _host_pcg_sequence(A, gt, spai, epsilon, rtol, max_iter, repeat, dtype, device, method, False)
     Ad = _prepare(A, dtype)
     Ld = spai if isinstance(spai, DeviceMatrix) else _prepare(spai, dtype)

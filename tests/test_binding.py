@@ -139,3 +139,18 @@ def test_random_rhs_seeded_per_sample():
     a = rhs_for("random", m, rng=np.random.default_rng(3))
     b = rhs_for("random", m, rng=np.random.default_rng(3))
     assert np.array_equal(a, b) and not np.array_equal(a, rhs_for("random", m, rng=np.random.default_rng(4)))
+
+
+def test_cpu_device_rejects_device_only_options(stub_pymathprim):
+    """info / dot_order / dot_threads belong to the HIP path; with device='cpu' (the
+    reference's default, pymathprim's row) they raise a clear ValueError instead of leaving info empty."""
+    A = P.kuhn_laplacian(4)
+    gt = np.ones(A.shape[0])
+    for kw in ({"info": {}}, {"dot_order": "openblas"}, {"dot_threads": 8}):
+        with pytest.raises(ValueError, match="device='cuda' only"):
+            validate.get_cg_iter_time(A, gt, method="none", **kw)
+        with pytest.raises(ValueError, match="device='cuda' only"):
+            validate.get_pcg_iter_time(A, gt, A.copy(), 1e-3, **kw)
+    assert not stub_pymathprim.calls  # nothing reached the CPU backend
+    validate.get_pcg_iter_time(A, gt, A.copy(), 1e-3)  # the reference's own call still goes through
+    assert len(stub_pymathprim.calls) == 1

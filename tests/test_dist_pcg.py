@@ -211,6 +211,39 @@ def test_split_plans_interior_first(world):
             assert np.array_equal(sent, got)
 
 
+def _agree_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from learningsparsepreconditioner4gpu_amd.dist_pcg import all_ranks_agree
+
+    A = sp.diags([-np.ones(5), np.full(6, 2.5), -np.ones(5)], [-1, 0, 1], format="csr")
+    bounds = [0, 2, 4, 6]
+    p = build_plan([A], bounds, rank, split=True)
+    q.put((rank, p.n_int, p.n_own, all_ranks_agree(0 < p.n_int < p.n_own), all_ranks_agree(True),
+           all_ranks_agree(rank != 2)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_split_decision_all_ranks_agree():
+    """ADVICE r5 (dist_pcg.py): the interior / boundary split changes the reductions' sizes, so it is
+    decided by all ranks together: on a 6-row chain over 3 ranks the middle rank has no interior rows
+    and every rank turns the split off; a flag true on all ranks stays true, false on one is false
+    everywhere (gloo, world 3)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 3, port, q)) for r in range(3)]
+    for pr in procs:
+        pr.start()
+    outs = sorted([q.get(timeout=120) for _ in range(3)])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert [o[1] for o in outs] == [1, 0, 1] and all(o[2] == 2 for o in outs)
+    assert all(o[3:] == (False, True, False) for o in outs)
+
+
 def test_sum_groups_two_halves():
     """Two 64-group halves per rank are summed rank-major, half by half: the same as treating every
     half as a rank (lspcg_part_scalars with world * 2)."""

@@ -21,6 +21,10 @@ EPS = 3e-3
 
 
 def _system(kind):
+    if kind == "chain":  # 6-row 1-D chain over 3 ranks: the middle rank's two rows are both boundary rows
+        A = sp.diags([-np.ones(5), np.full(6, 2.5), -np.ones(5)], [-1, 0, 1], format="csr")
+        A.sort_indices()
+        return A, _cases.spai_like(A), A @ np.ones(6)
     if kind == "kuhn":
         A, mask = P.kuhn_dirichlet(17)
     else:
@@ -87,7 +91,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port, kind, q, blocks=False, overlap=True):
+def _rank(rank, world, port, kind, q, blocks=False, overlap=True):  # noqa: C901
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LSPCG_DIST_OVERLAP="1" if overlap else "0")
@@ -108,7 +112,7 @@ def _rank(rank, world, port, kind, q, blocks=False, overlap=True):
     it_h, conv_h, x_h, hist_h = d.solve_host(b, rtol=1e-8, return_history=True)
     same = (it_h, conv_h) == (it, conv) and np.array_equal(hist_h, hist) and torch.equal(x_h, x)
     xg = d.gather_solution(x)
-    q.put((rank, it, bool(conv), xg, hist, d.plan.n_own, len(d.plan.halo), same, d.split))
+    q.put((rank, it, bool(conv), xg, hist, d.plan.n_own, len(d.plan.halo), same, d.split, d.plan.n_int))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -132,13 +136,38 @@ def test_multi_rank_matches_oracle(gpu_ctx, world, blocks, overlap):
     A, L, b = _system(kind)
     it_o, x_o, h_o = _oracle(A, L, b, 1e-8)
     assert sum(o[5] for o in outs) == A.shape[0] and all(o[6] > 0 for o in outs)
-    for rank, it, conv, xg, hist, _, _, same, split in outs:
+    for rank, it, conv, xg, hist, _, _, same, split, _ in outs:
         assert split == overlap, rank
         assert same, rank  # device-side scalars = the host recurrence, bit for bit
         assert conv and it == it_o, (rank, it, it_o)
         np.testing.assert_allclose(hist, h_o[: it + 1], rtol=1e-12, atol=0)
         assert np.linalg.norm(xg - x_o) <= 1e-12 * np.linalg.norm(x_o)
     assert all(np.array_equal(outs[0][3], o[3]) for o in outs)  # every rank holds the same solution
+
+
+def test_multi_rank_split_decision_is_collective(gpu_ctx):
+    """a rank with no interior rows (the middle of a 6-row chain over 3 ranks) cannot
+    overlap; the split is decided by all ranks together, so every rank runs one row range and the
+    reductions keep one size on all ranks (the solve then matches the oracle)."""
+    world, kind = 3, "chain"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, kind, q, False, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = sorted([q.get(timeout=100) for _ in range(world)], key=lambda o: o[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    A, L, b = _system(kind)
+    it_o, x_o, h_o = _oracle(A, L, b, 1e-8)
+    assert [o[9] for o in outs][1] == 0  # the middle rank: no interior rows
+    for rank, it, conv, xg, hist, _, _, same, split, _ in outs:
+        assert not split and same, rank
+        assert it == it_o, (rank, it, it_o)  # (6 rows: the oracle too runs its max_iter = n = 6 iterations)
+        np.testing.assert_allclose(hist, h_o[: it + 1], rtol=1e-12, atol=0)
+        assert np.linalg.norm(xg - x_o) <= 1e-12 * np.linalg.norm(x_o)
 
 
 def _rank_rccl(port, q):

@@ -99,6 +99,31 @@ def test_gnn_weights_past_f16_range_run_fp32(gpu_ctx):
     _close(got, want.numpy())
 
 
+def test_gnn_tiny_last_layer_weights_run_fp32(gpu_ctx):
+    """the split-f16 kernels carry a layer's output scaled by 2^s (max |W| 2^s in
+    [2^10, 2^11)) and sum the messages still scaled; a message MLP with tiny last-layer weights
+    (x 1e-30) beside O(1) biases has 2^s ~ 2^110, so its scaled messages could overflow fp32.
+    lspcg_gnn_create runs such weights on the fp32-MFMA kernels (no scaling): a finite forward within
+    1e-5 of the oracle."""
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+
+    A, mask, _ = P.poisson2d_grid(10, 10)
+    s = make_sample(A, mask)
+    ref, gpu = _pair(s.x.shape[1], s.edge_attr.shape[1], 1, seed=3)
+    with torch.no_grad():
+        for m in (gpu, ref):
+            for name, p in m.named_parameters():
+                if "msg_mlp.proj" in name and name.endswith("weight"):
+                    p.mul_(1e-30)
+        _, want = ref(s.x, s.edge_index, s.edge_attr)
+    _, got = gpu(s.x.cuda(), s.edge_index.cuda(), s.edge_attr.cuda())
+    p1 = gpu.precision()
+    assert p1["f32"] and p1["hidden_bound"] < 2 ** 15, p1  # chosen for the scaled range, not the f16 bound
+    got = got.cpu().numpy()
+    assert np.isfinite(got).all()
+    _close(got, want.numpy())
+
+
 @pytest.mark.parametrize("case", ["poisson", "synthetic", "bunny", "elast"])
 def test_gnn_forced_fp32_kernels_match_reference_fixture(gpu_ctx, monkeypatch, case):
     """The fp32-MFMA kernels (LSPCG_GNN_F32=1 forces them at create) on the reference's own

@@ -104,14 +104,20 @@ def test_reordered_fp32(gpu_ctx, monkeypatch):
 
 
 def test_parity_mode_switches_reordering_off(gpu_ctx, monkeypatch):
+    """set_spai on a reordered solver, then set_dot_order('openblas'): A's views are rebuilt for the
+    unpermuted A (a pattern at the same host address, padding differently), so L's and Lᵀ's value
+    arrays are rebuilt too, not refilled in place (the refill checks the array's entry
+    count); the solve equals a parity solver that never reordered, and the recorded scipy run."""
     A, L, b = _system("kuhn27rand")
     monkeypatch.setenv("LSPCG_REORDER", "1")
     s1 = _solver(A, L, "ext_spai")
     assert s1.reorder_info["applied"]
+    v_perm = s1.views
     s1.set_dot_order("openblas", 1)
     assert not s1.reorder_info["applied"]
     monkeypatch.setenv("LSPCG_REORDER", "0")
     s2 = _solver(A, L, "ext_spai", dot_order="openblas", dot_threads=1)
+    assert s1.views == s2.views, (v_perm, s1.views, s2.views)
     it1, c1, x1, h1 = _run(s1, b)
     it2, c2, x2, h2 = _run(s2, b)
     assert c1 and it1 == it2 and np.array_equal(h1, h2) and np.array_equal(x1, x2)
