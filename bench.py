@@ -402,6 +402,7 @@ def irregular_row(workload: str, eps: float, rtol: float, reps: int) -> dict:
             "bandwidth": int(np.abs(Ah.indices - np.repeat(np.arange(A.n), np.diff(Ah.indptr))).max()),
             "spmv_column_storage": KIND_TEXT[kind_loop], "solver_views": s.views, "iters": it, "converged": bool(conv),
             "time_to_rtol_ms": med * 1e3, "pcg_iter_us": med / it * 1e6,
+            "pcg_iter_ps_per_nnz": med / it * 1e12 / max(A.nnz, 1),
             "loop_kernels_us": {k: v * 1e6 for k, v in loop.items()},
             "spmv": {"kernel": f"{KERNEL_NAME.get(kind, 'k_spmv')}<double,double>", "avg_launch_ms_cold": cold,
                      "avg_launch_ms_warm": warm, "alg_bytes": alg, "achieved_GBs_cold": alg / (cold * 1e-3) / 1e9,
@@ -443,18 +444,19 @@ def c1_rows(rtol: float, all_threads: bool = False) -> dict:
             "gpu": gpu, "reference_iters": {"1_openblas_thread": 3236, "8_openblas_threads": 3229}, "cpu": cpu}
 
 
-def c5_rows(rtol: float, concurrency: int = 4) -> dict:
+def c5_rows(rtol: float, concurrency: int = 4, dataset: str = "heat_batch8") -> dict:
     """C5 (the heat-tet batch, 8 systems of 400-32 k vertices -- the reference's real
-    dataset sizes): the batch's ext_spai solves one after another (the reference's loop), with
-    `concurrency` in flight (linalg.solve_many) and as ONE lockstep batch
-    (linalg.BatchedConjugateGradient), best of 3 each; every system keeps its own count."""
+    dataset sizes; ``delaunay_batch8``: the same sizes on unstructured Delaunay tet meshes): the
+    batch's ext_spai solves one after another (the reference's loop), with `concurrency` in flight
+    (linalg.solve_many) and as ONE lockstep batch (linalg.BatchedConjugateGradient), best of 3
+    each; every system keeps its own count."""
     import torch
 
     from learningsparsepreconditioner4gpu_amd.infer import synthetic_dataset
     from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient, solve_many
     from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
 
-    samples = synthetic_dataset("heat_batch8")
+    samples = synthetic_dataset(dataset)
     ws = SimpleInferenceWorkspace(node_features=samples[0].x.shape[1], edge_features=1, seed=0)
     jobs = []
     for smp in samples:
@@ -466,8 +468,9 @@ def c5_rows(rtol: float, concurrency: int = 4) -> dict:
         s.set_spai(L, ws.epsilon)
         jobs.append((s, b, torch.zeros_like(b)))
     solve_many(jobs, rtol, concurrency=1)  # graphs built
-    out = {"workload": "C5 heat_batch8: 8 heat-tet systems (n = %d..%d), ext_spai, rtol %g"
-                       % (min(j[0].n for j in jobs), max(j[0].n for j in jobs), rtol)}
+    out = {"workload": "C5 %s: 8 heat-tet systems (n = %d..%d), ext_spai, rtol %g"
+                       % (dataset, min(j[0].n for j in jobs), max(j[0].n for j in jobs), rtol),
+           "views": sorted({j[0].views["A"]["columns"] for j in jobs})}
     for k in (1, concurrency):
         best = None
         for _ in range(3):
@@ -545,7 +548,8 @@ def config_rows() -> dict:
         M = O._Op(O.spai_operator(L_h, ws.epsilon), A_h.shape, np.float64)
         mi = cpu_max_iter or A_h.shape[0]
         cpu = cpu_rate(A_h, b_h, M, rtol, mi, 1, reps=3)
-        return {"n": A.n, "nnz": A.nnz, "iters": it, "converged": bool(conv), "gpu_ms": t_gpu * 1e3,
+        return {"n": A.n, "nnz": A.nnz, "views": s.views["A"]["columns"], "iters": it, "converged": bool(conv),
+                "gpu_ms": t_gpu * 1e3, "gpu_us_per_iter": t_gpu * 1e6 / max(it, 1),
                 "gpu_it_per_s": it / t_gpu, "cpu_iters": cpu["iters_per_solve"], "cpu_s": cpu["median_s"],
                 "cpu_it_per_s": cpu["it_per_s"], "cpu_bounded": bool(cpu_max_iter)}
 
@@ -555,10 +559,11 @@ def config_rows() -> dict:
 
     out = {"C2_poisson256": one(wl("poisson256"), 1e-8, 0), "C3_heat_bunny": one(wl("bunny"), 1e-6, 0),
            "C4_elasticity": one(wl("elast"), 1e-8, 60)}
-    rows = [one(smp, 1e-8, 0) for smp in synthetic_dataset("heat_batch8")]
-    out["C5_heat_batch8"] = {
-        "systems": rows, "gpu_ms_sum": sum(r["gpu_ms"] for r in rows), "gpu_ms_max": max(r["gpu_ms"] for r in rows),
-        "cpu_s_sum": sum(r["cpu_s"] for r in rows), "cpu_s_max": max(r["cpu_s"] for r in rows)}
+    for ds in ("heat_batch8", "delaunay_batch8"):  # C5 and its variant on unstructured Delaunay meshes
+        rows = [one(smp, 1e-8, 0) for smp in synthetic_dataset(ds)]
+        out[f"C5_{ds}"] = {
+            "systems": rows, "gpu_ms_sum": sum(r["gpu_ms"] for r in rows), "gpu_ms_max": max(r["gpu_ms"] for r in rows),
+            "cpu_s_sum": sum(r["cpu_s"] for r in rows), "cpu_s_max": max(r["cpu_s"] for r in rows)}
     return out
 
 
@@ -772,6 +777,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_variants:
         try:
             c5 = c5_rows(args.rtol)
+            c5["delaunay_batch8"] = c5_rows(args.rtol, dataset="delaunay_batch8")
         except Exception as e:  # pragma: no cover
             c5 = {"failed": str(e)}
         try:
@@ -781,7 +787,7 @@ def main():
         if args.workload == "kuhn101":
             try:
                 irregular = {w: irregular_row(w, args.epsilon, args.rtol, args.spmv_reps)
-                             for w in ("kuhn101rcm", "kuhn101rand")}
+                             for w in ("kuhn101rcm", "kuhn101rand", "delaunay1m")}
             except Exception as e:  # pragma: no cover
                 irregular = {"failed": str(e)}
 

@@ -57,6 +57,8 @@ Fixtures (inputs and the reference's outputs, data only):
     python tests/golden/make_golden.py ichol      # ic_traj.npz only
     python tests/golden/make_golden.py infer      # infer_folder_free.npz only
     python tests/golden/make_golden.py headline kuhn101 gpurun_out/.../kuhn101.npy   # traj_kuhn101.npz
+    python tests/golden/make_golden.py batch delaunay_batch8 gpurun_out/...         # traj_delaunay_batch8.npz
+    python tests/golden/make_golden.py delaunay   # delaunay_sha.json
     python tests/golden/make_golden.py bunny      # bunny_grid.npz only
 """
 from __future__ import annotations
@@ -486,6 +488,58 @@ def headline_fixtures(rval, workload: str, boo_path: str):
     np.savez_compressed(OUT / f"traj_{workload}.npz", **out)
 
 
+def batch_fixtures(rval, dataset: str, boo_dir: str):
+    """traj_<dataset>.npz: the reference's ext_spai PCG on every system of a C5-style dataset
+    (infer.synthetic_dataset, e.g. delaunay_batch8: 8 unstructured Delaunay heat systems of
+    400-32 k vertices) with the bench's own L per system (the HIP GNN's output, dumped on the GPU
+    box by ``tools/dump_gnn_l.py --dataset``; one workspace for the batch, as bench.c5_rows):
+    ``to_csr_cpu`` of A and L and ``get_pcg_iter_time_scipy(A, mask, L, 3e-3, rtol=1e-8)`` through
+    RecordingCG at 1 / 2 / 4 / 8 OpenBLAS threads.  Stored per system k: counts, the 1- and
+    8-thread ‖r_k‖ histories and sha256(x), sha256 of boo, A and L, the oracle's correctly
+    rounded-dot count."""
+    import json
+
+    import threadpoolctl
+
+    from learningsparsepreconditioner4gpu_amd.infer import synthetic_dataset
+    from oracle import linalg as O
+
+    samples = synthetic_dataset(dataset)
+    eps, rtol = 3e-3, 1e-8
+    out = {"dataset": np.array(dataset), "count": np.array(len(samples)), "eps": np.array(eps),
+           "rtol": np.array(rtol), "ref_threads": np.array(HEADLINE_THREADS), "blas_info": np.array(blas_info())}
+    rec = RecordingCG()
+    rval.cg = rec
+    for k, smp in enumerate(samples):
+        path = f"{boo_dir}/{dataset}_{k}.npy"
+        meta = json.load(open(path[:-4] + ".json"))
+        boo = np.load(path)
+        assert boo.dtype == np.float32 and _sha(boo) == meta["sha256"]
+        n = smp.num_nodes
+        A = rval.to_csr_cpu(smp.edge_index, smp.matrix_values, n, smp.mask)
+        L = rval.to_csr_cpu(smp.edge_index, torch.from_numpy(boo), n, smp.mask, dtype=np.float64)
+        gt = smp.mask.numpy().reshape(-1).astype(np.float64)
+        out[f"{k}__n"] = np.array(n)
+        out[f"{k}__boo_sha256"] = np.array(meta["sha256"])
+        out[f"{k}__A_sha256"] = np.array(_sha(A.indptr, A.indices, A.data))
+        out[f"{k}__L_sha256"] = np.array(_sha(L.indptr, L.indices, L.data))
+        counts = []
+        for th in HEADLINE_THREADS:
+            with threadpoolctl.threadpool_limits(th):
+                cnt = rval.get_pcg_iter_time_scipy(A, gt, L, eps, rtol=rtol)
+            assert cnt == rec.count and len(rec.hist) == cnt
+            counts.append(cnt)
+            if th in (1, 8):
+                out[f"{k}__t{th}__hist"] = np.array(rec.hist)
+                out[f"{k}__t{th}__x_sha256"] = np.array(_sha(rec.x))
+        out[f"{k}__ref_counts"] = np.array(counts)
+        b = A @ gt
+        out[f"{k}__oracle_exact_count"] = np.array(O.pcg(A, b, O.spai_operator(L, eps), rtol=rtol, dot="exact")[0])
+        print(dataset, k, "n", n, "reference counts", counts, "exact-dot", int(out[f"{k}__oracle_exact_count"]),
+              flush=True)
+    np.savez_compressed(OUT / f"traj_{dataset}.npz", **out)
+
+
 REFGNN_STRIDE = 127  # every 127th edge's reference output is stored (the GPU test compares there)
 
 
@@ -807,6 +861,12 @@ def main():
 
         sys.path.insert(0, str(ROOT))
         headline_fixtures(rval, sys.argv[2], sys.argv[3])
+        return
+    if sys.argv[1:2] == ["batch"]:  # batch <dataset> <dir of tools/dump_gnn_l.py --dataset output>
+        from neural_cg.utils import validate as rval
+
+        sys.path.insert(0, str(ROOT))
+        batch_fixtures(rval, sys.argv[2], sys.argv[3])
         return
     if sys.argv[1:2] == ["refgnn"]:  # refgnn <workload> <boo .npy from tools/dump_gnn_l.py>
         from neural_cg import data as rdata

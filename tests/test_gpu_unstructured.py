@@ -202,3 +202,153 @@ def test_sell16x_solve_equals_csr_and_oracle(gpu_ctx, monkeypatch, pre):
     assert np.linalg.norm(x - x2) <= 1e-12 * np.linalg.norm(x2) and np.allclose(h, h2, rtol=1e-10, atol=0)
     it_o, x_o, _ = O.pcg(A, b, O.spai_operator(L, 3e-3) if pre == "ext_spai" else None, rtol=1e-10, dot="exact")
     assert it == it_o and np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
+
+
+# ---- the reference's own runs on the Delaunay systems (make_golden.py batch / headline) -----------
+def _shaB(*arrs):
+    import hashlib
+
+    h = hashlib.sha256()
+    for a in arrs:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+_BATCH = {}
+
+
+def _delaunay_batch():
+    """The C5 Delaunay variant as bench.c5_rows builds it (one seeded workspace for the batch), with
+    every system's boo / A / L checked against the sha256 the reference's run recorded."""
+    if _BATCH:
+        return _BATCH["v"]
+    from learningsparsepreconditioner4gpu_amd.infer import synthetic_dataset
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    z = np.load(GOLDEN / "traj_delaunay_batch8.npz")
+    samples = synthetic_dataset("delaunay_batch8")
+    ws = SimpleInferenceWorkspace(node_features=samples[0].x.shape[1], edge_features=1, seed=0)
+    out = []
+    for k, smp in enumerate(samples):
+        d = smp.to("cuda")
+        boo = ws.forward(d.x, d.edge_index, d.edge_attr)
+        L = ws._assemble(d, boo, None)
+        A = ws.system_matrix(d)
+        Ah, Lh = sp.csr_matrix(A.to_scipy()), sp.csr_matrix(L.to_scipy())
+        assert _shaB(boo.cpu().numpy()) == str(z[f"{k}__boo_sha256"]), k
+        assert _shaB(Ah.indptr, Ah.indices, Ah.data) == str(z[f"{k}__A_sha256"]), k
+        assert _shaB(Lh.indptr, Lh.indices, Lh.data) == str(z[f"{k}__L_sha256"]), k
+        b = A.matvec(d.mask.reshape(-1).to(torch.float64))
+        out.append((A, L, b))
+    _BATCH["v"] = (z, ws.epsilon, out)
+    return _BATCH["v"]
+
+
+def _solve_full(A, L, b, eps, rtol, **kw):
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai", **kw)
+    s.set_spai(L, eps)
+    x = torch.zeros_like(b)
+    it, conv, _t, h = s.solve(b, x, rtol=rtol, return_history=True)
+    return it, conv, x, np.asarray(h)
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_delaunay_batch_parity_mode_equals_reference_runs(gpu_ctx, threads):
+    """Parity mode (numpy's ddot order at T OpenBLAS threads) on every system of the C5 Delaunay
+    variant: count, every ‖r_k‖ and sha256(x) equal to the reference's recorded scipy run."""
+    z, eps, systems = _delaunay_batch()
+    for k, (A, L, b) in enumerate(systems):
+        it, conv, x, h = _solve_full(A, L, b, eps, float(z["rtol"]), dot_order="openblas", dot_threads=threads)
+        want = int(z[f"{k}__ref_counts"][[1, 2, 4, 8].index(threads)])
+        assert conv and it == want, (k, it, want)
+        assert np.array_equal(h[:want], z[f"{k}__t{threads}__hist"]), k
+        assert _shaB(x.cpu().numpy()) == str(z[f"{k}__t{threads}__x_sha256"]), k
+
+
+def test_delaunay_batch_default_mode_equals_correctly_rounded_oracle(gpu_ctx):
+    """Default (compensated) order: every system's count equals the oracle's correctly-rounded-dot
+    count recorded beside the reference's runs (on these unstructured 1-1.6 k-iteration solves the
+    reference's OpenBLAS order itself spreads over up to 10 iterations across thread counts and lies up
+    to 9 above the correctly rounded count: the fixture's ref_counts), the true residual is below
+    rtol, and the lockstep batch (BatchedConjugateGradient) gives every system the same count."""
+    from learningsparsepreconditioner4gpu_amd.linalg import BatchedConjugateGradient
+
+    z, eps, systems = _delaunay_batch()
+    rtol = float(z["rtol"])
+    its = []
+    for k, (A, L, b) in enumerate(systems):
+        it, conv, x, _ = _solve_full(A, L, b, eps, rtol)
+        assert conv and it == int(z[f"{k}__oracle_exact_count"]), (k, it, int(z[f"{k}__oracle_exact_count"]),
+                                                                      z[f"{k}__ref_counts"])
+        tres = float(torch.linalg.vector_norm(b - A.matvec(x)) / torch.linalg.vector_norm(b))
+        assert tres < rtol, (k, tres)
+        its.append(it)
+    B = BatchedConjugateGradient([s[0] for s in systems], [s[1] for s in systems], eps)
+    xs = [torch.zeros_like(s[2]) for s in systems]
+    res, _ = B.solve([s[2] for s in systems], xs, rtol)
+    assert [r[0] for r in res] == its
+
+
+def _delaunay1m():
+    if "1m" in _BATCH:
+        return _BATCH["1m"]
+    from learningsparsepreconditioner4gpu_amd import problems as P
+    from learningsparsepreconditioner4gpu_amd.data import make_sample
+    from learningsparsepreconditioner4gpu_amd.workspace import SimpleInferenceWorkspace
+
+    if not (GOLDEN / "traj_delaunay1m.npz").exists():  # (make_golden.py headline delaunay1m: ~2 h of scipy)
+        pytest.skip("traj_delaunay1m.npz not generated yet")
+    z = np.load(GOLDEN / "traj_delaunay1m.npz")
+    fx = _sha_fixture()["delaunay1m"]
+    A_raw, mask, feats, bs, e2n = P.workload("delaunay1m")
+    assert P.matrix_sha256(A_raw) == fx["A_sha256"]  # the container's mesh, bit for bit
+    s = make_sample(A_raw, mask, node_features=feats, block_size=bs, use_edge_features_as_node_feature=e2n)
+    ws = SimpleInferenceWorkspace(node_features=s.x.shape[1], edge_features=s.edge_attr.shape[1], seed=0)
+    d = s.to("cuda")
+    boo = ws.forward(d.x, d.edge_index, d.edge_attr)
+    assert _shaB(boo.cpu().numpy()) == str(z["boo_sha256"]), "GNN output differs from the recorded bench L"
+    L = ws._assemble(d, boo, None)
+    A = ws.system_matrix(d)
+    Ah = sp.csr_matrix(A.to_scipy())
+    assert _shaB(Ah.indptr, Ah.indices, Ah.data) == str(z["A_sha256"])
+    del Ah
+    b = A.matvec(d.mask.reshape(-1).to(torch.float64))
+    _BATCH.clear()
+    _BATCH["1m"] = (z, A, L, b)
+    return _BATCH["1m"]
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_delaunay1m_parity_mode_equals_reference_run(gpu_ctx, threads):
+    """The 1 M-vertex Delaunay system (bench irregular_1m.delaunay1m, SELL-64X views), the bench's GNN
+    L, full 16 k-iteration solve in parity mode: count, every ‖r_k‖ and sha256(x) equal to the
+    reference's recorded run (make_golden.py headline delaunay1m)."""
+    z, A, L, b = _delaunay1m()
+    it, conv, x, h = _solve_full(A, L, b, float(z["eps"]), float(z["rtol"]), dot_order="openblas",
+                                 dot_threads=threads)
+    want = int(z[f"t{threads}__count"])
+    assert conv and it == want, (it, want)
+    assert np.array_equal(h[:want], z[f"t{threads}__hist"])
+    assert _shaB(x.cpu().numpy()) == str(z[f"t{threads}__x_sha256"])
+
+
+def test_delaunay1m_default_mode(gpu_ctx):
+    """Default order on the 1 M Delaunay system: the views are SELL-64X, the count is within 0.2 % of
+    the oracle's correctly-rounded-dot count (16 k iterations: the compensated dots are ~correctly
+    rounded, not exactly) and of the reference's spread, and the true residual is below rtol."""
+    z, A, L, b = _delaunay1m()
+    from learningsparsepreconditioner4gpu_amd.linalg import PreconditionedConjugateGradient
+
+    s = PreconditionedConjugateGradient(A, device="cuda", preconditioner="ext_spai")
+    assert s.views["A"]["columns"] == "sell16x"
+    del s
+    rtol = float(z["rtol"])
+    it, conv, x, _ = _solve_full(A, L, b, float(z["eps"]), rtol)
+    ex = int(z["oracle_exact_count"])
+    counts = [int(c) for c in z["ref_counts"]]
+    assert conv and abs(it - ex) <= 0.002 * ex, (it, ex, counts)
+    assert min(counts) - 0.002 * ex <= it <= max(counts) + 0.002 * ex, (it, counts)
+    tres = float(torch.linalg.vector_norm(b - A.matvec(x)) / torch.linalg.vector_norm(b))
+    assert tres < rtol, tres

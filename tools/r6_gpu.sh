@@ -9,7 +9,7 @@ for s in "$@"; do
   case $s in
     t=*)
       files=$(echo "${s#t=}" | tr ',' ' ')
-      timeout -k 10 900 python -u -m pytest $files -m gpu -x -q --timeout 300 --timeout-method thread > "$out/tests.txt" 2>&1
+      timeout -k 10 900 python -u -m pytest $files -m gpu -x -q --timeout 300 --timeout-method thread ${PYK:+-k "$PYK"} > "$out/tests.txt" 2>&1
       rc=$?; echo "tests rc=$rc"; tail -4 "$out/tests.txt"; [ $rc -eq 0 ] || exit $rc ;;
     probe=*)
       wls=$(echo "${s#probe=}" | tr ',' ' ')
