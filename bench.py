@@ -384,6 +384,7 @@ def irregular_row(workload: str, eps: float, rtol: float, reps: int) -> dict:
     p = torch.randn(A.n, dtype=torch.float64, device="cuda")
     q = torch.empty_like(p)
     kind = A.prepare_spmv()
+    spmv_ro = A.spmv_reorder_info  # (reordered: the timing covers x's gather, the SpMV and y's scatter)
     cold = A.spmv_timed(p, q, reps, flush_bytes=FLUSH_BYTES)
     warm = A.spmv_timed(p, q, 3 * reps)
     alg = spmv_bytes(A.n, A.nnz)
@@ -404,7 +405,9 @@ def irregular_row(workload: str, eps: float, rtol: float, reps: int) -> dict:
             "time_to_rtol_ms": med * 1e3, "pcg_iter_us": med / it * 1e6,
             "pcg_iter_ps_per_nnz": med / it * 1e12 / max(A.nnz, 1),
             "loop_kernels_us": {k: v * 1e6 for k, v in loop.items()},
-            "spmv": {"kernel": f"{KERNEL_NAME.get(kind, 'k_spmv')}<double,double>", "avg_launch_ms_cold": cold,
+            "spmv": {"kernel": f"{KERNEL_NAME.get(kind, 'k_spmv')}<double,double>"
+                               + (" on P A P^T (device RCM): x gathered, y scattered, all three launches timed"
+                                  if spmv_ro["applied"] else ""), "reorder": spmv_ro, "avg_launch_ms_cold": cold,
                      "avg_launch_ms_warm": warm, "alg_bytes": alg, "achieved_GBs_cold": alg / (cold * 1e-3) / 1e9,
                      "frac_cold": alg / (cold * 1e-3) / 1e9 / HBM_PEAK_GBS}}
 

@@ -112,10 +112,20 @@ int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y);
  * same values and dtype and 16-bit column offsets where they fit, that lspcg_spmv then uses -- the
  * results keep the same bits.  *kind (nullable) = the column storage: 1 (SELL-DIA: a sorted scalar
  * CSR whose 64-row slices have <= 16 distinct row-relative offsets col - row, one value slot per
- * offset and a row mask, no column array), 16 (16-bit offsets from the slice's first row), 32
- * (int32 columns), or 0 when the matrix stays on the CSR / BSR kernel (irregular row lengths).
+ * offset and a row mask, no column array), 16 (16-bit offsets from the slice's first row), 17
+ * (SELL-64J: lanes sorted by row length, each 4-entry group stored for its active lanes only), 18
+ * (SELL-64X: SELL-64J reading x from an LDS copy of each 256-row tile's blocks), 32 (int32
+ * columns), or 0 when the matrix stays on the CSR / BSR kernel (irregular row lengths).  A numbering
+ * far from banded (the solver's rule: mean |col - row| > 4 n^(2/3), n >= 16384, env LSPCG_REORDER) is
+ * analysed on P A P^T, P the device reverse Cuthill-McKee permutation, every row's entries in their
+ * original order; lspcg_spmv then gathers x into that numbering and scatters y back (same bits).
  * lspcg_mat_scale_columns drops it. */
 int lspcg_mat_prepare_spmv(lspcg_mat* A, int* kind);
+/* the analysis step's reordering (lspcg_mat_prepare_spmv): *applied = 1 when the SpMV runs on
+ * P A P^T; mean |col - row| before / after (either pointer may be NULL).  Replaces nothing in the
+ * reference (its SpMV is scipy's, on the caller's numbering). */
+int lspcg_mat_spmv_reorder_info(const lspcg_mat* A, int* applied, double* mean_offset_before,
+                                double* mean_offset_after);
 /* average device ms of one SpMV launch, HIP events on the ctx stream.  flush_bytes == 0:
  * reps back-to-back launches (warm caches); > 0: before every launch a read of a flush_bytes
  * buffer evicts the 256 MiB Infinity Cache (cold); the launch time is (reps x (flush + SpMV)

@@ -53,6 +53,7 @@ SIGNATURES = {
     "lspcg_spmv_variant_timed": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int64, p_f64]),
     "lspcg_spmv_sell_timed": (C.c_int, [vp, vp, C.c_int, vp, vp, C.c_int, C.c_int64, p_f64]),
     "lspcg_mat_prepare_spmv": (C.c_int, [vp, C.POINTER(C.c_int)]),
+    "lspcg_mat_spmv_reorder_info": (C.c_int, [vp, C.POINTER(C.c_int), p_f64, p_f64]),
     "lspcg_read_timed": (C.c_int, [vp, C.c_int64, C.c_int, C.c_int64, p_f64]),
     "lspcg_ic0": (C.c_int, [vp, pp, p_f64]),
     "lspcg_ainv0": (C.c_int, [vp, pp, p_f64]),

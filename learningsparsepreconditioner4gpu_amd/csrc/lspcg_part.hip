@@ -274,8 +274,8 @@ template <typename T, class Epi>
 int part_spmv(lspcg_part* p, const lspcg_mat* M, const void* x, Epi epi) {
   hipStream_t st = p->ctx->stream;
   const T* xv = static_cast<const T*>(x);
-  if (const SellCopy* c = M->sell) {
-    launch_spmv_sell_cfg<T, T>(c->P, c->vals, GatherVec<T>{xv}, ProNone{}, epi, st);
+  if (const SellCopy* c = M->sell; c && !c->ro.perm) {  // (a reordered copy is of P M Pᵀ: the row epilogues
+    launch_spmv_sell_cfg<T, T>(c->P, c->vals, GatherVec<T>{xv}, ProNone{}, epi, st);  // need M's rows)
     return LSPCG_OK;
   }
   return launch_spmv_any<T>(M, xv, ProNone{}, epi, st);

@@ -845,13 +845,25 @@ inline void launch_spmv_sell_cfg(const SellPattern& P, const void* vals, Gx gx, 
 }  // namespace lspcg
 
 // SELL copy attached to a matrix handle for the standalone SpMV (same values, same dtype)
+// (reordered: the copy is of P A Pᵀ; lspcg_spmv gathers x into xs and the SpMV stores each row at
+// its original place, EpiStorePerm; ys is unused)
 struct SellCopy {
   lspcg::SellPattern P;
   void* vals = nullptr;
+  lspcg::Reorder ro;
+  lspcg_mat* Ap = nullptr;  // P A Pᵀ (owned), its rowptr is P.rowptr
+  void* xs = nullptr;
+  void* ys = nullptr;
   void release() {
     P.release();
     (void)hipFree(vals);
     vals = nullptr;
+    ro.release();
+    if (Ap) lspcg_mat_destroy(Ap);
+    Ap = nullptr;
+    (void)hipFree(xs);
+    (void)hipFree(ys);
+    xs = ys = nullptr;
   }
 };
 

@@ -60,6 +60,24 @@ struct EpiStore {
   unsigned* ticket = nullptr;
 };
 
+// Epilogue of the reordered standalone SpMV (lspcg_spmv on P A Pᵀ): row r of the permuted system is
+// row perm[r / BS] (block row) of the caller's, so the result goes straight to its place:
+// y[BS perm[r / BS] + r % BS] = s (no scatter pass).
+template <typename T, int BS>
+struct EpiStorePerm {
+  static constexpr int NDOT = 0;
+  T* y;
+  const int32_t* perm;
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ void row(int64_t r, T s, DD*) const {
+    const int64_t I = r / BS;
+    gst(y + int64_t(BS) * perm[I] + (r - I * BS), s);
+  }
+  __device__ __forceinline__ void fin(const double*) const {}
+  double* partials = nullptr;
+  unsigned* ticket = nullptr;
+};
+
 // Entries are loaded in groups of 4 consecutive scalar entries (16-B column-index loads,
 // 2x16-B fp64 value loads) with NO per-element predicate: group indices are clamped to the
 // chunk, and the index/value arrays carry kEntryPad padding entries (column 0, value 0),

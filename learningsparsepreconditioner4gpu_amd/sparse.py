@@ -219,11 +219,19 @@ class DeviceMatrix:
 
     def prepare_spmv(self) -> int:
         """Analysis step: attach a SELL-64 copy that :meth:`matvec` then uses (same bits).
-        Returns the column storage (1 = SELL-DIA, 16 = 16-bit offsets, 32 = int32) or 0
-        when the CSR kernel stays in use."""
+        Returns the column storage (1 = SELL-DIA, 16 = 16-bit offsets, 17 = SELL-64J, 18 = SELL-64X,
+        32 = int32) or 0 when the CSR kernel stays in use.  A numbering far from banded is analysed
+        on its reverse-Cuthill-McKee permutation (:attr:`spmv_reorder_info`)."""
         kind = C.c_int()
         _lib.call("lspcg_mat_prepare_spmv", self.handle, C.byref(kind))
         return kind.value
+
+    @property
+    def spmv_reorder_info(self) -> dict:
+        """The analysis step's reordering: applied, mean |col - row| before / after (lspcg_mat_spmv_reorder_info)."""
+        ap, before, after = C.c_int(), C.c_double(), C.c_double()
+        _lib.call("lspcg_mat_spmv_reorder_info", self.handle, C.byref(ap), C.byref(before), C.byref(after))
+        return {"applied": bool(ap.value), "mean_offset_before": before.value, "mean_offset_after": after.value}
 
     def spmv_timed(self, x: torch.Tensor, y: torch.Tensor, reps: int, flush_bytes: int = 0) -> float:
         """Average device ms of one SpMV launch: ``reps`` back-to-back launches (warm), or with

@@ -411,3 +411,49 @@ def test_sellc_views_equal_sell16_and_csr(gpu_ctx, monkeypatch, kind, pre, dtype
     if dtype == np.float64:
         it_o, x_o, _ = O.pcg(A, b, O.spai_operator(L, 3e-3) if pre == "ext_spai" else None, rtol=1e-8, dot="exact")
         assert it == it_o and np.linalg.norm(x - x_o) <= 1e-12 * np.linalg.norm(x_o)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("kind", ["kuhn27rand", "poisson160rand", "elast_rand"])
+def test_prepare_spmv_reorders_far_from_banded(gpu_ctx, monkeypatch, kind, dtype):
+    """The standalone SpMV's analysis step (lspcg_mat_prepare_spmv) applies the solver's rule: a
+    numbering far from banded is analysed on P A Pᵀ (device RCM) and lspcg_spmv gathers x into that
+    numbering and scatters y back -- scipy's bits (every row's entries keep their order).  BSR 3x3:
+    the block graph's permutation, 3 scalars per block row.  Banded numberings are left alone."""
+    from learningsparsepreconditioner4gpu_amd.sparse import DeviceMatrix
+
+    monkeypatch.delenv("LSPCG_REORDER", raising=False)
+    bs = 1
+    if kind == "elast_rand":  # 19,440 block rows, block rows randomly renumbered
+        A0, _, _ = P.elasticity_box(60, 18, 18)
+        nb = A0.shape[0] // 3
+        pb = np.random.default_rng(1).permutation(nb)
+        p = (3 * pb[:, None] + np.arange(3)[None, :]).ravel()
+        B = sp.bsr_matrix(sp.csr_matrix(sp.csr_matrix(A0)[p][:, p]), blocksize=(3, 3))
+        B.sort_indices()
+        bs = 3
+    else:
+        A = _system(kind)[0]
+        A.sort_indices()
+        if dtype == np.float32:
+            A.data = A.data.astype(np.float32).astype(np.float64)
+    D = (DeviceMatrix.from_scipy(B, dtype=dtype, block_size=3) if bs == 3
+         else DeviceMatrix.from_scipy(A, dtype=dtype))
+    kind_v = D.prepare_spmv()
+    info = D.spmv_reorder_info
+    assert info["applied"] and info["mean_offset_after"] < 0.1 * info["mean_offset_before"], info
+    assert kind_v != 0
+    n = D.n
+    x = np.random.default_rng(2).normal(size=n).astype(dtype)
+    y = D.matvec(torch.as_tensor(x, device="cuda")).cpu().numpy()
+    if bs == 3:  # scipy's bsr_matvec order: blocks by column, c = 0, 1, 2 inside a block
+        ref = sp.bsr_matrix((B.data.astype(dtype), B.indices, B.indptr), shape=B.shape) @ x
+    else:
+        ref = (sp.csr_matrix((A.data.astype(dtype), A.indices, A.indptr), shape=A.shape) if dtype == np.float32
+               else A) @ x
+    assert np.array_equal(y, ref), (kind, dtype)
+    ms = D.spmv_timed(torch.as_tensor(x, device="cuda"), torch.empty(n, dtype=torch.float64 if
+                      dtype == np.float64 else torch.float32, device="cuda"), 3)
+    assert ms > 0
+    K = DeviceMatrix.from_scipy(sp.csr_matrix(P.kuhn_dirichlet(27)[0]))  # banded: analysed as given
+    assert K.prepare_spmv() == 1 and not K.spmv_reorder_info["applied"]

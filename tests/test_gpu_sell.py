@@ -34,6 +34,13 @@ def _sell_spmv(Ad, x, compact):
     return y.cpu().numpy()
 
 
+@pytest.fixture(autouse=True)
+def _given_numbering(monkeypatch):
+    """The layouts are tested on the numbering given: the analysis step's reverse-Cuthill-McKee
+    reordering of far-from-banded matrices (tests/test_gpu_reorder.py) is turned off here."""
+    monkeypatch.setenv("LSPCG_REORDER", "0")
+
+
 MATS = {
     "synthetic": lambda: P.generate_spd_sparse_matrix(3000, 3e-3, 1e-5, np.random.RandomState(0)),
     "kuhn": lambda: P.kuhn_laplacian(13),
