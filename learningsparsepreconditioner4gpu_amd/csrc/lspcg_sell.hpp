@@ -805,6 +805,9 @@ inline void launch_spmv_bsdia3(const SellPattern& P, const void* vals, Gx gx, Pr
 }
 
 // SELL-64J / SELL-64X launch: 256-row tiles (4 slices), the SELL-64 grid rules
+#ifndef LSPCG_JAG_QB
+#define LSPCG_JAG_QB 2  // groups of 4 entries per batch
+#endif
 template <typename T, typename VT, class Pro, class Gx, class Epi>
 inline void launch_spmv_sellj(const SellPattern& P, const void* vals, Gx gx, Pro pro, Epi epi, hipStream_t st,
                               bool one_tile_per_wg = false) {
@@ -821,13 +824,13 @@ inline void launch_spmv_sellj(const SellPattern& P, const void* vals, Gx gx, Pro
   if constexpr (std::is_same<Gx, GatherVec<T>>::value) {
     if (P.col_bits == kSellJagX) {
       const size_t lds = size_t(P.kx) * kSellXBlk * sizeof(T);
-      LSPCG_LAUNCH_SPMV((k_spmv_sellj<T, VT, 2, kSellWG, MINW, true, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
+      LSPCG_LAUNCH_SPMV((k_spmv_sellj<T, VT, LSPCG_JAG_QB, kSellWG, MINW, true, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
                          lds, st, a, pro, gx, epi);
       return;
     }
   }
   if (P.col_bits != kSellJag) return;  // (SELL-64X needs a plain vector gather: sell_build_pattern's callers)
-  LSPCG_LAUNCH_SPMV((k_spmv_sellj<T, VT, 2, kSellWG, MINW, false, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
+  LSPCG_LAUNCH_SPMV((k_spmv_sellj<T, VT, LSPCG_JAG_QB, kSellWG, MINW, false, Pro, Gx, Epi>), dim3(unsigned(grid)), dim3(kSellWG),
                      0, st, a, pro, gx, epi);
 }
 

@@ -13,10 +13,10 @@ import json
 import re
 import sys
 
-KERNELS = {"KA t=L^T r": r"k_spmv_s(?:ell|dia)<double, float.*EpiT<double, false>",
-           "KB z=L t+eps r, rho": r"k_spmv_s(?:ell|dia)<double, float.*EpiZG<double, false>",
+KERNELS = {"KA t=L^T r": r"k_spmv_s(?:ellj?|dia)<double, float.*EpiT<double, false>",
+           "KB z=L t+eps r, rho": r"k_spmv_s(?:ellj?|dia)<double, float.*EpiZG<double, false>",
            "UP p, x": r"k_update_p_g<double",
-           "KC q=A p, pi": r"k_spmv_s(?:ell|dia)<double, float.*EpiQG<double>",
+           "KC q=A p, pi": r"k_spmv_s(?:ellj?|dia)<double, float.*EpiQG<double>",
            "UR r": r"k_update_r_g<double"}
 
 

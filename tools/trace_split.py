@@ -52,9 +52,12 @@ def main(path, alg_bytes=ALG_BYTES):
             res[kern].update(alg_bytes=alg_bytes, cold_TBps=tbs, cold_frac_of_8TBps=tbs / PEAK_TBS)
     # the PCG loop's five launches (graph-replayed and direct), average duration per kind
     import re
-    loop = {"KA t=L^T r": r"k_spmv_s(?:ell|dia)<double, float.*EpiT<double, false>",
-            "KB z=L t+eps r, rho": r"k_spmv_s(?:ell|dia)<double, float.*EpiZG<double, false>",
-            "UP p, x": r"k_update_p_g<double", "KC q=A p, pi": r"k_spmv_s(?:ell|dia)<double, float.*EpiQG<double>",
+    # (KA / KB / KC: the headline's SELL-DIA kernels only -- the bench's irregular rows run systems of
+    # the same size on SELL-64 / SELL-64C / SELL-64X kernels; UP / UR are the same kernels for all of
+    # them and pooled)
+    loop = {"KA t=L^T r": r"k_spmv_sdia<double, float.*EpiT<double, false>",
+            "KB z=L t+eps r, rho": r"k_spmv_sdia<double, float.*EpiZG<double, false>",
+            "UP p, x": r"k_update_p_g<double", "KC q=A p, pi": r"k_spmv_sdia<double, float.*EpiQG<double>",
             "UR r": r"k_update_r_g<double"}
     # the bench system's launches only: the largest grid of each kind (smaller systems -- C1, C5 --
     # launch smaller grids), without the predicated launches that exit at once after convergence
