@@ -359,9 +359,39 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sellj(SellArgs<VT, int16_t> a
     c1 = cp[1];
     rl = a.lmap[kSellC * sl + lane];
   };
-  {
+  // QB groups' loads (values, column words) of the lane's row, issued for the active lanes only;
+  // advances the element offset and the count shift register
+  struct Batch {
+    VT v[QB][4];
+    i16x4 cc[QB];
+  };
+  auto issue = [&](Batch& B, int32_t& eo, uint64_t& lo, uint64_t& hi) {
+#pragma unroll
+    for (int u = 0; u < QB; ++u) {
+      const int cq = int((lo >> (8 * u)) & 0xffu);
+      B.cc[u] = i16x4{kSellPad16, kSellPad16, kSellPad16, kSellPad16};
+      B.v[u][0] = B.v[u][1] = B.v[u][2] = B.v[u][3] = VT(0);
+      if (lane < cq) {
+        Vec4Ld<VT>::load(a.vals + int64_t(eo) + 4 * lane, B.v[u]);
+        B.cc[u] = *(const __attribute__((address_space(1))) i16x4*)(a.col + int64_t(eo) + 4 * lane);
+      }
+      eo += 4 * cq;
+    }
+    lo = (lo >> (8 * QB)) | (hi << (64 - 8 * QB));
+    hi >>= 8 * QB;
+  };
+  uint64_t lo = 0, hi = 0;
+  int32_t eo = 0;
+  Batch cur;
+  {  // the first tile's metadata and first batch (matrix data only) before the prologue's state read
     const int64_t s = int64_t(blockIdx.x) * (TH / 64) + w;
-    if (int64_t(blockIdx.x) < ntiles && s < a.ns) meta(s);
+    if (int64_t(blockIdx.x) < ntiles && s < a.ns) {
+      meta(s);
+      lo = c0;
+      hi = c1;
+      eo = e0;
+      if (lo & 0xffu) issue(cur, eo, lo, hi);
+    }
   }
   if (pro.exit()) return;
   gx.prepare();
@@ -370,6 +400,15 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sellj(SellArgs<VT, int16_t> a
 #pragma unroll
   for (int j = 0; j < ND; ++j) d[j] = dd_zero();
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t s = tile * (TH / 64) + w;
+    const bool live = s < a.ns;  // wave-uniform
+    if (live && tile != int64_t(blockIdx.x)) {  // the first batch's loads fly during the staging
+      meta(s);
+      lo = c0;
+      hi = c1;
+      eo = e0;
+      if (lo & 0xffu) issue(cur, eo, lo, hi);
+    }
     if constexpr (XS) {  // the tile's x blocks -> LDS (16-B loads; a block past n element by element)
       if (tile != int64_t(blockIdx.x)) __syncthreads();  // the previous tile's LDS reads are done
       const int32_t b0 = a.xlp[tile], nbk = a.xlp[tile + 1] - b0;
@@ -388,9 +427,7 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sellj(SellArgs<VT, int16_t> a
       }
       __syncthreads();
     }
-    const int64_t s = tile * (TH / 64) + w;
-    if (s < a.ns) {  // wave-uniform
-      if (tile != int64_t(blockIdx.x)) meta(s);
+    if (live) {
       const int32_t base = int32_t(s * kSellC);
       const int64_t i = int64_t(base) + rl;
       T acc = T(0);
@@ -398,49 +435,30 @@ __global__ void __launch_bounds__(TH, MINW) k_spmv_sellj(SellArgs<VT, int16_t> a
       if constexpr (epi_prefetch<Epi>::value) {
         if (i < a.n) pf = epi.prefetch(i);
       }
-      uint64_t lo = c0, hi = c1;
-      int32_t eo = e0;
-      while (lo & 0xffu) {  // wave-uniform: groups left
-        VT v[QB][4];
-        int c[QB][4];
+      bool have = (c0 & 0xffu) != 0;
+      while (have) {  // wave-uniform: software-pipelined, the next batch's loads beside this one's gathers
+        const bool more = (lo & 0xffu) != 0;
+        Batch nxt;
+        if (more) issue(nxt, eo, lo, hi);
         bool m[QB][4];
-        [[maybe_unused]] int o16[QB][4];
-        int32_t eu = eo;
+        T xv[QB][4];
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
-          const int cq = int((lo >> (8 * u)) & 0xffu);
-          const bool act = lane < cq;
-          i16x4 cc = {kSellPad16, kSellPad16, kSellPad16, kSellPad16};
-          v[u][0] = v[u][1] = v[u][2] = v[u][3] = VT(0);
-          if (act) {
-            Vec4Ld<VT>::load(a.vals + int64_t(eu) + 4 * lane, v[u]);
-            cc = *(const __attribute__((address_space(1))) i16x4*)(a.col + int64_t(eu) + 4 * lane);
-          }
-          const int o[4] = {cc.x, cc.y, cc.z, cc.w};
+          const int o[4] = {cur.cc[u].x, cur.cc[u].y, cur.cc[u].z, cur.cc[u].w};
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             m[u][j] = o[j] != kSellPad16;
-            c[u][j] = base + (o[j] != kSellPad16 ? o[j] : 0);
-            o16[u][j] = o[j];
+            if constexpr (XS) xv[u][j] = sx[m[u][j] ? o[j] : 0];
+            else xv[u][j] = gx(base + (m[u][j] ? o[j] : 0));
           }
-          eu += 4 * cq;
         }
-        T xv[QB][4];
-#pragma unroll
-        for (int u = 0; u < QB; ++u)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if constexpr (XS) xv[u][j] = sx[m[u][j] ? o16[u][j] : 0];
-            else xv[u][j] = gx(c[u][j]);
-          }
 #pragma unroll
         for (int u = 0; u < QB; ++u)
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            if (m[u][j]) acc = acc + T(v[u][j]) * xv[u][j];
-        eo = eu;
-        lo = (lo >> (8 * QB)) | (hi << (64 - 8 * QB));
-        hi >>= 8 * QB;
+            if (m[u][j]) acc = acc + T(cur.v[u][j]) * xv[u][j];
+        if (more) cur = nxt;
+        have = more;
       }
       if constexpr (epi_prefetch<Epi>::value) {
         if (i < a.n) epi.row_pf(i, acc, d, pf);
