@@ -211,11 +211,10 @@ int lspcg_solver_set_dot_order(lspcg_solver* s, int order, int threads);
 /* The iteration views the solver built for A (0), L (1), Lᵀ (2): col_kind[w] = 0 (staged CSR kernel),
  * 1 (SELL-DIA: no column array), 16 / 32 (SELL-64 with 16-bit / int32 columns), 8 (SELL-64C: one-byte
  * codes into per-slice dictionaries of <= 64 row-relative offsets, 16-bit columns for slices with
- * more; unstructured orderings, LSPCG_SELLC=0 turns it off); value_bytes[w] = 8
- * (fp64), 4 (fp64 matrix stored exactly as fp32), 1 (one-byte codes into a <= 256-entry dictionary
- * of the view's exact values, SELL-DIA only: matrices with few distinct values, e.g. a structured
- * grid's stencil; opt-in with LSPCG_VALUE_CODES=1: it saves memory, not time), 0 (no view).  Same bits
- * in every case. */
+ * more; unstructured orderings, LSPCG_SELLC=0 turns it off), 17 (SELL-64J: unstructured meshes, each
+ * slice's rows sorted by length, no padded slots), 18 (SELL-64X: SELL-64J reading x through the row
+ * tile's LDS-staged blocks); value_bytes[w] = 8 (fp64), 4 (fp64 matrix stored exactly as fp32),
+ * 0 (no view).  Same bits in every case. */
 int lspcg_solver_views(const lspcg_solver* s, int* col_kind, int* value_bytes);
 int lspcg_solver_reorder_info(const lspcg_solver* s, int* applied, double* mean_offset_before,
                               double* mean_offset_after);
