@@ -105,7 +105,9 @@ int lspcg_mat_rcm(const lspcg_mat* A, int32_t* perm, int* applied, double* mean_
                   double* mean_offset_after);
 
 /* ---- kernels ---- */
-/* y = A x (scipy csr_matvec bit pattern: per-row sequential sum in index order) */
+/* y = A x (scipy csr_matvec bit pattern: per-row sequential sum in index order).  x and y must not
+ * overlap.  After a reordering lspcg_mat_prepare_spmv (lspcg_mat_spmv_reorder_info) the call gathers x
+ * into a scratch vector owned by A, so calls on one matrix must run on one stream at a time. */
 int lspcg_spmv(lspcg_ctx* ctx, const lspcg_mat* A, const void* x, void* y);
 /* analysis step (cf. rocSPARSE csrmv_analysis): attach a SELL-64 copy of a scalar CSR matrix, or
  * the BSELL-64 block copy of a BSR 3x3 (one column per block, block values in 16-B lane chunks), with the
