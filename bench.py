@@ -395,9 +395,23 @@ def irregular_row(workload: str, eps: float, rtol: float, reps: int) -> dict:
             "cloud, P1 Laplacian + lumped mass, heat_tetmesh.py)" if workload.startswith("delaunay")
             else "the headline system renumbered")
     lens = np.diff(Ah.indptr)
+    pad = sell_slots(Ah.indptr) / max(A.nnz, 1)
+    # why these views (a mesh whose loop misses the structured headline's per-entry time
+    # names the format it runs on and the reason)
+    view_text = {"sdia": "SELL-DIA", "sell16": "SELL-64 with 16-bit column offsets", "sell32": "SELL-64 with int32 columns",
+                 "sellc": "SELL-64C (one-byte offset codes)", "sell16j": "SELL-64J (jagged: no padded slots)",
+                 "sell16x": "SELL-64X (jagged, x blocks staged in LDS per 256-row tile)", "csr": "the staged CSR kernel"}
+    ro = s.reorder_info
+    reason = (f"input numbering: {dc.mean():.0f} distinct row-relative offsets per 64-row slice on average (max "
+              f"{int(dc.max())}; SELL-DIA needs <= 16 in every slice, SELL-64C <= 64 in most), rows of "
+              f"{int(lens.min())}-{int(lens.max())} entries (SELL-64 would store {pad:.2f} slots per entry); "
+              + ("the solver runs on its device-RCM placement (mean |col - row| %.0f -> %.0f) with "
+                 % (ro["mean_offset_before"], ro["mean_offset_after"]) if ro["applied"] else "the solver runs ")
+              + view_text.get(s.views["A"]["columns"], s.views["A"]["columns"]) + " views")
     return {"workload": f"{workload}: {what} ({how}), n={A.n}, nnz={A.nnz}, ext_spai, rtol {rtol:g}",
+            "views_reason": reason,
             "row_entries": {"mean": float(lens.mean()), "min": int(lens.min()), "max": int(lens.max())},
-            "sell_slots_per_nnz": sell_slots(Ah.indptr) / max(A.nnz, 1),
+            "sell_slots_per_nnz": pad,
             "solver_reorder": s.reorder_info, "solver_setup_ms": setup_ms,
             "distinct_offsets_per_slice": {"mean": float(dc.mean()), "max": int(dc.max())},
             "bandwidth": int(np.abs(Ah.indices - np.repeat(np.arange(A.n), np.diff(Ah.indptr))).max()),
@@ -791,6 +805,8 @@ def main():
             try:
                 irregular = {w: irregular_row(w, args.epsilon, args.rtol, args.spmv_reps)
                              for w in ("kuhn101rcm", "kuhn101rand", "delaunay1m")}
+                for row in irregular.values():  # per-entry loop time against this run's structured headline
+                    row["pcg_iter_per_nnz_vs_headline"] = row["pcg_iter_ps_per_nnz"] / (t_iter * 1e12 / max(A.nnz, 1))
             except Exception as e:  # pragma: no cover
                 irregular = {"failed": str(e)}
 
